@@ -1,0 +1,105 @@
+"""ctypes binding of libdetrpose_hip.so (include/detrpose_hip.h).
+
+Loading fails loudly: there is no CPU or eager-PyTorch fallback for any op of the
+forward. Build the library with `python -m detrpose_amd.build` (or
+__graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DETRPOSE_HIP_LIB", os.path.join(_HERE, "lib", "libdetrpose_hip.so"))
+
+DP_F32, DP_BF16 = 0, 1
+ACT = {None: 0, "none": 0, "relu": 1, "silu": 2, "gelu": 3}
+
+i32, i64, f32, vp = C.c_int32, C.c_int64, C.c_float, C.c_void_p
+
+
+class ConvDesc(C.Structure):
+    """Mirror of dp_conv_desc."""
+    _fields_ = [
+        ("in_", vp), ("in_bstride", i64), ("in_pstride", i32), ("in_h", i32), ("in_w", i32), ("cin", i32),
+        ("weight", vp), ("kpad", i32),
+        ("bias", vp),
+        ("kh", i32), ("kw", i32), ("stride", i32), ("pad_t", i32), ("pad_l", i32),
+        ("out", vp), ("out_bstride", i64), ("out_pstride", i32), ("out_h", i32), ("out_w", i32), ("cout", i32),
+        ("res", vp), ("res_bstride", i64), ("res_pstride", i32),
+        ("batch", i32),
+        ("act", i32), ("has_lab", i32), ("lab_scale", f32), ("lab_bias", f32),
+        ("dtype", i32),
+        ("up", vp), ("up_bstride", i64), ("up_pstride", i32),
+    ]
+
+
+class RowMap(C.Structure):
+    """Mirror of dp_rowmap: row r -> base + (r // group) * stride_g + (r % group) * stride_r."""
+    _fields_ = [("base", i64), ("group", i32), ("stride_g", i64), ("stride_r", i64)]
+
+
+def rowmap(base=0, group=1, stride_g=0, stride_r=0) -> RowMap:
+    return RowMap(int(base), int(group), int(stride_g), int(stride_r))
+
+
+def contiguous_rows(ld: int, base: int = 0) -> RowMap:
+    return RowMap(int(base), 1, int(ld), 0)
+
+
+_SIGS = {
+    "dp_last_error": (C.c_char_p, []),
+    "dp_version": (i32, []),
+    "dp_conv2d": (i32, [C.POINTER(ConvDesc), vp]),
+    "dp_dwconv2d": (i32, [C.POINTER(ConvDesc), vp]),
+    "dp_stem_conv": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, f32, f32, vp, i64, i32, i32, vp]),
+    "dp_maxpool2x2_pad_rb": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, vp]),
+    "dp_add_rows": (i32, [vp, RowMap, vp, RowMap, vp, RowMap, i32, i32, i32, vp]),
+    "dp_layernorm": (i32, [vp, RowMap, vp, RowMap, vp, RowMap, vp, vp, f32, i32, i32, vp, RowMap, i32, i32,
+                           vp, i32, vp, i32, vp]),
+    "dp_gate_layernorm": (i32, [vp, i32, vp, vp, vp, vp, f32, i32, i32, i32, vp]),
+    "dp_attention": (i32, [vp, i32, vp, vp, i32, vp, i32, i32, i32, i64, i64, i64, i32, i32, i32, i32, vp]),
+    "dp_msda": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "dp_topk": (i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
+    "dp_class_max": (i32, [vp, i32, i32, vp, vp, i32, vp, i32, vp]),
+    "dp_gather_rows": (i32, [vp, i64, vp, i32, i32, i32, vp, i32, vp]),
+    "dp_refpoint_init": (i32, [vp, vp, vp, i32, i32, i32, vp, vp]),
+    "dp_broadcast": (i32, [vp, i64, vp, i32, vp]),
+    "dp_sine_embed": (i32, [vp, i32, i32, i32, vp, vp, i32, vp]),
+    "dp_linear_small": (i32, [vp, RowMap, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp, vp]),
+    "dp_pose_refine": (i32, [vp, vp, i32, vp, f32, i32, i32, vp, vp, vp]),
+    "dp_pre_pose": (i32, [vp, vp, i32, i32, vp, vp]),
+    "dp_lqe_stats": (i32, [vp, i64, i32, i32, i32, vp, i32, i32, i32, vp, i32, vp]),
+    "dp_postprocess": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+}
+
+EXPORTED = tuple(k for k in _SIGS)
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load and prototype the library (once). Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HipError(f"libdetrpose_hip.so not found at {LIB_PATH}: the DETRPose forward runs only on the HIP "
+                       f"kernels (no CPU fallback). Build it with `python -m detrpose_amd.build`.")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = ""):
+    if rc:
+        msg = load().dp_last_error().decode(errors="replace")
+        raise HipError(f"{what or 'dp call'} failed (rc={rc}): {msg}")

@@ -1,0 +1,91 @@
+// Shared device helpers for the DETRPose gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/detrpose_hip.h"
+
+typedef __bf16 bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- error reporting
+void dp_set_error(const char* fmt, ...);
+int dp_check_launch(const char* what);
+
+#define DP_REQUIRE(cond, ...)                 \
+  do {                                        \
+    if (!(cond)) {                            \
+      dp_set_error(__VA_ARGS__);              \
+      return DP_EINVAL;                       \
+    }                                         \
+  } while (0)
+
+// ---------------------------------------------------------------- scalar conversions
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16_t x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float x) { return (bf16_t)x; }
+
+// 16-byte vector of T: 8 bf16 or 4 f32
+template <typename T> struct Vec16;
+template <> struct Vec16<bf16_t> {
+  static constexpr int N = 8;
+  bf16x8 v;
+  __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
+  __device__ __forceinline__ void set(int i, float x) { v[i] = (bf16_t)x; }
+};
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  f32x4 v;
+  __device__ __forceinline__ float get(int i) const { return v[i]; }
+  __device__ __forceinline__ void set(int i, float x) { v[i] = x; }
+};
+
+template <typename T>
+__device__ __forceinline__ Vec16<T> load16(const T* p) {
+  Vec16<T> r;
+  *reinterpret_cast<uint4*>(&r.v) = *reinterpret_cast<const uint4*>(p);
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void store16(T* p, const Vec16<T>& r) {
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(&r.v);
+}
+
+// ---------------------------------------------------------------- activations
+__device__ __forceinline__ float apply_act(float x, int act) {
+  switch (act) {
+    case DP_ACT_RELU: return fmaxf(x, 0.f);
+    case DP_ACT_SILU: return x / (1.f + __expf(-x));
+    case DP_ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    default: return x;
+  }
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// ---------------------------------------------------------------- wave reductions (64 lanes)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ int64_t rowmap_off(const dp_rowmap& m, int64_t r) {
+  int64_t g = r / m.group;
+  int64_t i = r - g * m.group;
+  return m.base + g * m.stride_g + i * m.stride_r;
+}
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

@@ -1,0 +1,190 @@
+// Bandwidth-bound spatial kernels of the HGNetv2 backbone / SCDown, NHWC:
+//  * depthwise k x k conv + folded BN + act (LightConvBNAct.conv2, hgnetv2.py:137-166;
+//    HG_Stage downsample, hgnetv2.py:349-358; SCDown.cv2, hybrid_encoder.py:130-137)
+//  * StemBlock.stem1 3x3 s2 conv straight from the f32 NCHW image (hgnetv2.py:171-177)
+//  * StemBlock's F.pad(0,1,0,1) + MaxPool2d(2,1,ceil_mode) (hgnetv2.py:215,217)
+// These run at arithmetic intensity 2-12 FLOP/B, far under the MFMA ridge (~312), so
+// they are plain 16-byte-vector VALU kernels: one thread = one pixel x 16 bytes of
+// channels, consecutive threads on consecutive channel chunks (coalesced rows).
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv_kernel(dp_conv_desc d, int64_t total, int nchunk) {
+  constexpr int VEC = Vec16<T>::N;
+  int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const int cc = (int)(gid % nchunk);
+  int64_t pix = gid / nchunk;
+  const int hw = d.out_h * d.out_w;
+  const int b = (int)(pix / hw);
+  const int rem = (int)(pix - (int64_t)b * hw);
+  const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
+  const int c0 = cc * VEC;
+  const T* in = reinterpret_cast<const T*>(d.in) + (int64_t)b * d.in_bstride + c0;
+  const float* w = reinterpret_cast<const float*>(d.weight) + c0;
+  float acc[VEC];
+#pragma unroll
+  for (int t = 0; t < VEC; ++t) acc[t] = d.bias ? d.bias[c0 + t] : 0.f;
+  const int iy0 = oy * d.stride - d.pad_t, ix0 = ox * d.stride - d.pad_l;
+  for (int ky = 0; ky < d.kh; ++ky) {
+    const int iy = iy0 + ky;
+    if (iy < 0 || iy >= d.in_h) continue;
+    for (int kx = 0; kx < d.kw; ++kx) {
+      const int ix = ix0 + kx;
+      if (ix < 0 || ix >= d.in_w) continue;
+      Vec16<T> v = load16(in + ((int64_t)iy * d.in_w + ix) * d.in_pstride);
+      const float* wk = w + (ky * d.kw + kx) * d.cin;
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) acc[t] = fmaf(v.get(t), wk[t], acc[t]);
+    }
+  }
+  Vec16<T> o;
+#pragma unroll
+  for (int t = 0; t < VEC; ++t) {
+    float v = apply_act(acc[t], d.act);
+    if (d.has_lab) v = d.lab_scale * v + d.lab_bias;
+    o.set(t, v);
+  }
+  T* out = reinterpret_cast<T*>(d.out) + (int64_t)b * d.out_bstride + (int64_t)rem * d.out_pstride + c0;
+  store16(out, o);
+}
+
+// one thread per output pixel, all cout channels (cout <= 64); image f32 NCHW, 3 channels
+template <typename T>
+__global__ __launch_bounds__(256) void stem_conv_kernel(const float* __restrict__ img, int batch, int h, int w,
+                                                        const float* __restrict__ wt, const float* __restrict__ bias,
+                                                        int cout, int has_lab, float ls, float lb, T* __restrict__ out,
+                                                        int64_t obs, int ops) {
+  __shared__ float sw[64 * 27];
+  __shared__ float sb[64];
+  for (int i = threadIdx.x; i < cout * 27; i += blockDim.x) sw[i] = wt[i];
+  for (int i = threadIdx.x; i < cout; i += blockDim.x) sb[i] = bias[i];
+  __syncthreads();
+  const int oh = (h + 1) / 2, ow = (w + 1) / 2;
+  int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)batch * oh * ow) return;
+  const int b = (int)(gid / (oh * ow));
+  const int rem = (int)(gid - (int64_t)b * oh * ow);
+  const int oy = rem / ow, ox = rem - oy * ow;
+  float x[27];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iy = 2 * oy - 1 + ky, ix = 2 * ox - 1 + kx;
+        const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+        x[(c * 3 + ky) * 3 + kx] = ok ? img[(((int64_t)b * 3 + c) * h + iy) * w + ix] : 0.f;
+      }
+  T* o = out + (int64_t)b * obs + (int64_t)rem * ops;
+  for (int n0 = 0; n0 < cout; n0 += 8) {
+    float r[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int n = n0 + t;
+      float a = 0.f;
+      if (n < cout) {
+        a = sb[n];
+#pragma unroll
+        for (int k = 0; k < 27; ++k) a = fmaf(x[k], sw[n * 27 + k], a);
+        a = fmaxf(a, 0.f);
+        if (has_lab) a = ls * a + lb;
+      }
+      r[t] = a;
+    }
+    for (int t = 0; t < 8 && n0 + t < cout; ++t) o[n0 + t] = from_f32<T>(r[t]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, int64_t ibs, int ips, int batch, int h,
+                                                      int w, int c, T* __restrict__ out, int64_t obs, int ops) {
+  constexpr int VEC = Vec16<T>::N;
+  const int nchunk = c / VEC;
+  int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)batch * h * w * nchunk) return;
+  const int cc = (int)(gid % nchunk);
+  const int64_t pix = gid / nchunk;
+  const int b = (int)(pix / (h * w));
+  const int rem = (int)(pix - (int64_t)b * h * w);
+  const int y = rem / w, x = rem - y * w;
+  const T* base = in + (int64_t)b * ibs + cc * VEC;
+  float m[VEC];
+#pragma unroll
+  for (int t = 0; t < VEC; ++t) m[t] = -INFINITY;
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int yy = y + dy, xx = x + dx;
+      if (yy < h && xx < w) {
+        Vec16<T> v = load16(base + ((int64_t)yy * w + xx) * ips);
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) m[t] = fmaxf(m[t], v.get(t));
+      } else {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) m[t] = fmaxf(m[t], 0.f);  // F.pad zero participates
+      }
+    }
+  Vec16<T> o;
+#pragma unroll
+  for (int t = 0; t < VEC; ++t) o.set(t, m[t]);
+  store16(out + (int64_t)b * obs + (int64_t)rem * ops + cc * VEC, o);
+}
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
+  DP_REQUIRE(dp != nullptr, "dp_dwconv2d: null descriptor");
+  const dp_conv_desc& d = *dp;
+  const int VEC = d.dtype == DP_BF16 ? 8 : 4;
+  DP_REQUIRE(d.cin == d.cout && d.cin % VEC == 0, "dp_dwconv2d: channels %d/%d must match and be a multiple of %d",
+             d.cin, d.cout, VEC);
+  DP_REQUIRE(d.in_pstride % VEC == 0 && d.out_pstride % VEC == 0 && d.in_bstride % VEC == 0 &&
+                 d.out_bstride % VEC == 0 && al16(d.in) && al16(d.out),
+             "dp_dwconv2d: 16-byte alignment required");
+  const int nchunk = d.cin / VEC;
+  const int64_t total = (int64_t)d.batch * d.out_h * d.out_w * nchunk;
+  dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  if (d.dtype == DP_BF16) hipLaunchKernelGGL(dwconv_kernel<bf16_t>, grid, block, 0, as_stream(stream), d, total, nchunk);
+  else hipLaunchKernelGGL(dwconv_kernel<float>, grid, block, 0, as_stream(stream), d, total, nchunk);
+  return dp_check_launch("dp_dwconv2d");
+}
+
+extern "C" int dp_stem_conv(const float* image, int32_t batch, int32_t h, int32_t w, const float* weight,
+                            const float* bias, int32_t cout, int32_t has_lab, float lab_scale, float lab_bias,
+                            void* out, int64_t out_bstride, int32_t out_pstride, int32_t dtype, void* stream) {
+  DP_REQUIRE(image && weight && bias && out, "dp_stem_conv: null pointer");
+  DP_REQUIRE(cout > 0 && cout <= 64, "dp_stem_conv: cout=%d (max 64)", cout);
+  const int64_t total = (int64_t)batch * ((h + 1) / 2) * ((w + 1) / 2);
+  dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(stem_conv_kernel<bf16_t>, grid, block, 0, as_stream(stream), image, batch, h, w, weight, bias,
+                       cout, has_lab, lab_scale, lab_bias, reinterpret_cast<bf16_t*>(out), out_bstride, out_pstride);
+  else
+    hipLaunchKernelGGL(stem_conv_kernel<float>, grid, block, 0, as_stream(stream), image, batch, h, w, weight, bias,
+                       cout, has_lab, lab_scale, lab_bias, reinterpret_cast<float*>(out), out_bstride, out_pstride);
+  return dp_check_launch("dp_stem_conv");
+}
+
+extern "C" int dp_maxpool2x2_pad_rb(const void* in, int64_t in_bstride, int32_t in_pstride, int32_t batch, int32_t h,
+                                    int32_t w, int32_t c, void* out, int64_t out_bstride, int32_t out_pstride,
+                                    int32_t dtype, void* stream) {
+  const int VEC = dtype == DP_BF16 ? 8 : 4;
+  DP_REQUIRE(c % VEC == 0 && in_pstride % VEC == 0 && out_pstride % VEC == 0 && al16(in) && al16(out),
+             "dp_maxpool2x2_pad_rb: 16-byte alignment required");
+  const int64_t total = (int64_t)batch * h * w * (c / VEC);
+  dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(maxpool_kernel<bf16_t>, grid, block, 0, as_stream(stream), reinterpret_cast<const bf16_t*>(in),
+                       in_bstride, in_pstride, batch, h, w, c, reinterpret_cast<bf16_t*>(out), out_bstride, out_pstride);
+  else
+    hipLaunchKernelGGL(maxpool_kernel<float>, grid, block, 0, as_stream(stream), reinterpret_cast<const float*>(in),
+                       in_bstride, in_pstride, batch, h, w, c, reinterpret_cast<float*>(out), out_bstride, out_pstride);
+  return dp_check_launch("dp_maxpool2x2_pad_rb");
+}

@@ -1,0 +1,81 @@
+"""DETRPose top level: the drop-in for src/models/detrpose/detrpose.py.
+
+`DETRPose(backbone, encoder, transformer)` keeps the reference constructor and
+state_dict layout (detrpose.py:15-67), `.deploy()` returns self (69-74) and
+`forward(samples) -> {'pred_logits', 'pred_keypoints'}` (76-81, eval/deploy output
+layout: logits (B,Q,2), keypoints (B,Q,17,2)). The forward runs entirely on the HIP
+kernels of libdetrpose_hip.so through detrpose_amd.engine; there is no eager-torch or
+CPU fallback.
+
+`build_model(size)` is the constructor the north star names ("build_model"); the
+reference has no such function (only LazyConfig + instantiate), so it reads the
+N/L/X kwargs from detrpose_amd.configs.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .configs import get_config
+from .hgnetv2 import HGNetv2
+from .hybrid_encoder import HybridEncoder
+from .postprocesses import PostProcess
+from .transformer import Transformer
+
+
+class DETRPose(nn.Module):
+    def __init__(self, backbone, encoder, transformer, is_trainable=True, trainable_energy=False, dtype="bf16"):
+        super().__init__()
+        self.backbone = backbone
+        self.encoder = encoder
+        self.transformer = transformer
+        self.layer_loss = torch.zeros(1, dtype=torch.float32)
+        self.compute_dtype = dtype
+        self._engine = None
+
+    # -- reference API
+    def deploy(self):
+        self.eval()
+        return self
+
+    def set_dtype(self, dtype: str):
+        """'bf16' (default; bf16 storage, f32 accumulation) or 'fp32' (parity mode)."""
+        if dtype != self.compute_dtype:
+            self.compute_dtype = dtype
+            self._engine = None
+        return self
+
+    def engine(self, device="cuda"):
+        from .engine import Engine
+        dev = torch.device(device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        if self._engine is None or self._engine.device != dev:
+            self._engine = Engine(self, self.compute_dtype, dev)
+        return self._engine
+
+    def _load_from_state_dict(self, *args, **kw):
+        self._engine = None  # weights changed: repack on next forward
+        super()._load_from_state_dict(*args, **kw)
+
+    @torch.no_grad()
+    def forward(self, samples, targets=None):
+        if self.training or targets is not None:
+            raise NotImplementedError("training forward (DN queries, aux outputs) is outside the inference hot path")
+        if not samples.is_cuda:
+            raise RuntimeError("DETRPose (MI355X) runs on the GPU only: move the images to a HIP device")
+        eng = self.engine(samples.device)
+        B = samples.shape[0]
+        plan = eng.plan(B)
+        if samples.data_ptr() != plan.input.data_ptr():
+            plan.input.copy_(samples.to(torch.float32), non_blocking=True)
+        plan.run()
+        return {k: v.clone() for k, v in plan.outputs.items()}
+
+
+def build_model(size: str = "l", dtype: str = "bf16", cfg: dict | None = None):
+    """Build (DETRPose, PostProcess) for size 'n' | 'l' | 'x' with the reference kwargs."""
+    cfg = cfg or get_config(size)
+    model = DETRPose(HGNetv2(**cfg["backbone"]), HybridEncoder(**cfg["encoder"]),
+                     Transformer(**cfg["transformer"]), dtype=dtype)
+    return model, PostProcess(**cfg["postprocessor"])

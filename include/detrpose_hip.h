@@ -1,0 +1,184 @@
+/*
+ * detrpose_hip.h — C ABI of libdetrpose_hip.so, the MI355X (gfx950) kernels of the
+ * DETRPose inference forward.
+ *
+ * The reference has no native code and no FFI (SURVEY.md §1 key fact 1): its forward
+ * is DETRPose.forward (src/models/detrpose/detrpose.py:76-81) built from torch leaf
+ * ops. Each entry point below replaces one of those leaf ops / fused op groups; the
+ * comment on each names the reference code it stands in for. The Python host in
+ * detrpose_amd/ binds these with ctypes (detrpose_amd/_lib.py); INTEGRATION.md shows
+ * the binding a maintainer adds to the reference.
+ *
+ * Conventions
+ *  - Activations are channels-last (NHWC). Element (b, y, x, c) of a map lives at
+ *    base + b*bstride + (y*w + x)*pstride + c  (elements, not bytes), so a kernel can
+ *    read/write a channel slice of a wider concat buffer in place.
+ *  - dtype: DP_F32 (parity mode) or DP_BF16 (bf16 storage, fp32 accumulation).
+ *    Small decoder-head tensors (reference points, corners, logits) are always f32.
+ *  - Every call enqueues asynchronously on `stream` (a hipStream_t) and never
+ *    allocates device memory or synchronises. Buffers belong to the caller.
+ *  - Return 0 on success; non-zero is a hipError_t or DP_EINVAL, with a message in
+ *    dp_last_error(). Calls are stateless and re-entrant per stream.
+ */
+#ifndef DETRPOSE_HIP_H
+#define DETRPOSE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { DP_F32 = 0, DP_BF16 = 1 };
+enum { DP_ACT_NONE = 0, DP_ACT_RELU = 1, DP_ACT_SILU = 2, DP_ACT_GELU = 3 };
+enum { DP_EINVAL = 1000 };
+
+/* Descriptor of one convolution / linear layer run as an implicit GEMM:
+ * M = batch*out_h*out_w rows, N = cout, K = kh*kw*cin (k = (ky*kw + kx)*cin + c). */
+typedef struct dp_conv_desc {
+  const void* in;  int64_t in_bstride;  int32_t in_pstride;  int32_t in_h, in_w, cin;
+  const void* weight;  int32_t kpad;      /* [cout][kpad] of dtype, zero padded in k */
+  const float* bias;                      /* [cout] (folded BN shift) or NULL        */
+  int32_t kh, kw, stride, pad_t, pad_l;
+  void* out;       int64_t out_bstride; int32_t out_pstride; int32_t out_h, out_w, cout;
+  const void* res; int64_t res_bstride; int32_t res_pstride;  /* added after act, or NULL */
+  int32_t batch;
+  int32_t act;     int32_t has_lab;  float lab_scale, lab_bias;  /* y = lab(act(x)) + res */
+  int32_t dtype;
+  /* upsample2x > 0: also write nearest x2 copy to up (concat buffer slice) */
+  void* up;        int64_t up_bstride;  int32_t up_pstride;
+} dp_conv_desc;
+
+/* Row map: row r -> element offset  base + (r / group)*stride_g + (r % group)*stride_r. */
+typedef struct dp_rowmap {
+  int64_t base;  int32_t group;  int64_t stride_g;  int64_t stride_r;
+} dp_rowmap;
+
+const char* dp_last_error(void);
+int dp_version(void);
+
+/* nn.Conv2d (+ folded BatchNorm / FrozenBatchNorm2d) + act (+ LAB) (+ residual),
+ * dense groups=1. Replaces ConvBNAct (hgnetv2.py:82-134), ConvNormLayer(_fuse)
+ * (hybrid_encoder.py:56-128), VGGBlock deploy conv (139-189) and every nn.Linear of
+ * the path (as a 1x1 conv over rows). MFMA implicit GEMM. */
+int dp_conv2d(const dp_conv_desc* d, void* stream);
+
+/* Depthwise conv (groups == channels) + folded BN + act: LightConvBNAct.conv2
+ * (hgnetv2.py:137-166), HG_Stage downsample (349-358), SCDown.cv2
+ * (hybrid_encoder.py:130-137). weight is f32 [kh][kw][C]. */
+int dp_dwconv2d(const dp_conv_desc* d, void* stream);
+
+/* StemBlock.stem1 (hgnetv2.py:171-177): 3x3 s2 p1 conv over the f32 NCHW image,
+ * folded FrozenBN, ReLU (+ LAB); writes NHWC dtype. weight f32 [cout][3][3][3]. */
+int dp_stem_conv(const float* image, int32_t batch, int32_t h, int32_t w,
+                 const float* weight, const float* bias, int32_t cout,
+                 int32_t has_lab, float lab_scale, float lab_bias,
+                 void* out, int64_t out_bstride, int32_t out_pstride, int32_t dtype, void* stream);
+
+/* F.pad(x,(0,1,0,1)) + MaxPool2d(2, 1, ceil_mode=True) of StemBlock (hgnetv2.py:215,217). */
+int dp_maxpool2x2_pad_rb(const void* in, int64_t in_bstride, int32_t in_pstride,
+                         int32_t batch, int32_t h, int32_t w, int32_t c,
+                         void* out, int64_t out_bstride, int32_t out_pstride, int32_t dtype, void* stream);
+
+/* out[r] = a[r] + b[r] over `rows` rows of `c` elements (row maps as above). */
+int dp_add_rows(void* out, dp_rowmap om, const void* a, dp_rowmap am, const void* b, dp_rowmap bm,
+                int32_t rows, int32_t c, int32_t dtype, void* stream);
+
+/* out = LayerNorm(x + res) (+ post on rows selected by post map).  nn.LayerNorm with
+ * the residual adds of TransformerEncoderLayer (hybrid_encoder.py:281-296) and the
+ * decoder layer (transformer.py:405-442).  row_mask/mask_period/masked_row: rows whose
+ * mask[r % period] != 0 output masked_row (f32 [c]) instead: Transformer two-stage
+ * masked_fill + enc_output + LN of a zero row (transformer.py:1232-1236). */
+int dp_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, const void* res, dp_rowmap rm,
+                 const float* gamma, const float* beta, float eps, int32_t rows, int32_t c,
+                 const void* post, dp_rowmap pm, int32_t post_group, int32_t post_skip,
+                 const uint8_t* row_mask, int32_t mask_period, const float* masked_row,
+                 int32_t dtype, void* stream);
+
+/* Gate.forward (transformer.py:222-235) after its Linear: gates/xcat are [rows][2c]
+ * ([x1 | x2]); out = LN(sigmoid(g1)*x1 + sigmoid(g2)*x2). */
+int dp_gate_layernorm(void* out, int32_t out_ld, const void* gates, const void* xcat,
+                      const float* gamma, const float* beta, float eps, int32_t rows, int32_t c,
+                      int32_t dtype, void* stream);
+
+/* Scaled dot-product attention core of nn.MultiheadAttention (batch_first, no mask,
+ * eval): softmax(QK^T/sqrt(dh))V per head.  Sequence s = (o, i), o < n_outer,
+ * i < n_inner; token t of it is row o*so + i*si + t*st of q/k/v (leading dims ld_q,
+ * ld_kv) and of out (ld_o).  Within-/across-instance attention (transformer.py:
+ * 403-419) and AIFI (hybrid_encoder.py:276-279). */
+int dp_attention(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv,
+                 void* out, int32_t ld_o, int32_t n_outer, int32_t n_inner,
+                 int64_t so, int64_t si, int64_t st, int32_t seqlen, int32_t nhead, int32_t dh,
+                 int32_t dtype, void* stream);
+
+/* MSDeformAttn default branch (ms_deform_attn.py:384-444) + ms_deform_attn_core_pytorch
+ * (145-193): softmax of the attention logits over L*P, loc = ref + off/(W_l,H_l),
+ * bilinear (zeros, align_corners=False) gather from the head-major memory, weighted sum.
+ *  value:  [batch][S][nhead*dh] dtype; level l occupies rows [lvl_start[l], +h*w)
+ *  offattn:[batch*lq][nhead*L*P*3] dtype: offsets (h,l,p,xy) then logits (h,l,p)
+ *  ref:    [batch*lq][2] f32 (x, y) in [0,1];  out: [batch*lq] rows of ld_out, dtype */
+int dp_msda(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */,
+            int32_t nlevels, const void* offattn, const float* ref, void* out, int32_t ld_out,
+            int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, int32_t dtype, void* stream);
+
+/* Per-row top-k of f32 scores, sorted descending, ties to the lower index:
+ * torch.topk over the two-stage class score (transformer.py:1240) and in PostProcess
+ * (postprocesses.py:19).  k <= 256, n <= 65536. idx is int64. */
+int dp_topk(const float* x, int32_t rows, int32_t n, int32_t ld, int32_t k,
+            float* out_val, int64_t* out_idx, void* stream);
+
+/* out[r] = max_j (x[r] . w[j] + b[j]), j < nclass: enc_out_class_embed + .max(-1)
+ * (transformer.py:1239-1240). w f32 [nclass][c]. */
+int dp_class_max(const void* x, int32_t rows, int32_t c, const float* w, const float* b,
+                 int32_t nclass, float* out, int32_t dtype, void* stream);
+
+/* dst[b][j] = src[b][idx[b][j]] (rows of c elements): topk gather (transformer.py:1243-1248). */
+int dp_gather_rows(const void* src, int64_t src_bstride, const int64_t* idx, int32_t batch, int32_t k,
+                   int32_t c, void* dst, int32_t dtype, void* stream);
+
+/* Two-stage reference points (transformer.py:1250-1254): kp = sigmoid(delta + anchor[idx]),
+ * ref[b][q] = [mean(kp), kp...].  delta f32 [batch*k][nkp*2], anchors f32 [S][2]. */
+int dp_refpoint_init(const float* delta, const float* anchors, const int64_t* idx, int32_t batch,
+                     int32_t k, int32_t nkp, float* ref, void* stream);
+
+/* Repeat a `bytes`-long block `count` times (query construction, transformer.py:1256-1261). */
+int dp_broadcast(const void* src, int64_t bytes, void* dst, int32_t count, void* stream);
+
+/* TransformerDecoder.sine_embedding of the keypoint refs (transformer.py:518-540):
+ * ref f32 [rows][1+nkp][2] (centre skipped), dim_t f32 [c/2] (the decoder.dim_t buffer,
+ * transformer.py:501-503) -> out [rows*nkp][c] dtype (pos_y | pos_x). */
+int dp_sine_embed(const float* ref, int32_t rows, int32_t nkp, int32_t c, const float* dim_t,
+                  void* out, int32_t dtype, void* stream);
+
+/* Small-N linear in f32: out[r][n] = act(x[r] . w[:, n % nw] + b[n % nw]) + add[r][n]
+ * (add optional), w f32 TRANSPOSED [k][nw].  x rows via row map, dtype x_dtype
+ * (DP_F32 / DP_BF16); out rows contiguous [rows][n]. The f32 heads: pose / pre-pose /
+ * class / LQE layers (transformer.py:705-728), enc_pose_embed last layer (1250). */
+int dp_linear_small(const void* x, dp_rowmap xm, int32_t x_dtype, int32_t rows, int32_t k,
+                    const float* w, const float* b, int32_t nw, int32_t n, int32_t act,
+                    const float* add, float* out, void* stream);
+
+/* Integral + distance2pose + centre (transformer.py:238-260, 198-219, 712-719):
+ * corners f32 [rows*nkp][2*(reg_max+1)], project f32 [reg_max+1], ref_init f32
+ * [rows*nkp][2] -> kps f32 [rows][nkp][2] and ref f32 [rows][1+nkp][2]. */
+int dp_pose_refine(const float* corners, const float* project, int32_t reg_max, const float* ref_init,
+                   float reg_scale, int32_t rows, int32_t nkp, float* kps, float* ref, void* stream);
+
+/* pre_poses = sigmoid(pre + inverse_sigmoid(ref kp)) (transformer.py:705-709, utils.py:133-137). */
+int dp_pre_pose(const float* pre, const float* ref, int32_t rows, int32_t nkp, float* out, void* stream);
+
+/* LQE statistics (transformer.py:275-285): bilinear sample of feat (NHWC dtype, h x w x c)
+ * at each keypoint, top-4 over channels + their mean -> out f32 [batch*nq][nkp*5]. */
+int dp_lqe_stats(const void* feat, int64_t feat_bstride, int32_t h, int32_t w, int32_t c,
+                 const float* kps, int32_t batch, int32_t nq, int32_t nkp, float* out,
+                 int32_t dtype, void* stream);
+
+/* PostProcess deploy branch (postprocesses.py:15-30), any batch. */
+int dp_postprocess(const float* logits, const float* kps, const float* target_sizes, int32_t batch,
+                   int32_t nq, int32_t nclass, int32_t nkp, int32_t num_select,
+                   float* scores, int64_t* labels, float* out_kps, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DETRPOSE_HIP_H */

@@ -1,0 +1,362 @@
+"""Per-kernel parity: each C-ABI entry point vs a plain fp32 reference of the same op
+(torch CPU fp32 ops or the oracle restatement), fp32 and bf16 storage modes.
+Tolerances: fp32 2e-4 of the output scale; bf16 storage rounds inputs/outputs to 8
+mantissa bits (rel 2^-8), so 2.5e-2 of the output scale."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from detrpose_amd import _lib
+from detrpose_amd._lib import ConvDesc, contiguous_rows, rowmap
+from detrpose_amd.engine import DTYPES, Packer
+from oracle import detrpose_cpu as O
+
+pytestmark = pytest.mark.gpu
+DT = ["fp32", "bf16"]
+TOL = {"fp32": 2e-4, "bf16": 2.5e-2}
+_KEEP = []
+
+
+@pytest.fixture(autouse=True)
+def _keepalive():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
+
+
+def _s():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _d(x, dtype=None):
+    """Device copy kept alive until the test ends (kernels run asynchronously)."""
+    t = (x.to("cuda", dtype) if dtype is not None else x.cuda()).contiguous()
+    _KEEP.append(t)
+    return t.data_ptr()
+
+
+def _close(got, ref, dt, what=""):
+    got = got.float().cpu()
+    ref = ref.float().cpu()
+    scale = max(1.0, ref.abs().max().item())
+    err = (got - ref).abs().max().item()
+    assert err <= TOL[dt] * scale, f"{what}: max err {err:.3g} (scale {scale:.3g}, dtype {dt})"
+
+
+def _nhwc(x, dt):
+    t = x.permute(0, 2, 3, 1).contiguous().to("cuda", DTYPES[dt][0])
+    _KEEP.append(t)
+    return t
+
+
+def _run_conv(pc, x_nhwc, out, dt, res=None, up=None):
+    lib = _lib.load()
+    B, H, W, Cin = x_nhwc.shape
+    d = ConvDesc()
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = x_nhwc.data_ptr(), H * W * Cin, Cin, H, W, Cin
+    d.weight, d.kpad, d.bias = pc.w.data_ptr(), pc.kpad, pc.b.data_ptr()
+    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = pc.kh, pc.kw, pc.stride, pc.pad, pc.pad
+    _, Ho, Wo, Co = out.shape
+    d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out.data_ptr(), Ho * Wo * Co, Co, Ho, Wo, Co
+    if res is not None:
+        d.res, d.res_bstride, d.res_pstride = res.data_ptr(), Ho * Wo * Co, Co
+    if up is not None:
+        d.up, d.up_bstride, d.up_pstride = up.data_ptr(), 4 * Ho * Wo * Co, Co
+    d.batch, d.act, d.dtype = B, pc.act, DTYPES[dt][1]
+    if pc.lab:
+        d.has_lab, d.lab_scale, d.lab_bias = 1, pc.lab[0], pc.lab[1]
+    fn = lib.dp_dwconv2d if pc.depthwise else lib.dp_conv2d
+    _lib.check(fn(C.byref(d), _s()), "conv")
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("k,s,cin,cout,H,act", [
+    (1, 1, 64, 96, 13, "relu"), (3, 1, 48, 48, 17, "silu"), (3, 2, 64, 32, 20, None), (1, 1, 336, 64, 9, "relu"),
+    (3, 1, 24, 24, 11, "silu"), (1, 1, 256, 288, 7, None), (3, 1, 128, 128, 40, "gelu")])
+def test_conv2d(dt, k, s, cin, cout, H, act):
+    torch.manual_seed(k * 100 + cin)
+    pk = Packer({}, dt, torch.device("cuda"))
+    x = torch.randn(2, cin, H, H + 3)
+    w = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pk.conv(w.double(), b.double(), stride=s, act=act)
+    ref = F.conv2d(x, w, b, s, (k - 1) // 2)
+    ref = {"relu": F.relu, "silu": F.silu, "gelu": F.gelu, None: lambda t: t}[act](ref)
+    out = torch.empty(2, ref.shape[2], ref.shape[3], pc.cout, device="cuda", dtype=DTYPES[dt][0])
+    resid = torch.randn(2, ref.shape[2], ref.shape[3], pc.cout)
+    rd = resid.to("cuda", DTYPES[dt][0])
+    _run_conv(pc, _nhwc(x, dt), out, dt, res=rd)
+    torch.cuda.synchronize()
+    _close(out[..., :cout], ref.permute(0, 2, 3, 1) + resid[..., :cout], dt, f"conv k{k}s{s} {cin}->{cout}")
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_conv2d_stem_pad_and_upsample(dt):
+    """2x2 conv over F.pad(0,1,0,1) (StemBlock) and the x2 nearest upsample epilogue."""
+    torch.manual_seed(3)
+    pk = Packer({}, dt, torch.device("cuda"))
+    x = torch.randn(1, 32, 10, 12)
+    w = torch.randn(16, 32, 2, 2) / 11.0
+    b = torch.randn(16) * 0.1
+    pc = pk.conv(w.double(), b.double(), act="relu", pad=0, lab=(1.3, -0.2))
+    ref = 1.3 * F.relu(F.conv2d(F.pad(x, (0, 1, 0, 1)), w, b)) - 0.2
+    out = torch.empty(1, 10, 12, 16, device="cuda", dtype=DTYPES[dt][0])
+    up = torch.empty(1, 20, 24, 16, device="cuda", dtype=DTYPES[dt][0])
+    _run_conv(pc, _nhwc(x, dt), out, dt, up=up)
+    torch.cuda.synchronize()
+    _close(out, ref.permute(0, 2, 3, 1), dt, "stem2a")
+    _close(up, F.interpolate(ref, scale_factor=2.0, mode="nearest").permute(0, 2, 3, 1), dt, "upsample")
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("k,s", [(3, 2), (5, 1), (3, 1)])
+def test_dwconv(dt, k, s):
+    torch.manual_seed(k + s)
+    pk = Packer({}, dt, torch.device("cuda"))
+    Cc = 64
+    x = torch.randn(2, Cc, 15, 16)
+    w = torch.randn(Cc, 1, k, k) / k
+    b = torch.randn(Cc) * 0.1
+    pc = pk.dwconv(w.double(), b.double(), s, act="relu")
+    ref = F.relu(F.conv2d(x, w, b, s, (k - 1) // 2, groups=Cc))
+    out = torch.empty(2, ref.shape[2], ref.shape[3], Cc, device="cuda", dtype=DTYPES[dt][0])
+    _run_conv(pc, _nhwc(x, dt), out, dt)
+    torch.cuda.synchronize()
+    _close(out, ref.permute(0, 2, 3, 1), dt, f"dw{k}s{s}")
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_stem_conv_and_pool(dt):
+    lib = _lib.load()
+    torch.manual_seed(5)
+    img = torch.rand(2, 3, 22, 26)
+    w = torch.randn(32, 3, 3, 3) / 5
+    b = torch.randn(32) * 0.1
+    ref = F.relu(F.conv2d(img, w, b, 2, 1))
+    out = torch.empty(2, 11, 13, 32, device="cuda", dtype=DTYPES[dt][0])
+    _lib.check(lib.dp_stem_conv(_d(img), 2, 22, 26, _d(w.reshape(32, 27)), _d(b), 32, 0, C.c_float(1),
+                                C.c_float(0), out.data_ptr(), 11 * 13 * 32, 32, DTYPES[dt][1], _s()))
+    torch.cuda.synchronize()
+    _close(out, ref.permute(0, 2, 3, 1), dt, "stem1")
+    x = torch.randn(2, 16, 9, 7)
+    pool = torch.empty(2, 9, 7, 16, device="cuda", dtype=DTYPES[dt][0])
+    xi = _nhwc(x, dt)
+    _lib.check(lib.dp_maxpool2x2_pad_rb(xi.data_ptr(), 9 * 7 * 16, 16, 2, 9, 7, 16, pool.data_ptr(), 9 * 7 * 16, 16,
+                                        DTYPES[dt][1], _s()))
+    torch.cuda.synchronize()
+    refp = F.max_pool2d(F.pad(x.to(DTYPES[dt][0]).float(), (0, 1, 0, 1)), 2, 1, ceil_mode=True)
+    _close(pool, refp.permute(0, 2, 3, 1), dt, "pool")
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("c", [128, 256, 384])
+def test_layernorm_variants(dt, c):
+    lib = _lib.load()
+    torch.manual_seed(c)
+    rows, T = 36, 18
+    x = torch.randn(rows, c)
+    r = torch.randn(rows, c)
+    g, bb = 1 + 0.1 * torch.randn(c), 0.1 * torch.randn(c)
+    post = torch.randn(rows // T * (T - 1), c)
+    mask = (torch.arange(rows) % 5 == 0).to(torch.uint8)
+    mrow = torch.randn(c)
+    td = DTYPES[dt][0]
+    out = torch.empty(rows, 2 * c, device="cuda", dtype=td)
+    _lib.check(lib.dp_layernorm(out.data_ptr(), contiguous_rows(2 * c), _d(x, td), contiguous_rows(c), _d(r, td),
+                                contiguous_rows(c), _d(g), _d(bb), C.c_float(1e-5), rows, c, _d(post, td),
+                                contiguous_rows(c), T, 1, None, 1, None, DTYPES[dt][1], _s()))
+    ref = F.layer_norm(x.to(td).float() + r.to(td).float(), (c,), g, bb)
+    kp = (torch.arange(rows) % T) != 0
+    ref[kp] += post.to(td).float()
+    torch.cuda.synchronize()
+    _close(out[:, :c], ref, dt, "ln+post")
+    out2 = torch.empty(rows, c, device="cuda", dtype=td)
+    _lib.check(lib.dp_layernorm(out2.data_ptr(), contiguous_rows(c), _d(x, td), contiguous_rows(c), None,
+                                rowmap(group=1), _d(g), _d(bb), C.c_float(1e-5), rows, c, None, rowmap(group=1), 1, 0,
+                                _d(mask), 7, _d(mrow), DTYPES[dt][1], _s()))
+    ref2 = F.layer_norm(x.to(td).float(), (c,), g, bb)
+    ref2[torch.arange(rows) % 7 % 5 == 0] = mrow
+    torch.cuda.synchronize()
+    _close(out2, ref2, dt, "ln+mask")
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_gate_layernorm(dt):
+    lib = _lib.load()
+    torch.manual_seed(9)
+    rows, c = 40, 256
+    gt, xc = torch.randn(rows, 2 * c), torch.randn(rows, 2 * c)
+    g, bb = 1 + 0.1 * torch.randn(c), 0.1 * torch.randn(c)
+    td = DTYPES[dt][0]
+    out = torch.empty(rows, c, device="cuda", dtype=td)
+    _lib.check(lib.dp_gate_layernorm(out.data_ptr(), c, _d(gt, td), _d(xc, td), _d(g), _d(bb), C.c_float(1e-5),
+                                     rows, c, DTYPES[dt][1], _s()))
+    gt, xc = gt.to(td).float(), xc.to(td).float()
+    s = torch.sigmoid(gt)
+    ref = F.layer_norm(s[:, :c] * xc[:, :c] + s[:, c:] * xc[:, c:], (c,), g, bb)
+    torch.cuda.synchronize()
+    _close(out, ref, dt, "gate")
+
+
+def _attn_ref(q, k, v, nh):
+    B, L, Cc = q.shape
+    dh = Cc // nh
+    q = q.reshape(B, L, nh, dh).transpose(1, 2)
+    k = k.reshape(B, -1, nh, dh).transpose(1, 2)
+    v = v.reshape(B, -1, nh, dh).transpose(1, 2)
+    a = torch.softmax(q @ k.transpose(-1, -2) / dh ** 0.5, -1)
+    return (a @ v).transpose(1, 2).reshape(B, L, Cc)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("geom", ["within", "across", "aifi", "aifi_x", "within_n"])
+def test_attention(dt, geom):
+    lib = _lib.load()
+    torch.manual_seed(len(geom))
+    B, nq, T = 2, 60, 18
+    Cc = {"aifi_x": 384, "within_n": 128}.get(geom, 256)
+    nh = 8
+    rows = B * 400 if geom.startswith("aifi") else B * nq * T
+    qkv = torch.randn(rows, 3 * Cc)
+    td = DTYPES[dt][0]
+    qd = qkv.to("cuda", td)
+    out = torch.empty(rows, Cc, device="cuda", dtype=td)
+    e = qd.element_size()
+    q32 = qkv.to(td).float()
+    if geom.startswith("within"):
+        args = (B * nq, 1, T, 0, 1, T)
+        seqs = q32.reshape(B * nq, T, 3 * Cc)
+    elif geom == "across":
+        args = (B, T, nq * T, 1, T, nq)
+        seqs = q32.reshape(B, nq, T, 3 * Cc).transpose(1, 2).reshape(B * T, nq, 3 * Cc)
+    else:
+        args = (B, 1, 400, 0, 1, 400)
+        seqs = q32.reshape(B, 400, 3 * Cc)
+    _lib.check(lib.dp_attention(qd.data_ptr(), 3 * Cc, qd.data_ptr() + Cc * e, qd.data_ptr() + 2 * Cc * e, 3 * Cc,
+                                out.data_ptr(), Cc, *args, nh, Cc // nh, DTYPES[dt][1], _s()))
+    ref = _attn_ref(seqs[..., :Cc], seqs[..., Cc:2 * Cc], seqs[..., 2 * Cc:], nh)
+    if geom == "across":
+        ref = ref.reshape(B, T, nq, Cc).transpose(1, 2)
+    torch.cuda.synchronize()
+    _close(out.reshape(-1, Cc), ref.reshape(-1, Cc), dt, geom)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("size", ["n", "l", "x"])
+def test_msda_golden(golden_dir, dt, size):
+    """dp_msda vs the reference's ms_deform_attn_core_pytorch vectors (tests/golden/msda_*.npz).
+    The kernel takes offsets + logits (as the projection GEMM emits them); the fixture's
+    absolute locations are re-expressed as offsets from a per-token reference point."""
+    lib = _lib.load()
+    g = np.load(os.path.join(golden_dir, f"msda_{size}.npz"))
+    value, loc, logits = (torch.from_numpy(g[k]) for k in ("value", "loc", "attn_logits"))
+    shapes = [tuple(int(v) for v in s) for s in g["shapes"]]
+    N, Lq, H, L, P, _ = loc.shape
+    ref_pt = torch.rand(N, Lq, 2, generator=torch.Generator().manual_seed(1))
+    wh = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32)
+    off = (loc - ref_pt[:, :, None, None, None, :]) * wh[None, None, None, :, None, :]
+    offattn = torch.cat([off.reshape(N * Lq, -1), logits.reshape(N * Lq, -1)], 1)
+    td = DTYPES[dt][0]
+    oad = offattn.to("cuda", td).contiguous()
+    vd = value.to("cuda", td).contiguous()
+    Cc = value.shape[2]
+    out = torch.empty(N * Lq, Cc, device="cuda", dtype=td)
+    hw = (C.c_int32 * (2 * L))(*[v for s in shapes for v in s])
+    _lib.check(lib.dp_msda(vd.data_ptr(), N, value.shape[1], hw, L, oad.data_ptr(), _d(ref_pt), out.data_ptr(), Cc,
+                           Lq, H, Cc // H, P, DTYPES[dt][1], _s()))
+    torch.cuda.synchronize()
+    if dt == "fp32":
+        _close(out.reshape(N, Lq, Cc), torch.from_numpy(g["out"]), dt, "msda vs reference")
+    else:
+        # bf16: compare with the oracle on the bf16-rounded inputs
+        oa = oad.float().cpu()
+        loc2 = ref_pt[:, :, None, None, None, :] + oa[:, :H * L * P * 2].reshape(N, Lq, H, L, P, 2) / \
+            wh[None, None, None, :, None, :]
+        a2 = torch.softmax(oa[:, H * L * P * 2:].reshape(N, Lq, H, L * P), -1).reshape(N, Lq, H, L, P)
+        _close(out.reshape(N, Lq, Cc), O.msda_core(vd.float().cpu(), shapes, loc2, a2), dt, "msda vs oracle(bf16)")
+
+
+@pytest.mark.parametrize("n,k", [(8400, 60), (2000, 60), (120, 60), (300, 256), (17, 4)])
+def test_topk(n, k):
+    lib = _lib.load()
+    torch.manual_seed(n)
+    rows = 3
+    x = torch.randn(rows, n)
+    x[1, : n // 3] = 0.25  # ties: lower index first
+    ov = torch.empty(rows, k, device="cuda")
+    oi = torch.empty(rows, k, dtype=torch.int64, device="cuda")
+    _lib.check(lib.dp_topk(_d(x), rows, n, n, k, ov.data_ptr(), oi.data_ptr(), _s()))
+    torch.cuda.synchronize()
+    key = torch.stack([torch.tensor(sorted(range(n), key=lambda i: (-x[r, i].item(), i))[:k]) for r in range(rows)])
+    np.testing.assert_array_equal(oi.cpu().numpy(), key.numpy())
+    np.testing.assert_array_equal(ov.cpu().numpy(), torch.gather(x, 1, key).numpy())
+
+
+def test_decoder_head_kernels():
+    """sine embed, linear_small (+add, broadcast weight), pose refine, pre-pose, LQE, postprocess."""
+    lib = _lib.load()
+    torch.manual_seed(11)
+    B, nq, K, Cc = 2, 60, 17, 256
+    rows = B * nq
+    ref = torch.rand(B, nq, K + 1, 2)
+    dim_t = (10000 ** (2 * torch.div(torch.arange(Cc // 2), 2, rounding_mode="floor") / (Cc // 2))).float()
+    se = torch.empty(rows * K, Cc, device="cuda")
+    _lib.check(lib.dp_sine_embed(_d(ref), rows, K, Cc, _d(dim_t), se.data_ptr(), 0, _s()))
+    torch.cuda.synchronize()
+    _close(se, O.sine_embedding(ref[:, :, 1:], dim_t).reshape(-1, Cc), "fp32", "sine")
+    # linear_small with weight broadcast (nw=1, n=2) and add
+    x = torch.randn(rows, 85)
+    w = torch.randn(1, 85)
+    b = torch.randn(1)
+    add = torch.randn(rows, 2)
+    out = torch.empty(rows, 2, device="cuda")
+    _lib.check(lib.dp_linear_small(_d(x), contiguous_rows(85), 0, rows, 85, _d(w.t()), _d(b), 1, 2, 0, _d(add),
+                                   out.data_ptr(), _s()))
+    torch.cuda.synchronize()
+    _close(out, (x @ w.t() + b) + add, "fp32", "linear_small")
+    # pose refine (Integral + distance2pose + centre)
+    corners = torch.randn(rows * K, 66)
+    ref_init = torch.rand(rows * K, 2)
+    project = O.weighting_function(32, 0.5, 4.0)
+    kps = torch.empty(B, nq, K, 2, device="cuda")
+    refo = torch.empty(B, nq, K + 1, 2, device="cuda")
+    _lib.check(lib.dp_pose_refine(_d(corners), _d(project), 32, _d(ref_init), C.c_float(4.0), rows, K,
+                                  kps.data_ptr(), refo.data_ptr(), _s()))
+    prob = torch.softmax(corners.reshape(-1, 33), 1)
+    d = (prob @ project).reshape(B, nq, K, 2)
+    kref = ref_init.reshape(B, nq, K, 2) + d / 4.0
+    torch.cuda.synchronize()
+    _close(kps, kref, "fp32", "refine")
+    _close(refo, torch.cat([kref.mean(2, keepdim=True), kref], 2), "fp32", "refine ref")
+    # pre-pose
+    pre = torch.randn(rows * K, 2)
+    outp = torch.empty(rows * K, 2, device="cuda")
+    _lib.check(lib.dp_pre_pose(_d(pre), _d(ref), rows, K, outp.data_ptr(), _s()))
+    torch.cuda.synchronize()
+    _close(outp, torch.sigmoid(pre + O.inverse_sigmoid(ref[:, :, 1:].reshape(-1, 2))), "fp32", "pre_pose")
+    # LQE stats
+    feat = torch.randn(B, 20, 24, Cc)
+    kp = torch.rand(B, nq, K, 2) * 1.1 - 0.05
+    st = torch.empty(rows, K * 5, device="cuda")
+    _lib.check(lib.dp_lqe_stats(_d(feat), 20 * 24 * Cc, 20, 24, Cc, _d(kp), B, nq, K, st.data_ptr(), 0, _s()))
+    s = O.bilinear_gather(feat, kp.reshape(B, nq * K, 2)).reshape(B, nq, K, Cc)
+    top = s.topk(4, dim=-1)[0]
+    torch.cuda.synchronize()
+    _close(st, torch.cat([top, top.mean(-1, keepdim=True)], -1).reshape(rows, -1), "fp32", "lqe")
+    # postprocess
+    logits = torch.randn(B, nq, 2)
+    ts = torch.tensor([[640.0, 480.0], [320.0, 200.0]])
+    sc = torch.empty(B, 60, device="cuda")
+    lb = torch.empty(B, 60, dtype=torch.int64, device="cuda")
+    ok = torch.empty(B, 60, K, 2, device="cuda")
+    _lib.check(lib.dp_postprocess(_d(logits), _d(kp), _d(ts), B, nq, 2, K, 60, sc.data_ptr(), lb.data_ptr(),
+                                  ok.data_ptr(), _s()))
+    rs, rl, rk = O.postprocess(logits, kp, ts)
+    torch.cuda.synchronize()
+    _close(sc, rs, "fp32", "pp scores")
+    np.testing.assert_array_equal(lb.cpu().numpy(), rl.numpy())
+    _close(ok, rk, "fp32", "pp kps")
