@@ -1,0 +1,201 @@
+"""Throughput benchmark of the DETRPose inference forward on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size l] [--batch 64]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric (BASELINE.json): images/sec + p50 ms/img, DETRPose-L bf16 640x640, batch 64 per
+GPU. One step = one forward of the HIP plan over one resident batch of synthetic
+640x640 images + PostProcess (the reference benchmark's Model = model + postprocessor,
+tools/benchmark/torch_benchmark.py:82-91), replayed as one hipGraph; with N>1 ranks
+each rank forwards its own batch (data parallel, weak scaling) and the outputs are
+all-gathered over RCCL (one all_gather_into_tensor of 8,640 B/img). Rank 0 prints one
+JSON line. Weights: seeded fan-in random init (no checkpoint offline); data synthetic.
+
+Also reported (rank 0):
+  roofline     the dominant kernel family (implicit-GEMM conv/linear, dp_conv2d):
+               algorithmic FLOPs of its launches / their HIP-event time, vs bf16 dense
+               MFMA peak;
+  cpu_baseline the CPU oracle restatement (oracle/detrpose_cpu.py, kind "port") timed on
+               the host cores on a bounded sample (N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+METRIC = "images/sec + p50 ms/img, DETRPose-L bf16 640x640 at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", default="l", choices=["n", "l", "x"])
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-ops", type=str, default="", help="write per-op times (JSON) to this path")
+    return ap.parse_args()
+
+
+def cpu_baseline(size, seconds):
+    """Oracle (CPU fp32 restatement of the reference forward) on host cores, batch 1."""
+    from detrpose_amd import build_model
+    from detrpose_amd.configs import get_config
+    from detrpose_amd.synthetic import load_synthetic, synthetic_images
+    from oracle.detrpose_cpu import OracleDETRPose
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    torch.set_num_threads(cores)
+    m, _ = build_model(size)
+    load_synthetic(m, 0)
+    orc = OracleDETRPose(get_config(size), m.state_dict())
+    img = synthetic_images(1, 1)
+    orc(img)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        orc(img)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 2:
+            break
+    return {"value": round(n / el, 3), "unit": "images/sec", "cores": cores, "kind": "port",
+            "sample": f"DETRPose-{size.upper()} fp32 CPU oracle, batch 1, {n} forwards in {el:.1f}s "
+                      f"(oracle/detrpose_cpu.py, torch CPU ops, {cores} threads)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from detrpose_amd import GFLOP_PER_IMAGE, build_model
+    from detrpose_amd.synthetic import load_synthetic, synthetic_images
+
+    model, _ = build_model(a.size, dtype=a.dtype)
+    load_synthetic(model, 0)
+    model.deploy()
+    eng = model.engine(dev)
+    plan = eng.plan(a.batch)
+    plan.add_postprocess()
+    plan.input.copy_(synthetic_images(a.batch, seed=1 + rank).to(dev))   # resident in HBM before timing
+    gathered = None
+    if dist is not None:
+        gathered = torch.empty(world * plan.out_flat.numel(), dtype=torch.float32, device=dev)
+
+    def step():
+        if a.no_graph:
+            plan.run()
+        else:
+            g.replay()
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, plan.out_flat)
+
+    g = None if a.no_graph else plan.graph()
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record()
+        step()
+        e1.record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    step_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_imgs = a.batch * a.steps * world
+    value = total_imgs / elapsed
+    ms_per_step = elapsed * 1000.0 / a.steps
+    p50_ms_img = statistics.median(step_ms) / a.batch
+
+    if rank == 0:
+        # per-op HIP-event pass over the same plan (outside the timed region)
+        op_ms = plan.profile(reps=3)
+        conv_names = [n for n in plan.op_flops if n in op_ms]
+        conv_ms = sum(op_ms[n] for n in conv_names)
+        conv_flops = sum(plan.op_flops[n] for n in conv_names)
+        total_ms = sum(op_ms.values())
+        achieved = conv_flops / (conv_ms * 1e-3) / 1e12
+        peak = PEAK_BF16_TFLOPS if a.dtype == "bf16" else PEAK_F32_TFLOPS
+        fam = {}
+        for n, ms in op_ms.items():
+            fn = next(f for nm, f, _ in plan.ops if nm == n).__name__
+            fam[fn] = fam.get(fn, 0.0) + ms
+        msda = [n for n in plan.op_bytes if n in op_ms]
+        msda_gbs = sum(plan.op_bytes[n] for n in msda) / (sum(op_ms[n] for n in msda) * 1e-3) / 1e9 if msda else None
+        if a.profile_ops:
+            with open(a.profile_ops, "w") as f:
+                json.dump({"op_ms": op_ms, "op_flops": plan.op_flops, "op_bytes": plan.op_bytes}, f, indent=1)
+        gflop = GFLOP_PER_IMAGE[a.size]
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "p50_ms_per_img": round(p50_ms_img, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (uniform [0,1) 640x640 images; seeded fan-in random weights, no checkpoint offline)",
+            "config": {"workload": f"DETRPose-{a.size.upper()} inference forward + PostProcess, 640x640, "
+                                   f"batch {a.batch} per GPU, hipGraph replay", "batch_per_gpu": a.batch,
+                       "global_batch": a.batch * world, "image": "640x640", "parallelism": f"dp{world}",
+                       "graph": not a.no_graph},
+            "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel (dp_conv2d: all dense conv/linear launches)",
+                         "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "launches_per_step": len(conv_names), "time_share": round(conv_ms / total_ms, 3)},
+            "e2e_mfma_frac": round(value / world * gflop * 1e9 / (peak * 1e12), 4),
+            "kernel_ms_per_step": {k: round(v, 3) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])},
+            "msda_algorithmic_gbs": round(msda_gbs, 1) if msda_gbs else None,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(a.size, a.cpu_baseline_seconds)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -179,6 +179,9 @@ class Plan:
         self.arena = []          # every device buffer the launches point into
         self.bufs = {}           # named FMaps / tensors for inspection
         self.op_out = {}         # op name -> output FMap (debug / tests)
+        self.op_flops = {}       # op name -> algorithmic FLOPs (conv / linear launches)
+        self.op_bytes = {}       # op name -> algorithmic HBM bytes (MSDA)
+        self.out_flat = None
         self.input = None
         self.outputs = {}
         self._graph = None
@@ -196,6 +199,44 @@ class Plan:
             if debug is not None:
                 torch.cuda.synchronize()
                 debug(name, self.op_out.get(name))
+
+    def profile(self, reps=3):
+        """Per-op device time (ms, median of `reps` passes) with HIP events around each launch."""
+        s = torch.cuda.current_stream()
+        times = {name: [] for name, _, _ in self.ops}
+        for _ in range(reps):
+            evs = []
+            for name, fn, args in self.ops:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                rc = fn(*args, C.c_void_p(s.cuda_stream))
+                e1.record(s)
+                if rc:
+                    _lib.check(rc, name)
+                evs.append((name, e0, e1))
+            torch.cuda.synchronize()
+            for name, e0, e1 in evs:
+                times[name].append(e0.elapsed_time(e1))
+        return {k: sorted(v)[len(v) // 2] for k, v in times.items()}
+
+    def add_postprocess(self, num_select=60, target_size=(640.0, 640.0)):
+        """Append PostProcess (deploy) to the plan: outputs scores / labels / keypoints."""
+        eng = self.engine
+        logits, kps = self.outputs["pred_logits"], self.outputs["pred_keypoints"]
+        B, Q, NC = logits.shape
+        K = kps.shape[2]
+        eng._cur = self
+        ts = eng._empty(B, 2, dtype=torch.float32)
+        ts[:, 0], ts[:, 1] = target_size
+        sc = eng._empty(B, num_select, dtype=torch.float32)
+        lb = eng._empty(B, num_select, dtype=torch.int64)
+        ok = eng._empty(B, num_select, K, 2, dtype=torch.float32)
+        self._op("postprocess", eng.lib.dp_postprocess, logits.data_ptr(), kps.data_ptr(), ts.data_ptr(), B, Q, NC, K,
+                 num_select, sc.data_ptr(), lb.data_ptr(), ok.data_ptr())
+        self.post = {"scores": sc, "labels": lb, "keypoints": ok, "target_sizes": ts}
+        self._graph = None
+        return self.post
 
     def graph(self):
         """Capture the plan into a hipGraph once; returns the graph (replay with .replay())."""
@@ -443,6 +484,10 @@ class Engine:
             d.has_lab, d.lab_scale, d.lab_bias = 1, pc.lab[0], pc.lab[1]
         plan.keep.append(d)
         plan.op_out[name] = out
+        if not pc.depthwise:
+            plan.op_flops[name] = 2.0 * x.B * out.H * out.W * out.C * pc.kh * pc.kw * x.C
+        else:
+            plan.op_flops[name] = 2.0 * x.B * out.H * out.W * out.C * pc.kh * pc.kw
         fn = self.lib.dp_dwconv2d if pc.depthwise else self.lib.dp_conv2d
         plan._op(name, fn, C.byref(d))
 
@@ -709,7 +754,12 @@ class Engine:
         corners = [self._empty(krows, nb, dtype=torch.float32) for _ in range(2)]
         pre = self._empty(krows, 2, dtype=torch.float32)
         ref_init = self._empty(krows, 2, dtype=torch.float32)
-        kps = self._empty(B, nq, K, 2, dtype=torch.float32)
+        # outputs share one contiguous f32 buffer [logits (B,nq,ncls) | keypoints (B,nq,K,2)]
+        # so a data-parallel run gathers them with a single collective
+        ncls = tr.num_classes
+        out_flat = self._empty(B * nq * (ncls + 2 * K), dtype=torch.float32)
+        plan.out_flat = out_flat
+        kps = out_flat[B * nq * ncls:].view(B, nq, K, 2)
         lvl_hw = (C.c_int32 * (2 * len(shapes)))(*[v for hw in shapes for v in hw])
         plan.keep.append(lvl_hw)
         e = qkv.element_size()
@@ -752,6 +802,8 @@ class Engine:
             self._conv(plan, n + ".offattn", gx_f.ch(0, Cc), L["offattn"], oa)
             plan._op(n + ".msda", lib.dp_msda, memory.data_ptr(), B, S, lvl_hw, len(shapes), oa.ptr, ref.data_ptr(),
                      gx.data_ptr() + Cc * e, 2 * Cc, nq * T, nh, Cc // nh, npnt, self.code)
+            # SURVEY.md §8d algorithmic bytes: value once + offsets/logits + ref + output
+            plan.op_bytes[n + ".msda"] = e * (B * S * Cc + rows * oa.C + rows * Cc) + 4 * rows * 2
             # Gate (transformer.py:222-235)
             self._conv(plan, n + ".gate", gx_f, L["gate"], gt)
             plan._op(n + ".gate_ln", lib.dp_gate_layernorm, dst.data_ptr(), Cc, gt.ptr, gx.data_ptr(),
@@ -801,7 +853,7 @@ class Engine:
                 plan._op(n + ".lqe0", lib.dp_linear_small, st.data_ptr(), contiguous_rows(K * 5), DP_F32, B * nq,
                          lqe[0].k, lqe[0].wt.data_ptr(), lqe[0].b.data_ptr(), lqe[0].n, lqe[0].n, lqe[0].act, None,
                          hid.data_ptr())
-                logits = self._empty(B, nq, cls.n, dtype=torch.float32)
+                logits = out_flat[:B * nq * ncls].view(B, nq, ncls)
                 plan._op(n + ".lqe1", lib.dp_linear_small, hid.data_ptr(), contiguous_rows(lqe[0].n), DP_F32, B * nq,
                          lqe[1].k, lqe[1].wt.data_ptr(), lqe[1].b.data_ptr(), lqe[1].n, cls.n, 0,
                          score2.data_ptr(), logits.data_ptr())
