@@ -31,6 +31,7 @@ class ConvDesc(C.Structure):
         ("act", i32), ("has_lab", i32), ("lab_scale", f32), ("lab_bias", f32),
         ("dtype", i32),
         ("up", vp), ("up_bstride", i64), ("up_pstride", i32),
+        ("out_f32", i32),
     ]
 
 

@@ -28,24 +28,24 @@ struct Geo {
   static constexpr int BKP = BK + VEC;          // LDS row pitch (+16 B pad)
 };
 
-template <typename T, int BM, int BN>
+template <typename T, typename TO, int BM, int BN>
 struct Smem {
-  static constexpr int AB = 2 * (BM + BN) * Geo<T>::BKP;   // double-buffered A|B
-  static constexpr int CP = BN + Geo<T>::VEC;              // epilogue tile pitch
-  static constexpr int C = BM * CP;
-  static constexpr int ELEMS = AB > C ? AB : C;
+  static constexpr int AB = 2 * (BM + BN) * Geo<T>::BKP * (int)sizeof(T);   // double-buffered A|B
+  static constexpr int CP = BN + Geo<TO>::VEC;                               // epilogue tile pitch
+  static constexpr int C = BM * CP * (int)sizeof(TO);
+  static constexpr int BYTES = AB > C ? AB : C;
 };
 
-template <typename T, int BM, int BN, bool K1X1>
+template <typename T, typename TO, int BM, int BN, bool K1X1>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(dp_conv_desc d, int M, int nt_n, int vec_ok) {
   using G = Geo<T>;
   constexpr int VEC = G::VEC, BK = G::BK, BKP = G::BKP;
   constexpr int AR = BM / 32, BR = BN / 32;          // rows per thread per K-step
   constexpr int WM = BM / 2, WN = BN / 2;            // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;          // 16x16 MFMA tiles per wave
-  __shared__ __attribute__((aligned(16))) T smem[Smem<T, BM, BN>::ELEMS];
-  T* As = smem;                         // [2][BM][BKP]
-  T* Bs = smem + 2 * BM * BKP;          // [2][BN][BKP]
+  __shared__ __attribute__((aligned(16))) char smem_raw[Smem<T, TO, BM, BN>::BYTES];
+  T* As = reinterpret_cast<T*>(smem_raw);   // [2][BM][BKP]
+  T* Bs = As + 2 * BM * BKP;                // [2][BN][BKP]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -169,8 +169,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(dp_conv_desc d, int M, i
   }
 
   // ---- epilogue: bias + act + LAB into an LDS tile, then 16-byte row writes
-  constexpr int CP = Smem<T, BM, BN>::CP;
-  T* Cs = smem;
+  constexpr int CP = Smem<T, TO, BM, BN>::CP;
+  constexpr int VO = Geo<TO>::VEC;
+  TO* Cs = reinterpret_cast<TO*>(smem_raw);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int nl = wn * WN + j * 16 + (lane & 15);
@@ -183,31 +184,31 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(dp_conv_desc d, int M, i
         const int ml = wm * WM + i * 16 + (lane >> 4) * 4 + r;
         float v = apply_act(acc[i][j][r] + bias, d.act);
         if (d.has_lab) v = d.lab_scale * v + d.lab_bias;
-        Cs[ml * CP + nl] = from_f32<T>(v);
+        Cs[ml * CP + nl] = from_f32<TO>(v);
       }
     }
   }
   __syncthreads();
 
-  T* __restrict__ out = reinterpret_cast<T*>(d.out);
-  const T* __restrict__ res = reinterpret_cast<const T*>(d.res);
-  T* __restrict__ up = reinterpret_cast<T*>(d.up);
-  constexpr int CPR = BN / VEC;  // chunks per row
+  TO* __restrict__ out = reinterpret_cast<TO*>(d.out);
+  const TO* __restrict__ res = reinterpret_cast<const TO*>(d.res);
+  TO* __restrict__ up = reinterpret_cast<TO*>(d.up);
+  constexpr int CPR = BN / VO;  // chunks per row
   for (int e = tid; e < BM * CPR; e += 256) {
     const int ml = e / CPR, cc = e - ml * CPR;
     const int m = m0 + ml;
-    const int n = n0 + cc * VEC;
+    const int n = n0 + cc * VO;
     if (m >= M || n >= d.cout) continue;
     const int b = m / hwo, rem = m - b * hwo;
     const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
     const int64_t pix = (int64_t)oy * d.out_w + ox;
     const int64_t oo = (int64_t)b * d.out_bstride + pix * d.out_pstride + n;
-    Vec16<T> v = load16(Cs + ml * CP + cc * VEC);
-    if (vec_ok && n + VEC <= d.cout) {
+    Vec16<TO> v = load16(Cs + ml * CP + cc * VO);
+    if (vec_ok && n + VO <= d.cout) {
       if (res) {
-        Vec16<T> rv = load16(res + (int64_t)b * d.res_bstride + pix * d.res_pstride + n);
+        Vec16<TO> rv = load16(res + (int64_t)b * d.res_bstride + pix * d.res_pstride + n);
 #pragma unroll
-        for (int t = 0; t < VEC; ++t) v.set(t, v.get(t) + rv.get(t));
+        for (int t = 0; t < VO; ++t) v.set(t, v.get(t) + rv.get(t));
       }
       store16(out + oo, v);
       if (up) {
@@ -219,45 +220,54 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(dp_conv_desc d, int M, i
             store16(up + ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride, v);
       }
     } else {
-      const int nn = min(VEC, d.cout - n);
+      const int nn = min(VO, d.cout - n);
       for (int t = 0; t < nn; ++t) {
         float x = v.get(t);
         if (res) x += to_f32(res[(int64_t)b * d.res_bstride + pix * d.res_pstride + n + t]);
-        out[oo + t] = from_f32<T>(x);
+        out[oo + t] = from_f32<TO>(x);
         if (up) {
           const int64_t ub = (int64_t)b * d.up_bstride + n + t;
           for (int dy = 0; dy < 2; ++dy)
             for (int dx = 0; dx < 2; ++dx)
-              up[ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride] = from_f32<T>(x);
+              up[ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride] = from_f32<TO>(x);
         }
       }
     }
   }
 }
 
-template <typename T, int BM, int BN>
+template <typename T, typename TO, int BM, int BN>
 int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   const int M = d.batch * d.out_h * d.out_w;
   const int mt = (M + BM - 1) / BM, nt = (d.cout + BN - 1) / BN;
   const bool k1 = d.kh == 1 && d.kw == 1 && d.pad_t == 0 && d.pad_l == 0;
   dim3 grid(mt * nt), block(256);
-  if (k1) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, true>), grid, block, 0, s, d, M, nt, vec_ok);
-  else hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, false>), grid, block, 0, s, d, M, nt, vec_ok);
+  if constexpr (sizeof(TO) != sizeof(T)) {
+    hipLaunchKernelGGL((conv_gemm_kernel<T, TO, BM, BN, true>), grid, block, 0, s, d, M, nt, vec_ok);
+  } else {
+    if (k1) hipLaunchKernelGGL((conv_gemm_kernel<T, TO, BM, BN, true>), grid, block, 0, s, d, M, nt, vec_ok);
+    else hipLaunchKernelGGL((conv_gemm_kernel<T, TO, BM, BN, false>), grid, block, 0, s, d, M, nt, vec_ok);
+  }
   return dp_check_launch("dp_conv2d");
 }
 
-template <typename T>
+template <typename T, typename TO>
 int dispatch(const dp_conv_desc& d, hipStream_t s) {
-  constexpr int VEC = Geo<T>::VEC;
+  constexpr int VEC = Geo<TO>::VEC;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   int vec_ok = (d.out_pstride % VEC == 0) && (d.out_bstride % VEC == 0) && al(d.out);
   if (d.res) vec_ok = vec_ok && (d.res_pstride % VEC == 0) && (d.res_bstride % VEC == 0) && al(d.res);
   if (d.up) vec_ok = vec_ok && (d.up_pstride % VEC == 0) && (d.up_bstride % VEC == 0) && al(d.up);
   const int M = d.batch * d.out_h * d.out_w;
-  if (d.cout <= 32) return launch<T, 128, 32>(d, s, vec_ok);
-  if (d.cout <= 64) return launch<T, 128, 64>(d, s, vec_ok);
-  if (M <= 8192) return launch<T, 64, 128>(d, s, vec_ok);
-  return launch<T, 128, 128>(d, s, vec_ok);
+  if constexpr (sizeof(TO) != sizeof(T)) {  // f32-output heads: few shapes
+    if (M <= 8192) return launch<T, TO, 64, 128>(d, s, vec_ok);
+    return launch<T, TO, 128, 128>(d, s, vec_ok);
+  } else {
+    if (d.cout <= 32) return launch<T, TO, 128, 32>(d, s, vec_ok);
+    if (d.cout <= 64) return launch<T, TO, 128, 64>(d, s, vec_ok);
+    if (M <= 8192) return launch<T, TO, 64, 128>(d, s, vec_ok);
+    return launch<T, TO, 128, 128>(d, s, vec_ok);
+  }
 }
 
 }  // namespace
@@ -278,7 +288,9 @@ extern "C" int dp_conv2d(const dp_conv_desc* dp, void* stream) {
              d.kpad, d.kh * d.kw * d.cin, BK);
   DP_REQUIRE((reinterpret_cast<uintptr_t>(d.weight) & 15) == 0, "dp_conv2d: weight not 16-byte aligned");
   DP_REQUIRE((int64_t)d.batch * d.out_h * d.out_w < (1ll << 31), "dp_conv2d: M too large");
+  DP_REQUIRE(!d.out_f32 || (d.kh == 1 && d.kw == 1 && d.pad_t == 0 && d.pad_l == 0 && !d.up),
+             "dp_conv2d: out_f32 is supported for 1x1 / linear layers without upsample");
   hipStream_t s = as_stream(stream);
-  if (d.dtype == DP_BF16) return dispatch<bf16_t>(d, s);
-  return dispatch<float>(d, s);
+  if (d.dtype == DP_BF16) return d.out_f32 ? dispatch<bf16_t, float>(d, s) : dispatch<bf16_t, bf16_t>(d, s);
+  return dispatch<float, float>(d, s);
 }

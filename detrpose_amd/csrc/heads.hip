@@ -243,38 +243,39 @@ __global__ __launch_bounds__(256) void linear_small_kernel(const T* __restrict__
   }
 }
 
-__global__ void pose_refine_kernel(const float* __restrict__ corners, const float* __restrict__ project, int reg_max,
-                                   const float* __restrict__ ref_init, float reg_scale, int rows, int nkp,
-                                   float* __restrict__ kps, float* __restrict__ ref) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+// one wave per query row: lane j < 2*nkp owns (keypoint j/2, coordinate j&1)
+__global__ __launch_bounds__(256) void pose_refine_kernel(const float* __restrict__ corners,
+                                                          const float* __restrict__ project, int reg_max,
+                                                          const float* __restrict__ ref_init, float reg_scale,
+                                                          int rows, int nkp, float* __restrict__ kps,
+                                                          float* __restrict__ ref) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int nb = reg_max + 1;
-  float sx = 0.f, sy = 0.f;
-  for (int j = 0; j < nkp; ++j) {
-    float d[2];
-    for (int c = 0; c < 2; ++c) {
-      const float* z = corners + ((int64_t)(r * nkp + j) * 2 + c) * nb;
-      float mx = -INFINITY;
-      for (int i = 0; i < nb; ++i) mx = fmaxf(mx, z[i]);
-      float se = 0.f, acc = 0.f;
-      for (int i = 0; i < nb; ++i) {
-        const float e = expf(z[i] - mx);
-        se += e;
-        acc = fmaf(e, project[i], acc);
-      }
-      d[c] = acc / se;
+  const bool act = lane < 2 * nkp;
+  const int kp = lane >> 1, c = lane & 1;
+  float val = 0.f;
+  if (act) {
+    const float* z = corners + ((int64_t)(r * nkp + kp) * 2 + c) * nb;
+    float mx = -INFINITY;
+    for (int i = 0; i < nb; ++i) mx = fmaxf(mx, z[i]);
+    float se = 0.f, acc = 0.f;
+    for (int i = 0; i < nb; ++i) {
+      const float e = expf(z[i] - mx);
+      se += e;
+      acc = fmaf(e, project[i], acc);
     }
-    const float x = ref_init[((int64_t)r * nkp + j) * 2] + d[0] / reg_scale;
-    const float y = ref_init[((int64_t)r * nkp + j) * 2 + 1] + d[1] / reg_scale;
-    kps[((int64_t)r * nkp + j) * 2] = x;
-    kps[((int64_t)r * nkp + j) * 2 + 1] = y;
-    ref[((int64_t)r * (nkp + 1) + 1 + j) * 2] = x;
-    ref[((int64_t)r * (nkp + 1) + 1 + j) * 2 + 1] = y;
-    sx += x;
-    sy += y;
+    val = ref_init[((int64_t)r * nkp + kp) * 2 + c] + (acc / se) / reg_scale;
+    kps[((int64_t)r * nkp + kp) * 2 + c] = val;
+    ref[((int64_t)r * (nkp + 1) + 1 + kp) * 2 + c] = val;
   }
-  ref[(int64_t)r * (nkp + 1) * 2] = sx / nkp;
-  ref[(int64_t)r * (nkp + 1) * 2 + 1] = sy / nkp;
+  const float sx = wave_sum(act && c == 0 ? val : 0.f);
+  const float sy = wave_sum(act && c == 1 ? val : 0.f);
+  if (lane == 0) {
+    ref[(int64_t)r * (nkp + 1) * 2] = sx / nkp;
+    ref[(int64_t)r * (nkp + 1) * 2 + 1] = sy / nkp;
+  }
 }
 
 __global__ void pre_pose_kernel(const float* __restrict__ pre, const float* __restrict__ ref, int rows, int nkp,
@@ -449,7 +450,8 @@ extern "C" int dp_linear_small(const void* x, dp_rowmap xm, int32_t x_dtype, int
 
 extern "C" int dp_pose_refine(const float* corners, const float* project, int32_t reg_max, const float* ref_init,
                               float reg_scale, int32_t rows, int32_t nkp, float* kps, float* ref, void* stream) {
-  hipLaunchKernelGGL(pose_refine_kernel, dim3(nblk(rows, 64)), dim3(64), 0, as_stream(stream), corners, project,
+  DP_REQUIRE(2 * nkp <= 64, "dp_pose_refine: nkp=%d (max 32)", nkp);
+  hipLaunchKernelGGL(pose_refine_kernel, dim3(nblk(rows, 4)), dim3(256), 0, as_stream(stream), corners, project,
                      reg_max, ref_init, reg_scale, rows, nkp, kps, ref);
   return dp_check_launch("dp_pose_refine");
 }

@@ -1,6 +1,7 @@
 // Row-wise kernels: residual add, LayerNorm (+residual, +post-add, +masked rows) and the
-// decoder Gate.  One 64-lane wave per row, each lane owns c/64 contiguous elements,
-// statistics in f32 with wave shuffles (no LDS).
+// decoder Gate.  One 64-lane wave per row; each lane owns E = c/64 contiguous elements,
+// moved with one vector load/store where E*sizeof(T) is 4/8/16 bytes; statistics in f32
+// with wave shuffles (no LDS).  HBM-bound: ~3 row passes of c elements each.
 //   nn.LayerNorm post-norm residuals: hybrid_encoder.py:281-296, transformer.py:405-442
 //   Gate: transformer.py:222-235
 //   two-stage masked_fill + enc_output + enc_output_norm: transformer.py:1232-1236
@@ -8,96 +9,175 @@
 
 namespace {
 
-constexpr int MAXE = 8;  // c <= 512
-
-template <typename T>
-__device__ __forceinline__ void load_row(const T* p, int e, float* v) {
-  for (int t = 0; t < e; ++t) v[t] = to_f32(p[t]);
+template <typename T, int E>
+__device__ __forceinline__ void vload(const T* p, float* v) {
+  constexpr int BYTES = E * (int)sizeof(T);
+  if constexpr (BYTES == 16) {
+    uint4 u = *reinterpret_cast<const uint4*>(p);
+    const T* q = reinterpret_cast<const T*>(&u);
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] = to_f32(q[t]);
+  } else if constexpr (BYTES == 8) {
+    uint2 u = *reinterpret_cast<const uint2*>(p);
+    const T* q = reinterpret_cast<const T*>(&u);
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] = to_f32(q[t]);
+  } else if constexpr (BYTES == 4) {
+    uint32_t u = *reinterpret_cast<const uint32_t*>(p);
+    const T* q = reinterpret_cast<const T*>(&u);
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] = to_f32(q[t]);
+  } else {
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] = to_f32(p[t]);
+  }
 }
 
-template <typename T>
+template <typename T, int E>
+__device__ __forceinline__ void vstore(T* p, const float* v) {
+  constexpr int BYTES = E * (int)sizeof(T);
+  if constexpr (BYTES == 16 || BYTES == 8 || BYTES == 4) {
+    T q[E];
+#pragma unroll
+    for (int t = 0; t < E; ++t) q[t] = from_f32<T>(v[t]);
+    if constexpr (BYTES == 16) *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(q);
+    else if constexpr (BYTES == 8) *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(q);
+    else *reinterpret_cast<uint32_t*>(p) = *reinterpret_cast<const uint32_t*>(q);
+  } else {
+#pragma unroll
+    for (int t = 0; t < E; ++t) p[t] = from_f32<T>(v[t]);
+  }
+}
+
+template <typename T, int VEC>
 __global__ __launch_bounds__(256) void add_rows_kernel(T* out, dp_rowmap om, const T* a, dp_rowmap am, const T* b,
                                                        dp_rowmap bm, int rows, int c) {
+  const int nch = c / VEC;
   int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)rows * c) return;
-  const int64_t r = gid / c;
-  const int i = (int)(gid - r * c);
-  out[rowmap_off(om, r) + i] = from_f32<T>(to_f32(a[rowmap_off(am, r) + i]) + to_f32(b[rowmap_off(bm, r) + i]));
+  if (gid >= (int64_t)rows * nch) return;
+  const int64_t r = gid / nch;
+  const int i = (int)(gid - r * nch) * VEC;
+  float x[VEC], y[VEC];
+  vload<T, VEC>(a + rowmap_off(am, r) + i, x);
+  vload<T, VEC>(b + rowmap_off(bm, r) + i, y);
+#pragma unroll
+  for (int t = 0; t < VEC; ++t) x[t] += y[t];
+  vstore<T, VEC>(out + rowmap_off(om, r) + i, x);
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void layernorm_kernel(T* out, dp_rowmap om, const T* x, dp_rowmap xm, const T* res,
-                                                        dp_rowmap rm, const float* __restrict__ g,
-                                                        const float* __restrict__ bta, float eps, int rows, int c,
-                                                        const T* post, dp_rowmap pm, int post_group, int post_skip,
-                                                        const uint8_t* mask, int mask_period, const float* masked_row) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const int e = c >> 6;
-  const int c0 = lane * e;
-  float v[MAXE];
-  T* o = out + rowmap_off(om, r) + c0;
-  if (mask && mask[r % mask_period]) {
-    for (int t = 0; t < e; ++t) o[t] = from_f32<T>(masked_row[c0 + t]);
-    return;
-  }
-  load_row(x + rowmap_off(xm, r) + c0, e, v);
-  if (res) {
-    float rv[MAXE];
-    load_row(res + rowmap_off(rm, r) + c0, e, rv);
-    for (int t = 0; t < e; ++t) v[t] += rv[t];
-  }
+template <int E>
+__device__ __forceinline__ void ln_apply(float* v, const float* __restrict__ g, const float* __restrict__ bta, int c0,
+                                         int c, float eps) {
   float s = 0.f;
-  for (int t = 0; t < e; ++t) s += v[t];
+#pragma unroll
+  for (int t = 0; t < E; ++t) s += v[t];
   const float mean = wave_sum(s) / c;
   float q = 0.f;
-  for (int t = 0; t < e; ++t) {
+#pragma unroll
+  for (int t = 0; t < E; ++t) {
     const float dlt = v[t] - mean;
     q += dlt * dlt;
   }
   const float rstd = rsqrtf(wave_sum(q) / c + eps);
-  for (int t = 0; t < e; ++t) v[t] = (v[t] - mean) * rstd * g[c0 + t] + bta[c0 + t];
+#pragma unroll
+  for (int t = 0; t < E; ++t) v[t] = (v[t] - mean) * rstd * g[c0 + t] + bta[c0 + t];
+}
+
+template <typename T, int E>
+__global__ __launch_bounds__(256) void layernorm_kernel(T* out, dp_rowmap om, const T* x, dp_rowmap xm, const T* res,
+                                                        dp_rowmap rm, const float* __restrict__ g,
+                                                        const float* __restrict__ bta, float eps, int rows,
+                                                        const T* post, dp_rowmap pm, int post_group, int post_skip,
+                                                        const uint8_t* mask, int mask_period, const float* masked_row) {
+  constexpr int c = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int c0 = lane * E;
+  float v[E];
+  T* o = out + rowmap_off(om, r) + c0;
+  if (mask && mask[r % mask_period]) {
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] = masked_row[c0 + t];
+    vstore<T, E>(o, v);
+    return;
+  }
+  vload<T, E>(x + rowmap_off(xm, r) + c0, v);
+  if (res) {
+    float rv[E];
+    vload<T, E>(res + rowmap_off(rm, r) + c0, rv);
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] += rv[t];
+  }
+  ln_apply<E>(v, g, bta, c0, c, eps);
   if (post) {
     const int64_t grp = r / post_group;
     const int w = (int)(r - grp * post_group);
     if (w >= post_skip) {
       const int64_t pr = grp * (post_group - post_skip) + (w - post_skip);
-      float pv[MAXE];
-      load_row(post + rowmap_off(pm, pr) + c0, e, pv);
-      for (int t = 0; t < e; ++t) v[t] += pv[t];
+      float pv[E];
+      vload<T, E>(post + rowmap_off(pm, pr) + c0, pv);
+#pragma unroll
+      for (int t = 0; t < E; ++t) v[t] += pv[t];
     }
   }
-  for (int t = 0; t < e; ++t) o[t] = from_f32<T>(v[t]);
+  vstore<T, E>(o, v);
 }
 
-template <typename T>
+template <typename T, int E>
 __global__ __launch_bounds__(256) void gate_ln_kernel(T* out, int out_ld, const T* gates, const T* xcat,
                                                       const float* __restrict__ g, const float* __restrict__ bta,
-                                                      float eps, int rows, int c) {
+                                                      float eps, int rows) {
+  constexpr int c = 64 * E;
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
-  const int e = c >> 6;
-  const int c0 = lane * e;
+  const int c0 = lane * E;
   const T* gr = gates + r * 2 * c;
   const T* xr = xcat + r * 2 * c;
-  float v[MAXE];
-  float s = 0.f;
-  for (int t = 0; t < e; ++t) {
-    const float g1 = sigmoidf_(to_f32(gr[c0 + t])), g2 = sigmoidf_(to_f32(gr[c + c0 + t]));
-    v[t] = g1 * to_f32(xr[c0 + t]) + g2 * to_f32(xr[c + c0 + t]);
-    s += v[t];
+  float g1[E], g2[E], x1[E], x2[E], v[E];
+  vload<T, E>(gr + c0, g1);
+  vload<T, E>(gr + c + c0, g2);
+  vload<T, E>(xr + c0, x1);
+  vload<T, E>(xr + c + c0, x2);
+#pragma unroll
+  for (int t = 0; t < E; ++t) v[t] = sigmoidf_(g1[t]) * x1[t] + sigmoidf_(g2[t]) * x2[t];
+  ln_apply<E>(v, g, bta, c0, c, eps);
+  vstore<T, E>(out + r * out_ld + c0, v);
+}
+
+template <typename T>
+int launch_ln(int e, dim3 grid, hipStream_t s, T* out, dp_rowmap om, const T* x, dp_rowmap xm, const T* res,
+              dp_rowmap rm, const float* g, const float* b, float eps, int rows, const T* post, dp_rowmap pm, int pg,
+              int ps, const uint8_t* mask, int mp, const float* mrow) {
+#define DP_LN(E_)                                                                                                   \
+  case E_:                                                                                                          \
+    hipLaunchKernelGGL((layernorm_kernel<T, E_>), grid, dim3(256), 0, s, out, om, x, xm, res, rm, g, b, eps, rows, \
+                       post, pm, pg, ps, mask, mp, mrow);                                                           \
+    break;
+  switch (e) {
+    DP_LN(2) DP_LN(4) DP_LN(6) DP_LN(8)
+    default: dp_set_error("dp_layernorm: c=%d unsupported (128/256/384/512)", 64 * e); return DP_EINVAL;
   }
-  const float mean = wave_sum(s) / c;
-  float q = 0.f;
-  for (int t = 0; t < e; ++t) {
-    const float dlt = v[t] - mean;
-    q += dlt * dlt;
+#undef DP_LN
+  return dp_check_launch("dp_layernorm");
+}
+
+template <typename T>
+int launch_gate(int e, dim3 grid, hipStream_t s, T* out, int ld, const T* gates, const T* xcat, const float* g,
+                const float* b, float eps, int rows) {
+  switch (e) {
+    case 2: hipLaunchKernelGGL((gate_ln_kernel<T, 2>), grid, dim3(256), 0, s, out, ld, gates, xcat, g, b, eps, rows); break;
+    case 4: hipLaunchKernelGGL((gate_ln_kernel<T, 4>), grid, dim3(256), 0, s, out, ld, gates, xcat, g, b, eps, rows); break;
+    case 6: hipLaunchKernelGGL((gate_ln_kernel<T, 6>), grid, dim3(256), 0, s, out, ld, gates, xcat, g, b, eps, rows); break;
+    case 8: hipLaunchKernelGGL((gate_ln_kernel<T, 8>), grid, dim3(256), 0, s, out, ld, gates, xcat, g, b, eps, rows); break;
+    default: dp_set_error("dp_gate_layernorm: c=%d unsupported", 64 * e); return DP_EINVAL;
   }
-  const float rstd = rsqrtf(wave_sum(q) / c + eps);
-  T* o = out + r * out_ld + c0;
-  for (int t = 0; t < e; ++t) o[t] = from_f32<T>((v[t] - mean) * rstd * g[c0 + t] + bta[c0 + t]);
+  return dp_check_launch("dp_gate_layernorm");
+}
+
+bool rm_aligned(const dp_rowmap& m, int vec) {
+  return m.base % vec == 0 && m.stride_g % vec == 0 && m.stride_r % vec == 0;
 }
 
 }  // namespace
@@ -105,14 +185,19 @@ __global__ __launch_bounds__(256) void gate_ln_kernel(T* out, int out_ld, const 
 extern "C" int dp_add_rows(void* out, dp_rowmap om, const void* a, dp_rowmap am, const void* b, dp_rowmap bm,
                            int32_t rows, int32_t c, int32_t dtype, void* stream) {
   DP_REQUIRE(om.group > 0 && am.group > 0 && bm.group > 0, "dp_add_rows: row map group must be > 0");
-  const int64_t total = (int64_t)rows * c;
+  const int vec = dtype == DP_BF16 ? 8 : 4;
+  const bool al = c % vec == 0 && rm_aligned(om, vec) && rm_aligned(am, vec) && rm_aligned(bm, vec) &&
+                  ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(a) |
+                    reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+  DP_REQUIRE(al, "dp_add_rows: rows must be 16-byte aligned (c=%d)", c);
+  const int64_t total = (int64_t)rows * (c / vec);
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(add_rows_kernel<bf16_t>, grid, block, 0, as_stream(stream), (bf16_t*)out, om, (const bf16_t*)a,
-                       am, (const bf16_t*)b, bm, rows, c);
+    hipLaunchKernelGGL((add_rows_kernel<bf16_t, 8>), grid, block, 0, as_stream(stream), (bf16_t*)out, om,
+                       (const bf16_t*)a, am, (const bf16_t*)b, bm, rows, c);
   else
-    hipLaunchKernelGGL(add_rows_kernel<float>, grid, block, 0, as_stream(stream), (float*)out, om, (const float*)a, am,
-                       (const float*)b, bm, rows, c);
+    hipLaunchKernelGGL((add_rows_kernel<float, 4>), grid, block, 0, as_stream(stream), (float*)out, om,
+                       (const float*)a, am, (const float*)b, bm, rows, c);
   return dp_check_launch("dp_add_rows");
 }
 
@@ -121,31 +206,29 @@ extern "C" int dp_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm
                             const void* post, dp_rowmap pm, int32_t post_group, int32_t post_skip,
                             const uint8_t* row_mask, int32_t mask_period, const float* masked_row, int32_t dtype,
                             void* stream) {
-  DP_REQUIRE(c % 64 == 0 && c / 64 <= MAXE, "dp_layernorm: c=%d must be a multiple of 64 and <= 512", c);
+  DP_REQUIRE(c % 64 == 0 && c / 64 <= 8, "dp_layernorm: c=%d must be a multiple of 64 and <= 512", c);
   DP_REQUIRE(om.group > 0 && xm.group > 0 && (!res || rm.group > 0), "dp_layernorm: row map group must be > 0");
   DP_REQUIRE(!post || (post_group > post_skip && pm.group > 0), "dp_layernorm: bad post map");
   DP_REQUIRE(!row_mask || (mask_period > 0 && masked_row), "dp_layernorm: bad mask");
-  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const int e = c / 64;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = as_stream(stream);
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(layernorm_kernel<bf16_t>, grid, block, 0, as_stream(stream), (bf16_t*)out, om, (const bf16_t*)x,
-                       xm, (const bf16_t*)res, rm, gamma, beta, eps, rows, c, (const bf16_t*)post, pm, post_group,
-                       post_skip, row_mask, mask_period, masked_row);
-  else
-    hipLaunchKernelGGL(layernorm_kernel<float>, grid, block, 0, as_stream(stream), (float*)out, om, (const float*)x, xm,
-                       (const float*)res, rm, gamma, beta, eps, rows, c, (const float*)post, pm, post_group, post_skip,
-                       row_mask, mask_period, masked_row);
-  return dp_check_launch("dp_layernorm");
+    return launch_ln<bf16_t>(e, grid, s, (bf16_t*)out, om, (const bf16_t*)x, xm, (const bf16_t*)res, rm, gamma, beta,
+                             eps, rows, (const bf16_t*)post, pm, post_group, post_skip, row_mask, mask_period,
+                             masked_row);
+  return launch_ln<float>(e, grid, s, (float*)out, om, (const float*)x, xm, (const float*)res, rm, gamma, beta, eps,
+                          rows, (const float*)post, pm, post_group, post_skip, row_mask, mask_period, masked_row);
 }
 
 extern "C" int dp_gate_layernorm(void* out, int32_t out_ld, const void* gates, const void* xcat, const float* gamma,
                                  const float* beta, float eps, int32_t rows, int32_t c, int32_t dtype, void* stream) {
-  DP_REQUIRE(c % 64 == 0 && c / 64 <= MAXE, "dp_gate_layernorm: c=%d must be a multiple of 64 and <= 512", c);
-  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  DP_REQUIRE(c % 64 == 0 && c / 64 <= 8, "dp_gate_layernorm: c=%d must be a multiple of 64 and <= 512", c);
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = as_stream(stream);
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(gate_ln_kernel<bf16_t>, grid, block, 0, as_stream(stream), (bf16_t*)out, out_ld,
-                       (const bf16_t*)gates, (const bf16_t*)xcat, gamma, beta, eps, rows, c);
-  else
-    hipLaunchKernelGGL(gate_ln_kernel<float>, grid, block, 0, as_stream(stream), (float*)out, out_ld,
-                       (const float*)gates, (const float*)xcat, gamma, beta, eps, rows, c);
-  return dp_check_launch("dp_gate_layernorm");
+    return launch_gate<bf16_t>(c / 64, grid, s, (bf16_t*)out, out_ld, (const bf16_t*)gates, (const bf16_t*)xcat,
+                               gamma, beta, eps, rows);
+  return launch_gate<float>(c / 64, grid, s, (float*)out, out_ld, (const float*)gates, (const float*)xcat, gamma, beta,
+                            eps, rows);
 }

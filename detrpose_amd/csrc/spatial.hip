@@ -4,64 +4,87 @@
 //  * StemBlock.stem1 3x3 s2 conv straight from the f32 NCHW image (hgnetv2.py:171-177)
 //  * StemBlock's F.pad(0,1,0,1) + MaxPool2d(2,1,ceil_mode) (hgnetv2.py:215,217)
 // These run at arithmetic intensity 2-12 FLOP/B, far under the MFMA ridge (~312), so
-// they are plain 16-byte-vector VALU kernels: one thread = one pixel x 16 bytes of
-// channels, consecutive threads on consecutive channel chunks (coalesced rows).
+// they are plain 16-byte-vector VALU kernels with consecutive threads on consecutive
+// channel chunks (coalesced pixel rows).
 #include "common.h"
 
 namespace {
 
-template <typename T>
-__global__ __launch_bounds__(256) void dwconv_kernel(dp_conv_desc d, int64_t total, int nchunk) {
+// Depthwise k x k, stride S: one thread = PX consecutive output pixels of one row x one
+// 16-byte channel chunk. Per kernel row the (PX-1)*S+KS input pixels are loaded once and
+// reused by all KS taps and PX outputs (register sliding window); the per-channel
+// weights of a tap are read once for all PX outputs.
+template <typename T, int KS, int S, int PX>
+__global__ __launch_bounds__(256) void dwconv_kernel(dp_conv_desc d, int64_t total, int nchunk, int ntx) {
   constexpr int VEC = Vec16<T>::N;
+  constexpr int NIN = (PX - 1) * S + KS;
   int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= total) return;
   const int cc = (int)(gid % nchunk);
-  int64_t pix = gid / nchunk;
-  const int hw = d.out_h * d.out_w;
-  const int b = (int)(pix / hw);
-  const int rem = (int)(pix - (int64_t)b * hw);
-  const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
+  int64_t rest = gid / nchunk;
+  const int tx = (int)(rest % ntx);
+  rest /= ntx;
+  const int oy = (int)(rest % d.out_h);
+  const int b = (int)(rest / d.out_h);
+  const int ox0 = tx * PX;
   const int c0 = cc * VEC;
   const T* in = reinterpret_cast<const T*>(d.in) + (int64_t)b * d.in_bstride + c0;
   const float* w = reinterpret_cast<const float*>(d.weight) + c0;
-  float acc[VEC];
-#pragma unroll
-  for (int t = 0; t < VEC; ++t) acc[t] = d.bias ? d.bias[c0 + t] : 0.f;
-  const int iy0 = oy * d.stride - d.pad_t, ix0 = ox * d.stride - d.pad_l;
-  for (int ky = 0; ky < d.kh; ++ky) {
-    const int iy = iy0 + ky;
-    if (iy < 0 || iy >= d.in_h) continue;
-    for (int kx = 0; kx < d.kw; ++kx) {
-      const int ix = ix0 + kx;
-      if (ix < 0 || ix >= d.in_w) continue;
-      Vec16<T> v = load16(in + ((int64_t)iy * d.in_w + ix) * d.in_pstride);
-      const float* wk = w + (ky * d.kw + kx) * d.cin;
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) acc[t] = fmaf(v.get(t), wk[t], acc[t]);
-    }
-  }
-  Vec16<T> o;
+  float acc[PX][VEC];
 #pragma unroll
   for (int t = 0; t < VEC; ++t) {
-    float v = apply_act(acc[t], d.act);
-    if (d.has_lab) v = d.lab_scale * v + d.lab_bias;
-    o.set(t, v);
+    const float bv = d.bias ? d.bias[c0 + t] : 0.f;
+#pragma unroll
+    for (int p = 0; p < PX; ++p) acc[p][t] = bv;
   }
-  T* out = reinterpret_cast<T*>(d.out) + (int64_t)b * d.out_bstride + (int64_t)rem * d.out_pstride + c0;
-  store16(out, o);
+  const int iy0 = oy * S - d.pad_t, ix0 = ox0 * S - d.pad_l;
+#pragma unroll
+  for (int ky = 0; ky < KS; ++ky) {
+    const int iy = iy0 + ky;
+    if (iy < 0 || iy >= d.in_h) continue;
+    Vec16<T> xin[NIN];
+#pragma unroll
+    for (int j = 0; j < NIN; ++j) {
+      const int ix = ix0 + j;
+      if (ix >= 0 && ix < d.in_w) xin[j] = load16(in + ((int64_t)iy * d.in_w + ix) * d.in_pstride);
+      else *reinterpret_cast<uint4*>(&xin[j].v) = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) {
+      const float* wk = w + (ky * KS + kx) * d.cin;
+      float wv[VEC];
+#pragma unroll
+      for (int t = 0; t < VEC; t += 4) *reinterpret_cast<float4*>(&wv[t]) = *reinterpret_cast<const float4*>(wk + t);
+#pragma unroll
+      for (int p = 0; p < PX; ++p)
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) acc[p][t] = fmaf(xin[p * S + kx].get(t), wv[t], acc[p][t]);
+    }
+  }
+  T* out = reinterpret_cast<T*>(d.out) + (int64_t)b * d.out_bstride + c0;
+#pragma unroll
+  for (int p = 0; p < PX; ++p) {
+    const int ox = ox0 + p;
+    if (ox >= d.out_w) break;
+    Vec16<T> o;
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) {
+      float v = apply_act(acc[p][t], d.act);
+      if (d.has_lab) v = d.lab_scale * v + d.lab_bias;
+      o.set(t, v);
+    }
+    store16(out + ((int64_t)oy * d.out_w + ox) * d.out_pstride, o);
+  }
 }
 
-// one thread per output pixel, all cout channels (cout <= 64); image f32 NCHW, 3 channels
-template <typename T>
+// One thread per output pixel, all COUT channels; image f32 NCHW, 3 channels. The
+// weights are wave-uniform, so they are read with scalar loads (SGPR operands of the
+// FMAs) rather than staged through LDS.
+template <typename T, int COUT>
 __global__ __launch_bounds__(256) void stem_conv_kernel(const float* __restrict__ img, int batch, int h, int w,
                                                         const float* __restrict__ wt, const float* __restrict__ bias,
-                                                        int cout, int has_lab, float ls, float lb, T* __restrict__ out,
+                                                        int has_lab, float ls, float lb, T* __restrict__ out,
                                                         int64_t obs, int ops) {
-  __shared__ float sw[64 * 27];
-  __shared__ float sb[64];
-  for (int i = threadIdx.x; i < cout * 27; i += blockDim.x) sw[i] = wt[i];
-  for (int i = threadIdx.x; i < cout; i += blockDim.x) sb[i] = bias[i];
-  __syncthreads();
   const int oh = (h + 1) / 2, ow = (w + 1) / 2;
   int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)batch * oh * ow) return;
@@ -80,22 +103,26 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float* __restrict_
         x[(c * 3 + ky) * 3 + kx] = ok ? img[(((int64_t)b * 3 + c) * h + iy) * w + ix] : 0.f;
       }
   T* o = out + (int64_t)b * obs + (int64_t)rem * ops;
-  for (int n0 = 0; n0 < cout; n0 += 8) {
+#pragma unroll
+  for (int n0 = 0; n0 < COUT; n0 += 8) {
     float r[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      const int n = n0 + t;
-      float a = 0.f;
-      if (n < cout) {
-        a = sb[n];
+      float a = bias[n0 + t];
 #pragma unroll
-        for (int k = 0; k < 27; ++k) a = fmaf(x[k], sw[n * 27 + k], a);
-        a = fmaxf(a, 0.f);
-        if (has_lab) a = ls * a + lb;
-      }
+      for (int k = 0; k < 27; ++k) a = fmaf(x[k], wt[(n0 + t) * 27 + k], a);
+      a = fmaxf(a, 0.f);
+      if (has_lab) a = ls * a + lb;
       r[t] = a;
     }
-    for (int t = 0; t < 8 && n0 + t < cout; ++t) o[n0 + t] = from_f32<T>(r[t]);
+    constexpr int V = Vec16<T>::N;
+#pragma unroll
+    for (int h0 = 0; h0 < 8; h0 += V) {
+      Vec16<T> v;
+#pragma unroll
+      for (int t = 0; t < V; ++t) v.set(t, r[h0 + t]);
+      store16(o + n0 + h0, v);
+    }
   }
 }
 
@@ -126,7 +153,7 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, 
         for (int t = 0; t < VEC; ++t) m[t] = fmaxf(m[t], v.get(t));
       } else {
 #pragma unroll
-        for (int t = 0; t < VEC; ++t) m[t] = fmaxf(m[t], 0.f);  // F.pad zero participates
+        for (int t = 0; t < VEC; ++t) m[t] = fmaxf(m[t], 0.f);  // the F.pad zero takes part in the max
       }
     }
   Vec16<T> o;
@@ -146,30 +173,51 @@ extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
   DP_REQUIRE(d.cin == d.cout && d.cin % VEC == 0, "dp_dwconv2d: channels %d/%d must match and be a multiple of %d",
              d.cin, d.cout, VEC);
   DP_REQUIRE(d.in_pstride % VEC == 0 && d.out_pstride % VEC == 0 && d.in_bstride % VEC == 0 &&
-                 d.out_bstride % VEC == 0 && al16(d.in) && al16(d.out),
+                 d.out_bstride % VEC == 0 && al16(d.in) && al16(d.out) && al16(d.weight),
              "dp_dwconv2d: 16-byte alignment required");
   const int nchunk = d.cin / VEC;
-  const int64_t total = (int64_t)d.batch * d.out_h * d.out_w * nchunk;
+  constexpr int PX = 4;
+  const int ntx = (d.out_w + PX - 1) / PX;
+  const int64_t total = (int64_t)d.batch * d.out_h * ntx * nchunk;
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
-  if (d.dtype == DP_BF16) hipLaunchKernelGGL(dwconv_kernel<bf16_t>, grid, block, 0, as_stream(stream), d, total, nchunk);
-  else hipLaunchKernelGGL(dwconv_kernel<float>, grid, block, 0, as_stream(stream), d, total, nchunk);
-  return dp_check_launch("dp_dwconv2d");
+  hipStream_t s = as_stream(stream);
+#define DP_DW(T_, KS_, S_)                                                                            \
+  if (d.kh == KS_ && d.kw == KS_ && d.stride == S_) {                                                \
+    hipLaunchKernelGGL((dwconv_kernel<T_, KS_, S_, PX>), grid, block, 0, s, d, total, nchunk, ntx); \
+    return dp_check_launch("dp_dwconv2d");                                                           \
+  }
+  if (d.dtype == DP_BF16) {
+    DP_DW(bf16_t, 3, 1) DP_DW(bf16_t, 3, 2) DP_DW(bf16_t, 5, 1) DP_DW(bf16_t, 5, 2)
+  } else {
+    DP_DW(float, 3, 1) DP_DW(float, 3, 2) DP_DW(float, 5, 1) DP_DW(float, 5, 2)
+  }
+#undef DP_DW
+  dp_set_error("dp_dwconv2d: kernel %dx%d stride %d not supported (3/5, stride 1/2)", d.kh, d.kw, d.stride);
+  return DP_EINVAL;
 }
 
 extern "C" int dp_stem_conv(const float* image, int32_t batch, int32_t h, int32_t w, const float* weight,
                             const float* bias, int32_t cout, int32_t has_lab, float lab_scale, float lab_bias,
                             void* out, int64_t out_bstride, int32_t out_pstride, int32_t dtype, void* stream) {
   DP_REQUIRE(image && weight && bias && out, "dp_stem_conv: null pointer");
-  DP_REQUIRE(cout > 0 && cout <= 64, "dp_stem_conv: cout=%d (max 64)", cout);
+  DP_REQUIRE(out_pstride % 8 == 0 && out_bstride % 8 == 0 && al16(out), "dp_stem_conv: output alignment");
   const int64_t total = (int64_t)batch * ((h + 1) / 2) * ((w + 1) / 2);
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
-  if (dtype == DP_BF16)
-    hipLaunchKernelGGL(stem_conv_kernel<bf16_t>, grid, block, 0, as_stream(stream), image, batch, h, w, weight, bias,
-                       cout, has_lab, lab_scale, lab_bias, reinterpret_cast<bf16_t*>(out), out_bstride, out_pstride);
-  else
-    hipLaunchKernelGGL(stem_conv_kernel<float>, grid, block, 0, as_stream(stream), image, batch, h, w, weight, bias,
-                       cout, has_lab, lab_scale, lab_bias, reinterpret_cast<float*>(out), out_bstride, out_pstride);
-  return dp_check_launch("dp_stem_conv");
+  hipStream_t s = as_stream(stream);
+#define DP_STEM(T_, N_)                                                                                     \
+  if (cout == N_) {                                                                                        \
+    hipLaunchKernelGGL((stem_conv_kernel<T_, N_>), grid, block, 0, s, image, batch, h, w, weight, bias,     \
+                       has_lab, lab_scale, lab_bias, reinterpret_cast<T_*>(out), out_bstride, out_pstride); \
+    return dp_check_launch("dp_stem_conv");                                                                \
+  }
+  if (dtype == DP_BF16) {
+    DP_STEM(bf16_t, 16) DP_STEM(bf16_t, 24) DP_STEM(bf16_t, 32) DP_STEM(bf16_t, 48) DP_STEM(bf16_t, 64)
+  } else {
+    DP_STEM(float, 16) DP_STEM(float, 24) DP_STEM(float, 32) DP_STEM(float, 48) DP_STEM(float, 64)
+  }
+#undef DP_STEM
+  dp_set_error("dp_stem_conv: cout=%d not instantiated (16/24/32/48/64)", cout);
+  return DP_EINVAL;
 }
 
 extern "C" int dp_maxpool2x2_pad_rb(const void* in, int64_t in_bstride, int32_t in_pstride, int32_t batch, int32_t h,

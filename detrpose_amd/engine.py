@@ -125,8 +125,9 @@ class Packer:
         wt = w[:, 0].permute(1, 2, 0).contiguous().float().to(self.device)  # [kh][kw][C]
         return PConv(wt, b.float().to(self.device), kh, kw, stride, (kh - 1) // 2, c, c, ACT[act], lab, True)
 
-    def linear(self, w, b, act=None) -> PConv:
-        return self.conv(w.double()[:, :, None, None], b.double(), act=act)
+    def linear(self, w, b, act=None, exact=False) -> PConv:
+        """exact=True keeps cout unpadded (f32-output head layers: 2 / 34 / 66 columns)."""
+        return self.conv(w.double()[:, :, None, None], b.double(), act=act, cout=w.shape[0] if exact else None)
 
     def small(self, w, b, act=None) -> PSmall:
         w = w.float()
@@ -396,7 +397,7 @@ class Engine:
         P["enc_cls"] = (pk.t(sd[t + "enc_out_class_embed.weight"]), pk.t(sd[t + "enc_out_class_embed.bias"]))
         ep = t + "enc_pose_embed.layers."
         P["enc_pose"] = [pk.linear(sd[ep + f"{i}.weight"], sd[ep + f"{i}.bias"], act="relu") for i in range(3)]
-        P["enc_pose_last"] = pk.small(sd[ep + "3.weight"], sd[ep + "3.bias"])
+        P["enc_pose_last"] = pk.linear(sd[ep + "3.weight"], sd[ep + "3.bias"], exact=True)
         # query template: [instance | keypoint + tgt_embed[q]]  (transformer.py:1253-1261)
         nq, K = tr.num_queries, tr.num_body_points
         tmpl = torch.cat([sd[t + "instance_embedding.weight"][None].expand(nq, 1, Cc),
@@ -411,7 +412,7 @@ class Engine:
         pp = t + "pre_pose_embed.layers."
         P["pre_pose"] = [pk.linear(sd[pp + "0.weight"], sd[pp + "0.bias"], act="relu"),
                          pk.linear(sd[pp + "1.weight"], sd[pp + "1.bias"], act="relu"),
-                         pk.small(sd[pp + "2.weight"], sd[pp + "2.bias"])]
+                         pk.linear(sd[pp + "2.weight"], sd[pp + "2.bias"], exact=True)]
         P["layers"] = []
         for l in range(tr.num_decoder_layers):
             lp = f"{t}decoder.layers.{l}."
@@ -434,7 +435,7 @@ class Engine:
                 "norm2": (pk.t(sd[lp + "norm2.weight"]), pk.t(sd[lp + "norm2.bias"])),
                 "pose": [pk.linear(sd[pe + "0.weight"], sd[pe + "0.bias"], act="relu"),
                          pk.linear(sd[pe + "1.weight"], sd[pe + "1.bias"], act="relu"),
-                         pk.small(sd[pe + "2.weight"], sd[pe + "2.bias"])],
+                         pk.linear(sd[pe + "2.weight"], sd[pe + "2.bias"], exact=True)],
             }
             if l == tr.num_decoder_layers - 1:
                 qp = f"{t}lqe_embed.{l}.reg_conf.layers."
@@ -455,7 +456,8 @@ class Engine:
         t = self._empty(B * H * W * Cc, dtype=dtype)
         return FMap(t, 0, B, H, W, Cc, Cc, H * W * Cc)
 
-    def _conv(self, plan, name, x: FMap, pc: PConv, out: FMap, res: FMap | None = None, up: FMap | None = None):
+    def _conv(self, plan, name, x: FMap, pc: PConv, out: FMap, res: FMap | None = None, up: FMap | None = None,
+              out_f32: bool = False):
         if pc.depthwise:
             assert x.C == pc.cin == out.C, (name, x.C, pc.cin, out.C)
         else:
@@ -480,6 +482,9 @@ class Engine:
             assert up.C == out.C and up.H == 2 * out.H and up.W == 2 * out.W
             d.up, d.up_bstride, d.up_pstride = up.ptr, up.bs, up.ps
         d.batch, d.act, d.dtype = x.B, pc.act, self.code
+        if out_f32:
+            assert out.t.dtype == torch.float32 and (res is None or res.t.dtype == torch.float32)
+            d.out_f32 = 1
         if pc.lab is not None:
             d.has_lab, d.lab_scale, d.lab_bias = 1, pc.lab[0], pc.lab[1]
         plan.keep.append(d)
@@ -719,9 +724,9 @@ class Engine:
             self._conv(plan, f"ts.enc_pose{i}", x, pc, y)
             x = y
         last = P["enc_pose_last"]
-        delta = self._empty(B * nq, last.n, dtype=torch.float32)
-        plan._op("ts.enc_pose3", lib.dp_linear_small, x.ptr, contiguous_rows(x.C), self.code, B * nq, last.k,
-                 last.wt.data_ptr(), last.b.data_ptr(), last.n, last.n, last.act, None, delta.data_ptr())
+        delta = self._empty(B * nq, last.cout, dtype=torch.float32)
+        self._conv(plan, "ts.enc_pose3", x, last, FMap(delta, 0, 1, 1, B * nq, last.cout, last.cout, delta.numel()),
+                   out_f32=True)
         ref = self._empty(B, nq, T, 2, dtype=torch.float32)
         plan._op("ts.refpoints", lib.dp_refpoint_init, delta.data_ptr(), P["anchors"].data_ptr(), topi.data_ptr(), B,
                  nq, K, ref.data_ptr())
@@ -820,8 +825,7 @@ class Engine:
                 pp = P["pre_pose"]
                 self._conv(plan, n + ".pre0", pose_f, pp[0], ph1)
                 self._conv(plan, n + ".pre1", ph1, pp[1], ph2)
-                plan._op(n + ".pre2", lib.dp_linear_small, ph2.ptr, contiguous_rows(Cc), self.code, krows, pp[2].k,
-                         pp[2].wt.data_ptr(), pp[2].b.data_ptr(), pp[2].n, pp[2].n, 0, None, pre.data_ptr())
+                self._conv(plan, n + ".pre2", ph2, pp[2], FMap(pre, 0, 1, 1, krows, 2, 2, pre.numel()), out_f32=True)
                 plan._op(n + ".pre_pose", lib.dp_pre_pose, pre.data_ptr(), ref.data_ptr(), B * nq, K,
                          ref_init.data_ptr())
                 x_in = pose_f
@@ -835,9 +839,9 @@ class Engine:
             self._conv(plan, n + ".pose0", x_in, ph[0], ph1)
             self._conv(plan, n + ".pose1", ph1, ph[1], ph2)
             cur, prev = corners[l % 2], corners[(l + 1) % 2]
-            plan._op(n + ".pose2", lib.dp_linear_small, ph2.ptr, contiguous_rows(Cc), self.code, krows, ph[2].k,
-                     ph[2].wt.data_ptr(), ph[2].b.data_ptr(), ph[2].n, ph[2].n, 0,
-                     prev.data_ptr() if l > 0 else None, cur.data_ptr())
+            # pred_corners = pose_head(...) + pred_corners_undetach (transformer.py:712), f32 out + f32 residual
+            self._conv(plan, n + ".pose2", ph2, ph[2], FMap(cur, 0, 1, 1, krows, nb, nb, cur.numel()),
+                       res=FMap(prev, 0, 1, 1, krows, nb, nb, prev.numel()) if l > 0 else None, out_f32=True)
             plan._op(n + ".refine", lib.dp_pose_refine, cur.data_ptr(), P["project"].data_ptr(), tr.reg_max,
                      ref_init.data_ptr(), C.c_float(P["reg_scale"]), B * nq, K, kps.data_ptr(), ref.data_ptr())
             if l == nlayers - 1:

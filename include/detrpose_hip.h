@@ -45,8 +45,10 @@ typedef struct dp_conv_desc {
   int32_t batch;
   int32_t act;     int32_t has_lab;  float lab_scale, lab_bias;  /* y = lab(act(x)) + res */
   int32_t dtype;
-  /* upsample2x > 0: also write nearest x2 copy to up (concat buffer slice) */
+  /* up != NULL: also write a nearest x2 copy of the output to up (concat buffer slice) */
   void* up;        int64_t up_bstride;  int32_t up_pstride;
+  /* out_f32 != 0: out (and res) are f32 whatever dtype is (1x1 / linear layers only) */
+  int32_t out_f32;
 } dp_conv_desc;
 
 /* Row map: row r -> element offset  base + (r / group)*stride_g + (r % group)*stride_r. */

@@ -360,3 +360,33 @@ def test_decoder_head_kernels():
     _close(sc, rs, "fp32", "pp scores")
     np.testing.assert_array_equal(lb.cpu().numpy(), rl.numpy())
     _close(ok, rk, "fp32", "pp kps")
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("cout", [2, 34, 66])
+def test_linear_f32_out(dt, cout):
+    """bf16/f32 activations in, f32 out (+ f32 residual): the head layers (corners, enc pose, pre-pose)."""
+    torch.manual_seed(cout)
+    pk = Packer({}, dt, torch.device("cuda"))
+    rows, k = 1000, 256
+    x = torch.randn(rows, k)
+    w = torch.randn(cout, k) / 16
+    b = torch.randn(cout)
+    pc = pk.linear(w, b, exact=True)
+    assert pc.cout == cout
+    out = torch.empty(1, 1, rows, cout, device="cuda")
+    res = torch.randn(1, 1, rows, cout)
+    resd = res.cuda()
+    xd = x.to("cuda", DTYPES[dt][0]).reshape(1, 1, rows, k)
+    lib = _lib.load()
+    d = ConvDesc()
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = xd.data_ptr(), rows * k, k, 1, rows, k
+    d.weight, d.kpad, d.bias = pc.w.data_ptr(), pc.kpad, pc.b.data_ptr()
+    d.kh = d.kw = d.stride = 1
+    d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out.data_ptr(), rows * cout, cout, 1, rows, cout
+    d.res, d.res_bstride, d.res_pstride = resd.data_ptr(), rows * cout, cout
+    d.batch, d.dtype, d.out_f32 = 1, DTYPES[dt][1], 1
+    _lib.check(lib.dp_conv2d(C.byref(d), _s()))
+    torch.cuda.synchronize()
+    ref = x.to(DTYPES[dt][0]).float() @ w.to(DTYPES[dt][0]).float().t() + b + res.reshape(rows, cout)
+    _close(out.reshape(rows, cout), ref, "fp32" if dt == "fp32" else "bf16", f"f32-out {cout}")
