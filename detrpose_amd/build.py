@@ -34,8 +34,9 @@ def _hipcc() -> str:
 
 
 def _flags() -> list[str]:
+    extra = os.environ.get("DETRPOSE_EXTRA_FLAGS", "").split()
     return ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-            "-I", os.path.join(REPO, "include")]
+            "-I", os.path.join(REPO, "include")] + extra
 
 
 def _stale(obj: str, src: str, deps: list[str]) -> bool:
@@ -45,9 +46,15 @@ def _stale(obj: str, src: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(p) > t for p in [src] + deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
+    """variant != '': build into build/csrc-<variant> and lib/variants/<variant>/ (A/B experiments,
+    with DETRPOSE_EXTRA_FLAGS) instead of the production library."""
+    global BUILD, LIB
+    if variant:
+        BUILD = os.path.join(REPO, "build", "csrc-" + variant)
+        LIB = os.path.join(LIBDIR, "variants", variant, "libdetrpose_hip.so")
     os.makedirs(BUILD, exist_ok=True)
-    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     hipcc = _hipcc()
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     deps = glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(REPO, "include", "detrpose_hip.h")]
@@ -80,5 +87,6 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--variant", default="")
     a = ap.parse_args()
-    print(build(force=a.force, verbose=a.verbose))
+    print(build(force=a.force, verbose=a.verbose, variant=a.variant))
