@@ -125,6 +125,175 @@ int dispatch(const void* q, int ld_q, const void* k, const void* v, int ld_kv, v
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// bf16 MFMA path. One wave = one (sequence, head, 64-query block). S = Q K^T runs on
+// v_mfma_f32_16x16x32_bf16 with Q (A operand, query rows) and K (B operand, key rows)
+// loaded straight from global in fragment layout; softmax is online over 64-key blocks
+// with the row max / row sum reduced across the 16 lanes that share a row; P (bf16) and
+// V^T go through the wave's private LDS slice to become the A / B operands of O = P V.
+// No block-level synchronisation: the 4 waves of a block are independent work items.
+constexpr int AP = 72;  // LDS pitch (elements) of P [64][AP] and V^T [DH][AP]
+
+template <int DH>
+__global__ __launch_bounds__(256) void attn_mfma_kernel(const bf16_t* __restrict__ q, int ld_q,
+                                                        const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                        int ld_kv, bf16_t* __restrict__ out, int ld_o, int n_inner,
+                                                        int64_t so, int64_t si, int64_t st, int seqlen, int nhead,
+                                                        int npairs, int nqb, float scale) {
+  constexpr int KS = (DH + 31) / 32;   // 32-wide k-steps over the head dim (zero padded)
+  constexpr int ND = DH / 16;          // 16-wide output column tiles
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4][(64 + DH) * AP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int item = blockIdx.x * 4 + wave;
+  if (item >= npairs * nqb) return;
+  const int pair = item / nqb, qb = item - pair * nqb;
+  const int h = pair % nhead, sq = pair / nhead;
+  const int o = sq / n_inner, ii = sq - o * n_inner;
+  const int64_t base = (int64_t)o * so + (int64_t)ii * si;
+  bf16_t* Ps = lds[wave];            // [64][AP]  P (query rows x keys)
+  bf16_t* Vt = lds[wave] + 64 * AP;  // [DH][AP]  V^T (head dims x keys)
+  const int lr = lane & 15, lg = lane >> 4;
+
+  bf16x8 qf[4][KS];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qi = qb * 64 + 16 * i + lr;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int d0 = 32 * ks + 8 * lg;
+      if (qi < seqlen && d0 < DH)
+        qf[i][ks] = *reinterpret_cast<const bf16x8*>(q + (base + (int64_t)qi * st) * ld_q + h * DH + d0);
+      else
+        qf[i][ks] = bf16x8{};
+    }
+  }
+  f32x4 oacc[4][ND];
+  float mrow[4][4], lrow[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) oacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mrow[i][r] = -INFINITY;
+      lrow[i][r] = 0.f;
+    }
+  }
+  const int nkb = (seqlen + 63) / 64;
+  for (int kb = 0; kb < nkb; ++kb) {
+    // ---- S = Q K^T
+    f32x4 sacc[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kj = kb * 64 + 16 * j + lr;
+      bf16x8 kf[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int d0 = 32 * ks + 8 * lg;
+        if (kj < seqlen && d0 < DH)
+          kf[ks] = *reinterpret_cast<const bf16x8*>(k + (base + (int64_t)kj * st) * ld_kv + h * DH + d0);
+        else
+          kf[ks] = bf16x8{};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[i][ks], kf[ks], a, 0, 0, 0);
+        sacc[i][j] = a;
+      }
+    }
+    // ---- V block -> V^T in LDS (keys beyond seqlen are zero)
+    constexpr int VCH = DH / 8;  // 16-byte chunks per key row
+#pragma unroll
+    for (int t = 0; t < VCH; ++t) {
+      const int c = lane + 64 * t;
+      const int key = c / VCH, dc = c - key * VCH;
+      const int kg = kb * 64 + key;
+      bf16x8 vv = bf16x8{};
+      if (kg < seqlen) vv = *reinterpret_cast<const bf16x8*>(v + (base + (int64_t)kg * st) * ld_kv + h * DH + dc * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Vt[(dc * 8 + e) * AP + key] = vv[e];
+    }
+    // ---- online softmax over this key block
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kj = kb * 64 + 16 * j + lr;
+          const float sv = kj < seqlen ? sacc[i][j][r] * scale : -INFINITY;
+          sacc[i][j][r] = sv;
+          mx = fmaxf(mx, sv);
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        const float mn = fmaxf(mrow[i][r], mx);
+        const float corr = __expf(mrow[i][r] - mn);
+        mrow[i][r] = mn;
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = __expf(sacc[i][j][r] - mn);
+          sum += p;
+          Ps[(16 * i + 4 * lg + r) * AP + 16 * j + lr] = (bf16_t)p;
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
+        lrow[i][r] = lrow[i][r] * corr + sum;
+#pragma unroll
+        for (int jd = 0; jd < ND; ++jd) oacc[i][jd][r] *= corr;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- O += P V
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 pf[4], vf[ND];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pf[i] = *reinterpret_cast<const bf16x8*>(Ps + (16 * i + lr) * AP + 32 * ks + 8 * lg);
+#pragma unroll
+      for (int jd = 0; jd < ND; ++jd)
+        vf[jd] = *reinterpret_cast<const bf16x8*>(Vt + (16 * jd + lr) * AP + 32 * ks + 8 * lg);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jd = 0; jd < ND; ++jd)
+          oacc[i][jd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[i], vf[jd], oacc[i][jd], 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- normalise and store (row = query, lane column = head dim)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qi = qb * 64 + 16 * i + 4 * lg + r;
+      if (qi >= seqlen) continue;
+      const float inv = 1.f / lrow[i][r];
+      bf16_t* op = out + (base + (int64_t)qi * st) * ld_o + h * DH;
+#pragma unroll
+      for (int jd = 0; jd < ND; ++jd) op[16 * jd + lr] = (bf16_t)(oacc[i][jd][r] * inv);
+    }
+  }
+}
+
+template <int DH>
+int launch_mfma(const void* q, int ld_q, const void* k, const void* v, int ld_kv, void* out, int ld_o, int n_outer,
+                int n_inner, int64_t so, int64_t si, int64_t st, int seqlen, int nhead, hipStream_t s) {
+  const int npairs = n_outer * n_inner * nhead;
+  const int nqb = (seqlen + 63) / 64;
+  const int64_t items = (int64_t)npairs * nqb;
+  dim3 grid((unsigned)((items + 3) / 4)), block(256);
+  hipLaunchKernelGGL((attn_mfma_kernel<DH>), grid, block, 0, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
+                     (const bf16_t*)v, ld_kv, (bf16_t*)out, ld_o, n_inner, so, si, st, seqlen, nhead, npairs, nqb,
+                     1.f / sqrtf((float)DH));
+  return dp_check_launch("dp_attention");
+}
+
 }  // namespace
 
 extern "C" int dp_attention(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out,
@@ -133,6 +302,13 @@ extern "C" int dp_attention(const void* q, int32_t ld_q, const void* k, const vo
   DP_REQUIRE(q && k && v && out, "dp_attention: null pointer");
   DP_REQUIRE(seqlen > 0 && n_outer > 0 && n_inner > 0 && nhead > 0, "dp_attention: bad shape");
   hipStream_t s = as_stream(stream);
+  const bool al = ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) | reinterpret_cast<uintptr_t>(v)) &
+                   15) == 0 && ld_q % 8 == 0 && ld_kv % 8 == 0;
+  if (dtype == DP_BF16 && al) {
+    if (dh == 16) return launch_mfma<16>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+    if (dh == 32) return launch_mfma<32>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+    if (dh == 48) return launch_mfma<48>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+  }
   if (dtype == DP_BF16)
     return dispatch<bf16_t>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, dh, s);
   return dispatch<float>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, dh, s);
