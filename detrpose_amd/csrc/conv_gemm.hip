@@ -23,6 +23,8 @@
 // Blocks are remapped so each XCD walks a contiguous range of tiles: the N-tiles that
 // share one A tile run on one XCD (L2 reuse of the gathered activations).
 #include "common.h"
+#include "conv_epilogue.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -202,71 +204,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(dp_conv_desc d, int M, i
     }
   }
 
-  // ---- epilogue: bias + act + LAB into an LDS tile, then 16-byte row writes
-  constexpr int CP = G::CP, VO = G::VO;
-  TO* Cs = reinterpret_cast<TO*>(smem_raw);
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int nl = wn * WN + j * 16 + (lane & 15);
-    const int n = n0 + nl;
-    const float bias = (d.bias && n < d.cout) ? d.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ml = wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        float v = apply_act(acc[i][j][r] + bias, d.act);
-        if (d.has_lab) v = d.lab_scale * v + d.lab_bias;
-        Cs[ml * CP + nl] = from_f32<TO>(v);
-      }
-    }
-  }
-  __syncthreads();
-
-  TO* __restrict__ out = reinterpret_cast<TO*>(d.out);
-  const TO* __restrict__ res = reinterpret_cast<const TO*>(d.res);
-  TO* __restrict__ up = reinterpret_cast<TO*>(d.up);
-  constexpr int CPR = BN / VO;  // chunks per row
-  for (int e = tid; e < BM * CPR; e += 256) {
-    const int ml = e / CPR, cc = e - ml * CPR;
-    const int m = m0 + ml;
-    const int n = n0 + cc * VO;
-    if (m >= M || n >= d.cout) continue;
-    const int b = m / hwo, rem = m - b * hwo;
-    const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
-    const int64_t pix = (int64_t)oy * d.out_w + ox;
-    const int64_t oo = (int64_t)b * d.out_bstride + pix * d.out_pstride + n;
-    Vec16<TO> v = load16(Cs + ml * CP + cc * VO);
-    if (vec_ok && n + VO <= d.cout) {
-      if (res) {
-        Vec16<TO> rv = load16(res + (int64_t)b * d.res_bstride + pix * d.res_pstride + n);
-#pragma unroll
-        for (int t = 0; t < VO; ++t) v.set(t, v.get(t) + rv.get(t));
-      }
-      store16(out + oo, v);
-      if (up) {
-        const int64_t ub = (int64_t)b * d.up_bstride + n;
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-          for (int dx = 0; dx < 2; ++dx)
-            store16(up + ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride, v);
-      }
-    } else {
-      const int nn = min(VO, d.cout - n);
-      for (int t = 0; t < nn; ++t) {
-        float x = v.get(t);
-        if (res) x += to_f32(res[(int64_t)b * d.res_bstride + pix * d.res_pstride + n + t]);
-        out[oo + t] = from_f32<TO>(x);
-        if (up) {
-          const int64_t ub = (int64_t)b * d.up_bstride + n + t;
-          for (int dy = 0; dy < 2; ++dy)
-            for (int dx = 0; dx < 2; ++dx)
-              up[ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride] = from_f32<TO>(x);
-        }
-      }
-    }
-  }
+  conv_epilogue<TO, BM, BN, WGM, TM, TN>(d, acc, smem_raw, M, m0, n0, vec_ok);
 }
 
 #ifndef DP_CONV_PD
@@ -292,6 +230,20 @@ int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   return dp_check_launch("dp_conv2d");
 }
 
+// conv_glds.hip
+}  // namespace
+int dp_conv2d_glds(const dp_conv_desc& d, hipStream_t s, int vec_ok);
+namespace {
+
+// bf16 convs run on the LDS-DMA kernel unless DETRPOSE_CONV_PATH=v2 (A/B switch)
+bool use_glds() {
+  static const int v = [] {
+    const char* e = getenv("DETRPOSE_CONV_PATH");
+    return (e && strcmp(e, "v2") == 0) ? 0 : 1;
+  }();
+  return v != 0;
+}
+
 template <typename T, typename TO>
 int dispatch(const dp_conv_desc& d, hipStream_t s) {
   constexpr int VO = 16 / sizeof(TO);
@@ -301,6 +253,9 @@ int dispatch(const dp_conv_desc& d, hipStream_t s) {
   if (d.res) vec_ok = vec_ok && (d.res_pstride % VO == 0) && (d.res_bstride % VO == 0) && al(d.res);
   if (d.up) vec_ok = vec_ok && (d.up_pstride % VO == 0) && (d.up_bstride % VO == 0) && al(d.up);
   const int M = d.batch * d.out_h * d.out_w;
+  if constexpr (sizeof(T) == 2) {
+    if (use_glds()) return dp_conv2d_glds(d, s, vec_ok);
+  }
   if constexpr (sizeof(TO) != sizeof(T)) {  // f32-output heads: few shapes
     if (d.cout <= 16) return launch<T, TO, 128, 16, BK, 4>(d, s, vec_ok);
     if (M <= 8192) return launch<T, TO, 64, 128, BK, 2>(d, s, vec_ok);
