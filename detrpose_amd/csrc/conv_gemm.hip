@@ -230,18 +230,22 @@ int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   return dp_check_launch("dp_conv2d");
 }
 
-// conv_glds.hip
+// conv_glds.hip / conv_stream.hip
 }  // namespace
 int dp_conv2d_glds(const dp_conv_desc& d, hipStream_t s, int vec_ok);
+int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok);
 namespace {
 
-// bf16 convs run on the LDS-DMA kernel unless DETRPOSE_CONV_PATH=v2 (A/B switch)
-bool use_glds() {
+// bf16 conv path: persistent LDS-DMA kernel by default; DETRPOSE_CONV_PATH=glds|v2 selects
+// the one-tile-per-block LDS-DMA kernel or the register-staged kernel (A/B switch)
+int bf16_path() {
   static const int v = [] {
     const char* e = getenv("DETRPOSE_CONV_PATH");
-    return (e && strcmp(e, "v2") == 0) ? 0 : 1;
+    if (e && strcmp(e, "v2") == 0) return 0;
+    if (e && strcmp(e, "glds") == 0) return 1;
+    return 2;
   }();
-  return v != 0;
+  return v;
 }
 
 template <typename T, typename TO>
@@ -254,7 +258,9 @@ int dispatch(const dp_conv_desc& d, hipStream_t s) {
   if (d.up) vec_ok = vec_ok && (d.up_pstride % VO == 0) && (d.up_bstride % VO == 0) && al(d.up);
   const int M = d.batch * d.out_h * d.out_w;
   if constexpr (sizeof(T) == 2) {
-    if (use_glds()) return dp_conv2d_glds(d, s, vec_ok);
+    const int path = bf16_path();
+    if (path == 2) return dp_conv2d_stream(d, s, vec_ok);
+    if (path == 1) return dp_conv2d_glds(d, s, vec_ok);
   }
   if constexpr (sizeof(TO) != sizeof(T)) {  // f32-output heads: few shapes
     if (d.cout <= 16) return launch<T, TO, 128, 16, BK, 4>(d, s, vec_ok);

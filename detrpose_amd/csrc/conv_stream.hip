@@ -1,0 +1,388 @@
+// Persistent bf16 implicit-GEMM convolution (gfx950): the default path of dp_conv2d for
+// bf16 activations. conv_glds.hip (one tile per block, LDS-staged epilogue) and
+// conv_gemm.hip (register-staged, f32 parity mode) stay as A/B and fallback paths.
+//
+// Why persistent: most DETRPose convs are short in K (1x1 with cin 64..512, 2x2 stem
+// convs) and near the HBM ridge, so a one-tile block spends most of its life in the
+// first DMA round trip and the epilogue. Here each block walks a strided list of tiles
+// and its LDS-DMA ring runs straight across tile boundaries: while tile T's epilogue
+// writes, tile T+1's first K-steps are already landing in LDS.
+//
+// Operands: the MFMA is fed weights as the A operand and gathered activations as the B
+// operand (C^T = W A^T), so each lane ends with 4 consecutive output channels of one
+// pixel per 16x16 tile; the weight rows are permuted on their way into LDS (the DMA
+// lane->row mapping is free) so that a lane's TN tiles hold 4*TN CONTIGUOUS channels.
+// The epilogue then needs no LDS: bias/act/LAB/residual in registers, 16-byte stores
+// straight from the accumulators (and the nearest-x2 copy for the FPN concat).
+//
+// LDS-DMA details as in conv_glds.hip: one `buffer_load_dwordx4 ... lds` moves 8 rows x
+// 128 B; chunks are XOR-swizzled by row so fragment reads are conflict-free; OOB offsets
+// return 0 (conv padding, K/M/N tails). Blocks are remapped so each XCD owns a
+// contiguous slice of every round of tiles (the N-tiles sharing an A tile hit one L2).
+#include "common.h"
+#include <stdlib.h>
+#include <type_traits>
+
+namespace {
+
+constexpr int OOB = 0x7fffffff;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7ffffff0, 0x00020000);
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_t(float x) {
+  if constexpr (ACT == DP_ACT_RELU) return fmaxf(x, 0.f);
+  else if constexpr (ACT == DP_ACT_SILU) return x / (1.f + __expf(-x));
+  else if constexpr (ACT == DP_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  else return x;
+}
+
+// Epilogue of one tile from registers. Lane (g = lane>>4, q = lane&15) owns pixel row
+// m = m0 + wm*WM + 16 i + q and channels nb .. nb + NPL - 1, value acc[i][j][r] is
+// channel nb + 4 j + r.
+template <int ACT, typename TO, int TM, int TN, int WM>
+__device__ __forceinline__ void stream_epilogue(const dp_conv_desc& d, const f32x4 (&acc)[TM][TN], int M, int mw,
+                                                int nb, int vec_ok) {
+  constexpr int NPL = 4 * TN;
+  constexpr int VO = 16 / (int)sizeof(TO);
+  constexpr int CPL = NPL / VO;   // 16-byte chunks per lane per pixel
+  static_assert(NPL % VO == 0, "lane channel group must be whole 16-byte chunks");
+  const int q = threadIdx.x & 15;
+  const int hwo = d.out_h * d.out_w;
+  TO* __restrict__ out = reinterpret_cast<TO*>(d.out);
+  const TO* __restrict__ res = reinterpret_cast<const TO*>(d.res);
+  TO* __restrict__ up = reinterpret_cast<TO*>(d.up);
+  const bool full = vec_ok && nb + NPL <= d.cout;
+  float bias[NPL];
+#pragma unroll
+  for (int c = 0; c < NPL; ++c) bias[c] = 0.f;
+  if (d.bias) {
+    if (nb + NPL <= d.cout) {
+#pragma unroll
+      for (int c = 0; c < NPL; c += 4) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(d.bias + nb + c);
+        bias[c] = b4[0], bias[c + 1] = b4[1], bias[c + 2] = b4[2], bias[c + 3] = b4[3];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < NPL; ++c) bias[c] = nb + c < d.cout ? d.bias[nb + c] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = mw + 16 * i + q;
+    if (m >= M || nb >= d.cout) continue;
+    const int b = m / hwo, rem = m - b * hwo;
+    const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
+    const int64_t pix = (int64_t)oy * d.out_w + ox;
+    float v[NPL];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = act_t<ACT>(acc[i][j][r] + bias[4 * j + r]);
+        if (d.has_lab) x = d.lab_scale * x + d.lab_bias;
+        v[4 * j + r] = x;
+      }
+    const int64_t oo = (int64_t)b * d.out_bstride + pix * d.out_pstride + nb;
+    if (full) {
+      Vec16<TO> ch[CPL];
+      if (res) {
+        const TO* rp = res + (int64_t)b * d.res_bstride + pix * d.res_pstride + nb;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) ch[c] = load16(rp + c * VO);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+          for (int t = 0; t < VO; ++t) ch[c].set(t, v[c * VO + t] + ch[c].get(t));
+      } else {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+          for (int t = 0; t < VO; ++t) ch[c].set(t, v[c * VO + t]);
+      }
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) store16(out + oo + c * VO, ch[c]);
+      if (up) {
+        const int64_t ub = (int64_t)b * d.up_bstride + nb;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 2; ++dx) {
+            TO* upp = up + ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) store16(upp + c * VO, ch[c]);
+          }
+      }
+    } else {
+      const int nn = min(NPL, d.cout - nb);
+#pragma unroll
+      for (int c = 0; c < NPL; ++c) {
+        if (c >= nn) break;
+        float x = v[c];
+        if (res) x += to_f32(res[(int64_t)b * d.res_bstride + pix * d.res_pstride + nb + c]);
+        const TO y = from_f32<TO>(x);
+        out[oo + c] = y;
+        if (up) {
+          const int64_t ub = (int64_t)b * d.up_bstride + nb + c;
+          for (int dy = 0; dy < 2; ++dy)
+            for (int dx = 0; dx < 2; ++dx)
+              up[ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride] = y;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int S, bool K1X1, int ACT, typename TO>
+__global__ __launch_bounds__(256) void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok) {
+  constexpr int WGN = 4 / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int NPL = 4 * TN;
+  constexpr int GA = BM / 32, GB = BN / 32;           // DMA instructions (8 rows) per wave per K-step
+  constexpr int LPS = GA + GB;
+  constexpr int STAGE = (BM + BN) * 128;
+  static_assert(BM % 32 == 0 && BN % 32 == 0 && TM >= 1 && TN >= 1 && S >= 2 && S <= 4, "tile");
+  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int G = gridDim.x;                                  // multiple of 8
+  const int L = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  if (L >= ntiles) return;
+
+  const int hwo = d.out_h * d.out_w;
+  const int r8 = lane >> 3;
+  const int chunk = (lane & 7) ^ r8;
+  const int ntap = d.kh * d.kw;
+  const int nk = d.kpad / 64;
+  const __amdgpu_buffer_rsrc_t rb_src = make_rsrc(d.weight);
+
+  // weight row landing in LDS row R: permuted so lane group g of wave column wn ends with
+  // channels wn*WN + g*NPL + [0, NPL) (see header)
+  int b_ch[GB];
+#pragma unroll
+  for (int t = 0; t < GB; ++t) {
+    const int R = (wave + 4 * t) * 8 + r8;
+    const int wq = R / WN, p16 = R % WN, j = p16 / 16, p = p16 % 16;
+    b_ch[t] = wq * WN + (p >> 2) * NPL + 4 * j + (p & 3);
+  }
+
+  // ---- issue cursor: the tile whose K-steps are being fetched
+  int itile = L, ikt = 0;
+  __amdgpu_buffer_rsrc_t ra_src;
+  int a_off[GA], a_iy0[GA], a_ix0[GA], b_off[GB];
+  auto setup = [&](int tile) {
+    const int tm = tile / nt_n, tn = tile - tm * nt_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int b_first = m0 / hwo;
+    ra_src = make_rsrc(reinterpret_cast<const bf16_t*>(d.in) + (int64_t)b_first * d.in_bstride);
+#pragma unroll
+    for (int t = 0; t < GA; ++t) {
+      const int m = m0 + (wave + 4 * t) * 8 + r8;
+      const bool ok = m < M;
+      const int mm = ok ? m : m0;
+      const int b = mm / hwo, rem = mm - b * hwo;
+      const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
+      const int iy0 = oy * d.stride - d.pad_t;
+      a_iy0[t] = ok ? iy0 : -0x4000000;
+      a_ix0[t] = ox * d.stride - d.pad_l;
+      int off = (b - b_first) * (int)d.in_bstride;
+      if (K1X1) off += (iy0 * d.in_w + a_ix0[t]) * d.in_pstride;
+      a_off[t] = ok ? off : OOB;
+    }
+#pragma unroll
+    for (int t = 0; t < GB; ++t) {
+      const int n = n0 + b_ch[t];
+      b_off[t] = n < d.cout ? n * d.kpad + chunk * 8 : OOB;
+    }
+  };
+  auto issue = [&](int kt, int stage) {
+    char* sb = smem + stage * STAGE;
+    const int kk = kt * 64 + chunk * 8;
+    if (K1X1) {
+      const bool kv = kk < d.cin;
+#pragma unroll
+      for (int t = 0; t < GA; ++t) {
+        const int o = (a_off[t] != OOB && kv) ? (a_off[t] + kk) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_src, (lds_ptr_t)(sb + BN * 128 + (wave + 4 * t) * 1024), 16, o,
+                                                 0, 0, 0);
+      }
+    } else {
+      const int tap = kk / d.cin, ci = kk - tap * d.cin;
+      const int ky = tap / d.kw, kx = tap - ky * d.kw;
+      const bool kv = tap < ntap;
+#pragma unroll
+      for (int t = 0; t < GA; ++t) {
+        const int iy = a_iy0[t] + ky, ix = a_ix0[t] + kx;
+        const bool ok = kv && (unsigned)iy < (unsigned)d.in_h && (unsigned)ix < (unsigned)d.in_w;
+        const int o = ok ? (a_off[t] + (iy * d.in_w + ix) * d.in_pstride + ci) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_src, (lds_ptr_t)(sb + BN * 128 + (wave + 4 * t) * 1024), 16, o,
+                                                 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < GB; ++t) {
+      const int o = b_off[t] != OOB ? (b_off[t] + kt * 64) * 2 : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb_src, (lds_ptr_t)(sb + (wave + 4 * t) * 1024), 16, o, 0, 0, 0);
+    }
+  };
+
+  setup(itile);
+  int issued = 0;
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p) {
+    if (itile < ntiles) {
+      issue(ikt, p);
+      ++issued;
+      if (++ikt == nk) {
+        ikt = 0;
+        itile += G;
+        if (itile < ntiles) setup(itile);
+      }
+    }
+  }
+
+  const int lr = lane & 15, lg = lane >> 4;
+  const int wrow = wn * WN + lr;   // weight fragment rows (A operand), stage offset 0
+  const int prow = wm * WM + lr;   // pixel fragment rows (B operand), stage offset BN*128
+  int c = 0;                       // K-steps consumed
+  bool dirty = false;              // epilogue stores since the last wait (vmcnt order unknown)
+  f32x4 acc[TM][TN];
+  // one K-step: wait for its stage, publish it, refill the ring, 2 x TMxTN MFMAs. The
+  // first K-step of a tile starts from a zero C operand instead of re-zeroing acc (a
+  // zeroing loop makes the register allocator pin a second set of zero AGPRs).
+  auto step = [&](auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    const int ahead = min(S - 2, issued - c - 1);
+    if (dirty || ahead <= 0) wait_vmcnt<0>();
+    else if (ahead == 1) wait_vmcnt<LPS>();
+    else wait_vmcnt<2 * LPS>();
+    dirty = false;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (itile < ntiles) {
+      issue(ikt, issued % S);
+      ++issued;
+      if (++ikt == nk) {
+        ikt = 0;
+        itile += G;
+        if (itile < ntiles) setup(itile);
+      }
+    }
+    const char* sb = smem + (c % S) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int cc = 4 * ks + lg;
+      bf16x8 wf[TN], pf[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wrow + 16 * j;
+        wf[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + ((cc ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = prow + 16 * i;
+        pf[i] = *reinterpret_cast<const bf16x8*>(sb + BN * 128 + r * 128 + ((cc ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              wf[j], pf[i], (FIRST && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
+    }
+    ++c;
+  };
+  for (int ctile = L; ctile < ntiles; ctile += G) {
+    step(std::true_type{});
+    for (int kt = 1; kt < nk; ++kt) step(std::false_type{});
+    const int tm = ctile / nt_n, tn = ctile - tm * nt_n;
+    const int mw = tm * BM + wm * WM;
+    const int nb = tn * BN + wn * WN + lg * NPL;
+    stream_epilogue<ACT, TO, TM, TN, WM>(d, acc, M, mw, nb, vec_ok);
+    dirty = true;
+  }
+  wait_vmcnt<0>();
+}
+
+#ifndef DP_STREAM_S
+#define DP_STREAM_S 2
+#endif
+
+int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+template <typename K>
+int occupancy(K kern) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256, 0) != hipSuccess || n <= 0) n = 1;
+  return n;
+}
+
+// the activation is a template parameter: a runtime switch in the epilogue costs ~20 VGPRs
+// and with them the second wave per SIMD of the 128x128 kernel
+template <int BM, int BN, int WGM, bool K1, int ACT, typename TO>
+int launch_one(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
+  constexpr int S = DP_STREAM_S;
+  auto kern = conv_stream_kernel<BM, BN, WGM, S, K1, ACT, TO>;
+  static const int occ = occupancy(kern);
+  const int M = d.batch * d.out_h * d.out_w;
+  const int mt = (M + BM - 1) / BM, nt = (d.cout + BN - 1) / BN;
+  const int ntiles = mt * nt;
+  int grid = occ * num_cus();
+  const int need = (ntiles + 7) / 8 * 8;
+  if (grid > need) grid = need;
+  grid = grid / 8 * 8;
+  if (grid < 8) grid = 8;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, d, M, nt, ntiles, vec_ok);
+  return dp_check_launch("dp_conv2d(stream)");
+}
+
+template <int BM, int BN, int WGM, bool K1, typename TO>
+int launch_act(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
+  switch (d.act) {
+    case DP_ACT_RELU: return launch_one<BM, BN, WGM, K1, DP_ACT_RELU, TO>(d, s, vec_ok);
+    case DP_ACT_SILU: return launch_one<BM, BN, WGM, K1, DP_ACT_SILU, TO>(d, s, vec_ok);
+    case DP_ACT_GELU: return launch_one<BM, BN, WGM, K1, DP_ACT_GELU, TO>(d, s, vec_ok);
+    default: return launch_one<BM, BN, WGM, K1, DP_ACT_NONE, TO>(d, s, vec_ok);
+  }
+}
+
+template <int BM, int BN, int WGM, typename TO>
+int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
+  const bool k1 = d.kh == 1 && d.kw == 1 && d.pad_t == 0 && d.pad_l == 0;
+  return k1 ? launch_act<BM, BN, WGM, true, TO>(d, s, vec_ok) : launch_act<BM, BN, WGM, false, TO>(d, s, vec_ok);
+}
+
+}  // namespace
+
+// bf16 entry used by dp_conv2d (conv_gemm.hip); vec_ok computed by the caller.
+int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
+  const int M = d.batch * d.out_h * d.out_w;
+  const bool f32o = d.out_f32 != 0;
+  if (d.cout <= 32) return f32o ? launch<128, 32, 4, float>(d, s, vec_ok) : launch<128, 32, 4, bf16_t>(d, s, vec_ok);
+  if (d.cout <= 64) return f32o ? launch<128, 64, 4, float>(d, s, vec_ok) : launch<128, 64, 4, bf16_t>(d, s, vec_ok);
+  if (M <= 8192) return f32o ? launch<64, 128, 2, float>(d, s, vec_ok) : launch<64, 128, 2, bf16_t>(d, s, vec_ok);
+  return f32o ? launch<128, 128, 2, float>(d, s, vec_ok) : launch<128, 128, 2, bf16_t>(d, s, vec_ok);
+}

@@ -182,6 +182,7 @@ class Plan:
         self.op_out = {}         # op name -> output FMap (debug / tests)
         self.op_flops = {}       # op name -> algorithmic FLOPs (conv / linear launches)
         self.op_bytes = {}       # op name -> algorithmic HBM bytes (MSDA)
+        self.conv_bytes = {}     # op name -> algorithmic HBM bytes of a dense conv/linear launch
         self.out_flat = None
         self.input = None
         self.outputs = {}
@@ -491,6 +492,12 @@ class Engine:
         plan.op_out[name] = out
         if not pc.depthwise:
             plan.op_flops[name] = 2.0 * x.B * out.H * out.W * out.C * pc.kh * pc.kw * x.C
+            # compulsory traffic: input read once, weights once, output (+residual, +x2 copy)
+            e = self.tdtype.itemsize
+            eo = 4 if out_f32 else e
+            rows = x.B * out.H * out.W
+            plan.conv_bytes[name] = (e * x.B * x.H * x.W * x.C + e * pc.cout * pc.kh * pc.kw * pc.cin
+                                     + eo * rows * out.C * (1 + (res is not None) + 4 * (up is not None)))
         else:
             plan.op_flops[name] = 2.0 * x.B * out.H * out.W * out.C * pc.kh * pc.kw
         fn = self.lib.dp_dwconv2d if pc.depthwise else self.lib.dp_conv2d

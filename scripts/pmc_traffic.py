@@ -1,0 +1,52 @@
+"""Per-forward HBM traffic by kernel family from two rocprofv3 --pmc passes
+(FETCH_SIZE and WRITE_SIZE, KB per dispatch). gfx950 correction (MI355X_MICROARCH.md
+§HBM): FETCH_SIZE counts half the bytes of 16-byte-per-lane streaming reads, so reads
+are doubled; WRITE_SIZE is exact for 16-byte stores.
+
+    python scripts/pmc_traffic.py <fetch counter_collection.csv> <write ...csv> [out.json]
+"""
+import collections
+import csv
+import json
+import sys
+
+
+def family(name):
+    for key in ("conv_glds_kernel", "conv_gemm_kernel", "dwconv_kernel", "layernorm_kernel", "attn_mfma_kernel",
+                "msda_kernel", "add_rows_kernel", "stem_conv_kernel", "maxpool_kernel", "class_max_kernel",
+                "topk_kernel", "gate_ln_kernel", "sine_embed_kernel", "lqe_kernel", "pose_refine_kernel"):
+        if key in name:
+            return "conv" if key.startswith("conv_") else key
+    return "other"
+
+
+def agg(path, counter):
+    tot = collections.defaultdict(float)
+    calls = collections.Counter()
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        f = family(r["Kernel_Name"])
+        tot[f] += float(r["Counter_Value"]) * 1024.0
+        calls[f] += 1
+    return tot, calls
+
+
+def main():
+    fetch, calls = agg(sys.argv[1], "FETCH_SIZE")
+    write, _ = agg(sys.argv[2], "WRITE_SIZE")
+    nfwd = calls["topk_kernel"]
+    out = {"forwards_profiled": nfwd, "families": {}}
+    for f in sorted(fetch, key=lambda k: -fetch[k]):
+        rd = 2.0 * fetch[f] / nfwd
+        wr = write.get(f, 0.0) / nfwd
+        out["families"][f] = {"read_bytes_corrected": rd, "write_bytes": wr, "total_bytes": rd + wr,
+                              "launches": calls[f] / nfwd}
+        print(f"{f:22s} read {rd / 1e9:7.3f} GB  write {wr / 1e9:7.3f} GB  per forward ({calls[f] / nfwd:.0f} launches)")
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -76,7 +76,10 @@ def _run_conv(pc, x_nhwc, out, dt, res=None, up=None):
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("k,s,cin,cout,H,act", [
     (1, 1, 64, 96, 13, "relu"), (3, 1, 48, 48, 17, "silu"), (3, 2, 64, 32, 20, None), (1, 1, 336, 64, 9, "relu"),
-    (3, 1, 24, 24, 11, "silu"), (1, 1, 256, 288, 7, None), (3, 1, 128, 128, 40, "gelu")])
+    (3, 1, 24, 24, 11, "silu"), (1, 1, 256, 288, 7, None), (3, 1, 128, 128, 40, "gelu"),
+    # 128x128 tiles with an N tail, and grids where each persistent block walks several tiles
+    (3, 1, 64, 160, 70, "silu"), (1, 1, 64, 128, 200, "relu"), (3, 1, 32, 64, 256, None),
+    (1, 1, 96, 32, 256, "gelu")])
 def test_conv2d(dt, k, s, cin, cout, H, act):
     torch.manual_seed(k * 100 + cin)
     pk = Packer({}, dt, torch.device("cuda"))
