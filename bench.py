@@ -97,17 +97,9 @@ def cpu_baseline(size, seconds):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        dist = None
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    from detrpose_amd import dist as dp
+    rank, world, dev = dp.init("nccl")
+    dist = dp.dist if world > 1 else None
 
     from detrpose_amd import GFLOP_PER_IMAGE, build_model
     from detrpose_amd.synthetic import load_synthetic, synthetic_images
@@ -129,7 +121,7 @@ def main():
         else:
             g.replay()
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, plan.out_flat)
+            dp.gather_outputs(plan.out_flat, world, gathered)
 
     g = None if a.no_graph else plan.graph()
     for _ in range(a.warmup):
@@ -150,10 +142,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     step_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = dp.max_over_ranks(elapsed, world, dev)
     total_imgs = a.batch * a.steps * world
     value = total_imgs / elapsed
     ms_per_step = elapsed * 1000.0 / a.steps

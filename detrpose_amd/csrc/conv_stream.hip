@@ -143,8 +143,16 @@ __device__ __forceinline__ void stream_epilogue(const dp_conv_desc& d, const f32
   }
 }
 
+// target waves per SIMD: LDS allows 2 blocks (8 waves) per CU for 128x128 S=2 and 3 for the
+// 48 KB tiles; ask the register allocator for the matching budget
+template <int BM, int BN, int S>
+constexpr int stream_waves() {
+  return (160 * 1024) / (S * (BM + BN) * 128) >= 3 ? 3 : 2;
+}
+
 template <int BM, int BN, int WGM, int S, bool K1X1, int ACT, typename TO>
-__global__ __launch_bounds__(256) void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(stream_waves<BM, BN, S>())))
+void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok) {
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -171,18 +179,16 @@ __global__ __launch_bounds__(256) void conv_stream_kernel(dp_conv_desc d, int M,
 
   // weight row landing in LDS row R: permuted so lane group g of wave column wn ends with
   // channels wn*WN + g*NPL + [0, NPL) (see header)
-  int b_ch[GB];
-#pragma unroll
-  for (int t = 0; t < GB; ++t) {
+  auto b_chan = [&](int t) {
     const int R = (wave + 4 * t) * 8 + r8;
     const int wq = R / WN, p16 = R % WN, j = p16 / 16, p = p16 % 16;
-    b_ch[t] = wq * WN + (p >> 2) * NPL + 4 * j + (p & 3);
-  }
+    return wq * WN + (p >> 2) * NPL + 4 * j + (p & 3);
+  };
 
   // ---- issue cursor: the tile whose K-steps are being fetched
   int itile = L, ikt = 0;
   __amdgpu_buffer_rsrc_t ra_src;
-  int a_off[GA], a_iy0[GA], a_ix0[GA], b_off[GB];
+  int a_off[GA], a_yx[GA], b_off[GB];   // a_yx: (iy0 << 16) | (ix0 & 0xffff)
   auto setup = [&](int tile) {
     const int tm = tile / nt_n, tn = tile - tm * nt_n;
     const int m0 = tm * BM, n0 = tn * BN;
@@ -195,16 +201,15 @@ __global__ __launch_bounds__(256) void conv_stream_kernel(dp_conv_desc d, int M,
       const int mm = ok ? m : m0;
       const int b = mm / hwo, rem = mm - b * hwo;
       const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
-      const int iy0 = oy * d.stride - d.pad_t;
-      a_iy0[t] = ok ? iy0 : -0x4000000;
-      a_ix0[t] = ox * d.stride - d.pad_l;
+      const int iy0 = oy * d.stride - d.pad_t, ix0 = ox * d.stride - d.pad_l;
+      a_yx[t] = (iy0 << 16) | (ix0 & 0xffff);
       int off = (b - b_first) * (int)d.in_bstride;
-      if (K1X1) off += (iy0 * d.in_w + a_ix0[t]) * d.in_pstride;
+      if (K1X1) off += (iy0 * d.in_w + ix0) * d.in_pstride;
       a_off[t] = ok ? off : OOB;
     }
 #pragma unroll
     for (int t = 0; t < GB; ++t) {
-      const int n = n0 + b_ch[t];
+      const int n = n0 + b_chan(t);
       b_off[t] = n < d.cout ? n * d.kpad + chunk * 8 : OOB;
     }
   };
@@ -225,8 +230,8 @@ __global__ __launch_bounds__(256) void conv_stream_kernel(dp_conv_desc d, int M,
       const bool kv = tap < ntap;
 #pragma unroll
       for (int t = 0; t < GA; ++t) {
-        const int iy = a_iy0[t] + ky, ix = a_ix0[t] + kx;
-        const bool ok = kv && (unsigned)iy < (unsigned)d.in_h && (unsigned)ix < (unsigned)d.in_w;
+        const int iy = (a_yx[t] >> 16) + ky, ix = (int)(short)(a_yx[t] & 0xffff) + kx;
+        const bool ok = kv && a_off[t] != OOB && (unsigned)iy < (unsigned)d.in_h && (unsigned)ix < (unsigned)d.in_w;
         const int o = ok ? (a_off[t] + (iy * d.in_w + ix) * d.in_pstride + ci) * 2 : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_src, (lds_ptr_t)(sb + BN * 128 + (wave + 4 * t) * 1024), 16, o,
                                                  0, 0, 0);

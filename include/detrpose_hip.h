@@ -125,7 +125,7 @@ int dp_msda(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /
 
 /* Per-row top-k of f32 scores, sorted descending, ties to the lower index:
  * torch.topk over the two-stage class score (transformer.py:1240) and in PostProcess
- * (postprocesses.py:19).  k <= 256, n <= 65536. idx is int64. */
+ * (postprocesses.py:19).  k <= 256, n <= 16384. idx is int64. */
 int dp_topk(const float* x, int32_t rows, int32_t n, int32_t ld, int32_t k,
             float* out_val, int64_t* out_idx, void* stream);
 
