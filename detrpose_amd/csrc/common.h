@@ -82,10 +82,12 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// row r < 2^31 (every launch checks its row count): 32-bit division, 64-bit offsets
 __device__ __forceinline__ int64_t rowmap_off(const dp_rowmap& m, int64_t r) {
-  int64_t g = r / m.group;
-  int64_t i = r - g * m.group;
-  return m.base + g * m.stride_g + i * m.stride_r;
+  const unsigned ri = (unsigned)r, gs = (unsigned)m.group;
+  const unsigned g = ri / gs;
+  const unsigned i = ri - g * gs;
+  return m.base + (int64_t)g * m.stride_g + (int64_t)i * m.stride_r;
 }
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

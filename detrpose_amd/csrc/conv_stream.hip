@@ -27,15 +27,35 @@ namespace {
 
 constexpr int OOB = 0x7fffffff;
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7ffffff0, 0x00020000);
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Buffer resource words (base, no stride, 2 GB range, gfx950 raw-buffer flags) in SGPRs.
+__device__ __forceinline__ i32x4 make_rsrc(const void* base) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffffu));
+  r[2] = 0x7ffffff0;
+  r[3] = 0x00020000;
+  return r;
 }
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
+// 16 bytes per lane HBM/L2 -> LDS (M0 = wave-uniform LDS byte address; lane L lands at
+// M0 + 16 L). Inline asm rather than the builtin: the compiler would otherwise treat every
+// later ds_read as a possible alias of the DMA and insert s_waitcnt vmcnt(0), draining the
+// ring; completion is tracked by hand (wait_vmcnt + barrier) below.
+__device__ __forceinline__ void dma16(const i32x4& rsrc, const char* lds, int voff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(rsrc)
+               : "memory");
+}
 
+// s_waitcnt vmcnt(N) (expcnt/lgkmcnt untouched) as the builtin, so the compiler's own
+// wait insertion sees it and does not add a second vmcnt(0) for its epilogue loads/stores.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xf << 8));
 }
 
 template <int ACT>
@@ -143,25 +163,34 @@ __device__ __forceinline__ void stream_epilogue(const dp_conv_desc& d, const f32
   }
 }
 
-// target waves per SIMD: LDS allows 2 blocks (8 waves) per CU for 128x128 S=2 and 3 for the
-// 48 KB tiles; ask the register allocator for the matching budget
-template <int BM, int BN, int S>
+// target waves per SIMD = (blocks per CU the LDS allows) x (waves per block) / 4; ask the
+// register allocator for the matching budget
+template <int BM, int BN, int SA, int NW>
 constexpr int stream_waves() {
-  return (160 * 1024) / (S * (BM + BN) * 128) >= 3 ? 3 : 2;
+  const int blocks = (160 * 1024) / ((SA * BM + 2 * BN) * 128);
+  const int w = blocks * NW / 4;
+  return w >= 3 ? 3 : (w >= 2 ? 2 : 1);
 }
 
-template <int BM, int BN, int WGM, int S, bool K1X1, int ACT, typename TO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(stream_waves<BM, BN, S>())))
+// NW = waves per block (4, or 8 for the 256-row tiles of the large GEMMs).
+// SA = depth of the activation (A) ring; the weight (B) ring is 2 deep. Weights are a few
+// hundred KB and stay in L2, activations stream from HBM: the extra A stages are the bytes
+// in flight that hide HBM latency (Little's law), where a deeper B ring would only burn LDS.
+template <int BM, int BN, int WGM, int NW, int SA, bool K1X1, int ACT, typename TO>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(stream_waves<BM, BN, SA, NW>())))
 void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok) {
-  constexpr int WGN = 4 / WGM;
+  constexpr int WGN = NW / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int NPL = 4 * TN;
-  constexpr int GA = BM / 32, GB = BN / 32;           // DMA instructions (8 rows) per wave per K-step
-  constexpr int LPS = GA + GB;
-  constexpr int STAGE = (BM + BN) * 128;
-  static_assert(BM % 32 == 0 && BN % 32 == 0 && TM >= 1 && TN >= 1 && S >= 2 && S <= 4, "tile");
-  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
+  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);   // DMA instructions (8 rows) per wave per K-step
+  constexpr int SB = 2;
+  constexpr int BBYTES = BN * 128, ABYTES = BM * 128;     // one K-step of B / A
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0 && WGM * WGN == NW && TM >= 1 && TN >= 1 && SA >= 2 &&
+                    SA <= 4, "tile");
+  // LDS: [B ring: SB x BN rows][A ring: SA x BM rows], rows of 128 B (one 64-wide K-step)
+  __shared__ __attribute__((aligned(1024))) char smem[SB * BBYTES + SA * ABYTES];
+  char* const sa_base = smem + SB * BBYTES;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -175,28 +204,31 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
   const int chunk = (lane & 7) ^ r8;
   const int ntap = d.kh * d.kw;
   const int nk = d.kpad / 64;
-  const __amdgpu_buffer_rsrc_t rb_src = make_rsrc(d.weight);
+  const int total = ((ntiles - 1 - L) / G + 1) * nk;       // K-steps this block runs
+  const i32x4 rb_src = make_rsrc(d.weight);
 
   // weight row landing in LDS row R: permuted so lane group g of wave column wn ends with
   // channels wn*WN + g*NPL + [0, NPL) (see header)
   auto b_chan = [&](int t) {
-    const int R = (wave + 4 * t) * 8 + r8;
+    const int R = (wave + NW * t) * 8 + r8;
     const int wq = R / WN, p16 = R % WN, j = p16 / 16, p = p16 % 16;
     return wq * WN + (p >> 2) * NPL + 4 * j + (p & 3);
   };
 
-  // ---- issue cursor: the tile whose K-steps are being fetched
-  int itile = L, ikt = 0;
-  __amdgpu_buffer_rsrc_t ra_src;
+  // ---- A issue cursor (activations) and B issue cursor (weights) run SA-1 and 1 K-steps
+  // ahead of the consumer, each across tile boundaries
+  int a_tile = L, a_kt = 0, a_n = 0;
+  int b_tile = L, b_kt = 0, b_n = 0;
+  i32x4 ra_src;
   int a_off[GA], a_yx[GA], b_off[GB];   // a_yx: (iy0 << 16) | (ix0 & 0xffff)
-  auto setup = [&](int tile) {
-    const int tm = tile / nt_n, tn = tile - tm * nt_n;
-    const int m0 = tm * BM, n0 = tn * BN;
+  auto setup_a = [&](int tile) {
+    const int tm = tile / nt_n;
+    const int m0 = tm * BM;
     const int b_first = m0 / hwo;
     ra_src = make_rsrc(reinterpret_cast<const bf16_t*>(d.in) + (int64_t)b_first * d.in_bstride);
 #pragma unroll
     for (int t = 0; t < GA; ++t) {
-      const int m = m0 + (wave + 4 * t) * 8 + r8;
+      const int m = m0 + (wave + NW * t) * 8 + r8;
       const bool ok = m < M;
       const int mm = ok ? m : m0;
       const int b = mm / hwo, rem = mm - b * hwo;
@@ -207,22 +239,25 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
       if (K1X1) off += (iy0 * d.in_w + ix0) * d.in_pstride;
       a_off[t] = ok ? off : OOB;
     }
+  };
+  auto setup_b = [&](int tile) {
+    const int tm = tile / nt_n, tn = tile - tm * nt_n;
+    const int n0 = tn * BN;
 #pragma unroll
     for (int t = 0; t < GB; ++t) {
       const int n = n0 + b_chan(t);
       b_off[t] = n < d.cout ? n * d.kpad + chunk * 8 : OOB;
     }
   };
-  auto issue = [&](int kt, int stage) {
-    char* sb = smem + stage * STAGE;
-    const int kk = kt * 64 + chunk * 8;
+  auto issue_a = [&]() {
+    char* sb = sa_base + (a_n % SA) * ABYTES;
+    const int kk = a_kt * 64 + chunk * 8;
     if (K1X1) {
       const bool kv = kk < d.cin;
 #pragma unroll
       for (int t = 0; t < GA; ++t) {
         const int o = (a_off[t] != OOB && kv) ? (a_off[t] + kk) * 2 : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_src, (lds_ptr_t)(sb + BN * 128 + (wave + 4 * t) * 1024), 16, o,
-                                                 0, 0, 0);
+        dma16(ra_src, sb + (wave + NW * t) * 1024, o);
       }
     } else {
       const int tap = kk / d.cin, ci = kk - tap * d.cin;
@@ -233,61 +268,65 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
         const int iy = (a_yx[t] >> 16) + ky, ix = (int)(short)(a_yx[t] & 0xffff) + kx;
         const bool ok = kv && a_off[t] != OOB && (unsigned)iy < (unsigned)d.in_h && (unsigned)ix < (unsigned)d.in_w;
         const int o = ok ? (a_off[t] + (iy * d.in_w + ix) * d.in_pstride + ci) * 2 : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_src, (lds_ptr_t)(sb + BN * 128 + (wave + 4 * t) * 1024), 16, o,
-                                                 0, 0, 0);
+        dma16(ra_src, sb + (wave + NW * t) * 1024, o);
       }
     }
+    ++a_n;
+    if (++a_kt == nk) {
+      a_kt = 0;
+      a_tile += G;
+      if (a_tile < ntiles) setup_a(a_tile);
+    }
+  };
+  auto issue_b = [&]() {
+    char* sb = smem + (b_n % SB) * BBYTES;
 #pragma unroll
     for (int t = 0; t < GB; ++t) {
-      const int o = b_off[t] != OOB ? (b_off[t] + kt * 64) * 2 : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb_src, (lds_ptr_t)(sb + (wave + 4 * t) * 1024), 16, o, 0, 0, 0);
+      const int o = b_off[t] != OOB ? (b_off[t] + b_kt * 64) * 2 : OOB;
+      dma16(rb_src, sb + (wave + NW * t) * 1024, o);
+    }
+    ++b_n;
+    if (++b_kt == nk) {
+      b_kt = 0;
+      b_tile += G;
+      if (b_tile < ntiles) setup_b(b_tile);
     }
   };
 
-  setup(itile);
-  int issued = 0;
+  // prologue: B(0), then A(0 .. SA-2). Steady state, per consumed K-step c: B(c+1), A(c+SA-1).
+  setup_a(a_tile);
+  setup_b(b_tile);
+  issue_b();
 #pragma unroll
-  for (int p = 0; p < S - 1; ++p) {
-    if (itile < ntiles) {
-      issue(ikt, p);
-      ++issued;
-      if (++ikt == nk) {
-        ikt = 0;
-        itile += G;
-        if (itile < ntiles) setup(itile);
-      }
-    }
-  }
+  for (int p = 0; p < SA - 1; ++p)
+    if (a_n < total) issue_a();
 
   const int lr = lane & 15, lg = lane >> 4;
-  const int wrow = wn * WN + lr;   // weight fragment rows (A operand), stage offset 0
-  const int prow = wm * WM + lr;   // pixel fragment rows (B operand), stage offset BN*128
+  const int wrow = wn * WN + lr;   // weight fragment rows (MFMA A operand)
+  const int prow = wm * WM + lr;   // pixel fragment rows (MFMA B operand)
   int c = 0;                       // K-steps consumed
-  bool dirty = false;              // epilogue stores since the last wait (vmcnt order unknown)
+  bool dirty = false;              // epilogue stores since the last wait (their vmcnt order vs loads is unknown)
   f32x4 acc[TM][TN];
-  // one K-step: wait for its stage, publish it, refill the ring, 2 x TMxTN MFMAs. The
-  // first K-step of a tile starts from a zero C operand instead of re-zeroing acc (a
+  // one K-step: wait for A(c) and B(c), publish them, refill both rings, 2 x TMxTN MFMAs.
+  // Waits: the loads complete in order, so it suffices to count the A groups issued after
+  // both A(c) and B(c): at c = 0 the prologue's A(1 .. SA-2), later the single A(c+SA-2)
+  // issued right after B(c) (for SA = 2 A(c) itself is the youngest: wait for all).
+  // The first K-step of a tile starts from a zero C operand instead of re-zeroing acc (a
   // zeroing loop makes the register allocator pin a second set of zero AGPRs).
   auto step = [&](auto first_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
-    const int ahead = min(S - 2, issued - c - 1);
-    if (dirty || ahead <= 0) wait_vmcnt<0>();
-    else if (ahead == 1) wait_vmcnt<LPS>();
-    else wait_vmcnt<2 * LPS>();
+    const int younger = SA == 2 ? 0 : (c == 0 ? min(SA - 2, a_n - 1) : (a_n > c + SA - 2 ? 1 : 0));
+    if (dirty || younger <= 0) wait_vmcnt<0>();
+    else if (younger == 1) wait_vmcnt<GA>();
+    else wait_vmcnt<2 * GA>();
     dirty = false;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (itile < ntiles) {
-      issue(ikt, issued % S);
-      ++issued;
-      if (++ikt == nk) {
-        ikt = 0;
-        itile += G;
-        if (itile < ntiles) setup(itile);
-      }
-    }
-    const char* sb = smem + (c % S) * STAGE;
+    if (b_n < total) issue_b();
+    if (a_n < total) issue_a();
+    const char* sbw = smem + (c % SB) * BBYTES;
+    const char* sbp = sa_base + (c % SA) * ABYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int cc = 4 * ks + lg;
@@ -295,12 +334,12 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wrow + 16 * j;
-        wf[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + ((cc ^ (r & 7)) << 4));
+        wf[j] = *reinterpret_cast<const bf16x8*>(sbw + r * 128 + ((cc ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = prow + 16 * i;
-        pf[i] = *reinterpret_cast<const bf16x8*>(sb + BN * 128 + r * 128 + ((cc ^ (r & 7)) << 4));
+        pf[i] = *reinterpret_cast<const bf16x8*>(sbp + r * 128 + ((cc ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -323,8 +362,8 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
   wait_vmcnt<0>();
 }
 
-#ifndef DP_STREAM_S
-#define DP_STREAM_S 2
+#ifndef DP_STREAM_SA
+#define DP_STREAM_SA 2
 #endif
 
 int num_cus() {
@@ -339,19 +378,38 @@ int num_cus() {
 }
 
 template <typename K>
-int occupancy(K kern) {
+int occupancy(K kern, int threads) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256, 0) != hipSuccess || n <= 0) n = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, 0) != hipSuccess || n <= 0) n = 1;
   return n;
 }
 
 // the activation is a template parameter: a runtime switch in the epilogue costs ~20 VGPRs
 // and with them the second wave per SIMD of the 128x128 kernel
-template <int BM, int BN, int WGM, bool K1, int ACT, typename TO>
+// A-ring depth: DP_STREAM_SA where it keeps the blocks per CU of a 2-deep ring (the narrow
+// tiles get their bytes in flight from more resident blocks instead)
+template <int BM, int BN, int NW>
+constexpr int ring_a() {
+  constexpr int want = DP_STREAM_SA;
+  constexpr int blocks2 = (160 * 1024) / ((2 * BM + 2 * BN) * 128);
+  constexpr int blocksw = (160 * 1024) / ((want * BM + 2 * BN) * 128);
+  return (blocksw >= 1 && blocksw >= blocks2) ? want : 2;
+}
+
+template <int BM, int BN, int WGM, int NW, bool K1, int ACT, typename TO>
 int launch_one(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
-  constexpr int S = DP_STREAM_S;
-  auto kern = conv_stream_kernel<BM, BN, WGM, S, K1, ACT, TO>;
-  static const int occ = occupancy(kern);
+  constexpr int SA = ring_a<BM, BN, NW>();
+  auto kern = conv_stream_kernel<BM, BN, WGM, NW, SA, K1, ACT, TO>;
+  static const int occ = [&] {
+    const int o = occupancy(kern, NW * 64);
+    if (getenv("DETRPOSE_CONV_DEBUG")) {
+      hipFuncAttributes fa{};
+      (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern));
+      fprintf(stderr, "conv_stream BM=%d BN=%d NW=%d SA=%d K1=%d act=%d: occupancy %d blocks/CU, regs %d, lds %zu\n", BM,
+              BN, NW, SA, (int)K1, ACT, o, fa.numRegs, fa.sharedSizeBytes);
+    }
+    return o;
+  }();
   const int M = d.batch * d.out_h * d.out_w;
   const int mt = (M + BM - 1) / BM, nt = (d.cout + BN - 1) / BN;
   const int ntiles = mt * nt;
@@ -360,25 +418,29 @@ int launch_one(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   if (grid > need) grid = need;
   grid = grid / 8 * 8;
   if (grid < 8) grid = 8;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, d, M, nt, ntiles, vec_ok);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), 0, s, d, M, nt, ntiles, vec_ok);
   return dp_check_launch("dp_conv2d(stream)");
 }
 
-template <int BM, int BN, int WGM, bool K1, typename TO>
+template <int BM, int BN, int WGM, int NW, bool K1, typename TO>
 int launch_act(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   switch (d.act) {
-    case DP_ACT_RELU: return launch_one<BM, BN, WGM, K1, DP_ACT_RELU, TO>(d, s, vec_ok);
-    case DP_ACT_SILU: return launch_one<BM, BN, WGM, K1, DP_ACT_SILU, TO>(d, s, vec_ok);
-    case DP_ACT_GELU: return launch_one<BM, BN, WGM, K1, DP_ACT_GELU, TO>(d, s, vec_ok);
-    default: return launch_one<BM, BN, WGM, K1, DP_ACT_NONE, TO>(d, s, vec_ok);
+    case DP_ACT_RELU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_RELU, TO>(d, s, vec_ok);
+    case DP_ACT_SILU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_SILU, TO>(d, s, vec_ok);
+    case DP_ACT_GELU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_GELU, TO>(d, s, vec_ok);
+    default: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_NONE, TO>(d, s, vec_ok);
   }
 }
 
-template <int BM, int BN, int WGM, typename TO>
+template <int BM, int BN, int WGM, typename TO, int NW = 4>
 int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   const bool k1 = d.kh == 1 && d.kw == 1 && d.pad_t == 0 && d.pad_l == 0;
-  return k1 ? launch_act<BM, BN, WGM, true, TO>(d, s, vec_ok) : launch_act<BM, BN, WGM, false, TO>(d, s, vec_ok);
+  return k1 ? launch_act<BM, BN, WGM, NW, true, TO>(d, s, vec_ok) : launch_act<BM, BN, WGM, NW, false, TO>(d, s, vec_ok);
 }
+
+#ifndef DP_BIG_TILES
+#define DP_BIG_TILES 1
+#endif
 
 }  // namespace
 
@@ -389,5 +451,11 @@ int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   if (d.cout <= 32) return f32o ? launch<128, 32, 4, float>(d, s, vec_ok) : launch<128, 32, 4, bf16_t>(d, s, vec_ok);
   if (d.cout <= 64) return f32o ? launch<128, 64, 4, float>(d, s, vec_ok) : launch<128, 64, 4, bf16_t>(d, s, vec_ok);
   if (M <= 8192) return f32o ? launch<64, 128, 2, float>(d, s, vec_ok) : launch<64, 128, 2, bf16_t>(d, s, vec_ok);
-  return f32o ? launch<128, 128, 2, float>(d, s, vec_ok) : launch<128, 128, 2, bf16_t>(d, s, vec_ok);
+  if (f32o) return launch<128, 128, 2, float>(d, s, vec_ok);
+  // large GEMMs: 256-row tiles with 8 waves halve the LDS-DMA bytes per MFMA flop
+  if (DP_BIG_TILES && M >= 32768 && d.kpad >= 256) {
+    if (d.cout > 128) return launch<256, 256, 2, bf16_t, 8>(d, s, vec_ok);
+    if (d.kpad >= 512) return launch<256, 128, 4, bf16_t, 8>(d, s, vec_ok);
+  }
+  return launch<128, 128, 2, bf16_t>(d, s, vec_ok);
 }

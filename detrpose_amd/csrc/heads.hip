@@ -137,22 +137,31 @@ __global__ __launch_bounds__(TOPK_THREADS) void topk_kernel(const float* __restr
 }
 
 // ------------------------------------------------------------------ two-stage
-template <typename T>
+// G lanes per row (64/G rows per wave), 16-byte chunks of the row per lane, weights f32.
+template <typename T, int G>
 __global__ __launch_bounds__(256) void class_max_kernel(const T* __restrict__ x, int rows, int c,
                                                         const float* __restrict__ w, const float* __restrict__ b,
                                                         int ncls, float* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const T* xr = x + r * c;
+  constexpr int VEC = Vec16<T>::N;
+  const int lane = threadIdx.x & 63, sub = lane % G;
+  const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / G) + lane / G;
+  const bool ok = r < rows;
+  const int nch = c / VEC;
+  const T* xr = x + (int64_t)(ok ? r : 0) * c;
   float best = -INFINITY;
   for (int j = 0; j < ncls; ++j) {
     float s = 0.f;
-    for (int i = lane; i < c; i += 64) s = fmaf(to_f32(xr[i]), w[j * c + i], s);
-    s = wave_sum(s) + b[j];
-    best = fmaxf(best, s);
+    for (int ch = sub; ch < nch; ch += G) {
+      const Vec16<T> v = load16(xr + ch * VEC);
+      const float* wj = w + j * c + ch * VEC;
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) s = fmaf(v.get(t), wj[t], s);
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    best = fmaxf(best, s + b[j]);
   }
-  if (lane == 0) out[r] = best;
+  if (ok && sub == 0) out[r] = best;
 }
 
 template <typename T>
@@ -200,21 +209,38 @@ __global__ void broadcast_kernel(const uint8_t* __restrict__ src, int64_t bytes,
   }
 }
 
+// one thread = 8 consecutive channels of one (row, keypoint): the chunk lies in one half
+// (pos_y | pos_x, c/2 % 8 == 0), so one coordinate; 16-byte (bf16) / 2x16-byte (f32) store
 template <typename T>
 __global__ __launch_bounds__(256) void sine_embed_kernel(const float* __restrict__ ref, int rows, int nkp, int c,
                                                          const float* __restrict__ dim_t, T* __restrict__ out) {
-  int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)rows * nkp * c) return;
-  const int64_t rk = gid / c;
-  const int ch = (int)(gid - rk * c);
-  const int64_t r = rk / nkp;
-  const int kp = (int)(rk - r * nkp);
+  const unsigned nch = (unsigned)(c >> 3);
+  const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (unsigned)(rows * nkp) * nch) return;
+  const unsigned rk = gid / nch;
+  const int ch0 = (int)(gid - rk * nch) * 8;
+  const unsigned r = rk / (unsigned)nkp;
+  const int kp = (int)(rk - r * (unsigned)nkp);
   const int half = c >> 1;
-  const float* p = ref + (r * (nkp + 1) + 1 + kp) * 2;
-  const int i = ch < half ? ch : ch - half;
-  const float coord = ch < half ? p[1] : p[0];  // cat(pos_y, pos_x)
-  const float v = coord * 6.283185307179586f / dim_t[i];
-  out[gid] = from_f32<T>((i & 1) ? cosf(v) : sinf(v));
+  const float* p = ref + ((int64_t)r * (nkp + 1) + 1 + kp) * 2;
+  const bool ylow = ch0 < half;
+  const int i0 = ylow ? ch0 : ch0 - half;
+  const float coord = (ylow ? p[1] : p[0]) * 6.283185307179586f;  // cat(pos_y, pos_x)
+  float v[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const float a = coord / dim_t[i0 + t];
+    v[t] = ((i0 + t) & 1) ? __cosf(a) : __sinf(a);
+  }
+  T* o = out + (int64_t)rk * c + ch0;
+  constexpr int V = Vec16<T>::N;
+#pragma unroll
+  for (int h0 = 0; h0 < 8; h0 += V) {
+    Vec16<T> q;
+#pragma unroll
+    for (int t = 0; t < V; ++t) q.set(t, v[h0 + t]);
+    store16(o + h0, q);
+  }
 }
 
 // ------------------------------------------------------------------ f32 heads
@@ -292,45 +318,58 @@ __global__ void pre_pose_kernel(const float* __restrict__ pre, const float* __re
   out[gid] = 1.f / (1.f + expf(-z));
 }
 
-template <typename T>
+// one wave per (b, q, kp); lane owns E = c/64 consecutive channels (static E: the
+// per-lane arrays stay in registers)
+template <typename T, int E>
 __global__ __launch_bounds__(256) void lqe_kernel(const T* __restrict__ feat, int64_t fbs, int h, int w, int c,
                                                   const float* __restrict__ kps, int nq, int nkp, int total,
                                                   float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // (b, q, kp)
   if (g >= total) return;
-  const int b = g / (nq * nkp);
+  const int b = (unsigned)g / (unsigned)(nq * nkp);
   const float x = kps[2 * (int64_t)g] * w - 0.5f, y = kps[2 * (int64_t)g + 1] * h - 0.5f;
   const float fx = floorf(x), fy = floorf(y);
   const int x0 = (int)fx, y0 = (int)fy;
   const float ax = x - fx, ay = y - fy;
   const float wt[4] = {(1.f - ax) * (1.f - ay), ax * (1.f - ay), (1.f - ax) * ay, ax * ay};
-  const int e = c >> 6;  // channels per lane (c % 64 == 0)
-  float v[8];
-  for (int t = 0; t < e; ++t) v[t] = 0.f;
-  const T* fb = feat + (int64_t)b * fbs + lane * e;
+  float v[E];
+#pragma unroll
+  for (int t = 0; t < E; ++t) v[t] = 0.f;
+  const T* fb = feat + (int64_t)b * fbs + lane * E;
+#pragma unroll
   for (int cn = 0; cn < 4; ++cn) {
     const int xi = x0 + (cn & 1), yi = y0 + (cn >> 1);
     if (xi < 0 || xi >= w || yi < 0 || yi >= h) continue;
     const T* p = fb + ((int64_t)yi * w + xi) * c;
-    for (int t = 0; t < e; ++t) v[t] = fmaf(wt[cn], to_f32(p[t]), v[t]);
+    T q[E];
+    if constexpr (E * sizeof(T) == 8) *reinterpret_cast<uint2*>(q) = *reinterpret_cast<const uint2*>(p);
+    else if constexpr (E * sizeof(T) == 16) *reinterpret_cast<uint4*>(q) = *reinterpret_cast<const uint4*>(p);
+    else {
+#pragma unroll
+      for (int t = 0; t < E; ++t) q[t] = p[t];
+    }
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] = fmaf(wt[cn], to_f32(q[t]), v[t]);
   }
-  // top-4 over all c channels of the wave
+  // top-4 over all c channels of the wave: 4 rounds of (lane max of the unused values,
+  // wave max, the lowest winning lane retires its element)
   float top[4];
-  bool used[8];
-  for (int t = 0; t < e; ++t) used[t] = false;
+  unsigned used = 0;
+#pragma unroll
   for (int s = 0; s < 4; ++s) {
     float lm = -INFINITY;
     int li = -1;
-    for (int t = 0; t < e; ++t)
-      if (!used[t] && v[t] > lm) {
+#pragma unroll
+    for (int t = 0; t < E; ++t)
+      if (!(used & (1u << t)) && v[t] > lm) {
         lm = v[t];
         li = t;
       }
     const float wm = wave_max(lm);
     const unsigned long long ball = __ballot(lm == wm && li >= 0);
     const int winner = __ffsll((long long)ball) - 1;
-    if (lane == winner) used[li] = true;
+    if (lane == winner) used |= 1u << li;
     top[s] = wm;
   }
   if (lane == 0) {
@@ -382,12 +421,20 @@ extern "C" int dp_topk(const float* x, int32_t rows, int32_t n, int32_t ld, int3
 extern "C" int dp_class_max(const void* x, int32_t rows, int32_t c, const float* w, const float* b, int32_t nclass,
                             float* out, int32_t dtype, void* stream) {
   DP_REQUIRE(x && w && b && out && nclass > 0, "dp_class_max: bad args");
-  if (dtype == DP_BF16)
-    hipLaunchKernelGGL(class_max_kernel<bf16_t>, dim3(nblk(rows, 4)), dim3(256), 0, as_stream(stream),
-                       (const bf16_t*)x, rows, c, w, b, nclass, out);
-  else
-    hipLaunchKernelGGL(class_max_kernel<float>, dim3(nblk(rows, 4)), dim3(256), 0, as_stream(stream),
-                       (const float*)x, rows, c, w, b, nclass, out);
+  const int vec = dtype == DP_BF16 ? 8 : 4;
+  DP_REQUIRE(c % vec == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
+             "dp_class_max: rows must be 16-byte aligned (c=%d)", c);
+  const int nch = c / vec;
+  const int g = nch <= 16 ? 16 : (nch <= 32 ? 32 : 64);
+  const int rpb = 4 * (64 / g);   // rows per 256-thread block
+  const dim3 grid((unsigned)((rows + rpb - 1) / rpb));
+#define DP_CM(T_, G_) hipLaunchKernelGGL((class_max_kernel<T_, G_>), grid, dim3(256), 0, as_stream(stream), (const T_*)x, rows, c, w, b, nclass, out)
+  if (dtype == DP_BF16) {
+    if (g == 16) DP_CM(bf16_t, 16); else if (g == 32) DP_CM(bf16_t, 32); else DP_CM(bf16_t, 64);
+  } else {
+    if (g == 16) DP_CM(float, 16); else if (g == 32) DP_CM(float, 32); else DP_CM(float, 64);
+  }
+#undef DP_CM
   return dp_check_launch("dp_class_max");
 }
 
@@ -422,8 +469,10 @@ extern "C" int dp_broadcast(const void* src, int64_t bytes, void* dst, int32_t c
 
 extern "C" int dp_sine_embed(const float* ref, int32_t rows, int32_t nkp, int32_t c, const float* dim_t, void* out,
                              int32_t dtype, void* stream) {
-  DP_REQUIRE(c % 2 == 0, "dp_sine_embed: c must be even");
-  const int64_t total = (int64_t)rows * nkp * c;
+  DP_REQUIRE(c % 16 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
+             "dp_sine_embed: c=%d must be a multiple of 16, out 16-byte aligned", c);
+  const int64_t total = (int64_t)rows * nkp * (c / 8);
+  DP_REQUIRE(total < (1ll << 31), "dp_sine_embed: too many rows");
   if (dtype == DP_BF16)
     hipLaunchKernelGGL(sine_embed_kernel<bf16_t>, dim3(nblk(total)), dim3(256), 0, as_stream(stream), ref, rows, nkp,
                        c, dim_t, (bf16_t*)out);
@@ -466,12 +515,20 @@ extern "C" int dp_lqe_stats(const void* feat, int64_t feat_bstride, int32_t h, i
                             int32_t batch, int32_t nq, int32_t nkp, float* out, int32_t dtype, void* stream) {
   DP_REQUIRE(c % 64 == 0 && c <= 512, "dp_lqe_stats: c=%d must be a multiple of 64, <= 512", c);
   const int total = batch * nq * nkp;
-  if (dtype == DP_BF16)
-    hipLaunchKernelGGL(lqe_kernel<bf16_t>, dim3(nblk(total, 4)), dim3(256), 0, as_stream(stream), (const bf16_t*)feat,
-                       feat_bstride, h, w, c, kps, nq, nkp, total, out);
-  else
-    hipLaunchKernelGGL(lqe_kernel<float>, dim3(nblk(total, 4)), dim3(256), 0, as_stream(stream), (const float*)feat,
-                       feat_bstride, h, w, c, kps, nq, nkp, total, out);
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(feat) & 15) == 0, "dp_lqe_stats: feat must be 16-byte aligned");
+#define DP_LQE(T_, E_)                                                                                          \
+  case E_:                                                                                                      \
+    hipLaunchKernelGGL((lqe_kernel<T_, E_>), dim3(nblk(total, 4)), dim3(256), 0, as_stream(stream),             \
+                       (const T_*)feat, feat_bstride, h, w, c, kps, nq, nkp, total, out);                       \
+    break;
+  if (dtype == DP_BF16) {
+    switch (c / 64) { DP_LQE(bf16_t, 1) DP_LQE(bf16_t, 2) DP_LQE(bf16_t, 3) DP_LQE(bf16_t, 4) DP_LQE(bf16_t, 5)
+                      DP_LQE(bf16_t, 6) DP_LQE(bf16_t, 7) DP_LQE(bf16_t, 8) }
+  } else {
+    switch (c / 64) { DP_LQE(float, 1) DP_LQE(float, 2) DP_LQE(float, 3) DP_LQE(float, 4) DP_LQE(float, 5)
+                      DP_LQE(float, 6) DP_LQE(float, 7) DP_LQE(float, 8) }
+  }
+#undef DP_LQE
   return dp_check_launch("dp_lqe_stats");
 }
 

@@ -52,10 +52,10 @@ __device__ __forceinline__ void vstore(T* p, const float* v) {
 template <typename T, int VEC>
 __global__ __launch_bounds__(256) void add_rows_kernel(T* out, dp_rowmap om, const T* a, dp_rowmap am, const T* b,
                                                        dp_rowmap bm, int rows, int c) {
-  const int nch = c / VEC;
-  int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)rows * nch) return;
-  const int64_t r = gid / nch;
+  const unsigned nch = (unsigned)(c / VEC);
+  const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (unsigned)rows * nch) return;
+  const unsigned r = gid / nch;
   const int i = (int)(gid - r * nch) * VEC;
   float x[VEC], y[VEC];
   vload<T, VEC>(a + rowmap_off(am, r) + i, x);
@@ -91,12 +91,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(T* out, dp_rowmap om, co
                                                         const uint8_t* mask, int mask_period, const float* masked_row) {
   constexpr int c = 64 * E;
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int c0 = lane * E;
   float v[E];
   T* o = out + rowmap_off(om, r) + c0;
-  if (mask && mask[r % mask_period]) {
+  if (mask && mask[(unsigned)r % (unsigned)mask_period]) {
 #pragma unroll
     for (int t = 0; t < E; ++t) v[t] = masked_row[c0 + t];
     vstore<T, E>(o, v);
@@ -111,10 +111,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(T* out, dp_rowmap om, co
   }
   ln_apply<E>(v, g, bta, c0, c, eps);
   if (post) {
-    const int64_t grp = r / post_group;
-    const int w = (int)(r - grp * post_group);
+    const int grp = (unsigned)r / (unsigned)post_group;
+    const int w = r - grp * post_group;
     if (w >= post_skip) {
-      const int64_t pr = grp * (post_group - post_skip) + (w - post_skip);
+      const int pr = grp * (post_group - post_skip) + (w - post_skip);
       float pv[E];
       vload<T, E>(post + rowmap_off(pm, pr) + c0, pv);
 #pragma unroll
@@ -130,11 +130,11 @@ __global__ __launch_bounds__(256) void gate_ln_kernel(T* out, int out_ld, const 
                                                       float eps, int rows) {
   constexpr int c = 64 * E;
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int c0 = lane * E;
-  const T* gr = gates + r * 2 * c;
-  const T* xr = xcat + r * 2 * c;
+  const T* gr = gates + (int64_t)r * 2 * c;
+  const T* xr = xcat + (int64_t)r * 2 * c;
   float g1[E], g2[E], x1[E], x2[E], v[E];
   vload<T, E>(gr + c0, g1);
   vload<T, E>(gr + c + c0, g2);
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void gate_ln_kernel(T* out, int out_ld, const 
 #pragma unroll
   for (int t = 0; t < E; ++t) v[t] = sigmoidf_(g1[t]) * x1[t] + sigmoidf_(g2[t]) * x2[t];
   ln_apply<E>(v, g, bta, c0, c, eps);
-  vstore<T, E>(out + r * out_ld + c0, v);
+  vstore<T, E>(out + (int64_t)r * out_ld + c0, v);
 }
 
 template <typename T>
@@ -190,6 +190,7 @@ extern "C" int dp_add_rows(void* out, dp_rowmap om, const void* a, dp_rowmap am,
                   ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(a) |
                     reinterpret_cast<uintptr_t>(b)) & 15) == 0;
   DP_REQUIRE(al, "dp_add_rows: rows must be 16-byte aligned (c=%d)", c);
+  DP_REQUIRE((int64_t)rows * c < (1ll << 31), "dp_add_rows: %d rows x %d too large", rows, c);
   const int64_t total = (int64_t)rows * (c / vec);
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
   if (dtype == DP_BF16)

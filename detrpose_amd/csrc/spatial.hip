@@ -18,14 +18,15 @@ template <typename T, int KS, int S, int PX>
 __global__ __launch_bounds__(256) void dwconv_kernel(dp_conv_desc d, int64_t total, int nchunk, int ntx) {
   constexpr int VEC = Vec16<T>::N;
   constexpr int NIN = (PX - 1) * S + KS;
-  int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;
-  const int cc = (int)(gid % nchunk);
-  int64_t rest = gid / nchunk;
-  const int tx = (int)(rest % ntx);
-  rest /= ntx;
-  const int oy = (int)(rest % d.out_h);
-  const int b = (int)(rest / d.out_h);
+  const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;   // total < 2^31 (host check)
+  if (gid >= (unsigned)total) return;
+  unsigned rest = gid / (unsigned)nchunk;
+  const int cc = (int)(gid - rest * (unsigned)nchunk);
+  unsigned r2 = rest / (unsigned)ntx;
+  const int tx = (int)(rest - r2 * (unsigned)ntx);
+  const unsigned b_ = r2 / (unsigned)d.out_h;
+  const int oy = (int)(r2 - b_ * (unsigned)d.out_h);
+  const int b = (int)b_;
   const int ox0 = tx * PX;
   const int c0 = cc * VEC;
   const T* in = reinterpret_cast<const T*>(d.in) + (int64_t)b * d.in_bstride + c0;
@@ -86,10 +87,10 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float* __restrict_
                                                         int has_lab, float ls, float lb, T* __restrict__ out,
                                                         int64_t obs, int ops) {
   const int oh = (h + 1) / 2, ow = (w + 1) / 2;
-  int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)batch * oh * ow) return;
-  const int b = (int)(gid / (oh * ow));
-  const int rem = (int)(gid - (int64_t)b * oh * ow);
+  const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (unsigned)(batch * oh * ow)) return;
+  const int b = (int)(gid / (unsigned)(oh * ow));
+  const int rem = (int)(gid - (unsigned)b * (unsigned)(oh * ow));
   const int oy = rem / ow, ox = rem - oy * ow;
   float x[27];
 #pragma unroll
@@ -131,12 +132,12 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, 
                                                       int w, int c, T* __restrict__ out, int64_t obs, int ops) {
   constexpr int VEC = Vec16<T>::N;
   const int nchunk = c / VEC;
-  int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)batch * h * w * nchunk) return;
-  const int cc = (int)(gid % nchunk);
-  const int64_t pix = gid / nchunk;
-  const int b = (int)(pix / (h * w));
-  const int rem = (int)(pix - (int64_t)b * h * w);
+  const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (unsigned)(batch * h * w * nchunk)) return;
+  const unsigned pix = gid / (unsigned)nchunk;
+  const int cc = (int)(gid - pix * (unsigned)nchunk);
+  const int b = (int)(pix / (unsigned)(h * w));
+  const int rem = (int)(pix - (unsigned)b * (unsigned)(h * w));
   const int y = rem / w, x = rem - y * w;
   const T* base = in + (int64_t)b * ibs + cc * VEC;
   float m[VEC];
@@ -179,6 +180,7 @@ extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
   constexpr int PX = 4;
   const int ntx = (d.out_w + PX - 1) / PX;
   const int64_t total = (int64_t)d.batch * d.out_h * ntx * nchunk;
+  DP_REQUIRE(total < (1ll << 31), "dp_dwconv2d: %lld work items exceed 2^31", (long long)total);
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
   hipStream_t s = as_stream(stream);
 #define DP_DW(T_, KS_, S_)                                                                            \
@@ -202,6 +204,7 @@ extern "C" int dp_stem_conv(const float* image, int32_t batch, int32_t h, int32_
   DP_REQUIRE(image && weight && bias && out, "dp_stem_conv: null pointer");
   DP_REQUIRE(out_pstride % 8 == 0 && out_bstride % 8 == 0 && al16(out), "dp_stem_conv: output alignment");
   const int64_t total = (int64_t)batch * ((h + 1) / 2) * ((w + 1) / 2);
+  DP_REQUIRE(total < (1ll << 31), "dp_stem_conv: batch too large");
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
   hipStream_t s = as_stream(stream);
 #define DP_STEM(T_, N_)                                                                                     \
@@ -227,6 +230,7 @@ extern "C" int dp_maxpool2x2_pad_rb(const void* in, int64_t in_bstride, int32_t 
   DP_REQUIRE(c % VEC == 0 && in_pstride % VEC == 0 && out_pstride % VEC == 0 && al16(in) && al16(out),
              "dp_maxpool2x2_pad_rb: 16-byte alignment required");
   const int64_t total = (int64_t)batch * h * w * (c / VEC);
+  DP_REQUIRE(total < (1ll << 31), "dp_maxpool2x2_pad_rb: batch too large");
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
   if (dtype == DP_BF16)
     hipLaunchKernelGGL(maxpool_kernel<bf16_t>, grid, block, 0, as_stream(stream), reinterpret_cast<const bf16_t*>(in),

@@ -79,7 +79,9 @@ def _run_conv(pc, x_nhwc, out, dt, res=None, up=None):
     (3, 1, 24, 24, 11, "silu"), (1, 1, 256, 288, 7, None), (3, 1, 128, 128, 40, "gelu"),
     # 128x128 tiles with an N tail, and grids where each persistent block walks several tiles
     (3, 1, 64, 160, 70, "silu"), (1, 1, 64, 128, 200, "relu"), (3, 1, 32, 64, 256, None),
-    (1, 1, 96, 32, 256, "gelu")])
+    (1, 1, 96, 32, 256, "gelu"),
+    # 8-wave 256x256 / 256x128 tiles (M >= 32768): N tail, 3x3 gather, 1x1
+    (1, 1, 256, 320, 130, "relu"), (3, 1, 64, 96, 130, "silu"), (1, 1, 512, 128, 128, None)])
 def test_conv2d(dt, k, s, cin, cout, H, act):
     torch.manual_seed(k * 100 + cin)
     pk = Packer({}, dt, torch.device("cuda"))
