@@ -234,6 +234,7 @@ int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
 }  // namespace
 int dp_conv2d_glds(const dp_conv_desc& d, hipStream_t s, int vec_ok);
 int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok);
+int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok);
 namespace {
 
 // bf16 conv path: persistent LDS-DMA kernel by default; DETRPOSE_CONV_PATH=glds|v2 selects
@@ -259,7 +260,13 @@ int dispatch(const dp_conv_desc& d, hipStream_t s) {
   const int M = d.batch * d.out_h * d.out_w;
   if constexpr (sizeof(T) == 2) {
     const int path = bf16_path();
-    if (path == 2) return dp_conv2d_stream(d, s, vec_ok);
+    if (path == 2) {
+      if (d.kh * d.kw > 1) {
+        const int r = dp_conv2d_halo(d, s, vec_ok);
+        if (r >= 0) return r;
+      }
+      return dp_conv2d_stream(d, s, vec_ok);
+    }
     if (path == 1) return dp_conv2d_glds(d, s, vec_ok);
   }
   if constexpr (sizeof(TO) != sizeof(T)) {  // f32-output heads: few shapes

@@ -1,0 +1,272 @@
+// Spatial convolutions (3x3 s1/s2, the stem's 2x2) with an LDS halo tile (gfx950, bf16):
+// dp_conv2d's path for KxK convs with cout <= 128.
+//
+// The implicit-GEMM kernels gather every output pixel's K = kh*kw*cin operand straight
+// from L2, i.e. each input pixel is DMA'd into LDS kh*kw times per N-tile; for the 48-128
+// channel 3x3 convs of HGNetv2 stages 0/1 and the encoder's VGG blocks that gather runs at
+// the chip's LDS-fill rate. Here a block owns a TH x 16 tile of output pixels and all
+// output channels, DMAs the ((TH-1)S+KH) x (15S+KW) input patch ONCE per tile (all input
+// channels, 128-byte rows per 64 channels, XOR-swizzled), and builds the MFMA pixel
+// fragments for every tap from the patch in LDS: lane (q, g) of K-step k reads patch pixel
+// (row(q)*S + ky, col(q)*S + kx) of tap k / cin, channel k % cin — the same K order as the
+// packed weights [cout][kpad] of the GEMM path, so the weights need no repacking.
+// Weights: resident in LDS for the whole persistent block when they fit (stem, stage 0),
+// otherwise streamed per K-step through a 2-deep ring. MFMA and register epilogue as in
+// conv_stream.hip (weights are the A operand, pixels the B operand, permuted weight rows so
+// a lane holds 4*TN contiguous output channels of one pixel).
+#include "conv_lds.h"
+#include <stdlib.h>
+#include <type_traits>
+
+namespace {
+
+using namespace dpconv;
+
+template <int TH, int KH, int KW, int S>
+struct HaloGeom {
+  static constexpr int TW = 16;
+  static constexpr int PH = (TH - 1) * S + KH, PW = (TW - 1) * S + KW;
+  static constexpr int PPX = PH * PW;
+  static constexpr int PPX8 = (PPX + 7) / 8 * 8;      // patch rows rounded to whole DMA groups
+  static constexpr int PLANE = PPX8 * 128;           // bytes per 64-channel plane of the patch
+};
+
+// RESW (weights resident): the patch is double-buffered and the next tile's patch is
+// DMA'd while the current tile computes (only patch DMAs are in flight, so the per-tile
+// vmcnt(0) retires exactly the prefetched patch). !RESW: one patch buffer, weights through a
+// 2-deep ring per K-step; the second resident block on the CU overlaps the patch loads.
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 2)))
+void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int vec_ok) {
+  using Gm = HaloGeom<TH, KH, KW, S>;
+  constexpr int TW = Gm::TW;
+  constexpr int BM = TH * TW, WM = BM / NW, TM = WM / 16, TN = BN / 16, NPL = 4 * TN;
+  constexpr int GB = BN / (8 * NW);                 // weight DMA instructions per wave per K-step (ring)
+  static_assert(TM >= 1 && WM % 16 == 0 && BN % 32 == 0 && (RESW || GB >= 1) && (RESW || !DBUF), "tile");
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;
+  const int L = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  if (L >= ntiles) return;
+
+  const int nk = d.kpad / 64;
+  const int nkc = (d.cin + 63) / 64;                 // 64-channel planes of the patch
+  const int pbytes = nkc * Gm::PLANE;                // one patch buffer
+  const int ktaps = KH * KW;
+  char* const wbase = smem;
+  char* const pbase0 = smem + (RESW ? nk : 2) * BN * 128;
+  const int r8 = lane >> 3;
+  const i32x4 rb_src = make_rsrc(d.weight);
+
+  // weight row -> LDS row R permuted for the register epilogue (single wave column)
+  auto w_off = [&](int R) {
+    const int j = R / 16, p = R % 16;
+    const int n = (p >> 2) * NPL + 4 * j + (p & 3);
+    return n < d.cout ? n * d.kpad + ((lane & 7) ^ (R & 7)) * 8 : OOB;
+  };
+  if (RESW) {
+    // all K-steps once: (kt, 8-row group) pairs spread over the waves
+    for (int t = wave; t < nk * (BN / 8); t += NW) {
+      const int kt = t / (BN / 8), grp = t - kt * (BN / 8);
+      const int ob = w_off(grp * 8 + r8);
+      dma16(rb_src, wbase + kt * BN * 128 + grp * 1024, ob != OOB ? (ob + kt * 64) * 2 : OOB);
+    }
+  }
+  int b_off[RESW ? 1 : GB];
+  if (!RESW) {
+#pragma unroll
+    for (int t = 0; t < GB; ++t) b_off[t] = w_off((wave + NW * t) * 8 + r8);
+  }
+  auto issue_w = [&](int kt, char* dst) {
+#pragma unroll
+    for (int t = 0; t < GB; ++t) {
+      const int o = b_off[t] != OOB ? (b_off[t] + kt * 64) * 2 : OOB;
+      dma16(rb_src, dst + (wave + NW * t) * 1024, o);
+    }
+  };
+  auto issue_patch = [&](int tile, char* pb) {
+    const int tx = tile % tiles_x, rest = tile / tiles_x;
+    const int ty = rest % tiles_y, b = rest / tiles_y;
+    const int iy0 = ty * TH * S - d.pad_t, ix0 = tx * TW * S - d.pad_l;
+    const i32x4 ra = make_rsrc(reinterpret_cast<const bf16_t*>(d.in) + (int64_t)b * d.in_bstride);
+    constexpr int GP = Gm::PPX8 / 8;                 // DMA groups per plane
+    for (int t = wave; t < GP * nkc; t += NW) {
+      const int pl = t / GP, grp = t - pl * GP;
+      const int p = grp * 8 + r8;
+      const int py = p / Gm::PW, px = p - py * Gm::PW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      const int ci = pl * 64 + (((lane & 7) ^ (p & 7)) << 3);
+      const bool ok = p < Gm::PPX && (unsigned)iy < (unsigned)d.in_h && (unsigned)ix < (unsigned)d.in_w && ci < d.cin;
+      const int o = ok ? ((iy * d.in_w + ix) * d.in_pstride + ci) * 2 : OOB;
+      dma16(ra, pb + pl * Gm::PLANE + grp * 1024, o);
+    }
+  };
+
+  // per-lane pixel fragment geometry: q = lane & 15 is the tile column, g = lane >> 4 the
+  // 8-channel group of the K-step half; rows yq_i = wave*TM + i
+  const int q = lane & 15, g = lane >> 4;
+  const int wm = wave;
+  const int cin = d.cin;
+
+  if (DBUF) issue_patch(L, pbase0);
+  f32x4 acc[TM][TN];
+  int u = 0;
+  for (int tile = L; tile < ntiles; tile += G, ++u) {
+    const int tx = tile % tiles_x, rest = tile / tiles_x;
+    const int ty = rest % tiles_y, b = rest / tiles_y;
+    const int oy0 = ty * TH, ox0 = tx * TW;
+    const char* pbase;
+    if (DBUF) {
+      // this tile's patch (prefetched during the previous tile) has landed; every wave is
+      // past the previous tile, so the other buffer is free for the next tile's patch
+      wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (tile + G < ntiles) issue_patch(tile + G, pbase0 + ((u + 1) & 1) * pbytes);
+      pbase = pbase0 + (u & 1) * pbytes;
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue_patch(tile, pbase0);
+      if (!RESW) issue_w(0, wbase);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      pbase = pbase0;
+    }
+
+    // one K-step; the first of a tile starts the MFMA chain from a zero C operand
+    auto step = [&](int kt, auto first_tag) {
+      constexpr bool FIRST = decltype(first_tag)::value;
+      const char* wsl;
+      if (RESW) {
+        wsl = wbase + kt * BN * 128;
+      } else {
+        if (!FIRST) {
+          wait_vmcnt<0>();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        if (kt + 1 < nk) issue_w(kt + 1, wbase + ((kt + 1) & 1) * BN * 128);
+        wsl = wbase + (kt & 1) * BN * 128;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int cc = 4 * ks + g;
+        // this lane's 8 channels of K: k = kt*64 + 32 ks + 8 g -> (tap, ci)
+        const int k = kt * 64 + cc * 8;
+        int tap = (unsigned)k / (unsigned)cin;
+        int ci = k - tap * cin;
+        if (tap >= ktaps) tap = 0, ci = 0;           // kpad tail: weights are zero there
+        const int ky = tap / KW, kx = tap - ky * KW;
+        const char* pl = pbase + (ci >> 6) * Gm::PLANE;
+        const int c8 = (ci >> 3) & 7;
+        bf16x8 wf[TN], pf[TM];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = 16 * j + (lane & 15);
+          wf[j] = *reinterpret_cast<const bf16x8*>(wsl + r * 128 + ((cc ^ (r & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int yq = wm * TM + i;
+          const int pr = (yq * S + ky) * Gm::PW + q * S + kx;
+          pf[i] = *reinterpret_cast<const bf16x8*>(pl + pr * 128 + ((c8 ^ (pr & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                wf[j], pf[i], (FIRST && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
+      }
+    };
+    step(0, std::true_type{});
+    for (int kt = 1; kt < nk; ++kt) step(kt, std::false_type{});
+    // epilogue: lane owns pixel (oy0 + yq, ox0 + q), channels nb .. nb + NPL - 1
+    const int nb = g * NPL;
+    if (nb < d.cout) {
+      float bias[NPL];
+      load_bias<NPL>(d, nb, bias);
+      const bool full = vec_ok && nb + NPL <= d.cout;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int oy = oy0 + wm * TM + i, ox = ox0 + q;
+        if (oy < d.out_h && ox < d.out_w) epi_pixel<ACT, bf16_t, TN>(d, acc[i], bias, b, oy, ox, nb, full);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+}
+
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT>
+int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds) {
+  auto kern = conv_halo_kernel<TH, NW, KH, KW, S, BN, RESW, DBUF, ACT>;
+  static const int occ = [&] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, NW * 64, lds) != hipSuccess || o <= 0) o = 1;
+    if (getenv("DETRPOSE_CONV_DEBUG"))
+      fprintf(stderr, "conv_halo TH=%d NW=%d K=%dx%d S=%d BN=%d resw=%d act=%d: lds %d, occupancy %d\n", TH, NW, KH,
+              KW, S, BN, (int)RESW, ACT, lds, o);
+    return o;
+  }();
+  const int tiles_x = (d.out_w + 15) / 16, tiles_y = (d.out_h + TH - 1) / TH;
+  const int ntiles = d.batch * tiles_x * tiles_y;
+  // occupancy at THIS layer's LDS size (the static value was queried for the first one)
+  int o = occ;
+  const int fit = (160 * 1024) / lds;
+  if (o > fit) o = fit;
+  if (o < 1) o = 1;
+  int grid = o * num_cus();
+  const int need = (ntiles + 7) / 8 * 8;
+  if (grid > need) grid = need;
+  grid = grid / 8 * 8;
+  if (grid < 8) grid = 8;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, d, tiles_x, tiles_y, ntiles, vec_ok);
+  return dp_check_launch("dp_conv2d(halo)");
+}
+
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF = false>
+int launch_halo_act(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds) {
+  switch (d.act) {
+    case DP_ACT_RELU: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_RELU>(d, s, vec_ok, lds);
+    case DP_ACT_SILU: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_SILU>(d, s, vec_ok, lds);
+    case DP_ACT_NONE: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_NONE>(d, s, vec_ok, lds);
+    default: return -1;
+  }
+}
+
+}  // namespace
+
+// bf16 KxK convs with cout <= 128; returns -1 when this shape has no halo instantiation
+// (the caller falls back to the implicit-GEMM path).
+int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
+  static const bool off = getenv("DETRPOSE_NO_HALO") != nullptr;
+  if (off || d.out_f32 || d.cout > 128 || d.act == DP_ACT_GELU) return -1;
+  const int bn = (d.cout + 31) / 32 * 32;
+  const int nk = d.kpad / 64, nkc = (d.cin + 63) / 64;
+  constexpr int LMAX = 160 * 1024;
+  auto lds_res = [&](int plane, int nbuf) { return nk * bn * 128 + nbuf * nkc * plane; };  // resident W
+  auto lds_str = [&](int plane) { return 2 * bn * 128 + nkc * plane; };                     // W ring, 1 patch
+  if (d.kh == 3 && d.kw == 3 && d.stride == 1) {
+    constexpr int P16 = HaloGeom<16, 3, 3, 1>::PLANE, P8 = HaloGeom<8, 3, 3, 1>::PLANE;
+    if (bn == 64 && lds_res(P16, 2) <= LMAX)
+      return launch_halo_act<16, 8, 3, 3, 1, 64, true, true>(d, s, vec_ok, lds_res(P16, 2));
+    if (bn == 32 && lds_res(P8, 1) <= 80 * 1024) return launch_halo_act<8, 4, 3, 3, 1, 32, true>(d, s, vec_ok, lds_res(P8, 1));
+    if (lds_str(P8) > 80 * 1024) return -1;
+    if (bn == 64) return launch_halo_act<8, 4, 3, 3, 1, 64, false>(d, s, vec_ok, lds_str(P8));
+    if (bn == 96) return launch_halo_act<8, 4, 3, 3, 1, 96, false>(d, s, vec_ok, lds_str(P8));
+    if (bn == 128) return launch_halo_act<8, 4, 3, 3, 1, 128, false>(d, s, vec_ok, lds_str(P8));
+    return -1;
+  }
+  if (d.kh == 2 && d.kw == 2 && d.stride == 1) {
+    constexpr int P = HaloGeom<8, 2, 2, 1>::PLANE;
+    if (bn == 32 && lds_res(P, 1) <= 80 * 1024) return launch_halo_act<8, 4, 2, 2, 1, 32, true>(d, s, vec_ok, lds_res(P, 1));
+    return -1;
+  }
+  return -1;
+}

@@ -23,143 +23,30 @@
 #include <stdlib.h>
 #include <type_traits>
 
+#include "conv_lds.h"
+
 namespace {
 
-constexpr int OOB = 0x7fffffff;
-
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-// Buffer resource words (base, no stride, 2 GB range, gfx950 raw-buffer flags) in SGPRs.
-__device__ __forceinline__ i32x4 make_rsrc(const void* base) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  i32x4 r;
-  r[0] = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
-  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffffu));
-  r[2] = 0x7ffffff0;
-  r[3] = 0x00020000;
-  return r;
-}
-
-// 16 bytes per lane HBM/L2 -> LDS (M0 = wave-uniform LDS byte address; lane L lands at
-// M0 + 16 L). Inline asm rather than the builtin: the compiler would otherwise treat every
-// later ds_read as a possible alias of the DMA and insert s_waitcnt vmcnt(0), draining the
-// ring; completion is tracked by hand (wait_vmcnt + barrier) below.
-__device__ __forceinline__ void dma16(const i32x4& rsrc, const char* lds, int voff) {
-  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds));
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(rsrc)
-               : "memory");
-}
-
-// s_waitcnt vmcnt(N) (expcnt/lgkmcnt untouched) as the builtin, so the compiler's own
-// wait insertion sees it and does not add a second vmcnt(0) for its epilogue loads/stores.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xf << 8));
-}
-
-template <int ACT>
-__device__ __forceinline__ float act_t(float x) {
-  if constexpr (ACT == DP_ACT_RELU) return fmaxf(x, 0.f);
-  else if constexpr (ACT == DP_ACT_SILU) return x / (1.f + __expf(-x));
-  else if constexpr (ACT == DP_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
-  else return x;
-}
+using namespace dpconv;
 
 // Epilogue of one tile from registers. Lane (g = lane>>4, q = lane&15) owns pixel row
-// m = m0 + wm*WM + 16 i + q and channels nb .. nb + NPL - 1, value acc[i][j][r] is
-// channel nb + 4 j + r.
+// m = mw + 16 i + q and channels nb .. nb + NPL - 1.
 template <int ACT, typename TO, int TM, int TN, int WM>
 __device__ __forceinline__ void stream_epilogue(const dp_conv_desc& d, const f32x4 (&acc)[TM][TN], int M, int mw,
                                                 int nb, int vec_ok) {
   constexpr int NPL = 4 * TN;
-  constexpr int VO = 16 / (int)sizeof(TO);
-  constexpr int CPL = NPL / VO;   // 16-byte chunks per lane per pixel
-  static_assert(NPL % VO == 0, "lane channel group must be whole 16-byte chunks");
   const int q = threadIdx.x & 15;
   const int hwo = d.out_h * d.out_w;
-  TO* __restrict__ out = reinterpret_cast<TO*>(d.out);
-  const TO* __restrict__ res = reinterpret_cast<const TO*>(d.res);
-  TO* __restrict__ up = reinterpret_cast<TO*>(d.up);
   const bool full = vec_ok && nb + NPL <= d.cout;
   float bias[NPL];
-#pragma unroll
-  for (int c = 0; c < NPL; ++c) bias[c] = 0.f;
-  if (d.bias) {
-    if (nb + NPL <= d.cout) {
-#pragma unroll
-      for (int c = 0; c < NPL; c += 4) {
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(d.bias + nb + c);
-        bias[c] = b4[0], bias[c + 1] = b4[1], bias[c + 2] = b4[2], bias[c + 3] = b4[3];
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < NPL; ++c) bias[c] = nb + c < d.cout ? d.bias[nb + c] : 0.f;
-    }
-  }
+  load_bias<NPL>(d, nb, bias);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = mw + 16 * i + q;
     if (m >= M || nb >= d.cout) continue;
     const int b = m / hwo, rem = m - b * hwo;
     const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
-    const int64_t pix = (int64_t)oy * d.out_w + ox;
-    float v[NPL];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float x = act_t<ACT>(acc[i][j][r] + bias[4 * j + r]);
-        if (d.has_lab) x = d.lab_scale * x + d.lab_bias;
-        v[4 * j + r] = x;
-      }
-    const int64_t oo = (int64_t)b * d.out_bstride + pix * d.out_pstride + nb;
-    if (full) {
-      Vec16<TO> ch[CPL];
-      if (res) {
-        const TO* rp = res + (int64_t)b * d.res_bstride + pix * d.res_pstride + nb;
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) ch[c] = load16(rp + c * VO);
-#pragma unroll
-        for (int c = 0; c < CPL; ++c)
-#pragma unroll
-          for (int t = 0; t < VO; ++t) ch[c].set(t, v[c * VO + t] + ch[c].get(t));
-      } else {
-#pragma unroll
-        for (int c = 0; c < CPL; ++c)
-#pragma unroll
-          for (int t = 0; t < VO; ++t) ch[c].set(t, v[c * VO + t]);
-      }
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) store16(out + oo + c * VO, ch[c]);
-      if (up) {
-        const int64_t ub = (int64_t)b * d.up_bstride + nb;
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-          for (int dx = 0; dx < 2; ++dx) {
-            TO* upp = up + ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) store16(upp + c * VO, ch[c]);
-          }
-      }
-    } else {
-      const int nn = min(NPL, d.cout - nb);
-#pragma unroll
-      for (int c = 0; c < NPL; ++c) {
-        if (c >= nn) break;
-        float x = v[c];
-        if (res) x += to_f32(res[(int64_t)b * d.res_bstride + pix * d.res_pstride + nb + c]);
-        const TO y = from_f32<TO>(x);
-        out[oo + c] = y;
-        if (up) {
-          const int64_t ub = (int64_t)b * d.up_bstride + nb + c;
-          for (int dy = 0; dy < 2; ++dy)
-            for (int dx = 0; dx < 2; ++dx)
-              up[ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride] = y;
-        }
-      }
-    }
+    epi_pixel<ACT, TO, TN>(d, acc[i], bias, b, oy, ox, nb, full);
   }
 }
 
@@ -366,17 +253,6 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
 #define DP_STREAM_SA 2
 #endif
 
-int num_cus() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                hipSuccess || v <= 0)
-      v = 256;
-    return v;
-  }();
-  return n;
-}
-
 template <typename K>
 int occupancy(K kern, int threads) {
   int n = 0;
@@ -443,6 +319,20 @@ int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
 #endif
 
 }  // namespace
+
+namespace dpconv {
+int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+}  // namespace dpconv
 
 // bf16 entry used by dp_conv2d (conv_gemm.hip); vec_ok computed by the caller.
 int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
