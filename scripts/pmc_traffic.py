@@ -6,17 +6,21 @@ are doubled; WRITE_SIZE is exact for 16-byte stores.
     python scripts/pmc_traffic.py <fetch counter_collection.csv> <write ...csv> [out.json]
 """
 import collections
+import re
 import csv
 import json
 import sys
 
 
 def family(name):
-    for key in ("conv_glds_kernel", "conv_gemm_kernel", "dwconv_kernel", "layernorm_kernel", "attn_mfma_kernel",
+    # every implicit-GEMM conv variant (conv_stream/halo/glds/gemm_kernel) is one family
+    if re.search(r"conv_(stream|halo|glds|gemm)_kernel", name):
+        return "conv"
+    for key in ("dwconv_kernel", "layernorm_kernel", "attn_mfma_kernel",
                 "msda_kernel", "add_rows_kernel", "stem_conv_kernel", "maxpool_kernel", "class_max_kernel",
                 "topk_kernel", "gate_ln_kernel", "sine_embed_kernel", "lqe_kernel", "pose_refine_kernel"):
         if key in name:
-            return "conv" if key.startswith("conv_") else key
+            return key
     return "other"
 
 
