@@ -63,7 +63,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   // weight row -> LDS row R permuted for the register epilogue (single wave column)
   auto w_off = [&](int R) {
     const int j = R / 16, p = R % 16;
-    const int n = (p >> 2) * NPL + 4 * j + (p & 3);
+    const int n = lane_chan<8>(p >> 2, 4 * j + (p & 3));
     return n < d.cout ? n * d.kpad + ((lane & 7) ^ (R & 7)) * 8 : OOB;
   };
   if (RESW) {
@@ -185,16 +185,15 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
     };
     step(0, std::true_type{});
     for (int kt = 1; kt < nk; ++kt) step(kt, std::false_type{});
-    // epilogue: lane owns pixel (oy0 + yq, ox0 + q), channels nb .. nb + NPL - 1
-    const int nb = g * NPL;
-    if (nb < d.cout) {
+    // epilogue: lane owns pixel (oy0 + yq, ox0 + q), channels lane_chan(g, 0 .. NPL-1)
+    {
       float bias[NPL];
-      load_bias<NPL>(d, nb, bias);
-      const bool full = vec_ok && nb + NPL <= d.cout;
+      load_bias<bf16_t, NPL>(d, 0, g, bias);
+      const bool full = lane_full<bf16_t, NPL>(d, 0, g, vec_ok);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int oy = oy0 + wm * TM + i, ox = ox0 + q;
-        if (oy < d.out_h && ox < d.out_w) epi_pixel<ACT, bf16_t, TN>(d, acc[i], bias, b, oy, ox, nb, full);
+        if (oy < d.out_h && ox < d.out_w) epi_pixel<ACT, bf16_t, TN>(d, acc[i], bias, b, oy, ox, 0, g, full);
       }
     }
   }

@@ -25,29 +25,145 @@
 
 #include "conv_lds.h"
 
+#ifndef DP_ABL_NOSTORE
+#define DP_ABL_NOSTORE 0   // ablation builds only (scripts/conv_bench.py): drop the epilogue stores
+#endif
+#ifndef DP_ABL_NODMA
+#define DP_ABL_NODMA 0     // ... drop the LDS-DMA loads
+#endif
+#ifndef DP_ABL_NOMFMA
+#define DP_ABL_NOMFMA 0    // ... drop the MFMAs (fragment reads kept live)
+#endif
+
 namespace {
 
 using namespace dpconv;
 
-// Epilogue of one tile from registers. Lane (g = lane>>4, q = lane&15) owns pixel row
-// m = mw + 16 i + q and channels nb .. nb + NPL - 1.
-template <int ACT, typename TO, int TM, int TN, int WM>
-__device__ __forceinline__ void stream_epilogue(const dp_conv_desc& d, const f32x4 (&acc)[TM][TN], int M, int mw,
-                                                int nb, int vec_ok) {
+// Epilogue modes (compile time, so the store path has no runtime branches or waits):
+// plain, + residual (added after act/LAB), + nearest-x2 copy into the FPN concat buffer.
+enum { EPI_PLAIN = 0, EPI_RES = 1, EPI_UP = 2 };
+
+// VMEM instructions one wave issues in the epilogue of a whole tile (every pixel row
+// in range, every lane's chunks whole): the count the next K-step's wait may leave in
+// flight, since loads/stores/LDS-DMA retire in issue order (MI355X_MICROARCH.md: vmcnt).
+template <int EPI, int TM, int CPL>
+constexpr int epi_vmem() {
+  const int n = TM * CPL * (EPI == EPI_PLAIN ? 1 : (EPI == EPI_RES ? 2 : 5));
+  return n > 63 ? 63 : n;
+}
+
+// Cout edge / unaligned rows (f32 heads with 2/34/66 columns, 48-channel convs in 64-wide
+// tiles): scalar stores. Inlined: an out-of-line call would put the descriptor in scratch
+// and make the caller save its accumulators.
+template <int EPI, typename TO, int NPL>
+__device__ __forceinline__ void epi_edge(const dp_conv_desc& d, const float* v, int b, int rem, int nbw,
+                                                   int g) {
+  constexpr int VO = 16 / (int)sizeof(TO);
+  const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
+  TO* __restrict__ out = reinterpret_cast<TO*>(d.out);
+  const TO* __restrict__ res = reinterpret_cast<const TO*>(d.res);
+  TO* __restrict__ up = reinterpret_cast<TO*>(d.up);
+  for (int e = 0; e < NPL; ++e) {
+    const int cc = nbw + lane_chan<VO>(g, e);
+    if (cc >= d.cout) continue;
+    float x = v[e];
+    if (EPI == EPI_RES) x += to_f32(res[(int64_t)b * d.res_bstride + (int64_t)rem * d.res_pstride + cc]);
+    const TO y = from_f32<TO>(x);
+    out[(int64_t)b * d.out_bstride + (int64_t)rem * d.out_pstride + cc] = y;
+    if (EPI == EPI_UP)
+      for (int dy = 0; dy < 2; ++dy)
+        for (int dx = 0; dx < 2; ++dx)
+          up[(int64_t)b * d.up_bstride + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride + cc] =
+              y;
+  }
+}
+
+// Epilogue of one tile from registers. Lane (g = lane>>4, q = lane&15) owns pixel rows
+// m = mw + 16 i + q and the wave's channels nbw + lane_chan(g, 0 .. NPL-1); the bias of
+// the tile's BN channels sits in LDS (bias_w = the wave's first channel there). Pixel
+// (image, offset) pairs advance incrementally: one division per tile, not per pixel.
+// Returns true when the tile was whole (every wave issued epi_vmem VMEM instructions).
+template <int ACT, typename TO, int TM, int TN, int EPI>
+__device__ __forceinline__ bool stream_epilogue(const dp_conv_desc& d, const f32x4 (&acc)[TM][TN],
+                                                const float* bias_w, int M, int mw, int nbw, int vec_ok) {
   constexpr int NPL = 4 * TN;
-  const int q = threadIdx.x & 15;
-  const int hwo = d.out_h * d.out_w;
-  const bool full = vec_ok && nb + NPL <= d.cout;
+  constexpr int VO = 16 / (int)sizeof(TO);
+  constexpr int CPL = NPL / VO;
+  static_assert(NPL % VO == 0, "lane channel group must be whole 16-byte chunks");
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
+  if (nbw >= d.cout) return false;
+  const bool wave_full = vec_ok && nbw + lane_chan<VO>(3, NPL - 1) < d.cout;
+  const bool full = wave_full || lane_full<TO, NPL>(d, nbw, g, vec_ok);
   float bias[NPL];
-  load_bias<NPL>(d, nb, bias);
+#pragma unroll
+  for (int e = 0; e < NPL; e += 4) {
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_w + lane_chan<VO>(g, e));
+    bias[e] = b4[0], bias[e + 1] = b4[1], bias[e + 2] = b4[2], bias[e + 3] = b4[3];
+  }
+  const int hwo = d.out_h * d.out_w;
+  int m = mw + q;
+  int b = m / hwo, rem = m - b * hwo;
+  TO* __restrict__ out = reinterpret_cast<TO*>(d.out);
+  const TO* __restrict__ res = reinterpret_cast<const TO*>(d.res);
+  TO* __restrict__ up = reinterpret_cast<TO*>(d.up);
+  const int cb = nbw + g * VO;   // the lane's chunk 0; chunk c at cb + 4 VO c
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int m = mw + 16 * i + q;
-    if (m >= M || nb >= d.cout) continue;
-    const int b = m / hwo, rem = m - b * hwo;
-    const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
-    epi_pixel<ACT, TO, TN>(d, acc[i], bias, b, oy, ox, nb, full);
+    if (m < M) {
+      float v[NPL];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = act_t<ACT>(acc[i][j][r] + bias[4 * j + r]);
+          if (d.has_lab) x = d.lab_scale * x + d.lab_bias;
+          v[4 * j + r] = x;
+        }
+#if DP_ABL_NOSTORE
+#pragma unroll
+      for (int e = 0; e < NPL; ++e) asm volatile("" ::"v"(v[e]), "v"(b), "v"(rem));
+#else
+      if (full) {
+        TO* op = out + (int64_t)b * d.out_bstride + (int64_t)rem * d.out_pstride + cb;
+        Vec16<TO> ch[CPL];
+        if constexpr (EPI == EPI_RES) {
+          const TO* rp = res + (int64_t)b * d.res_bstride + (int64_t)rem * d.res_pstride + cb;
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) ch[c] = load16(rp + c * 4 * VO);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int t = 0; t < VO; ++t) ch[c].set(t, v[c * VO + t] + ch[c].get(t));
+        } else {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int t = 0; t < VO; ++t) ch[c].set(t, v[c * VO + t]);
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) store16(op + c * 4 * VO, ch[c]);
+        if constexpr (EPI == EPI_UP) {
+          const int oy = rem / d.out_w, ox = rem - oy * d.out_w;
+          TO* ub = up + (int64_t)b * d.up_bstride + cb;
+#pragma unroll
+          for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+              TO* upp = ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride;
+#pragma unroll
+              for (int c = 0; c < CPL; ++c) store16(upp + c * 4 * VO, ch[c]);
+            }
+        }
+      } else {
+        epi_edge<EPI, TO, NPL>(d, v, b, rem, nbw, g);
+      }
+#endif
+    }
+    m += 16;
+    rem += 16;
+    while (rem >= hwo) rem -= hwo, ++b;
   }
+  return wave_full && mw + 16 * TM - 1 < M;
 }
 
 // target waves per SIMD = (blocks per CU the LDS allows) x (waves per block) / 4; ask the
@@ -63,7 +179,7 @@ constexpr int stream_waves() {
 // SA = depth of the activation (A) ring; the weight (B) ring is 2 deep. Weights are a few
 // hundred KB and stay in L2, activations stream from HBM: the extra A stages are the bytes
 // in flight that hide HBM latency (Little's law), where a deeper B ring would only burn LDS.
-template <int BM, int BN, int WGM, int NW, int SA, bool K1X1, int ACT, typename TO>
+template <int BM, int BN, int WGM, int NW, int SA, bool K1X1, int ACT, typename TO, int EPI>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(stream_waves<BM, BN, SA, NW>())))
 void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok) {
   constexpr int WGN = NW / WGM;
@@ -75,9 +191,14 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
   constexpr int BBYTES = BN * 128, ABYTES = BM * 128;     // one K-step of B / A
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0 && WGM * WGN == NW && TM >= 1 && TN >= 1 && SA >= 2 &&
                     SA <= 4, "tile");
-  // LDS: [B ring: SB x BN rows][A ring: SA x BM rows], rows of 128 B (one 64-wide K-step)
-  __shared__ __attribute__((aligned(1024))) char smem[SB * BBYTES + SA * ABYTES];
+  // LDS: [B ring: SB x BN rows][A ring: SA x BM rows], rows of 128 B (one 64-wide K-step),
+  // then 2 x 1 KB bias slots (tile parity): the tile's BN f32 biases, DMA'd by wave 0 in
+  // front of the tile's first weight K-step, so the epilogue reads them from LDS and the
+  // compiler never has a VMEM load of its own to wait for behind the in-flight DMAs.
+  __shared__ __attribute__((aligned(1024))) char smem[SB * BBYTES + SA * ABYTES + 2048];
   char* const sa_base = smem + SB * BBYTES;
+  char* const bias_base = sa_base + SA * ABYTES;
+  static_assert(BN * 4 <= 1024, "bias slot");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -95,17 +216,18 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
   const i32x4 rb_src = make_rsrc(d.weight);
 
   // weight row landing in LDS row R: permuted so lane group g of wave column wn ends with
-  // channels wn*WN + g*NPL + [0, NPL) (see header)
+  // channels wn*WN + lane_chan(g, 0 .. NPL-1) (see conv_lds.h)
+  constexpr int VO = 16 / (int)sizeof(TO);
   auto b_chan = [&](int t) {
     const int R = (wave + NW * t) * 8 + r8;
     const int wq = R / WN, p16 = R % WN, j = p16 / 16, p = p16 % 16;
-    return wq * WN + (p >> 2) * NPL + 4 * j + (p & 3);
+    return wq * WN + lane_chan<VO>(p >> 2, 4 * j + (p & 3));
   };
 
   // ---- A issue cursor (activations) and B issue cursor (weights) run SA-1 and 1 K-steps
   // ahead of the consumer, each across tile boundaries
   int a_tile = L, a_kt = 0, a_n = 0;
-  int b_tile = L, b_kt = 0, b_n = 0;
+  int b_tile = L, b_kt = 0, b_n = 0, b_t = 0;   // b_t: tiles whose weights were issued
   i32x4 ra_src;
   int a_off[GA], a_yx[GA], b_off[GB];   // a_yx: (iy0 << 16) | (ix0 & 0xffff)
   auto setup_a = [&](int tile) {
@@ -144,7 +266,7 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
 #pragma unroll
       for (int t = 0; t < GA; ++t) {
         const int o = (a_off[t] != OOB && kv) ? (a_off[t] + kk) * 2 : OOB;
-        dma16(ra_src, sb + (wave + NW * t) * 1024, o);
+        if (!DP_ABL_NODMA) dma16(ra_src, sb + (wave + NW * t) * 1024, o);
       }
     } else {
       const int tap = kk / d.cin, ci = kk - tap * d.cin;
@@ -155,7 +277,7 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
         const int iy = (a_yx[t] >> 16) + ky, ix = (int)(short)(a_yx[t] & 0xffff) + kx;
         const bool ok = kv && a_off[t] != OOB && (unsigned)iy < (unsigned)d.in_h && (unsigned)ix < (unsigned)d.in_w;
         const int o = ok ? (a_off[t] + (iy * d.in_w + ix) * d.in_pstride + ci) * 2 : OOB;
-        dma16(ra_src, sb + (wave + NW * t) * 1024, o);
+        if (!DP_ABL_NODMA) dma16(ra_src, sb + (wave + NW * t) * 1024, o);
       }
     }
     ++a_n;
@@ -167,14 +289,21 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
   };
   auto issue_b = [&]() {
     char* sb = smem + (b_n % SB) * BBYTES;
+    if (b_kt == 0 && wave == 0) {
+      // the tile's biases (older than its first weight K-step: covered by the same wait)
+      const int n0 = (b_tile - (b_tile / nt_n) * nt_n) * BN;
+      const int o = (d.bias && n0 + 4 * lane < d.cout && 4 * lane < BN) ? (n0 + 4 * lane) * 4 : OOB;
+      if (!DP_ABL_NODMA) dma16(make_rsrc(d.bias), bias_base + (b_t & 1) * 1024, o);
+    }
 #pragma unroll
     for (int t = 0; t < GB; ++t) {
       const int o = b_off[t] != OOB ? (b_off[t] + b_kt * 64) * 2 : OOB;
-      dma16(rb_src, sb + (wave + NW * t) * 1024, o);
+      if (!DP_ABL_NODMA) dma16(rb_src, sb + (wave + NW * t) * 1024, o);
     }
     ++b_n;
     if (++b_kt == nk) {
       b_kt = 0;
+      ++b_t;
       b_tile += G;
       if (b_tile < ntiles) setup_b(b_tile);
     }
@@ -192,7 +321,10 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
   const int wrow = wn * WN + lr;   // weight fragment rows (MFMA A operand)
   const int prow = wm * WM + lr;   // pixel fragment rows (MFMA B operand)
   int c = 0;                       // K-steps consumed
-  bool dirty = false;              // epilogue stores since the last wait (their vmcnt order vs loads is unknown)
+  // after an epilogue: 0 none, 1 whole tile (its epi_vmem stores/loads are the youngest VMEM
+  // ops and may stay in flight), 2 partial tile (unknown count: drain)
+  int dirty = 0;
+  constexpr int EPIV = epi_vmem<EPI, TM, (4 * TN) / (16 / (int)sizeof(TO))>();
   f32x4 acc[TM][TN];
   // one K-step: wait for A(c) and B(c), publish them, refill both rings, 2 x TMxTN MFMAs.
   // Waits: the loads complete in order, so it suffices to count the A groups issued after
@@ -203,10 +335,16 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
   auto step = [&](auto first_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
     const int younger = SA == 2 ? 0 : (c == 0 ? min(SA - 2, a_n - 1) : (a_n > c + SA - 2 ? 1 : 0));
-    if (dirty || younger <= 0) wait_vmcnt<0>();
+    if (dirty == 2) wait_vmcnt<0>();
+    else if (dirty == 1) {
+      // the epilogue's stores are younger than everything this step needs
+      if (younger <= 0) wait_vmcnt<EPIV>();
+      else if (younger == 1) wait_vmcnt<(EPIV + GA > 63 ? 63 : EPIV + GA)>();
+      else wait_vmcnt<(EPIV + 2 * GA > 63 ? 63 : EPIV + 2 * GA)>();
+    } else if (younger <= 0) wait_vmcnt<0>();
     else if (younger == 1) wait_vmcnt<GA>();
     else wait_vmcnt<2 * GA>();
-    dirty = false;
+    dirty = 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -232,19 +370,26 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
+#if DP_ABL_NOMFMA
+        {
+          asm volatile("" ::"v"(wf[j]), "v"(pf[i]));
+          if (FIRST && ks == 0) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#else
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               wf[j], pf[i], (FIRST && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
+#endif
     }
     ++c;
   };
-  for (int ctile = L; ctile < ntiles; ctile += G) {
+  int t_n = 0;
+  for (int ctile = L; ctile < ntiles; ctile += G, ++t_n) {
     step(std::true_type{});
     for (int kt = 1; kt < nk; ++kt) step(std::false_type{});
     const int tm = ctile / nt_n, tn = ctile - tm * nt_n;
     const int mw = tm * BM + wm * WM;
-    const int nb = tn * BN + wn * WN + lg * NPL;
-    stream_epilogue<ACT, TO, TM, TN, WM>(d, acc, M, mw, nb, vec_ok);
-    dirty = true;
+    const float* bias_w = reinterpret_cast<const float*>(bias_base + (t_n & 1) * 1024) + wn * WN;
+    dirty = stream_epilogue<ACT, TO, TM, TN, EPI>(d, acc, bias_w, M, mw, tn * BN + wn * WN, vec_ok) ? 1 : 2;
   }
   wait_vmcnt<0>();
 }
@@ -272,10 +417,10 @@ constexpr int ring_a() {
   return (blocksw >= 1 && blocksw >= blocks2) ? want : 2;
 }
 
-template <int BM, int BN, int WGM, int NW, bool K1, int ACT, typename TO>
+template <int BM, int BN, int WGM, int NW, bool K1, int ACT, typename TO, int EPI>
 int launch_one(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   constexpr int SA = ring_a<BM, BN, NW>();
-  auto kern = conv_stream_kernel<BM, BN, WGM, NW, SA, K1, ACT, TO>;
+  auto kern = conv_stream_kernel<BM, BN, WGM, NW, SA, K1, ACT, TO, EPI>;
   static const int occ = [&] {
     const int o = occupancy(kern, NW * 64);
     if (getenv("DETRPOSE_CONV_DEBUG")) {
@@ -298,20 +443,30 @@ int launch_one(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   return dp_check_launch("dp_conv2d(stream)");
 }
 
-template <int BM, int BN, int WGM, int NW, bool K1, typename TO>
+template <int BM, int BN, int WGM, int NW, bool K1, typename TO, int EPI>
 int launch_act(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   switch (d.act) {
-    case DP_ACT_RELU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_RELU, TO>(d, s, vec_ok);
-    case DP_ACT_SILU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_SILU, TO>(d, s, vec_ok);
-    case DP_ACT_GELU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_GELU, TO>(d, s, vec_ok);
-    default: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_NONE, TO>(d, s, vec_ok);
+    case DP_ACT_RELU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_RELU, TO, EPI>(d, s, vec_ok);
+    case DP_ACT_SILU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_SILU, TO, EPI>(d, s, vec_ok);
+    case DP_ACT_GELU: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_GELU, TO, EPI>(d, s, vec_ok);
+    default: return launch_one<BM, BN, WGM, NW, K1, DP_ACT_NONE, TO, EPI>(d, s, vec_ok);
   }
+}
+
+// epilogue mode (residual and upsample never come together on this path: the launcher
+// refuses that descriptor; f32 outputs have no upsample, dp_conv2d checks)
+template <int BM, int BN, int WGM, int NW, bool K1, typename TO>
+int launch_epi(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
+  if (d.res) return launch_act<BM, BN, WGM, NW, K1, TO, EPI_RES>(d, s, vec_ok);
+  if constexpr (sizeof(TO) == 2)
+    if (d.up) return launch_act<BM, BN, WGM, NW, K1, TO, EPI_UP>(d, s, vec_ok);
+  return launch_act<BM, BN, WGM, NW, K1, TO, EPI_PLAIN>(d, s, vec_ok);
 }
 
 template <int BM, int BN, int WGM, typename TO, int NW = 4>
 int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   const bool k1 = d.kh == 1 && d.kw == 1 && d.pad_t == 0 && d.pad_l == 0;
-  return k1 ? launch_act<BM, BN, WGM, NW, true, TO>(d, s, vec_ok) : launch_act<BM, BN, WGM, NW, false, TO>(d, s, vec_ok);
+  return k1 ? launch_epi<BM, BN, WGM, NW, true, TO>(d, s, vec_ok) : launch_epi<BM, BN, WGM, NW, false, TO>(d, s, vec_ok);
 }
 
 #ifndef DP_BIG_TILES
@@ -336,6 +491,7 @@ int num_cus() {
 
 // bf16 entry used by dp_conv2d (conv_gemm.hip); vec_ok computed by the caller.
 int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
+  DP_REQUIRE(!(d.res && d.up), "dp_conv2d: residual together with the x2 upsample copy is not supported");
   const int M = d.batch * d.out_h * d.out_w;
   const bool f32o = d.out_f32 != 0;
   if (d.cout <= 32) return f32o ? launch<128, 32, 4, float>(d, s, vec_ok) : launch<128, 32, 4, bf16_t>(d, s, vec_ok);
