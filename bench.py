@@ -1,4 +1,4 @@
-"""Throughput benchmark of the DETRPose inference forward on MI355X.
+"""Throughput (and bs=1 latency) benchmark of the DETRPose inference forward on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size l] [--batch 64]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -12,19 +12,31 @@ each rank forwards its own batch (data parallel, weak scaling) and the outputs a
 all-gathered over RCCL (one all_gather_into_tensor of 8,640 B/img). Rank 0 prints one
 JSON line. Weights: seeded fan-in random init (no checkpoint offline); data synthetic.
 
+`--gpus N` with no torch.distributed environment starts `torch.distributed.run` with N
+ranks as a child process (before anything touches the GPU) and exits with its code; a
+run whose world size differs from --gpus fails.
+
 Also reported (rank 0):
-  roofline     the dominant kernel family (implicit-GEMM conv/linear, dp_conv2d):
-               algorithmic FLOPs of its launches / their HIP-event time, vs bf16 dense
-               MFMA peak;
-  cpu_baseline the CPU oracle restatement (oracle/detrpose_cpu.py, kind "port") timed on
-               the host cores on a bounded sample (N=1 only).
+  roofline      the dominant kernel family (implicit-GEMM conv/linear, dp_conv2d):
+                algorithmic bytes (or FLOPs) of its launches / their HIP-event time;
+                `traffic` = measured HBM bytes of those launches from the committed
+                rocprofv3 PMC passes, quoted only when they were taken on this exact
+                source (detrpose_amd.build.source_hash);
+  latency_bs1   the reference's latency protocol (torch_benchmark.py:29-51): batch 1,
+                400 warm-up and 1000 timed Model(images, sizes) calls (hipGraph replay,
+                synchronised each), mean of the fastest 100 and the median;
+  secondary     DETRPose-N bf16 batch 32 throughput (BASELINE configs[1]);
+  cpu_baseline  the CPU oracle restatement (oracle/detrpose_cpu.py, kind "port") at
+                batch 1 and 8 (2 warm-up + 5 timed) on the host cores (N=1 only).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -37,40 +49,77 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sp
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 METRIC = "images/sec + p50 ms/img, DETRPose-L bf16 640x640 at 1/2/4/8 MI355X"
+PMC_FILE = "profiles/pmc_traffic.json"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", default="l", choices=["n", "l", "x"])
     ap.add_argument("--batch", type=int, default=64, help="images per GPU")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=25.0, help="cap on the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--latency-runs", type=int, default=1000)
+    ap.add_argument("--latency-warmup", type=int, default=400)
     ap.add_argument("--profile-ops", type=str, default="", help="write per-op times (JSON) to this path")
-    return ap.parse_args()
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="test hook: gloo on CPU with a stub step (checks launch, world size and gather order)")
+    return ap.parse_args(argv)
 
 
-PMC_FILE = "profiles/r1_pmc_traffic.json"
+# ----------------------------------------------------------------------------- launch
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def maybe_spawn(a) -> int | None:
+    """--gpus N>1 outside torch.distributed.run: run N ranks as a child torchrun (no GPU
+    call has happened in this process yet) and return its exit code."""
+    if a.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ----------------------------------------------------------------------------- legs
 
 
 def pmc_traffic(a, launches):
-    """Measured HBM bytes per step of the conv family, from the committed rocprofv3 PMC
-    passes of this exact workload (scripts/pmc_traffic.py); None for other workloads."""
+    """Measured HBM bytes per step of the conv family from the committed rocprofv3 PMC
+    passes (scripts/pmc_traffic.py), only if they were taken on this exact source and
+    workload; otherwise (None, reason)."""
+    from detrpose_amd.build import source_hash
     path = os.path.join(REPO, PMC_FILE)
-    if (a.size, a.batch, a.dtype) != ("l", 64, "bf16") or not os.path.exists(path):
-        return None
-    fam = json.load(open(path))["families"].get("conv")
+    if not os.path.exists(path):
+        return None, "no PMC profile committed"
+    d = json.load(open(path))
+    if d.get("source_hash") != source_hash():
+        return None, f"PMC profile is for source {d.get('source_hash')}, this is {source_hash()}: not quoted"
+    if tuple(d.get("workload", ())) != (a.size, a.batch, a.dtype):
+        return None, "PMC profile is for another workload"
+    fam = d["families"].get("conv")
     if not fam or round(fam["launches"]) != launches:
-        return None
-    return round(fam["total_bytes"])
+        return None, "PMC launch count differs"
+    return round(fam["total_bytes"]), f"rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE ({PMC_FILE}, source {d['source_hash']})"
 
 
-def cpu_baseline(size, seconds):
-    """Oracle (CPU fp32 restatement of the reference forward) on host cores, batch 1."""
+def cpu_baseline(size, cap_seconds):
+    """Oracle (CPU fp32 restatement of the reference forward) on host cores at batch 1 and
+    8, 2 warm-up + 5 timed forwards each, bounded by cap_seconds."""
     from detrpose_amd import build_model
     from detrpose_amd.configs import get_config
     from detrpose_amd.synthetic import load_synthetic, synthetic_images
@@ -81,30 +130,118 @@ def cpu_baseline(size, seconds):
     m, _ = build_model(size)
     load_synthetic(m, 0)
     orc = OracleDETRPose(get_config(size), m.state_dict())
-    img = synthetic_images(1, 1)
-    orc(img)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        orc(img)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= 2:
-            break
-    return {"value": round(n / el, 3), "unit": "images/sec", "cores": cores, "kind": "port",
-            "sample": f"DETRPose-{size.upper()} fp32 CPU oracle, batch 1, {n} forwards in {el:.1f}s "
-                      f"(oracle/detrpose_cpu.py, torch CPU ops, {cores} threads)"}
+    res, t_start = {}, time.perf_counter()
+    for bs in (1, 8):
+        img = synthetic_images(bs, 1)
+        for _ in range(2):
+            orc(img)
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            orc(img)
+            ts.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_start > cap_seconds and len(ts) >= 2:
+                break
+        res[bs] = (bs * len(ts) / sum(ts), len(ts))
+    best = max(res, key=lambda b: res[b][0])
+    return {"value": round(res[best][0], 3), "unit": "images/sec", "cores": cores, "kind": "port",
+            "by_batch": {str(b): round(v[0], 3) for b, v in res.items()},
+            "sample": f"DETRPose-{size.upper()} fp32 CPU oracle (oracle/detrpose_cpu.py, torch CPU ops, {cores} "
+                      f"threads), batch 1 and 8, 2 warm-up + " + " / ".join(f"{v[1]} timed at b{b}"
+                                                                                for b, v in res.items())
+                      + f"; value = best batch (b{best})"}
+
+
+def latency_bs1(model, pp, dev, runs, warmup):
+    """tools/benchmark/torch_benchmark.py:29-51 on the HIP path: Model(images, sizes) at
+    batch 1 (one hipGraph replay incl. the input copy), synchronised around every call."""
+    from detrpose_amd.export import DeployModel
+    from detrpose_amd.synthetic import synthetic_images
+    dm = DeployModel(model, pp)
+    img = synthetic_images(1, seed=7).to(dev)
+    size = torch.tensor([[640, 640]], device=dev)
+    for _ in range(warmup):
+        dm.replay(img, size)
+    ts = []
+    for _ in range(runs):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dm.replay(img, size)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    srt = sorted(ts)
+    fast = srt[:100]
+    return {"mean_fastest100_ms": round(1e3 * sum(fast) / len(fast), 4),
+            "p50_ms": round(1e3 * statistics.median(ts), 4), "runs": runs, "warmup": warmup,
+            "protocol": "torch_benchmark.py:29-51 (bs=1, Model = model + PostProcess, hipGraph replay)"}
+
+
+def throughput(model, dev, batch, steps, warmup, seed=1):
+    """Images/s of graph replays over one resident batch (single-rank secondary configs)."""
+    from detrpose_amd.synthetic import synthetic_images
+    plan = model.engine(dev).plan(batch)
+    plan.input.copy_(synthetic_images(batch, seed=seed).to(dev))
+    g = plan.graph()
+    for _ in range(warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = plan.out_flat
+    return batch * steps / el, bool(torch.isfinite(out).all())
+
+
+# ----------------------------------------------------------------------------- main
+
+
+def cpu_dry_run(a):
+    """Test hook for the N-rank launch: gloo on CPU, a stub 'forward' that writes each
+    image's rank/index into the out_flat layout, the same all-gather + unflatten as the GPU
+    path; prints the JSON line (n_gpus = world) with the gather check."""
+    from detrpose_amd import dist as dp
+    rank, world, dev = dp.init("gloo")
+    if world != a.gpus:
+        raise SystemExit(f"bench: world size {world} != --gpus {a.gpus}")
+    per = a.batch
+    flat = torch.empty(per * 60 * (2 + 34))
+    t0 = time.perf_counter()
+    for _ in range(a.warmup + a.steps):
+        flat.fill_(float(rank))
+        g = dp.gather_outputs(flat, world)
+    el = dp.max_over_ranks(time.perf_counter() - t0, world, dev)
+    outs = dp.unflatten(g, world, per)
+    ok = all(bool((outs["pred_logits"][r * per:(r + 1) * per] == r).all()) for r in range(world))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(per * a.steps * world / el, 2), "unit": "images/sec",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "dry_run": "cpu-gloo",
+                          "gather_check": "ok" if ok else "FAILED"}), flush=True)
+    if world > 1:
+        dp.dist.barrier()
+        dp.dist.destroy_process_group()
+    if not ok:
+        raise SystemExit(1)
 
 
 def main():
     a = parse()
+    rc = maybe_spawn(a)
+    if rc is not None:
+        sys.exit(rc)
+    if a.cpu_dry_run:
+        return cpu_dry_run(a)
     from detrpose_amd import dist as dp
     rank, world, dev = dp.init("nccl")
+    if world != a.gpus:
+        raise SystemExit(f"bench: torch.distributed world size {world} != --gpus {a.gpus}")
     dist = dp.dist if world > 1 else None
 
     from detrpose_amd import GFLOP_PER_IMAGE, build_model
     from detrpose_amd.synthetic import load_synthetic, synthetic_images
 
-    model, _ = build_model(a.size, dtype=a.dtype)
+    model, pp = build_model(a.size, dtype=a.dtype)
     load_synthetic(model, 0)
     model.deploy()
     eng = model.engine(dev)
@@ -147,6 +284,9 @@ def main():
     value = total_imgs / elapsed
     ms_per_step = elapsed * 1000.0 / a.steps
     p50_ms_img = statistics.median(step_ms) / a.batch
+    finite = bool(torch.isfinite(plan.out_flat).all())
+    if dist is not None:
+        finite = bool(torch.isfinite(gathered).all())
 
     if rank == 0:
         # per-op HIP-event pass over the same plan (outside the timed region)
@@ -156,35 +296,38 @@ def main():
         conv_ms = sum(op_ms[n] for n in conv_names)
         conv_flops = sum(plan.op_flops[n] for n in conv_names)
         conv_alg_bytes = sum(plan.conv_bytes[n] for n in conv_names)
-        traffic = pmc_traffic(a, len(conv_names))
+        traffic, traffic_note = pmc_traffic(a, len(conv_names))
         total_ms = sum(op_ms.values())
         achieved = conv_flops / (conv_ms * 1e-3) / 1e12
         peak = PEAK_BF16_TFLOPS if a.dtype == "bf16" else PEAK_F32_TFLOPS
         fam = {}
         for n, ms in op_ms.items():
-            fn = next(f for nm, f, _ in plan.ops if nm == n).__name__
-            fam[fn] = fam.get(fn, 0.0) + ms
+            fam[op_fn[n]] = fam.get(op_fn[n], 0.0) + ms
         msda = [n for n in plan.op_bytes if n in op_ms]
         msda_gbs = sum(plan.op_bytes[n] for n in msda) / (sum(op_ms[n] for n in msda) * 1e-3) / 1e9 if msda else None
         if a.profile_ops:
             with open(a.profile_ops, "w") as f:
-                json.dump({"op_ms": op_ms, "op_flops": plan.op_flops, "op_bytes": plan.op_bytes}, f, indent=1)
+                json.dump({"op_ms": op_ms, "op_flops": plan.op_flops, "op_bytes": plan.op_bytes,
+                           "conv_bytes": plan.conv_bytes}, f, indent=1)
         gflop = GFLOP_PER_IMAGE[a.size]
-        # the family's lower bound is the larger of its HBM time and its MFMA time; report
-        # against that one (for L bf16 b64 the compulsory bytes dominate: ~4.0 ms vs ~2.7 ms)
+        # the family's lower bound is the larger of its HBM time and its MFMA time
         gbs = conv_alg_bytes / (conv_ms * 1e-3) / 1e9
         hbm_bound = conv_alg_bytes / (PEAK_HBM_GBS * 1e9) >= conv_flops / (peak * 1e12)
+        # per-launch bound: sum over launches of max(bytes / HBM peak, flops / MFMA peak)
+        lb_ms = sum(max(plan.conv_bytes[n] / (PEAK_HBM_GBS * 1e9), plan.op_flops[n] / (peak * 1e12))
+                    for n in conv_names) * 1e3
         roofline = {"bound": "hbm" if hbm_bound else "mfma",
-                    "kernel": "conv_stream_kernel (dp_conv2d: all dense conv/linear launches of one step)",
+                    "kernel": "dp_conv2d family (conv_stream/conv_halo kernels: all dense conv/linear launches "
+                              "of one step)",
                     "achieved": round(gbs if hbm_bound else achieved, 2),
                     "peak": PEAK_HBM_GBS if hbm_bound else peak,
                     "unit": "GB/s" if hbm_bound else "TFLOP/s",
                     "frac": round(gbs / PEAK_HBM_GBS if hbm_bound else achieved / peak, 4),
                     "traffic": traffic,
-                    "traffic_note": "HBM bytes per step over these launches (rocprofv3 PMC FETCH_SIZE x2 + "
-                                    "WRITE_SIZE, " + PMC_FILE + ")",
+                    "traffic_note": traffic_note,
                     "algorithmic_bytes": round(conv_alg_bytes),
                     "achieved_tflops": round(achieved, 2), "mfma_frac": round(achieved / peak, 4),
+                    "per_launch_bound_ms": round(lb_ms, 3), "bound_over_actual": round(lb_ms / conv_ms, 4),
                     "launches_per_step": len(conv_names), "ms_per_step": round(conv_ms, 3),
                     "time_share": round(conv_ms / total_ms, 3)}
         out = {
@@ -205,17 +348,31 @@ def main():
                                    f"batch {a.batch} per GPU, hipGraph replay", "batch_per_gpu": a.batch,
                        "global_batch": a.batch * world, "image": "640x640", "parallelism": f"dp{world}",
                        "graph": not a.no_graph},
+            "outputs_finite": finite,
             "roofline": roofline,
             "e2e_mfma_frac": round(value / world * gflop * 1e9 / (peak * 1e12), 4),
             "kernel_ms_per_step": {k: round(v, 3) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])},
             "msda_algorithmic_gbs": round(msda_gbs, 1) if msda_gbs else None,
         }
+        if world == 1 and not a.no_latency:
+            out["latency_bs1"] = latency_bs1(model, pp, dev, a.latency_runs, a.latency_warmup)
+        if world == 1 and not a.no_secondary:
+            mn, _ = build_model("n", dtype=a.dtype)
+            load_synthetic(mn, 0)
+            mn.deploy()
+            v, fin = throughput(mn, dev, 32, max(20, a.steps // 2), 5)
+            out["secondary"] = [{"workload": "DETRPose-N bf16 batch 32 640x640 (BASELINE configs[1])",
+                                 "value": round(v, 2), "unit": "images/sec", "outputs_finite": fin}]
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.size, a.cpu_baseline_seconds)
+        if not finite:
+            out["error"] = "non-finite outputs"
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if not finite:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

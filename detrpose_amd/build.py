@@ -39,6 +39,23 @@ def _flags() -> list[str]:
             "-I", os.path.join(REPO, "include")] + extra
 
 
+def source_hash() -> str:
+    """Content hash of everything that decides which kernels a plan launches and how they
+    touch memory (kernel sources, the C-ABI header, the planner). Profiles committed under
+    profiles/ record it, so bench.py only quotes measured HBM traffic for the exact code it
+    is timing (the box receives no .git, so this is not a commit id)."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h")) +
+                   glob.glob(os.path.join(CSRC, "*.cpp")))
+    files += [os.path.join(REPO, "include", "detrpose_hip.h"), os.path.join(PKG, "engine.py")]
+    for f in files:
+        h.update(os.path.relpath(f, REPO).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _stale(obj: str, src: str, deps: list[str]) -> bool:
     if not os.path.exists(obj):
         return True

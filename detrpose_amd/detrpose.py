@@ -2,10 +2,14 @@
 
 `DETRPose(backbone, encoder, transformer)` keeps the reference constructor and
 state_dict layout (detrpose.py:15-67), `.deploy()` returns self (69-74) and
-`forward(samples) -> {'pred_logits', 'pred_keypoints'}` (76-81, eval/deploy output
-layout: logits (B,Q,2), keypoints (B,Q,17,2)). The forward runs entirely on the HIP
-kernels of libdetrpose_hip.so through detrpose_amd.engine; there is no eager-torch or
-CPU fallback.
+`forward(samples, targets=None) -> {'pred_logits', 'pred_keypoints'}` (76-81). As in
+the reference, the keypoint layout depends on deploy mode: (B,Q,34) before `.deploy()`
+(transformer.py:1320-1321 flattens the last two dims) and (B,Q,17,2) after it
+(convert_to_deploy, transformer.py:1202-1207); logits are (B,Q,2) either way. In eval
+`targets` is accepted and ignored, as the reference's evaluate() passes them
+(src/solver/engine.py:133-134) and only the training forward reads them
+(transformer.py:1265). The forward runs entirely on the HIP kernels of
+libdetrpose_hip.so through detrpose_amd.engine; there is no eager-torch or CPU fallback.
 
 `build_model(size)` is the constructor the north star names ("build_model"); the
 reference has no such function (only LazyConfig + instantiate), so it reads the
@@ -31,11 +35,15 @@ class DETRPose(nn.Module):
         self.transformer = transformer
         self.layer_loss = torch.zeros(1, dtype=torch.float32)
         self.compute_dtype = dtype
+        self.deploy_mode = False
         self._engine = None
 
     # -- reference API
     def deploy(self):
+        """detrpose.py:69-74: eval + convert_to_deploy (BN folding happens in the engine's
+        packer for every mode; what deploy changes visibly is the (B,Q,17,2) layout)."""
         self.eval()
+        self.deploy_mode = True
         return self
 
     def set_dtype(self, dtype: str):
@@ -60,17 +68,26 @@ class DETRPose(nn.Module):
 
     @torch.no_grad()
     def forward(self, samples, targets=None):
-        if self.training or targets is not None:
-            raise NotImplementedError("training forward (DN queries, aux outputs) is outside the inference hot path")
+        if self.training:
+            raise NotImplementedError("training forward (DN queries, aux outputs) is outside the inference hot path; "
+                                      "call .eval() or .deploy() first")
         if not samples.is_cuda:
             raise RuntimeError("DETRPose (MI355X) runs on the GPU only: move the images to a HIP device")
+        hw = tuple(self.encoder.eval_spatial_size)
+        if samples.dim() != 4 or tuple(samples.shape[1:]) != (3, *hw):
+            raise ValueError(f"DETRPose expects images (B, 3, {hw[0]}, {hw[1]}) (the plan is built for "
+                             f"eval_spatial_size {list(hw)}), got {tuple(samples.shape)}")
         eng = self.engine(samples.device)
         B = samples.shape[0]
         plan = eng.plan(B)
-        if samples.data_ptr() != plan.input.data_ptr():
-            plan.input.copy_(samples.to(torch.float32), non_blocking=True)
-        plan.run()
-        return {k: v.clone() for k, v in plan.outputs.items()}
+        with torch.cuda.device(samples.device):
+            if samples.data_ptr() != plan.input.data_ptr():
+                plan.input.copy_(samples.to(torch.float32), non_blocking=True)
+            plan.run()
+            out = {k: v.clone() for k, v in plan.outputs.items()}
+        if not self.deploy_mode:
+            out["pred_keypoints"] = out["pred_keypoints"].flatten(-2)
+        return out
 
 
 def build_model(size: str = "l", dtype: str = "bf16", cfg: dict | None = None):

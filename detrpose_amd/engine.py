@@ -186,6 +186,7 @@ class Plan:
         self.out_flat = None
         self.input = None
         self.outputs = {}
+        self.post = None         # PostProcess buffers once add_postprocess() appended it
         self._graph = None
 
     # -- recording
@@ -193,7 +194,7 @@ class Plan:
         self.ops.append((name, fn, args))
 
     def run(self, stream=None, debug=None):
-        s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream().cuda_stream)
+        s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.engine.device).cuda_stream)
         for name, fn, args in self.ops:
             rc = fn(*args, s)
             if rc:
@@ -204,7 +205,7 @@ class Plan:
 
     def profile(self, reps=3):
         """Per-op device time (ms, median of `reps` passes) with HIP events around each launch."""
-        s = torch.cuda.current_stream()
+        s = torch.cuda.current_stream(self.engine.device)
         times = {name: [] for name, _, _ in self.ops}
         for _ in range(reps):
             evs = []
@@ -243,16 +244,18 @@ class Plan:
     def graph(self):
         """Capture the plan into a hipGraph once; returns the graph (replay with .replay())."""
         if self._graph is None:
-            torch.cuda.synchronize()
-            side = torch.cuda.Stream()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                self.run()  # warm-up on the capture stream outside capture
-            torch.cuda.current_stream().wait_stream(side)
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self.run()
+            dev = self.engine.device
+            with torch.cuda.device(dev):
+                torch.cuda.synchronize(dev)
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    self.run()  # warm-up on the capture stream outside capture
+                torch.cuda.current_stream(dev).wait_stream(side)
+                torch.cuda.synchronize(dev)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.run()
             self._graph = g
         return self._graph
 

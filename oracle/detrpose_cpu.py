@@ -382,9 +382,14 @@ def lqe(scores, kps, feat_nhwc, sd, p, k=4):
     return scores + _mlp(stat, sd, p + ".reg_conf", 2)
 
 
-def transformer(feats, sd, cfg):
+def transformer(feats, sd, cfg, force_topk=None):
     """Transformer.forward (eval, deploy), transformer.py:1209-1387, and
-    TransformerDecoder.forward, transformer.py:558-925 (default path)."""
+    TransformerDecoder.forward, transformer.py:558-925 (default path).
+
+    force_topk (B, nq) int64, test-side only: replaces the two-stage selection's
+    topk indices (transformer.py:1240-1242) so a reduced-precision forward, whose
+    near-tied scores may select a different query set, can be compared with this
+    fp32 restatement query by query on the SAME selection."""
     C = cfg["hidden_dim"]
     nhead = cfg["nhead"]
     nq = cfg["num_queries"]
@@ -400,6 +405,8 @@ def transformer(feats, sd, cfg):
     om = _layer_norm(_linear(om, sd, "transformer.enc_output"), sd, "transformer.enc_output_norm")
     cls = _linear(om, sd, "transformer.enc_out_class_embed")
     topk_idx = torch.topk(cls.max(-1)[0], nq, dim=1)[1]
+    if force_topk is not None:
+        topk_idx = torch.as_tensor(force_topk, dtype=torch.int64).reshape(B, nq)
     tmem = torch.gather(om, 1, topk_idx.unsqueeze(-1).expand(-1, -1, C))
     tanc = torch.gather(anchors.expand(B, -1, -1), 1, topk_idx.unsqueeze(-1).expand(-1, -1, 2))
     delta = _mlp(tmem, sd, "transformer.enc_pose_embed", 4).reshape(B, nq, K, 2)
@@ -460,12 +467,12 @@ class OracleDETRPose:
         self.sd = {k: v.detach().to("cpu", torch.float32) for k, v in state_dict.items()}
 
     @torch.no_grad()
-    def forward(self, images: torch.Tensor, intermediates: bool = False):
+    def forward(self, images: torch.Tensor, intermediates: bool = False, force_topk=None):
         bcfg, ecfg, tcfg = self.cfg["backbone"], self.cfg["encoder"], self.cfg["transformer"]
         x = images.to(torch.float32)
         bb = backbone(x, self.sd, bcfg["name"], bcfg["return_idx"], bcfg["use_lab"])
         en = encoder(bb, self.sd, ecfg)
-        tr = transformer(en, self.sd, tcfg)
+        tr = transformer(en, self.sd, tcfg, force_topk=force_topk)
         out = {"pred_logits": tr["pred_logits"], "pred_keypoints": tr["pred_keypoints"]}
         if intermediates:
             out.update(backbone=bb, encoder=en, topk_idx=tr["topk_idx"], layers=tr["layers"])

@@ -6,10 +6,13 @@ are doubled; WRITE_SIZE is exact for 16-byte stores.
     python scripts/pmc_traffic.py <fetch counter_collection.csv> <write ...csv> [out.json]
 """
 import collections
-import re
 import csv
 import json
+import os
+import re
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def family(name):
@@ -40,7 +43,8 @@ def main():
     fetch, calls = agg(sys.argv[1], "FETCH_SIZE")
     write, _ = agg(sys.argv[2], "WRITE_SIZE")
     nfwd = calls["topk_kernel"]
-    out = {"forwards_profiled": nfwd, "families": {}}
+    from detrpose_amd.build import source_hash
+    out = {"forwards_profiled": nfwd, "source_hash": source_hash(), "workload": ["l", 64, "bf16"], "families": {}}
     for f in sorted(fetch, key=lambda k: -fetch[k]):
         rd = 2.0 * fetch[f] / nfwd
         wr = write.get(f, 0.0) / nfwd

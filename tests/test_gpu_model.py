@@ -1,8 +1,10 @@
 """End-to-end parity of the HIP forward against the reference (golden fixtures).
 
 fp32 mode: every stage within the north-star gate (1e-3 abs on logits / keypoints) and
-the two-stage top-k order identical. bf16 mode: the selection is order-sensitive
-(SURVEY.md header fact 5), so outputs are compared per matched query.
+the two-stage top-k order identical. bf16 mode (the benchmarked kernels): the selection
+is order-sensitive (SURVEY.md header fact 5), so the fp32 oracle is re-run on the HIP
+path's own selection and compared query by query; the headline batch-64 plan must be
+batch invariant. Also the reference's eval-loop and export call patterns.
 """
 import json
 import os
@@ -80,3 +82,127 @@ def test_bf16_tracks_reference(golden_dir, size, batch):
             errs.append(np.abs(kp[b, same] - g["out_pred_keypoints"][b, same]).max())
     if errs:
         assert max(errs) < 0.1, f"bf16 matched-query keypoint error {max(errs):.3g}"
+
+
+# ---------------------------------------------------------------- bf16 production path, pinned
+
+# bf16 storage (8 mantissa bits) through ~110 conv/linear layers, 3-6 decoder layers and an
+# fp32 head, vs the fp32 oracle on the SAME selection ("Parity of the bf16
+# path"). Keypoints are normalised image coordinates in [0, 1]. Measured on MI355X
+# (profiles/r2a_pytest_gpu.txt): max|dkp| 0.009 / 0.012 / 0.008 and mean 1.3-1.6e-3 for
+# N / L / X; max|dlogit| 0.037 / 0.016 / 0.017, mean 5-8e-3. Bounds: ~1.5x the worst max,
+# 2x the worst mean.
+BF16_TOL_KP, BF16_TOL_KP_MEAN = 2e-2, 3.5e-3
+BF16_TOL_LOGIT, BF16_TOL_LOGIT_MEAN = 5e-2, 1.6e-2
+
+
+def _oracle(size, model):
+    from detrpose_amd.configs import get_config
+    from oracle.detrpose_cpu import OracleDETRPose
+    return OracleDETRPose(get_config(size), model.state_dict())
+
+
+@pytest.mark.parametrize("size,batch", CASES)
+def test_bf16_forced_selection_matches_oracle(golden_dir, size, batch):
+    """The benchmarked kernels (conv_stream / conv_halo / attn_mfma, bf16) end to end: the
+    fp32 oracle is run on the HIP path's own top-k selection (force_topk), so every query
+    is compared slot by slot, logits and keypoints, always asserted."""
+    g = np.load(os.path.join(golden_dir, f"detrpose_{size}_b{batch}.npz"))
+    model, _ = _model(golden_dir, size, g, "bf16")
+    images = synthetic_images(batch, seed=int(g["meta"][2]))
+    out = model(images.cuda())
+    torch.cuda.synchronize()
+    idx = model.engine().plan(batch).bufs["topk_idx"].cpu()
+    ref = _oracle(size, model)(images, force_topk=idx)
+    kp = out["pred_keypoints"].float().cpu()
+    lg = out["pred_logits"].float().cpu()
+    assert torch.isfinite(kp).all() and torch.isfinite(lg).all()
+    dk = (kp - ref["pred_keypoints"]).abs()
+    dl = (lg - ref["pred_logits"]).abs()
+    msg = (f"{size} bf16 vs fp32 oracle (forced selection): max|dkp| {dk.max():.3g} (mean {dk.mean():.3g}), "
+           f"max|dlogit| {dl.max():.3g} (mean {dl.mean():.3g}), topk overlap with fp32 "
+           f"{len(set(idx.reshape(-1).tolist()) & set(g['topk_idx'].reshape(-1).tolist()))}/{idx.numel()}")
+    print(msg)
+    assert dk.max() <= BF16_TOL_KP and dl.max() <= BF16_TOL_LOGIT, msg
+    assert dk.mean() <= BF16_TOL_KP_MEAN and dl.mean() <= BF16_TOL_LOGIT_MEAN, msg
+
+
+def test_bf16_b64_headline_batch_is_batch_invariant(golden_dir):
+    """The headline plan (L bf16, batch 64: 256x256/256x128 8-wave tiles, persistent
+    multi-tile walks, the largest buffers) gives image 0 and image 63 the same outputs as
+    a batch-1 plan of that image, and every output of the batch is finite."""
+    g = np.load(os.path.join(golden_dir, "detrpose_l_b1.npz"))
+    model, _ = _model(golden_dir, "l", g, "bf16")
+    img = synthetic_images(1, seed=int(g["meta"][2]))
+    batch = synthetic_images(64, seed=1234)
+    batch[0] = img[0]
+    batch[63] = img[0]
+    o64 = model(batch.cuda())
+    i64 = model.engine().plan(64).bufs["topk_idx"].cpu()
+    o1 = model(img.cuda())
+    i1 = model.engine().plan(1).bufs["topk_idx"].cpu()
+    torch.cuda.synchronize()
+    for k in ("pred_logits", "pred_keypoints"):
+        assert torch.isfinite(o64[k]).all(), k
+    for r in (0, 63):
+        assert torch.equal(i64[r], i1[0]), f"row {r}: top-k differs from the batch-1 plan"
+        dk = (o64["pred_keypoints"][r] - o1["pred_keypoints"][0]).abs().max().item()
+        dl = (o64["pred_logits"][r] - o1["pred_logits"][0]).abs().max().item()
+        print(f"b64 row {r} vs b1: max|dkp| {dk:.3g} max|dlogit| {dl:.3g}")
+        assert dk <= 1e-4 and dl <= 1e-4, (r, dk, dl)
+    # the other 62 images are different, so their outputs are too
+    assert (o64["pred_keypoints"][1] - o64["pred_keypoints"][0]).abs().max() > 1e-3
+
+
+# ---------------------------------------------------------------- reference call patterns
+
+
+def test_eval_loop_call_pattern(golden_dir):
+    """src/solver/engine.py:133-137: model.eval(); outputs = model(samples, targets); then
+    the NON-deploy PostProcess (postprocesses.py:32-40) -> per-image dicts with (60, 51)
+    keypoints [x*w, y*h, 1]. Keypoints come out flattened (B, 60, 34) before deploy
+    (transformer.py:1320-1321)."""
+    from detrpose_amd import PostProcess
+    size, batch = "n", 2
+    g = np.load(os.path.join(golden_dir, f"detrpose_{size}_b{batch}.npz"))
+    with open(os.path.join(golden_dir, "manifest.json")) as f:
+        man = json.load(f)
+    model, _ = build_model(size, dtype="fp32")
+    model.load_state_dict(synthetic_state_dict(man[size], seed=int(g["meta"][1])), strict=False)
+    model.eval()
+    images = synthetic_images(batch, seed=int(g["meta"][2])).cuda()
+    targets = [{"labels": torch.zeros(1, dtype=torch.int64), "keypoints": torch.rand(1, 51)} for _ in range(batch)]
+    out = model(images, targets)
+    assert out["pred_keypoints"].shape == (batch, 60, 34)
+    np.testing.assert_allclose(out["pred_keypoints"].cpu().numpy(), g["out_pred_keypoints"].reshape(batch, 60, 34),
+                               atol=1e-3)
+    ts = torch.tensor(np.tile(g["pp_target_size"], (batch, 1)), device="cuda")
+    res = PostProcess(60, 17)(out, ts)
+    assert isinstance(res, list) and len(res) == batch
+    exp = np.concatenate([g["pp_keypoints"], np.ones_like(g["pp_keypoints"][..., :1])], -1).reshape(batch, 60, 51)
+    for b, r in enumerate(res):
+        np.testing.assert_allclose(r["scores"].cpu().numpy(), g["pp_scores"][b], atol=1e-3)
+        np.testing.assert_array_equal(r["labels"].cpu().numpy(), g["pp_labels"][b])
+        np.testing.assert_allclose(r["keypoints"].cpu().numpy(), exp[b], atol=640 * 1e-3)
+    with pytest.raises(NotImplementedError):
+        model.train()(images, targets)
+
+
+def test_deploy_model_boundary(golden_dir):
+    """tools/deployment/export_onnx.py:46-56: Model(images, orig_target_sizes) ->
+    (scores, labels, keypoints); eager and hipGraph-replay forms agree with the golden
+    deploy PostProcess."""
+    from detrpose_amd.export import DeployModel
+    size, batch = "n", 2
+    g = np.load(os.path.join(golden_dir, f"detrpose_{size}_b{batch}.npz"))
+    model, pp = _model(golden_dir, size, g, "fp32")
+    dm = DeployModel(model, pp)
+    images = synthetic_images(batch, seed=int(g["meta"][2])).cuda()
+    ts = torch.tensor(np.tile(g["pp_target_size"], (batch, 1)), device="cuda")
+    for s, l, k in (dm(images, ts), dm.replay(images, ts)):
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(s.cpu().numpy(), g["pp_scores"], atol=1e-3)
+        np.testing.assert_array_equal(l.cpu().numpy(), g["pp_labels"])
+        np.testing.assert_allclose(k.cpu().numpy(), g["pp_keypoints"], atol=640 * 1e-3)
+    with pytest.raises(ValueError):
+        model(torch.rand(1, 3, 320, 320, device="cuda"))

@@ -71,3 +71,18 @@ def test_oracle_misc(golden_dir):
                                    atol=1e-6)
     for size, C in (("n", 128), ("l", 256), ("x", 384)):
         np.testing.assert_allclose(sine_pos_embed_2d(20, 20, C // 2, 20).numpy(), g[f"pos_embed_{size}"], atol=1e-6)
+
+
+def test_oracle_forced_selection(golden_dir, manifest):
+    """force_topk (the hook the bf16 GPU test uses) with the reference's own selection
+    reproduces the reference outputs; a different selection changes them."""
+    g = _load(golden_dir, "n", 2)
+    sd = synthetic_state_dict(manifest["n"], seed=int(g["meta"][1]))
+    orc = OracleDETRPose(get_config("n"), sd)
+    img = synthetic_images(2, seed=int(g["meta"][2]))
+    out = orc(img, force_topk=torch.from_numpy(g["topk_idx"]))
+    np.testing.assert_allclose(out["pred_keypoints"].numpy(), g["out_pred_keypoints"], atol=1e-4)
+    np.testing.assert_allclose(out["pred_logits"].numpy(), g["out_pred_logits"], atol=1e-4)
+    other = torch.from_numpy(g["topk_idx"]).flip(1)
+    out2 = orc(img, force_topk=other)
+    assert (out2["pred_keypoints"] - out["pred_keypoints"]).abs().max() > 1e-3
