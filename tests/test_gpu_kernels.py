@@ -289,6 +289,39 @@ def test_msda_golden(golden_dir, dt, size):
         _close(out.reshape(N, Lq, Cc), O.msda_core(vd.float().cpu(), shapes, loc2, a2), dt, "msda vs oracle(bf16)")
 
 
+@pytest.mark.parametrize("size", ["n", "l", "x"])
+def test_msda_batched(size):
+    """dp_msda (bf16 wave-per-token path) on a multi-image batch at the model's real level
+    geometry: tokens of several images, XCD-sliced block order, points falling outside the
+    maps (zero corners) -- vs the oracle's ms_deform_attn_core restatement on the same
+    bf16-rounded inputs (tolerance: bf16 storage, 2.5e-2 of the output scale)."""
+    lib = _lib.load()
+    cfg = {"n": (2, 6, 16, [(40, 40), (20, 20)]), "l": (3, 4, 32, [(80, 80), (40, 40), (20, 20)]),
+           "x": (3, 4, 48, [(80, 80), (40, 40), (20, 20)])}[size]
+    L, P, dh, shapes = cfg
+    H, B, Lq = 8, 3, 1080
+    S = sum(h * w for h, w in shapes)
+    Cc = H * dh
+    g = torch.Generator().manual_seed(7)
+    value = torch.randn(B, S, Cc, generator=g).bfloat16()
+    ref_pt = torch.rand(B, Lq, 2, generator=g) * 1.2 - 0.1
+    off = torch.randn(B * Lq, H * L * P * 2, generator=g) * 3.0
+    logits = torch.randn(B * Lq, H * L * P, generator=g)
+    oad = torch.cat([off, logits], 1).to("cuda", torch.bfloat16).contiguous()
+    vd = value.cuda()
+    out = torch.empty(B * Lq, Cc, device="cuda", dtype=torch.bfloat16)
+    hw = (C.c_int32 * (2 * L))(*[v for s in shapes for v in s])
+    _lib.check(lib.dp_msda(vd.data_ptr(), B, S, hw, L, oad.data_ptr(), _d(ref_pt), out.data_ptr(), Cc,
+                           Lq, H, dh, P, DTYPES["bf16"][1], _s()))
+    torch.cuda.synchronize()
+    oa = oad.float().cpu()
+    wh = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32)
+    loc = ref_pt[:, :, None, None, None, :] + oa[:, :H * L * P * 2].reshape(B, Lq, H, L, P, 2) / \
+        wh[None, None, None, :, None, :]
+    a = torch.softmax(oa[:, H * L * P * 2:].reshape(B, Lq, H, L * P), -1).reshape(B, Lq, H, L, P)
+    _close(out.reshape(B, Lq, Cc), O.msda_core(value.float(), shapes, loc, a), "bf16", "msda batched vs oracle")
+
+
 @pytest.mark.parametrize("n,k", [(8400, 60), (2000, 60), (120, 60), (300, 256), (17, 4)])
 def test_topk(n, k):
     lib = _lib.load()
