@@ -12,6 +12,7 @@
 // the across-instance transpose of the reference (transformer.py:409,419) is only an
 // index change here.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -281,6 +282,174 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(const bf16_t* __restrict
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// bf16 short-sequence path (seq <= 16*KT, the decoder's within-instance 18 and
+// across-instance 60): one wave per (sequence, head), no online softmax, no LDS for P.
+//  * S^T = K Q^T on v_mfma_f32_16x16x32_bf16 (K as the A operand, Q as B, both loaded in
+//    fragment layout straight from the projection rows), so lane (lr, lg) of tile (j, i)
+//    holds S^T[key 16j+4lg+r][query 16i+lr]: the softmax axis (keys) sits in the lane's
+//    registers and across the 4 lane groups (2 xor-shuffles per reduction).
+//  * O^T = V^T P^T: the lane's P values of tiles (2m, 2m+1) ARE its B fragment for the
+//    32-key step m, with k-slot s <-> key 32m + (s < 4 ? 4lg+s : 16+4lg+s-4); the A fragment
+//    (V^T in the same k order) comes from V staged row-major in LDS through two
+//    ds_read_b64_tr_b16 per (m, 16 head-dim rows): group lg reads the 4x16 blocks at keys
+//    32m+4lg and 32m+16+4lg, delivered column-major (row pitch chosen bank-conflict free).
+//  * Output: lane holds O^T[dh 16d+4lg+r][query 16i+lr] -> 8-byte stores of 4 channels.
+// Padded keys get S = -inf and zero V rows; padded queries are computed and not stored.
+template <int DH, int KT>
+__global__ __launch_bounds__(256) void attn_short_kernel(const bf16_t* __restrict__ q, int ld_q,
+                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                         int ld_kv, bf16_t* __restrict__ out, int ld_o, int n_inner,
+                                                         int64_t so, int64_t si, int64_t st, int seqlen, int nhead,
+                                                         int npairs, float scale) {
+  constexpr int KS = (DH + 31) / 32;             // 32-deep k-steps over the head dim
+  constexpr int ND = DH / 16;                    // 16-row head-dim tiles of O^T
+  constexpr int NK = 16 * KT;                    // padded keys (= padded queries)
+  constexpr int DHP = DH == 16 ? 16 : 48;        // V row pitch (elements): conflict-free tr reads
+  constexpr int VCH = DH / 8;                    // 16-byte chunks per V row
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) bf16_t vl[4][NK * DHP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pair = blockIdx.x * 4 + wave;
+  if (pair >= npairs) return;                    // wave-uniform: EXEC stays full below
+  const int h = pair % nhead, sq = pair / nhead;
+  const int o = sq / n_inner, ii = sq - o * n_inner;
+  const int64_t base = (int64_t)o * so + (int64_t)ii * si;
+  const int lr = lane & 15, lg = lane >> 4;
+  bf16_t* V = vl[wave];
+
+  // V rows -> LDS (row-major, zero rows past seqlen)
+#pragma unroll
+  for (int t = 0; t < (NK * VCH + 63) / 64; ++t) {
+    const int c = lane + 64 * t;
+    if (c < NK * VCH) {
+      const int key = c / VCH, dc = c - key * VCH;
+      bf16x8 vv = bf16x8{};
+      if (key < seqlen) vv = *reinterpret_cast<const bf16x8*>(v + (base + (int64_t)key * st) * ld_kv + h * DH + dc * 8);
+      *reinterpret_cast<bf16x8*>(V + key * DHP + dc * 8) = vv;
+    }
+  }
+  // Q (B operand, query columns) and K (A operand, key rows) fragments
+  bf16x8 qf[KT][KS], kf[KT][KS];
+#pragma unroll
+  for (int i = 0; i < KT; ++i)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int row = 16 * i + lr, d0 = 32 * ks + 8 * lg;
+      const bool ok = row < seqlen && d0 < DH;
+      const int64_t rb = base + (int64_t)row * st;
+      qf[i][ks] = ok ? *reinterpret_cast<const bf16x8*>(q + rb * ld_q + h * DH + d0) : bf16x8{};
+      kf[i][ks] = ok ? *reinterpret_cast<const bf16x8*>(k + rb * ld_kv + h * DH + d0) : bf16x8{};
+    }
+  // S^T tiles
+  f32x4 s[KT][KT];   // [j key tile][i query tile]
+#pragma unroll
+  for (int j = 0; j < KT; ++j)
+#pragma unroll
+    for (int i = 0; i < KT; ++i) {
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[j][ks], qf[i][ks], a, 0, 0, 0);
+      s[j][i] = a;
+    }
+  // softmax over keys for each query column (lane lr of tile i)
+  float inv[KT];
+#pragma unroll
+  for (int i = 0; i < KT; ++i) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < KT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * j + 4 * lg + r;
+        const float x = key < seqlen ? s[j][i][r] * scale : -INFINITY;
+        s[j][i][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < KT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __expf(s[j][i][r] - mx);
+        s[j][i][r] = p;
+        sum += p;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    inv[i] = 1.f / sum;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // O^T = V^T P^T over 32-key steps
+  f32x4 oacc[ND][KT];
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int i = 0; i < KT; ++i) oacc[d][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q4 = (lane & 15) >> 2, p4 = lane & 3;   // tr-read address roles within the 16-lane group
+#pragma unroll
+  for (int m = 0; m < KT / 2; ++m) {
+    bf16x8 pf[KT];
+#pragma unroll
+    for (int i = 0; i < KT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[i][r] = (bf16_t)s[2 * m][i][r];
+        pf[i][4 + r] = (bf16_t)s[2 * m + 1][i][r];
+      }
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      const bf16_t* a0 = V + (32 * m + 4 * lg + q4) * DHP + 16 * d + 4 * p4;
+      const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0));
+      const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0 + 16 * DHP));
+      bf16x8 vf;
+      short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      vf = *reinterpret_cast<const bf16x8*>(tmp);
+#pragma unroll
+      for (int i = 0; i < KT; ++i) oacc[d][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[i], oacc[d][i], 0, 0, 0);
+    }
+  }
+  // store: query 16i+lr, channels 16d + 4lg .. +3 (8 bytes)
+#pragma unroll
+  for (int i = 0; i < KT; ++i) {
+    const int qi = 16 * i + lr;
+    if (qi >= seqlen) continue;
+    bf16_t* op = out + (base + (int64_t)qi * st) * ld_o + h * DH;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16_t)(oacc[d][i][r] * inv[i]);
+      *reinterpret_cast<bf16x4*>(op + 16 * d + 4 * lg) = w;
+    }
+  }
+}
+
+template <int DH, int KT>
+int launch_short(const void* q, int ld_q, const void* k, const void* v, int ld_kv, void* out, int ld_o, int n_outer,
+                 int n_inner, int64_t so, int64_t si, int64_t st, int seqlen, int nhead, hipStream_t s) {
+  const int npairs = n_outer * n_inner * nhead;
+  dim3 grid((unsigned)((npairs + 3) / 4)), block(256);
+  hipLaunchKernelGGL((attn_short_kernel<DH, KT>), grid, block, 0, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
+                     (const bf16_t*)v, ld_kv, (bf16_t*)out, ld_o, n_inner, so, si, st, seqlen, nhead, npairs,
+                     1.f / sqrtf((float)DH));
+  return dp_check_launch("dp_attention(short)");
+}
+
+template <int DH>
+int launch_short_any(const void* q, int ld_q, const void* k, const void* v, int ld_kv, void* out, int ld_o,
+                     int n_outer, int n_inner, int64_t so, int64_t si, int64_t st, int seqlen, int nhead,
+                     hipStream_t s) {
+  if (seqlen <= 32)
+    return launch_short<DH, 2>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+  return launch_short<DH, 4>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+}
+
 template <int DH>
 int launch_mfma(const void* q, int ld_q, const void* k, const void* v, int ld_kv, void* out, int ld_o, int n_outer,
                 int n_inner, int64_t so, int64_t si, int64_t st, int seqlen, int nhead, hipStream_t s) {
@@ -304,6 +473,13 @@ extern "C" int dp_attention(const void* q, int32_t ld_q, const void* k, const vo
   hipStream_t s = as_stream(stream);
   const bool al = ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) | reinterpret_cast<uintptr_t>(v)) &
                    15) == 0 && ld_q % 8 == 0 && ld_kv % 8 == 0;
+  const bool al8 = ((reinterpret_cast<uintptr_t>(out) & 7) == 0) && ld_o % 4 == 0;
+  static const bool no_short = getenv("DETRPOSE_ATTN_NO_SHORT") != nullptr;
+  if (dtype == DP_BF16 && al && al8 && seqlen <= 64 && !no_short) {
+    if (dh == 16) return launch_short_any<16>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+    if (dh == 32) return launch_short_any<32>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+    if (dh == 48) return launch_short_any<48>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+  }
   if (dtype == DP_BF16 && al) {
     if (dh == 16) return launch_mfma<16>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
     if (dh == 32) return launch_mfma<32>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);

@@ -222,12 +222,12 @@ def _attn_ref(q, k, v, nh):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("geom", ["within", "across", "aifi", "aifi_x", "within_n"])
+@pytest.mark.parametrize("geom", ["within", "across", "aifi", "aifi_x", "within_n", "across_n", "within_x", "across_x"])
 def test_attention(dt, geom):
     lib = _lib.load()
     torch.manual_seed(len(geom))
     B, nq, T = 2, 60, 18
-    Cc = {"aifi_x": 384, "within_n": 128}.get(geom, 256)
+    Cc = {"aifi_x": 384, "within_n": 128, "across_n": 128, "within_x": 384, "across_x": 384}.get(geom, 256)
     nh = 8
     rows = B * 400 if geom.startswith("aifi") else B * nq * T
     qkv = torch.randn(rows, 3 * Cc)
@@ -239,7 +239,7 @@ def test_attention(dt, geom):
     if geom.startswith("within"):
         args = (B * nq, 1, T, 0, 1, T)
         seqs = q32.reshape(B * nq, T, 3 * Cc)
-    elif geom == "across":
+    elif geom.startswith("across"):
         args = (B, T, nq * T, 1, T, nq)
         seqs = q32.reshape(B, nq, T, 3 * Cc).transpose(1, 2).reshape(B * T, nq, 3 * Cc)
     else:
@@ -248,7 +248,7 @@ def test_attention(dt, geom):
     _lib.check(lib.dp_attention(qd.data_ptr(), 3 * Cc, qd.data_ptr() + Cc * e, qd.data_ptr() + 2 * Cc * e, 3 * Cc,
                                 out.data_ptr(), Cc, *args, nh, Cc // nh, DTYPES[dt][1], _s()))
     ref = _attn_ref(seqs[..., :Cc], seqs[..., Cc:2 * Cc], seqs[..., 2 * Cc:], nh)
-    if geom == "across":
+    if geom.startswith("across"):
         ref = ref.reshape(B, T, nq, Cc).transpose(1, 2)
     torch.cuda.synchronize()
     _close(out.reshape(-1, Cc), ref.reshape(-1, Cc), dt, geom)
