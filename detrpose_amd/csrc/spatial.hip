@@ -7,6 +7,8 @@
 // they are plain 16-byte-vector VALU kernels with consecutive threads on consecutive
 // channel chunks (coalesced pixel rows).
 #include "common.h"
+#include "conv_lds.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -163,6 +165,133 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, 
   store16(out + (int64_t)b * obs + (int64_t)rem * ops + cc * VEC, o);
 }
 
+
+// Depthwise k x k, bf16, LDS-tiled (production path for channels % 64 == 0): a block owns
+// a TH x TW tile of output pixels x 64 channels. The ((TH-1)S+KS) x ((TW-1)S+KS) input
+// patch is read ONCE with whole 128-byte pixel lines (8 lanes per pixel) into LDS (zeros
+// outside the map = the conv padding), then each thread computes PX consecutive outputs of
+// one 16-byte channel chunk from LDS with a register sliding window per kernel row. Block
+// order is XCD-sliced (logical = (blockIdx % 8) * (G / 8) + blockIdx / 8, channel chunk
+// fastest), so the tiles that share a halo row run on one XCD and re-read it from its L2,
+// not from HBM (the per-thread kernel above re-fetched each input row from up to KS XCDs).
+template <int KS, int S, int TH, int TW, int PX, int ACT>
+__global__ __launch_bounds__(256) void dwconv_lds_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int nchk,
+                                                         int ntiles) {
+  constexpr int PH = (TH - 1) * S + KS, PW = (TW - 1) * S + KS;
+  constexpr int NIN = (PX - 1) * S + KS;
+  constexpr int GX = TW / PX;
+  static_assert(TW % PX == 0, "tile");
+  extern __shared__ __attribute__((aligned(16))) char patch[];   // [PH][PW][128 B]
+  const int G = gridDim.x;
+  const int L = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  if (L >= ntiles) return;
+  const int ck = L % nchk;
+  int rest = L / nchk;
+  const int tx = rest % tiles_x;
+  rest /= tiles_x;
+  const int ty = rest % tiles_y, b = rest / tiles_y;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - d.pad_t, ix0 = ox0 * S - d.pad_l;
+  const int tid = threadIdx.x;
+  const bf16_t* in = reinterpret_cast<const bf16_t*>(d.in) + (int64_t)b * d.in_bstride + ck * 64;
+
+  // ---- patch -> LDS by LDS-DMA: every 16-byte piece of the patch in flight at once
+  // (no staging VGPRs); the buffer descriptor returns 0 for the out-of-map offsets
+  {
+    const int wave = tid >> 6, lane = tid & 63;
+    const dpconv::i32x4 rs = dpconv::make_rsrc(in);
+    constexpr int NE = PH * PW * 8;
+    for (int e0 = wave * 64; e0 < NE; e0 += 256) {
+      const int e = e0 + lane;
+      const int px = e >> 3, c = e & 7;
+      const int py = px / PW, pxx = px - py * PW;
+      const int iy = iy0 + py, ix = ix0 + pxx;
+      const bool ok = e < NE && (unsigned)iy < (unsigned)d.in_h && (unsigned)ix < (unsigned)d.in_w;
+      const int o = ok ? ((iy * d.in_w + ix) * d.in_pstride + c * 8) * 2 : dpconv::OOB;
+      dpconv::dma16(rs, patch + e0 * 16, o);
+    }
+  }
+  // the block's 64 channels of the KS*KS tap weights (f32) behind the patch
+  float* wl = reinterpret_cast<float*>(patch + (PH * PW * 128 + 1023) / 1024 * 1024);   // past the last DMA group
+  for (int e = tid; e < KS * KS * 16; e += 256) {
+    const int tap = e >> 4, q = e & 15;
+    *reinterpret_cast<f32x4*>(wl + tap * 64 + 4 * q) =
+        *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(d.weight) + tap * d.cin + ck * 64 + 4 * q);
+  }
+  dpconv::wait_vmcnt<0>();
+  __syncthreads();
+
+  // ---- compute: item = ((row * GX) + xg) * 8 + chunk
+  const float* w = wl;
+  for (int it = tid; it < TH * GX * 8; it += 256) {
+    const int c = it & 7, pg = it >> 3;
+    const int row = pg / GX, xg = pg - row * GX;
+    const int oy = oy0 + row, oxb = ox0 + xg * PX;
+    if (oy >= d.out_h || oxb >= d.out_w) continue;
+    const int c0 = c * 8;
+    float acc[PX][8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float bv = d.bias ? d.bias[ck * 64 + c0 + t] : 0.f;
+#pragma unroll
+      for (int p = 0; p < PX; ++p) acc[p][t] = bv;
+    }
+#pragma unroll 1
+    for (int ky = 0; ky < KS; ++ky) {
+      const char* prow = patch + ((row * S + ky) * PW + xg * PX * S) * 128 + c * 16;
+      bf16x8 xin[NIN];
+#pragma unroll
+      for (int j = 0; j < NIN; ++j) xin[j] = *reinterpret_cast<const bf16x8*>(prow + j * 128);
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {
+        const float* wk = w + (ky * KS + kx) * 64 + c0;
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(wk), w1 = *reinterpret_cast<const f32x4*>(wk + 4);
+        const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+        for (int p = 0; p < PX; ++p)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[p][t] = fmaf((float)xin[p * S + kx][t], wv[t], acc[p][t]);
+      }
+    }
+    bf16_t* out = reinterpret_cast<bf16_t*>(d.out) + (int64_t)b * d.out_bstride + ck * 64 + c0;
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+      const int ox = oxb + p;
+      if (ox >= d.out_w) break;
+      bf16x8 o;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        float v = dpconv::act_t<ACT>(acc[p][t]);
+        if (d.has_lab) v = d.lab_scale * v + d.lab_bias;
+        o[t] = (bf16_t)v;
+      }
+      *reinterpret_cast<bf16x8*>(out + ((int64_t)oy * d.out_w + ox) * d.out_pstride) = o;
+    }
+  }
+}
+
+template <int KS, int S, int TH, int TW, int PX>
+int launch_dw_lds(const dp_conv_desc& d, hipStream_t s) {
+  constexpr int PH = (TH - 1) * S + KS, PW = (TW - 1) * S + KS;
+  constexpr int lds = (PH * PW * 128 + 1023) / 1024 * 1024 + KS * KS * 64 * 4;   // DMA groups are whole 1 KB
+  static_assert(lds <= 64 * 1024, "patch");
+  const int tiles_x = (d.out_w + TW - 1) / TW, tiles_y = (d.out_h + TH - 1) / TH, nchk = d.cin / 64;
+  const int64_t ntiles = (int64_t)d.batch * tiles_y * tiles_x * nchk;
+  DP_REQUIRE(ntiles < (1ll << 30), "dp_dwconv2d: too many tiles");
+  const int grid = (int)((ntiles + 7) / 8 * 8);
+#define DP_DWL(A_)                                                                                          \
+  hipLaunchKernelGGL((dwconv_lds_kernel<KS, S, TH, TW, PX, A_>), dim3(grid), dim3(256), lds, s, d, tiles_x, \
+                     tiles_y, nchk, (int)ntiles)
+  switch (d.act) {
+    case DP_ACT_RELU: DP_DWL(DP_ACT_RELU); break;
+    case DP_ACT_SILU: DP_DWL(DP_ACT_SILU); break;
+    case DP_ACT_GELU: DP_DWL(DP_ACT_GELU); break;
+    default: DP_DWL(DP_ACT_NONE); break;
+  }
+#undef DP_DWL
+  return dp_check_launch("dp_dwconv2d(lds)");
+}
+
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
@@ -176,13 +305,19 @@ extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
   DP_REQUIRE(d.in_pstride % VEC == 0 && d.out_pstride % VEC == 0 && d.in_bstride % VEC == 0 &&
                  d.out_bstride % VEC == 0 && al16(d.in) && al16(d.out) && al16(d.weight),
              "dp_dwconv2d: 16-byte alignment required");
+  hipStream_t s = as_stream(stream);
+  static const bool no_lds = getenv("DETRPOSE_DW_NO_LDS") != nullptr;
+  if (d.dtype == DP_BF16 && d.cin % 64 == 0 && !no_lds) {
+    if (d.kh == 5 && d.kw == 5 && d.stride == 1) return launch_dw_lds<5, 1, 8, 20, 5>(d, s);
+    if (d.kh == 3 && d.kw == 3 && d.stride == 1) return launch_dw_lds<3, 1, 8, 20, 5>(d, s);
+    if (d.kh == 3 && d.kw == 3 && d.stride == 2) return launch_dw_lds<3, 2, 4, 16, 2>(d, s);
+  }
   const int nchunk = d.cin / VEC;
   constexpr int PX = 4;
   const int ntx = (d.out_w + PX - 1) / PX;
   const int64_t total = (int64_t)d.batch * d.out_h * ntx * nchunk;
   DP_REQUIRE(total < (1ll << 31), "dp_dwconv2d: %lld work items exceed 2^31", (long long)total);
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
-  hipStream_t s = as_stream(stream);
 #define DP_DW(T_, KS_, S_)                                                                            \
   if (d.kh == KS_ && d.kw == KS_ && d.stride == S_) {                                                \
     hipLaunchKernelGGL((dwconv_kernel<T_, KS_, S_, PX>), grid, block, 0, s, d, total, nchunk, ntx); \

@@ -138,6 +138,23 @@ def test_dwconv(dt, k, s):
     _close(out, ref.permute(0, 2, 3, 1), dt, f"dw{k}s{s}")
 
 
+@pytest.mark.parametrize("k,s,c,hw", [(5, 1, 192, 40), (3, 2, 512, 80), (3, 2, 128, 33), (5, 1, 384, 20)])
+def test_dwconv_model_shapes(k, s, c, hw):
+    """The LDS-tiled bf16 depthwise path at HGNetv2-L stage shapes (several tiles per image,
+    partial edge tiles, 64-channel blocks) vs torch fp32 conv2d on the bf16-rounded input."""
+    torch.manual_seed(k * c)
+    pk = Packer({}, "bf16", torch.device("cuda"))
+    x = torch.randn(3, c, hw, hw).bfloat16().float()
+    w = torch.randn(c, 1, k, k) / k
+    b = torch.randn(c) * 0.1
+    pc = pk.dwconv(w.double(), b.double(), s, act="relu")
+    ref = F.relu(F.conv2d(x, w, b, s, (k - 1) // 2, groups=c))
+    out = torch.empty(3, ref.shape[2], ref.shape[3], c, device="cuda", dtype=torch.bfloat16)
+    _run_conv(pc, _nhwc(x, "bf16"), out, "bf16")
+    torch.cuda.synchronize()
+    _close(out, ref.permute(0, 2, 3, 1), "bf16", f"dw{k}s{s}c{c}")
+
+
 @pytest.mark.parametrize("dt", DT)
 def test_stem_conv_and_pool(dt):
     lib = _lib.load()
