@@ -19,8 +19,8 @@ def family(name):
     # every implicit-GEMM conv variant (conv_stream/halo/glds/gemm_kernel) is one family
     if re.search(r"conv_(stream|halo|glds|gemm)_kernel", name):
         return "conv"
-    for key in ("dwconv_kernel", "layernorm_kernel", "attn_mfma_kernel",
-                "msda_kernel", "add_rows_kernel", "stem_conv_kernel", "maxpool_kernel", "class_max_kernel",
+    for key in ("dwconv_kernel", "dwconv_lds_kernel", "layernorm_kernel", "attn_mfma_kernel", "attn_short_kernel",
+                "msda_kernel", "msda_wave_kernel", "add_rows_kernel", "stem_conv_kernel", "maxpool_kernel", "class_max_kernel",
                 "topk_kernel", "gate_ln_kernel", "sine_embed_kernel", "lqe_kernel", "pose_refine_kernel"):
         if key in name:
             return key
