@@ -55,6 +55,7 @@ _SIGS = {
     "dp_dwconv2d": (i32, [C.POINTER(ConvDesc), vp]),
     "dp_stem_conv": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, f32, f32, vp, i64, i32, i32, vp]),
     "dp_maxpool2x2_pad_rb": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, vp]),
+    "dp_conv2d_pool": (i32, [C.POINTER(ConvDesc), vp, i64, i32, vp]),
     "dp_add_rows": (i32, [vp, RowMap, vp, RowMap, vp, RowMap, i32, i32, i32, vp]),
     "dp_layernorm": (i32, [vp, RowMap, vp, RowMap, vp, RowMap, vp, vp, f32, i32, i32, vp, RowMap, i32, i32,
                            vp, i32, vp, i32, vp]),

@@ -1,4 +1,4 @@
-// Shared epilogue of the implicit-GEMM conv kernels (conv_gemm.hip, conv_glds.hip):
+// Epilogue of the f32 implicit-GEMM conv kernel (conv_gemm.hip):
 // bias (folded BN) + activation + LAB into an LDS tile, then 16-byte row writes with the
 // residual add, the optional nearest-x2 copy (FPN upsample + concat) and bf16/f32 output.
 #pragma once

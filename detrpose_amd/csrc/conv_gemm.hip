@@ -1,4 +1,5 @@
-// Implicit-GEMM convolution / linear for gfx950 (MFMA), NHWC.
+// Implicit-GEMM convolution / linear for gfx950 (MFMA), NHWC: the f32 (parity mode)
+// kernel and the dp_conv2d entry point; bf16 dispatches to conv_halo.hip / conv_stream.hip.
 //
 // Replaces every dense nn.Conv2d(+BN)(+act) and nn.Linear on the DETRPose forward:
 //   ConvBNAct (hgnetv2.py:82-134), ConvNormLayer(_fuse) (hybrid_encoder.py:56-128),
@@ -230,24 +231,12 @@ int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   return dp_check_launch("dp_conv2d");
 }
 
-// conv_glds.hip / conv_stream.hip
+// conv_stream.hip / conv_halo.hip
 }  // namespace
-int dp_conv2d_glds(const dp_conv_desc& d, hipStream_t s, int vec_ok);
 int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok);
 int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok);
+int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps);
 namespace {
-
-// bf16 conv path: persistent LDS-DMA kernel by default; DETRPOSE_CONV_PATH=glds|v2 selects
-// the one-tile-per-block LDS-DMA kernel or the register-staged kernel (A/B switch)
-int bf16_path() {
-  static const int v = [] {
-    const char* e = getenv("DETRPOSE_CONV_PATH");
-    if (e && strcmp(e, "v2") == 0) return 0;
-    if (e && strcmp(e, "glds") == 0) return 1;
-    return 2;
-  }();
-  return v;
-}
 
 template <typename T, typename TO>
 int dispatch(const dp_conv_desc& d, hipStream_t s) {
@@ -259,20 +248,14 @@ int dispatch(const dp_conv_desc& d, hipStream_t s) {
   if (d.up) vec_ok = vec_ok && (d.up_pstride % VO == 0) && (d.up_bstride % VO == 0) && al(d.up);
   const int M = d.batch * d.out_h * d.out_w;
   if constexpr (sizeof(T) == 2) {
-    const int path = bf16_path();
-    if (path == 2) {
-      if (d.kh * d.kw > 1) {
-        const int r = dp_conv2d_halo(d, s, vec_ok);
-        if (r >= 0) return r;
-      }
-      return dp_conv2d_stream(d, s, vec_ok);
+    // bf16: LDS halo-tile kernel for the KxK convs it covers, persistent LDS-DMA GEMM otherwise
+    if (d.kh * d.kw > 1) {
+      int r = d.kh == 2 ? dp_conv2d_stem2x2(d, s, nullptr, 0, 0) : -1;   // stem 2x2: register-direct
+      if (r >= 0) return r;
+      r = dp_conv2d_halo(d, s, vec_ok);
+      if (r >= 0) return r;
     }
-    if (path == 1) return dp_conv2d_glds(d, s, vec_ok);
-  }
-  if constexpr (sizeof(TO) != sizeof(T)) {  // f32-output heads: few shapes
-    if (d.cout <= 16) return launch<T, TO, 128, 16, BK, 4>(d, s, vec_ok);
-    if (M <= 8192) return launch<T, TO, 64, 128, BK, 2>(d, s, vec_ok);
-    return launch<T, TO, 128, 128, BK, 2>(d, s, vec_ok);
+    return dp_conv2d_stream(d, s, vec_ok);
   } else {
     constexpr int SB = DP_SMALLN_BM;
     if (d.cout <= 16) return launch<T, TO, SB, 16, BK, 4>(d, s, vec_ok);

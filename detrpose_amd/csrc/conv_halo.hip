@@ -14,6 +14,9 @@
 // otherwise streamed per K-step through a 2-deep ring. MFMA and register epilogue as in
 // conv_stream.hip (weights are the A operand, pixels the B operand, permuted weight rows so
 // a lane holds 4*TN contiguous output channels of one pixel).
+// POOL (the stem's 2x2 conv, stem2a): the patch in LDS is exactly the zero-padded 2x2 window
+// of F.pad(x,(0,1,0,1)) + MaxPool2d(2, 1), so the same kernel also writes the stem max-pool
+// (hgnetv2.py:213-220) from LDS: one pass over stem1's output instead of two.
 #include "conv_lds.h"
 #include <stdlib.h>
 #include <type_traits>
@@ -35,9 +38,17 @@ struct HaloGeom {
 // DMA'd while the current tile computes (only patch DMAs are in flight, so the per-tile
 // vmcnt(0) retires exactly the prefetched patch). !RESW: one patch buffer, weights through a
 // 2-deep ring per K-step; the second resident block on the CU overlaps the patch loads.
-template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT>
+// 2x2 max-pool output written by the POOL instantiation (NHWC bf16, cin channels)
+struct HaloPool {
+  bf16_t* out;
+  int64_t bstride;
+  int pstride;
+};
+
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 2)))
-void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int vec_ok) {
+void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int vec_ok, HaloPool pool) {
+  static_assert(!POOL || (KH == 2 && KW == 2 && S == 1 && !DBUF), "pool: 2x2 s1 window, single patch buffer");
   using Gm = HaloGeom<TH, KH, KW, S>;
   constexpr int TW = Gm::TW;
   constexpr int BM = TH * TW, WM = BM / NW, TM = WM / 16, TN = BN / 16, NPL = 4 * TN;
@@ -196,13 +207,38 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
         if (oy < d.out_h && ox < d.out_w) epi_pixel<ACT, bf16_t, TN>(d, acc[i], bias, b, oy, ox, 0, g, full);
       }
     }
+    if constexpr (POOL) {
+      // max over the 2x2 window (yq + dy, q + dx) of the patch, 8 channels (chunk c8) per
+      // lane; zero-filled patch pixels past the right/bottom edge are the F.pad zeros
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int yq = wm * TM + i;
+        const int oy = oy0 + yq, ox = ox0 + q;
+        if (oy >= d.out_h || ox >= d.out_w) continue;
+        bf16_t* po = pool.out + (int64_t)b * pool.bstride + (int64_t)(oy * d.out_w + ox) * pool.pstride;
+        for (int c8 = g; c8 < (cin >> 3); c8 += 4) {
+          float m[8];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int pr = (yq + (t >> 1)) * Gm::PW + q + (t & 1);
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(pbase + pr * 128 + ((c8 ^ (pr & 7)) << 4));
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m[e] = t ? fmaxf(m[e], (float)v[e]) : (float)v[e];
+          }
+          Vec16<bf16_t> o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.set(e, m[e]);
+          store16(po + c8 * 8, o);
+        }
+      }
+    }
   }
   wait_vmcnt<0>();
 }
 
-template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT>
-int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds) {
-  auto kern = conv_halo_kernel<TH, NW, KH, KW, S, BN, RESW, DBUF, ACT>;
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false>
+int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloPool pool = {}) {
+  auto kern = conv_halo_kernel<TH, NW, KH, KW, S, BN, RESW, DBUF, ACT, POOL>;
   static const int occ = [&] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
@@ -225,16 +261,16 @@ int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds) {
   if (grid > need) grid = need;
   grid = grid / 8 * 8;
   if (grid < 8) grid = 8;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, d, tiles_x, tiles_y, ntiles, vec_ok);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, d, tiles_x, tiles_y, ntiles, vec_ok, pool);
   return dp_check_launch("dp_conv2d(halo)");
 }
 
-template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF = false>
-int launch_halo_act(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds) {
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF = false, bool POOL = false>
+int launch_halo_act(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloPool pool = {}) {
   switch (d.act) {
-    case DP_ACT_RELU: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_RELU>(d, s, vec_ok, lds);
-    case DP_ACT_SILU: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_SILU>(d, s, vec_ok, lds);
-    case DP_ACT_NONE: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_NONE>(d, s, vec_ok, lds);
+    case DP_ACT_RELU: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_RELU, POOL>(d, s, vec_ok, lds, pool);
+    case DP_ACT_SILU: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_SILU, POOL>(d, s, vec_ok, lds, pool);
+    case DP_ACT_NONE: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_NONE, POOL>(d, s, vec_ok, lds, pool);
     default: return -1;
   }
 }
@@ -268,4 +304,38 @@ int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
     return -1;
   }
   return -1;
+}
+
+int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps);
+
+// dp_conv2d of a 2x2 s1 bf16 conv (pad 0, zero read past the right/bottom edge) that also
+// writes MaxPool2d(2, 1) of the same zero-padded input: StemBlock's stem2a + pool
+// (hgnetv2.py:213-220), i.e. dp_conv2d followed by dp_maxpool2x2_pad_rb in one pass.
+extern "C" int dp_conv2d_pool(const dp_conv_desc* dp, void* pool_out, int64_t pool_bstride, int32_t pool_pstride,
+                              void* stream) {
+  DP_REQUIRE(dp != nullptr && pool_out != nullptr, "dp_conv2d_pool: null pointer");
+  const dp_conv_desc& d = *dp;
+  DP_REQUIRE(d.dtype == DP_BF16 && !d.out_f32 && !d.res && !d.up, "dp_conv2d_pool: bf16 conv without res/up only");
+  DP_REQUIRE(d.kh == 2 && d.kw == 2 && d.stride == 1 && d.pad_t == 0 && d.pad_l == 0,
+             "dp_conv2d_pool: 2x2 stride-1 conv with right/bottom zero padding only");
+  DP_REQUIRE(d.out_h == d.in_h && d.out_w == d.in_w, "dp_conv2d_pool: output must keep the input size");
+  DP_REQUIRE(d.cin % 8 == 0 && d.cin <= 64 && d.cout <= 32, "dp_conv2d_pool: cin %% 8 == 0, cin <= 64, cout <= 32");
+  DP_REQUIRE(d.in && d.weight && d.out && d.batch > 0 && d.kpad % 64 == 0 && d.kpad >= 4 * d.cin,
+             "dp_conv2d_pool: bad descriptor");
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(d.in) & 15) == 0 && (reinterpret_cast<uintptr_t>(d.weight) & 15) == 0 &&
+                 d.in_pstride % 8 == 0 && d.in_bstride % 8 == 0,
+             "dp_conv2d_pool: input / weight must be 16-byte aligned");
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(pool_out) & 15) == 0 && pool_pstride % 8 == 0 && pool_bstride % 8 == 0,
+             "dp_conv2d_pool: pool output must be 16-byte aligned per pixel");
+  DP_REQUIRE(d.in_bstride * 2 < 0x7ff00000ll && (int64_t)d.batch * d.out_h * d.out_w < (1ll << 31),
+             "dp_conv2d_pool: image exceeds 32-bit buffer offsets");
+  constexpr int P = HaloGeom<8, 2, 2, 1>::PLANE;
+  const int lds = (d.kpad / 64) * 32 * 128 + P;
+  DP_REQUIRE(lds <= 80 * 1024, "dp_conv2d_pool: weights do not fit LDS");
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int vec_ok = (d.out_pstride % 8 == 0) && (d.out_bstride % 8 == 0) && al(d.out);
+  const int r = dp_conv2d_stem2x2(d, as_stream(stream), pool_out, pool_bstride, pool_pstride);
+  if (r >= 0) return r;   // stem shapes: register-direct kernel (stem.hip)
+  const HaloPool pool{reinterpret_cast<bf16_t*>(pool_out), pool_bstride, pool_pstride};
+  return launch_halo_act<8, 4, 2, 2, 1, 32, true, false, true>(d, as_stream(stream), vec_ok, lds, pool);
 }

@@ -1,6 +1,5 @@
-// Persistent bf16 implicit-GEMM convolution (gfx950): the default path of dp_conv2d for
-// bf16 activations. conv_glds.hip (one tile per block, LDS-staged epilogue) and
-// conv_gemm.hip (register-staged, f32 parity mode) stay as A/B and fallback paths.
+// Persistent bf16 implicit-GEMM convolution (gfx950): the path of dp_conv2d for bf16
+// activations (1x1 convs, linears, and the KxK convs conv_halo.hip does not cover).
 //
 // Why persistent: most DETRPose convs are short in K (1x1 with cin 64..512, 2x2 stem
 // convs) and near the HBM ridge, so a one-tile block spends most of its life in the
@@ -15,7 +14,7 @@
 // The epilogue then needs no LDS: bias/act/LAB/residual in registers, 16-byte stores
 // straight from the accumulators (and the nearest-x2 copy for the FPN concat).
 //
-// LDS-DMA details as in conv_glds.hip: one `buffer_load_dwordx4 ... lds` moves 8 rows x
+// LDS-DMA: one `buffer_load_dwordx4 ... lds` moves 8 rows x
 // 128 B; chunks are XOR-swizzled by row so fragment reads are conflict-free; OOB offsets
 // return 0 (conv padding, K/M/N tails). Blocks are remapped so each XCD owns a
 // contiguous slice of every round of tiles (the N-tiles sharing an A tile hit one L2).

@@ -1,0 +1,184 @@
+// StemBlock 2x2 convs (stem2a / stem2b, hgnetv2.py:171-220) as register-direct MFMA kernels.
+//
+// Both convs are 2x2 stride 1 over F.pad(x, (0,1,0,1)) with 8..32 channels in and out:
+// K = 4 * cin <= 128, so the arithmetic is a handful of MFMAs per 16 pixels and the layers
+// are pure HBM streams (stem1 output read once, stem2a/stem2b outputs written once). A
+// staged (LDS patch + barrier) kernel spends most of its life waiting for its patch; here
+// each wave gathers its MFMA B fragments straight from global memory into registers (lane
+// (q, g) of K-slab s loads the 8 channels ci of tap t = k / cin, k = 32 s + 8 g, of pixel
+// x0 + q: one 16-byte load, the 2x2 neighbours come from L1/L2), keeps G pixel groups of
+// loads in flight, and has no LDS and no barriers. The weights (A operand, [cout][kpad],
+// k = tap * cin + ci as every conv of the path) sit in registers for the wave's life.
+//
+// POOL (stem2a): the B fragments already hold the four taps of the zero-padded 2x2 window,
+// i.e. MaxPool2d(2, 1) of F.pad(x,(0,1,0,1)) (hgnetv2.py:215-217) is a max over registers:
+// cin 32 -> lane g holds taps 0..3 of channels 8g..8g+7; cin 16 -> taps {g>>1, 2+(g>>1)} of
+// channels 8(g&1)..+7, completed by one cross-half exchange (lane ^ 32).
+#include "common.h"
+
+namespace {
+
+template <int CIN, int COUT, bool POOL, int ACT>
+__global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __restrict__ in, int64_t ibs, int ips,
+                                                             int H, int W, int batch, const bf16_t* __restrict__ wt,
+                                                             int kpad, const float* __restrict__ bias, int has_lab,
+                                                             float ls, float lb, bf16_t* __restrict__ out, int64_t obs,
+                                                             int ops, bf16_t* __restrict__ pool, int64_t pbs, int pps) {
+  constexpr int NKS = (4 * CIN + 31) / 32;   // K slabs of 32
+  constexpr int NT = (COUT + 15) / 16;       // 16-channel output tiles
+  constexpr int G = 4;                       // pixel groups (16 px each) in flight per wave
+  static_assert(CIN % 8 == 0 && COUT % 4 == 0 && CIN <= 32 && COUT <= 32, "stem 2x2 shapes");
+  static_assert(!POOL || CIN == 32 || CIN == 16, "pool: cin 16 or 32");
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
+
+  bf16x8 wa[NT][NKS];
+  int tap_dy[NKS], tap_dx[NKS], tap_ci[NKS];
+  bool tap_ok[NKS];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const int k = 32 * s + 8 * g;
+    const int t = k / CIN;
+    tap_ok[s] = t < 4;
+    tap_dy[s] = t >> 1, tap_dx[s] = t & 1, tap_ci[s] = k - t * CIN;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int row = 16 * j + q;
+      bf16x8 w = {};
+      if (row < COUT && tap_ok[s]) w = *reinterpret_cast<const bf16x8*>(wt + (int64_t)row * kpad + k);
+      wa[j][s] = w;
+    }
+  }
+  float bsum[NT][4];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 16 * j + 4 * g + r;
+      bsum[j][r] = (bias && c < COUT) ? bias[c] : 0.f;
+    }
+
+  const int gx = (W + 15) >> 4;
+  const int ngroups = batch * H * gx;
+  const int nw = gridDim.x * 4;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  for (int base = wid * G; base < ngroups; base += nw * G) {
+    bf16x8 xb[G][NKS];
+    int pb[G], py[G], px[G];
+    bool pv[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int grp = base + i;
+      const int bb = grp / (H * gx), rem = grp - bb * (H * gx);
+      const int y = rem / gx, x = (rem - y * gx) * 16 + q;
+      pb[i] = bb, py[i] = y, px[i] = x;
+      pv[i] = grp < ngroups && x < W;
+      const bf16_t* ib = in + (int64_t)bb * ibs;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const int iy = y + tap_dy[s], ix = x + tap_dx[s];
+        bf16x8 v = {};
+        if (grp < ngroups && tap_ok[s] && iy < H && ix < W)
+          v = *reinterpret_cast<const bf16x8*>(ib + (int64_t)(iy * W + ix) * ips + tap_ci[s]);
+        xb[i][s] = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      f32x4 acc[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][s], xb[i][s], acc[j], 0, 0, 0);
+      }
+      // C layout: lane (q, g) holds channels 16 j + 4 g + r of pixel x0 + q
+      const int64_t pix = (int64_t)py[i] * W + px[i];
+      if (pv[i]) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int c = 16 * j + 4 * g;
+          if (c >= COUT) continue;
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[j][r] + bsum[j][r];
+            if (ACT == DP_ACT_RELU) v = fmaxf(v, 0.f);
+            if (has_lab) v = ls * v + lb;
+            o[r] = (bf16_t)v;
+          }
+          *reinterpret_cast<bf16x4*>(out + (int64_t)pb[i] * obs + pix * ops + c) = o;
+        }
+      }
+      if constexpr (POOL) {
+        bf16x8 m;
+        if constexpr (CIN == 32) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            m[e] = (bf16_t)fmaxf(fmaxf((float)xb[i][0][e], (float)xb[i][1][e]),
+                                 fmaxf((float)xb[i][2][e], (float)xb[i][3][e]));
+        } else {
+          // cin 16: this lane has 2 of the 4 taps; lane ^ 32 (g ^ 2) has the other two
+          bf16x8 h;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) h[e] = (bf16_t)fmaxf((float)xb[i][0][e], (float)xb[i][1][e]);
+          const uint4 hu = *reinterpret_cast<const uint4*>(&h);
+          uint4 ou;
+          ou.x = __shfl_xor(hu.x, 32, 64), ou.y = __shfl_xor(hu.y, 32, 64);
+          ou.z = __shfl_xor(hu.z, 32, 64), ou.w = __shfl_xor(hu.w, 32, 64);
+          const bf16x8 o = *reinterpret_cast<const bf16x8*>(&ou);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m[e] = (bf16_t)fmaxf((float)h[e], (float)o[e]);
+        }
+        // lane g stores channels 8g..8g+7 (cin 16: lanes g = 0, 1 hold the complete max)
+        if (pv[i] && g < CIN / 8) *reinterpret_cast<bf16x8*>(pool + (int64_t)pb[i] * pbs + pix * pps + 8 * g) = m;
+      }
+    }
+  }
+}
+
+template <int CIN, int COUT, bool POOL>
+int launch_direct(const dp_conv_desc& d, hipStream_t s, bf16_t* pool, int64_t pbs, int pps) {
+  const int gx = (d.in_w + 15) / 16;
+  const int64_t ngroups = (int64_t)d.batch * d.in_h * gx;
+  int blocks = (int)((ngroups + 4 * 4 - 1) / (4 * 4));   // 4 waves x G = 4 groups per block pass
+  if (blocks > 256 * 8) blocks = 256 * 8;   // about one resident pass of the chip
+  auto kern = d.act == DP_ACT_RELU ? conv2x2_direct_kernel<CIN, COUT, POOL, DP_ACT_RELU>
+                                   : conv2x2_direct_kernel<CIN, COUT, POOL, DP_ACT_NONE>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const bf16_t*>(d.in), d.in_bstride,
+                     d.in_pstride, d.in_h, d.in_w, d.batch, reinterpret_cast<const bf16_t*>(d.weight), d.kpad, d.bias,
+                     d.has_lab, d.lab_scale, d.lab_bias, reinterpret_cast<bf16_t*>(d.out), d.out_bstride, d.out_pstride,
+                     pool, pbs, pps);
+  return dp_check_launch("dp_conv2d(stem 2x2 direct)");
+}
+
+}  // namespace
+
+// bf16 2x2 stride-1 conv with right/bottom zero padding (StemBlock stem2a / stem2b), optionally
+// with the fused stem max-pool. Returns -1 when the shape has no instantiation (the caller
+// then uses the LDS halo kernel).
+int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps) {
+  if (d.dtype != DP_BF16 || d.out_f32 || d.res || d.up || d.kh != 2 || d.kw != 2 || d.stride != 1 || d.pad_t ||
+      d.pad_l || d.out_h != d.in_h || d.out_w != d.in_w || (d.act != DP_ACT_RELU && d.act != DP_ACT_NONE))
+    return -1;
+  auto a8 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; };
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!a8(d.out) || d.out_pstride % 4 || d.out_bstride % 4 || !a16(d.in) || !a16(d.weight) || d.in_pstride % 8 ||
+      d.in_bstride % 8)
+    return -1;
+  if ((int64_t)d.batch * d.in_h * ((d.in_w + 15) / 16) >= (1ll << 31)) return -1;
+  bf16_t* pl = reinterpret_cast<bf16_t*>(pool);
+  if (pool && (!a16(pool) || pps % 8 || pbs % 8)) return -1;
+#define DP_DIRECT(CI, CO)                                                          \
+  if (d.cin == CI && d.cout == CO) {                                               \
+    if (pool) return launch_direct<CI, CO, true>(d, s, pl, pbs, pps);              \
+    return launch_direct<CI, CO, false>(d, s, nullptr, 0, 0);                      \
+  }
+  // HGNetv2 stems: B0 [3,16,16], B4 (L) [3,32,48], B5 (X) [3,32,64]
+  DP_DIRECT(32, 16)
+  DP_DIRECT(16, 8)
+#undef DP_DIRECT
+  if (pool) return -1;
+  if (d.cin == 16 && d.cout == 32) return launch_direct<16, 32, false>(d, s, nullptr, 0, 0);
+  if (d.cin == 8 && d.cout == 16) return launch_direct<8, 16, false>(d, s, nullptr, 0, 0);
+  return -1;
+}

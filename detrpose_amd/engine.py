@@ -461,7 +461,7 @@ class Engine:
         return FMap(t, 0, B, H, W, Cc, Cc, H * W * Cc)
 
     def _conv(self, plan, name, x: FMap, pc: PConv, out: FMap, res: FMap | None = None, up: FMap | None = None,
-              out_f32: bool = False):
+              out_f32: bool = False, pool: FMap | None = None):
         if pc.depthwise:
             assert x.C == pc.cin == out.C, (name, x.C, pc.cin, out.C)
         else:
@@ -500,9 +500,15 @@ class Engine:
             eo = 4 if out_f32 else e
             rows = x.B * out.H * out.W
             plan.conv_bytes[name] = (e * x.B * x.H * x.W * x.C + e * pc.cout * pc.kh * pc.kw * pc.cin
-                                     + eo * rows * out.C * (1 + (res is not None) + 4 * (up is not None)))
+                                     + eo * rows * out.C * (1 + (res is not None) + 4 * (up is not None))
+                                     + (e * rows * pool.C if pool is not None else 0))
         else:
             plan.op_flops[name] = 2.0 * x.B * out.H * out.W * out.C * pc.kh * pc.kw
+        if pool is not None:
+            # conv + MaxPool2d(2, 1) of the same padded input in one pass (dp_conv2d_pool)
+            assert not pc.depthwise and pool.C == x.C and (pool.B, pool.H, pool.W) == (x.B, x.H, x.W)
+            plan._op(name, self.lib.dp_conv2d_pool, C.byref(d), pool.ptr, pool.bs, pool.ps)
+            return
         fn = self.lib.dp_dwconv2d if pc.depthwise else self.lib.dp_conv2d
         plan._op(name, fn, C.byref(d))
 
@@ -546,11 +552,15 @@ class Engine:
                  1 if lab else 0, C.c_float(lab[0] if lab else 1.0), C.c_float(lab[1] if lab else 0.0), s1.ptr, s1.bs,
                  s1.ps, self.code)
         s2a = self._fmap(B, h1, w1, P["stem2a"].cout)
-        self._conv(plan, "stem2a", s1, P["stem2a"], s2a)   # F.pad(0,1,0,1) == zero read past the edge
         cat = self._fmap(B, h1, w1, 2 * mid)
+        if self.code == _lib.DP_BF16 and mid % 8 == 0 and mid <= 64 and P["stem2a"].cout <= 32:
+            # stem2a and the stem max-pool read the same F.pad(0,1,0,1) windows of stem1: one pass
+            self._conv(plan, "stem2a", s1, P["stem2a"], s2a, pool=cat.ch(0, mid))
+        else:
+            self._conv(plan, "stem2a", s1, P["stem2a"], s2a)   # F.pad(0,1,0,1) == zero read past the edge
+            plan._op("stem_pool", self.lib.dp_maxpool2x2_pad_rb, s1.ptr, s1.bs, s1.ps, B, h1, w1, mid, cat.ptr,
+                     cat.bs, cat.ps, self.code)
         self._conv(plan, "stem2b", s2a, P["stem2b"], cat.ch(mid, mid))
-        plan._op("stem_pool", self.lib.dp_maxpool2x2_pad_rb, s1.ptr, s1.bs, s1.ps, B, h1, w1, mid, cat.ptr, cat.bs,
-                 cat.ps, self.code)
         h2, w2 = (h1 + 1) // 2, (w1 + 1) // 2
         s3 = self._fmap(B, h2, w2, mid)
         self._conv(plan, "stem3", cat, P["stem3"], s3)

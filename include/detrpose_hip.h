@@ -82,6 +82,13 @@ int dp_maxpool2x2_pad_rb(const void* in, int64_t in_bstride, int32_t in_pstride,
                          int32_t batch, int32_t h, int32_t w, int32_t c,
                          void* out, int64_t out_bstride, int32_t out_pstride, int32_t dtype, void* stream);
 
+/* dp_conv2d of StemBlock.stem2a (2x2 s1 over F.pad(x,(0,1,0,1)): pad 0, zero read past the
+ * right/bottom edge) that also writes MaxPool2d(2, 1, ceil_mode=True) of the same padded
+ * input to pool_out (hgnetv2.py:213-220): replaces the stem2a conv + dp_maxpool2x2_pad_rb pair
+ * with one pass over stem1's output. bf16, cin % 8 == 0, cin <= 64, cout <= 32. */
+int dp_conv2d_pool(const dp_conv_desc* d, void* pool_out, int64_t pool_bstride, int32_t pool_pstride,
+                   void* stream);
+
 /* out[r] = a[r] + b[r] over `rows` rows of `c` elements (row maps as above). */
 int dp_add_rows(void* out, dp_rowmap om, const void* a, dp_rowmap am, const void* b, dp_rowmap bm,
                 int32_t rows, int32_t c, int32_t dtype, void* stream);

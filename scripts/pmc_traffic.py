@@ -16,8 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def family(name):
-    # every implicit-GEMM conv variant (conv_stream/halo/glds/gemm_kernel) is one family
-    if re.search(r"conv_(stream|halo|glds|gemm)_kernel", name):
+    # every implicit-GEMM conv variant (conv_stream/halo/gemm_kernel) is one family
+    if re.search(r"conv_(stream|halo|gemm)_kernel", name):
         return "conv"
     for key in ("dwconv_kernel", "dwconv_lds_kernel", "layernorm_kernel", "attn_mfma_kernel", "attn_short_kernel",
                 "msda_kernel", "msda_wave_kernel", "add_rows_kernel", "stem_conv_kernel", "maxpool_kernel", "class_max_kernel",

@@ -178,6 +178,73 @@ def test_stem_conv_and_pool(dt):
     _close(pool, refp.permute(0, 2, 3, 1), dt, "pool")
 
 
+@pytest.mark.parametrize("cin,cout,H,W,lab", [(32, 16, 37, 45, None), (16, 8, 20, 17, (1.3, -0.2)),
+                                              (64, 32, 9, 70, None)])
+def test_conv2d_pool_fused(cin, cout, H, W, lab):
+    """dp_conv2d_pool (stem2a + stem max-pool in one pass): the conv as dp_conv2d's bf16
+    tolerance, the pool bit-exact vs F.max_pool2d(F.pad(x,(0,1,0,1)), 2, 1) of the same bf16
+    input, written into a channel slice of a wider (concat) buffer; ragged 8x16 tiles."""
+    lib = _lib.load()
+    torch.manual_seed(cin + H)
+    pk = Packer({}, "bf16", torch.device("cuda"))
+    # lab case: shifted negative, so the F.pad zeros must win the max at the right/bottom edge
+    x = (torch.randn(3, cin, H, W) - (0.5 if lab else 0.0)).bfloat16().float()
+    w = torch.randn(cout, cin, 2, 2) / (2 * cin ** 0.5)
+    b = torch.randn(cout) * 0.1
+    pc = pk.conv(w.double(), b.double(), act="relu", pad=0, lab=lab)
+    ref = F.relu(F.conv2d(F.pad(x, (0, 1, 0, 1)), w, b))
+    if lab:
+        ref = lab[0] * ref + lab[1]
+    xi = _nhwc(x, "bf16")
+    out = torch.empty(3, H, W, cout, device="cuda", dtype=torch.bfloat16)
+    cat = torch.full((3, H, W, 2 * cin), 7.0, device="cuda", dtype=torch.bfloat16)
+    d = ConvDesc()
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = xi.data_ptr(), H * W * cin, cin, H, W, cin
+    d.weight, d.kpad, d.bias = pc.w.data_ptr(), pc.kpad, pc.b.data_ptr()
+    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = 2, 2, 1, 0, 0
+    d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out.data_ptr(), H * W * cout, cout, H, W, cout
+    d.batch, d.act, d.dtype = 3, pc.act, _lib.DP_BF16
+    if lab:
+        d.has_lab, d.lab_scale, d.lab_bias = 1, lab[0], lab[1]
+    _lib.check(lib.dp_conv2d_pool(C.byref(d), cat.data_ptr(), H * W * 2 * cin, 2 * cin, _s()), "conv2d_pool")
+    torch.cuda.synchronize()
+    _close(out, ref.permute(0, 2, 3, 1), "bf16", "stem2a (fused)")
+    refp = F.max_pool2d(F.pad(x, (0, 1, 0, 1)), 2, 1, ceil_mode=True).permute(0, 2, 3, 1)
+    assert torch.equal(cat[..., :cin].float().cpu(), refp), "fused pool differs"
+    assert (cat[..., cin:] == 7.0).all(), "fused pool wrote outside its channel slice"
+
+
+@pytest.mark.parametrize("cin,cout,lab", [(16, 32, None), (8, 16, (0.9, 0.1)), (32, 16, None), (16, 8, None)])
+def test_conv2d_stem2x2_direct(cin, cout, lab):
+    """The stem's register-direct 2x2 kernel through dp_conv2d (stem2b writes a channel slice
+    of the concat buffer): vs torch fp32 on the bf16-rounded input, ragged 16-pixel groups."""
+    torch.manual_seed(cin * cout)
+    pk = Packer({}, "bf16", torch.device("cuda"))
+    B, H, W = 2, 23, 37
+    x = torch.randn(B, cin, H, W).bfloat16().float()
+    w = torch.randn(cout, cin, 2, 2) / (2 * cin ** 0.5)
+    b = torch.randn(cout) * 0.1
+    pc = pk.conv(w.double(), b.double(), act="relu", pad=0, lab=lab)
+    ref = F.relu(F.conv2d(F.pad(x, (0, 1, 0, 1)), w, b))
+    if lab:
+        ref = lab[0] * ref + lab[1]
+    wide = torch.full((B, H, W, 2 * cout), 5.0, device="cuda", dtype=torch.bfloat16)
+    xi = _nhwc(x, "bf16")
+    d = ConvDesc()
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = xi.data_ptr(), H * W * cin, cin, H, W, cin
+    d.weight, d.kpad, d.bias = pc.w.data_ptr(), pc.kpad, pc.b.data_ptr()
+    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = 2, 2, 1, 0, 0
+    d.out, d.out_bstride, d.out_pstride = wide.data_ptr() + 2 * cout, H * W * 2 * cout, 2 * cout
+    d.out_h, d.out_w, d.cout = H, W, cout
+    d.batch, d.act, d.dtype = B, pc.act, _lib.DP_BF16
+    if lab:
+        d.has_lab, d.lab_scale, d.lab_bias = 1, lab[0], lab[1]
+    _lib.check(_lib.load().dp_conv2d(C.byref(d), _s()), "conv2x2")
+    torch.cuda.synchronize()
+    _close(wide[..., cout:], ref.permute(0, 2, 3, 1), "bf16", f"stem 2x2 {cin}->{cout}")
+    assert (wide[..., :cout] == 5.0).all(), "wrote outside the channel slice"
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("c", [128, 256, 384])
 def test_layernorm_variants(dt, c):
