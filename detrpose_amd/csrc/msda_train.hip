@@ -1,0 +1,201 @@
+// MSDA core at the training interface: explicit sampling locations and (softmaxed) attention
+// weights, forward and backward. The first native piece of the training step.
+//
+// Reference: ms_deform_attn_core_pytorch (ms_deform_attn.py:145-193) = per level
+// F.grid_sample(value_l, 2*loc-1, bilinear, zeros, align_corners=False), then the
+// attention-weighted sum over (level, point). Its autograd is what these kernels compute:
+//   pixel coords  x = loc_x * W - 0.5, y = loc_y * H - 0.5, corners (x0 + dx, y0 + dy),
+//   weights w00 = (1-fx)(1-fy), w01 = fx(1-fy), w10 = (1-fx)fy, w11 = fx fy (0 outside);
+//   s = sum_k w_k v_k,  out += a * s
+//   d attn    = <go, s>
+//   d loc_x   = a * <go, (v01 - v00)(1-fy) + (v11 - v10) fy> * W   (floor is flat)
+//   d loc_y   = a * <go, (v10 - v00)(1-fx) + (v11 - v01) fx> * H
+//   d value_k += a * w_k * go    (f32 atomics: many (token, point) pairs hit one row)
+// Layouts: value [N][S][nH*Dh] (levels concatenated along S, the encoder memory layout of
+// the inference path), loc [N][Lq][nH][L][P][2], attn [N][Lq][nH][L][P], out / grad_out
+// [N][Lq][nH*Dh]. Lanes: CPT consecutive lanes own one (token, head), 16 bytes of channels
+// each; the three per-point dot products are reduced over those lanes with shuffles.
+#include "common.h"
+
+namespace {
+
+constexpr int MAXL = 4;
+
+struct TLevels {
+  int h[MAXL], w[MAXL], start[MAXL];
+};
+
+template <typename T>
+__device__ __forceinline__ void load_vec(const T* p, float (&v)[16 / sizeof(T)]) {
+  const Vec16<T> x = load16(p);
+#pragma unroll
+  for (int e = 0; e < Vec16<T>::N; ++e) v[e] = x.get(e);
+}
+
+// sum of v over the cpt lanes [g0, g0 + cpt) of the lane's (token, head) group
+__device__ __forceinline__ float group_sum(float v, int g0, int cpt) {
+  float t = 0.f;
+  for (int s = 0; s < cpt; ++s) t += __shfl(v, g0 + s, 64);
+  return t;
+}
+
+template <typename T, bool BWD>
+__global__ __launch_bounds__(256) void msda_core_kernel(const T* __restrict__ value, int S, TLevels lv, int L, int P,
+                                                        const float* __restrict__ loc, const float* __restrict__ attn,
+                                                        const T* __restrict__ gout, T* __restrict__ out,
+                                                        float* __restrict__ gvalue, float* __restrict__ gloc,
+                                                        float* __restrict__ gattn, int lq, int pairs, int nh, int dh) {
+  constexpr int VEC = Vec16<T>::N;
+  const int cpt = dh / VEC;
+  const int ppw = 64 / cpt;                       // (token, head) pairs per wave
+  const int lane = threadIdx.x & 63;
+  const int slot = lane / cpt, c = lane - slot * cpt;
+  const int pair = (blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw + slot;
+  if (slot >= ppw || pair >= pairs) return;   // whole (token, head) groups leave together
+  const int g0 = lane - c;
+  const int r = pair / nh, h = pair - r * nh;
+  const int b = r / lq;
+  const int C = nh * dh;
+  const int LP = L * P;
+  const int ch = h * dh + c * VEC;
+  const T* vb = value + (int64_t)b * S * C + ch;
+  float go[VEC], acc[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+  if (BWD) load_vec(gout + (int64_t)r * C + ch, go);
+  const float* lp = loc + (int64_t)pair * LP * 2;
+  const float* ap = attn + (int64_t)pair * LP;
+  for (int j = 0; j < LP; ++j) {
+    const int l = j / P;
+    const int H = lv.h[l], W = lv.w[l];
+    const float x = lp[2 * j] * W - 0.5f, y = lp[2 * j + 1] * H - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float fx = x - fx0, fy = y - fy0;
+    const float a = ap[j];
+    const float wk[4] = {(1.f - fx) * (1.f - fy), fx * (1.f - fy), (1.f - fx) * fy, fx * fy};
+    float v[4][VEC];
+    int row[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int xi = x0 + (k & 1), yi = y0 + (k >> 1);
+      const bool ok = xi >= 0 && xi < W && yi >= 0 && yi < H;
+      row[k] = ok ? lv.start[l] + yi * W + xi : -1;
+      if (ok) load_vec(vb + (int64_t)row[k] * C, v[k]);
+      else
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) v[k][e] = 0.f;
+    }
+    if (!BWD) {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        acc[e] += a * (wk[0] * v[0][e] + wk[1] * v[1][e] + wk[2] * v[2][e] + wk[3] * v[3][e]);
+      continue;
+    }
+    float ga = 0.f, gx = 0.f, gy = 0.f;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float s = wk[0] * v[0][e] + wk[1] * v[1][e] + wk[2] * v[2][e] + wk[3] * v[3][e];
+      ga += go[e] * s;
+      gx += go[e] * ((v[1][e] - v[0][e]) * (1.f - fy) + (v[3][e] - v[2][e]) * fy);
+      gy += go[e] * ((v[2][e] - v[0][e]) * (1.f - fx) + (v[3][e] - v[1][e]) * fx);
+    }
+    ga = group_sum(ga, g0, cpt);
+    gx = group_sum(gx, g0, cpt);
+    gy = group_sum(gy, g0, cpt);
+    if (c == 0) {
+      gattn[(int64_t)pair * LP + j] = ga;
+      gloc[((int64_t)pair * LP + j) * 2] = a * gx * W;
+      gloc[((int64_t)pair * LP + j) * 2 + 1] = a * gy * H;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (row[k] < 0) continue;
+      float* gp = gvalue + ((int64_t)b * S + row[k]) * C + ch;
+      const float s = a * wk[k];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) unsafeAtomicAdd(gp + e, s * go[e]);
+    }
+  }
+  if (!BWD) {
+    Vec16<T> o;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) o.set(e, acc[e]);
+    store16(out + (int64_t)r * C + ch, o);
+  }
+}
+
+template <typename T, bool BWD>
+int launch_core(const void* value, int batch, int S, const TLevels& lv, int L, int P, const float* loc,
+                const float* attn, const void* gout, void* out, float* gvalue, float* gloc, float* gattn, int lq, int nh,
+                int dh, hipStream_t s) {
+  const int cpt = dh / Vec16<T>::N;
+  const int ppw = 64 / cpt;
+  const int pairs = batch * lq * nh;
+  const int waves = (pairs + ppw - 1) / ppw;
+  const int grid = (waves + 3) / 4;
+  hipLaunchKernelGGL((msda_core_kernel<T, BWD>), dim3(grid), dim3(256), 0, s, reinterpret_cast<const T*>(value), S, lv,
+                     L, P, loc, attn, reinterpret_cast<const T*>(gout), reinterpret_cast<T*>(out), gvalue, gloc, gattn,
+                     lq, pairs, nh, dh);
+  return dp_check_launch(BWD ? "dp_msda_core_bwd" : "dp_msda_core_fwd");
+}
+
+int check_core(const void* value, int batch, int S, const int32_t* lvl_hw, int nlevels, const float* loc,
+               const float* attn, int lq, int nhead, int dh, int npoints, int dtype, TLevels* lv) {
+  const int VEC = dtype == DP_BF16 ? 8 : 4;
+  DP_REQUIRE(value && loc && attn && lvl_hw, "dp_msda_core: null pointer");
+  DP_REQUIRE(dtype == DP_BF16 || dtype == DP_F32, "dp_msda_core: bad dtype %d", dtype);
+  DP_REQUIRE(nlevels >= 1 && nlevels <= MAXL, "dp_msda_core: nlevels=%d (max %d)", nlevels, MAXL);
+  DP_REQUIRE(batch > 0 && lq > 0 && nhead > 0 && npoints > 0, "dp_msda_core: bad shape");
+  DP_REQUIRE(dh % VEC == 0 && dh / VEC <= 64, "dp_msda_core: dh=%d must be a multiple of %d (at most %d)", dh, VEC,
+             64 * VEC);
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(value) & 15) == 0, "dp_msda_core: value must be 16-byte aligned");
+  DP_REQUIRE((int64_t)batch * lq * nhead < (1ll << 31), "dp_msda_core: too many (token, head) pairs");
+  int start = 0;
+  for (int l = 0; l < nlevels; ++l) {
+    lv->h[l] = lvl_hw[2 * l];
+    lv->w[l] = lvl_hw[2 * l + 1];
+    lv->start[l] = start;
+    DP_REQUIRE(lv->h[l] > 0 && lv->w[l] > 0, "dp_msda_core: empty level %d", l);
+    start += lv->h[l] * lv->w[l];
+  }
+  DP_REQUIRE(start == S, "dp_msda_core: level sizes sum to %d, S=%d", start, S);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int dp_msda_core_fwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
+                                const float* loc, const float* attn, void* out, int32_t lq, int32_t nhead, int32_t dh,
+                                int32_t npoints, int32_t dtype, void* stream) {
+  TLevels lv;
+  const int rc = check_core(value, batch, S, lvl_hw, nlevels, loc, attn, lq, nhead, dh, npoints, dtype, &lv);
+  if (rc) return rc;
+  DP_REQUIRE(out && (reinterpret_cast<uintptr_t>(out) & 15) == 0, "dp_msda_core_fwd: out must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16)
+    return launch_core<bf16_t, false>(value, batch, S, lv, nlevels, npoints, loc, attn, nullptr, out, nullptr, nullptr,
+                                      nullptr, lq, nhead, dh, s);
+  return launch_core<float, false>(value, batch, S, lv, nlevels, npoints, loc, attn, nullptr, out, nullptr, nullptr,
+                                   nullptr, lq, nhead, dh, s);
+}
+
+extern "C" int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
+                                const float* loc, const float* attn, const void* grad_out, int32_t lq, int32_t nhead,
+                                int32_t dh, int32_t npoints, float* grad_value, float* grad_loc, float* grad_attn,
+                                int32_t dtype, void* stream) {
+  TLevels lv;
+  const int rc = check_core(value, batch, S, lvl_hw, nlevels, loc, attn, lq, nhead, dh, npoints, dtype, &lv);
+  if (rc) return rc;
+  DP_REQUIRE(grad_out && grad_value && grad_loc && grad_attn, "dp_msda_core_bwd: null gradient pointer");
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0, "dp_msda_core_bwd: grad_out must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  // grad_value is accumulated by atomics: clear it on the same stream first (graph-capturable)
+  if (hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess)
+    return dp_check_launch("dp_msda_core_bwd(memset)");
+  if (dtype == DP_BF16)
+    return launch_core<bf16_t, true>(value, batch, S, lv, nlevels, npoints, loc, attn, grad_out, nullptr, grad_value,
+                                     grad_loc, grad_attn, lq, nhead, dh, s);
+  return launch_core<float, true>(value, batch, S, lv, nlevels, npoints, loc, attn, grad_out, nullptr, grad_value,
+                                  grad_loc, grad_attn, lq, nhead, dh, s);
+}

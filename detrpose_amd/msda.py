@@ -1,0 +1,93 @@
+"""Differentiable MSDA core on the HIP kernels (training interface).
+
+`ms_deform_attn_core(value, value_spatial_shapes, sampling_locations, attention_weights)`
+is the drop-in for the reference's `ms_deform_attn_core_pytorch` default branch
+(/root/reference/src/models/detrpose/ms_deform_attn.py:145-193, called at :436-441):
+same math (per level F.grid_sample(bilinear, zeros, align_corners=False) at 2*loc-1, then
+the attention-weighted sum), forward by `dp_msda_core_fwd` and backward by
+`dp_msda_core_bwd` (grad_value by f32 atomics, grad_loc, grad_attn). Value is taken in the
+encoder-memory layout (N, S, nH*Dh) the rest of this package uses, rather than the
+reference's per-level (N*nH, Dh, H*W) list; `value_from_levels` converts.
+
+There is no CPU path: the HIP library must load (see _lib.load()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+_DT = {torch.float32: _lib.DP_F32, torch.bfloat16: _lib.DP_BF16}
+
+
+def _shapes_arg(shapes):
+    hw = [int(v) for hw in shapes for v in hw]
+    return (C.c_int32 * len(hw))(*hw), len(hw) // 2
+
+
+def _check(value, shapes, loc, attn):
+    N, S, Cc = value.shape
+    _, Lq, nH, L, P, two = loc.shape
+    if two != 2 or attn.shape != (N, Lq, nH, L, P) or loc.shape[0] != N:
+        raise ValueError(f"msda core: loc {tuple(loc.shape)} / attn {tuple(attn.shape)} do not match value {tuple(value.shape)}")
+    if Cc % nH:
+        raise ValueError(f"msda core: {Cc} channels not divisible by {nH} heads")
+    if sum(int(h) * int(w) for h, w in shapes) != S or len(shapes) != L:
+        raise ValueError("msda core: spatial shapes do not match value / loc")
+    if value.dtype not in _DT:
+        raise TypeError(f"msda core: value dtype {value.dtype} (f32 / bf16)")
+    if not value.is_cuda:
+        raise RuntimeError("msda core: tensors must be on the GPU (no CPU path)")
+    return N, S, Cc, Lq, nH, L, P
+
+
+class MSDeformAttnCoreFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, value, shapes, loc, attn):
+        N, S, Cc, Lq, nH, L, P = _check(value, shapes, loc, attn)
+        value = value.contiguous()
+        loc = loc.contiguous().float()
+        attn = attn.contiguous().float()
+        out = torch.empty(N, Lq, Cc, device=value.device, dtype=value.dtype)
+        hw, nl = _shapes_arg(shapes)
+        lib = _lib.load()
+        s = torch.cuda.current_stream(value.device).cuda_stream
+        _lib.check(lib.dp_msda_core_fwd(value.data_ptr(), N, S, hw, nl, loc.data_ptr(), attn.data_ptr(), out.data_ptr(),
+                                        Lq, nH, Cc // nH, P, _DT[value.dtype], C.c_void_p(s)), "dp_msda_core_fwd")
+        ctx.save_for_backward(value, loc, attn)
+        ctx.shapes = [tuple(int(v) for v in hw_) for hw_ in shapes]
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        value, loc, attn = ctx.saved_tensors
+        N, S, Cc = value.shape
+        _, Lq, nH, L, P, _ = loc.shape
+        go = grad_out.contiguous().to(value.dtype)
+        gv = torch.empty(N, S, Cc, device=value.device, dtype=torch.float32)
+        gl = torch.empty_like(loc)
+        ga = torch.empty_like(attn)
+        hw, nl = _shapes_arg(ctx.shapes)
+        lib = _lib.load()
+        s = torch.cuda.current_stream(value.device).cuda_stream
+        _lib.check(lib.dp_msda_core_bwd(value.data_ptr(), N, S, hw, nl, loc.data_ptr(), attn.data_ptr(), go.data_ptr(),
+                                        Lq, nH, Cc // nH, P, gv.data_ptr(), gl.data_ptr(), ga.data_ptr(),
+                                        _DT[value.dtype], C.c_void_p(s)), "dp_msda_core_bwd")
+        return gv.to(value.dtype), None, gl, ga
+
+
+def ms_deform_attn_core(value, value_spatial_shapes, sampling_locations, attention_weights):
+    """value (N, S, nH*Dh); shapes [(H, W)] per level; loc (N, Lq, nH, L, P, 2) in [0, 1];
+    attn (N, Lq, nH, L, P) softmaxed -> (N, Lq, nH*Dh). Differentiable in value, loc, attn."""
+    return MSDeformAttnCoreFunction.apply(value, value_spatial_shapes, sampling_locations, attention_weights)
+
+
+def value_from_levels(value_list, n_heads):
+    """The reference's per-level value list [(N*nH, Dh, H*W)] -> (N, S, nH*Dh)."""
+    parts = []
+    for v in value_list:
+        NM, Dh, HW = v.shape
+        parts.append(v.reshape(NM // n_heads, n_heads, Dh, HW).permute(0, 3, 1, 2).reshape(NM // n_heads, HW, n_heads * Dh))
+    return torch.cat(parts, 1)

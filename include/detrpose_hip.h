@@ -130,6 +130,22 @@ int dp_msda(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /
             int32_t nlevels, const void* offattn, const float* ref, void* out, int32_t ld_out,
             int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, int32_t dtype, void* stream);
 
+/* MSDA core at the training interface (explicit sampling locations and softmaxed attention
+ * weights): ms_deform_attn_core_pytorch (ms_deform_attn.py:145-193) forward, and its autograd
+ * (grid_sample bilinear/zeros/align_corners=False backward + weighted sum) for the training
+ * step. value [N][S][nH*Dh] (dtype), loc f32 [N][Lq][nH][L][P][2], attn f32 [N][Lq][nH][L][P],
+ * out / grad_out [N][Lq][nH*Dh] (dtype). Backward writes grad_value (f32, same shape as value;
+ * cleared, then accumulated with atomics), grad_loc and grad_attn (f32, shapes of loc / attn).
+ * The reference has no native MSDA op (CUDA-free build); these replace the autograd of the
+ * pytorch core at the same call site (ms_deform_attn.py:436-441). */
+int dp_msda_core_fwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */,
+                     int32_t nlevels, const float* loc, const float* attn, void* out, int32_t lq,
+                     int32_t nhead, int32_t dh, int32_t npoints, int32_t dtype, void* stream);
+int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */,
+                     int32_t nlevels, const float* loc, const float* attn, const void* grad_out,
+                     int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value,
+                     float* grad_loc, float* grad_attn, int32_t dtype, void* stream);
+
 /* Per-row top-k of f32 scores, sorted descending, ties to the lower index:
  * torch.topk over the two-stage class score (transformer.py:1240) and in PostProcess
  * (postprocesses.py:19).  k <= 256, n <= 16384. idx is int64. */
