@@ -21,9 +21,16 @@
 #include <stdlib.h>
 #include <type_traits>
 
+#ifndef DP_HALO_TAB
+#define DP_HALO_TAB 1   // per-K-step tap table in LDS (0: recompute tap / channel per step, A/B only)
+#endif
+
 namespace {
 
 using namespace dpconv;
+
+// LDS bytes in front of the weights: the K-step -> (tap offset, channel chunk, plane) table
+constexpr int TAB_BYTES = DP_HALO_TAB ? 2048 : 0;
 
 template <int TH, int KH, int KW, int S>
 struct HaloGeom {
@@ -66,8 +73,9 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   const int nkc = (d.cin + 63) / 64;                 // 64-channel planes of the patch
   const int pbytes = nkc * Gm::PLANE;                // one patch buffer
   const int ktaps = KH * KW;
-  char* const wbase = smem;
-  char* const pbase0 = smem + (RESW ? nk : 2) * BN * 128;
+  int* const tab = reinterpret_cast<int*>(smem);
+  char* const wbase = smem + TAB_BYTES;
+  char* const pbase0 = wbase + (RESW ? nk : 2) * BN * 128;
   const int r8 = lane >> 3;
   const i32x4 rb_src = make_rsrc(d.weight);
 
@@ -115,6 +123,17 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
     }
   };
 
+#if DP_HALO_TAB
+  // K-step table: entry kt*8 + cc (k = 64 kt + 8 cc -> tap = k / cin, ci = k % cin) holds the
+  // tap's patch-pixel offset ky*PW + kx, the 16-byte chunk (ci/8)%8 and the 64-channel plane
+  // ci/64, so the MFMA loop does no division. Published by the first tile's barrier.
+  for (int e = tid; e < nk * 8; e += NW * 64) {
+    int tap = (e * 8) / d.cin, ci = e * 8 - tap * d.cin;
+    if (tap >= ktaps) tap = 0, ci = 0;           // kpad tail: the weights are zero there
+    const int ky = tap / KW, kx = tap - ky * KW;
+    tab[e] = (ky * Gm::PW + kx) | (((ci >> 3) & 7) << 7) | ((ci >> 6) << 10);
+  }
+#endif
   // per-lane pixel fragment geometry: q = lane & 15 is the tile column, g = lane >> 4 the
   // 8-channel group of the K-step half; rows yq_i = wave*TM + i
   const int q = lane & 15, g = lane >> 4;
@@ -167,13 +186,20 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
       for (int ks = 0; ks < 2; ++ks) {
         const int cc = 4 * ks + g;
         // this lane's 8 channels of K: k = kt*64 + 32 ks + 8 g -> (tap, ci)
+#if DP_HALO_TAB
+        const int te = tab[kt * 8 + cc];
+        const int toff = te & 127, c8 = (te >> 7) & 7;
+        const char* pl = pbase + (te >> 10) * Gm::PLANE;
+#else
         const int k = kt * 64 + cc * 8;
         int tap = (unsigned)k / (unsigned)cin;
         int ci = k - tap * cin;
         if (tap >= ktaps) tap = 0, ci = 0;           // kpad tail: weights are zero there
         const int ky = tap / KW, kx = tap - ky * KW;
+        const int toff = ky * Gm::PW + kx;
         const char* pl = pbase + (ci >> 6) * Gm::PLANE;
         const int c8 = (ci >> 3) & 7;
+#endif
         bf16x8 wf[TN], pf[TM];
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -183,7 +209,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int yq = wm * TM + i;
-          const int pr = (yq * S + ky) * Gm::PW + q * S + kx;
+          const int pr = yq * S * Gm::PW + q * S + toff;
           pf[i] = *reinterpret_cast<const bf16x8*>(pl + pr * 128 + ((c8 ^ (pr & 7)) << 4));
         }
 #pragma unroll
@@ -285,8 +311,9 @@ int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   const int bn = (d.cout + 31) / 32 * 32;
   const int nk = d.kpad / 64, nkc = (d.cin + 63) / 64;
   constexpr int LMAX = 160 * 1024;
-  auto lds_res = [&](int plane, int nbuf) { return nk * bn * 128 + nbuf * nkc * plane; };  // resident W
-  auto lds_str = [&](int plane) { return 2 * bn * 128 + nkc * plane; };                     // W ring, 1 patch
+  if (nk * 8 * 4 > TAB_BYTES && DP_HALO_TAB) return -1;
+  auto lds_res = [&](int plane, int nbuf) { return TAB_BYTES + nk * bn * 128 + nbuf * nkc * plane; };  // resident W
+  auto lds_str = [&](int plane) { return TAB_BYTES + 2 * bn * 128 + nkc * plane; };                     // W ring, 1 patch
   if (d.kh == 3 && d.kw == 3 && d.stride == 1) {
     constexpr int P16 = HaloGeom<16, 3, 3, 1>::PLANE, P8 = HaloGeom<8, 3, 3, 1>::PLANE;
     if (bn == 64 && lds_res(P16, 2) <= LMAX)
@@ -330,7 +357,7 @@ extern "C" int dp_conv2d_pool(const dp_conv_desc* dp, void* pool_out, int64_t po
   DP_REQUIRE(d.in_bstride * 2 < 0x7ff00000ll && (int64_t)d.batch * d.out_h * d.out_w < (1ll << 31),
              "dp_conv2d_pool: image exceeds 32-bit buffer offsets");
   constexpr int P = HaloGeom<8, 2, 2, 1>::PLANE;
-  const int lds = (d.kpad / 64) * 32 * 128 + P;
+  const int lds = TAB_BYTES + (d.kpad / 64) * 32 * 128 + P;
   DP_REQUIRE(lds <= 80 * 1024, "dp_conv2d_pool: weights do not fit LDS");
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int vec_ok = (d.out_pstride % 8 == 0) && (d.out_bstride % 8 == 0) && al(d.out);
