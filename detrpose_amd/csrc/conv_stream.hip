@@ -410,9 +410,9 @@ int occupancy(K kern, int threads) {
 // tiles get their bytes in flight from more resident blocks instead)
 template <int BM, int BN, int NW>
 constexpr int ring_a() {
-  constexpr int want = DP_STREAM_SA;
-  constexpr int blocks2 = (160 * 1024) / ((2 * BM + 2 * BN) * 128);
-  constexpr int blocksw = (160 * 1024) / ((want * BM + 2 * BN) * 128);
+  constexpr int want = BM == 192 ? 3 : DP_STREAM_SA;   // the 192-row tile has LDS for a 3rd A stage
+  constexpr int blocks2 = (160 * 1024) / ((2 * BM + 2 * BN) * 128 + 2048);     // + the 2 KB bias slots
+  constexpr int blocksw = (160 * 1024) / ((want * BM + 2 * BN) * 128 + 2048);
   return (blocksw >= 1 && blocksw >= blocks2) ? want : 2;
 }
 
@@ -472,6 +472,8 @@ int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
 #define DP_BIG_TILES 1
 #endif
 
+
+
 }  // namespace
 
 namespace dpconv {
@@ -499,7 +501,16 @@ int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   if (f32o) return launch<128, 128, 2, float>(d, s, vec_ok);
   // large GEMMs: 256-row tiles with 8 waves halve the LDS-DMA bytes per MFMA flop
   if (DP_BIG_TILES && M >= 32768 && d.kpad >= 256) {
-    if (d.cout > 128) return launch<256, 256, 2, bf16_t, 8>(d, s, vec_ok);
+    if (d.cout > 128) {
+      // one block per CU: a launch runs ceil(tiles / CUs) rounds, each about as long as the
+      // tile has rows. Pick 256 or 192 rows by that quantization (the 192-row tile does ~4%
+      // less per row, measured): e.g. the decoder's M = 64*1080 GEMMs and enc_output gain
+      // 7-15%, the M = 409600 FPN/stage-1 GEMMs keep 256.
+      const int nt = (d.cout + 255) / 256, cus = num_cus();
+      auto rounds = [&](int bm) { return ((int64_t)((M + bm - 1) / bm) * nt + cus - 1) / cus; };
+      if (rounds(192) * 192 * 104 < rounds(256) * 256 * 100) return launch<192, 256, 2, bf16_t, 8>(d, s, vec_ok);
+      return launch<256, 256, 2, bf16_t, 8>(d, s, vec_ok);
+    }
     if (d.kpad >= 512) return launch<256, 128, 4, bf16_t, 8>(d, s, vec_ok);
   }
   return launch<128, 128, 2, bf16_t>(d, s, vec_ok);

@@ -80,8 +80,10 @@ def _run_conv(pc, x_nhwc, out, dt, res=None, up=None):
     # 128x128 tiles with an N tail, and grids where each persistent block walks several tiles
     (3, 1, 64, 160, 70, "silu"), (1, 1, 64, 128, 200, "relu"), (3, 1, 32, 64, 256, None),
     (1, 1, 96, 32, 256, "gelu"),
-    # 8-wave 256x256 / 256x128 tiles (M >= 32768): N tail, 3x3 gather, 1x1
-    (1, 1, 256, 320, 130, "relu"), (3, 1, 64, 96, 130, "silu"), (1, 1, 512, 128, 128, None),
+    # 8-wave 192x256 / 256x256 / 256x128 tiles (M >= 32768; 192 vs 256 rows by round
+    # quantization): N tails, 3x3 gather, 1x1
+    (1, 1, 256, 320, 130, "relu"), (1, 1, 128, 288, 200, "silu"), (3, 1, 64, 96, 130, "silu"),
+    (1, 1, 512, 128, 128, None),
     # LDS halo-tile path (3x3 / 2x2, cout <= 128): streamed weights with 2 / 1.5 channel
     # planes, resident weights, stride 2 with 64 outputs, ragged tile edges
     (3, 1, 128, 128, 37, "silu"), (3, 1, 96, 96, 33, "relu"), (3, 1, 48, 48, 50, "relu"), (3, 2, 64, 64, 45, None),
