@@ -333,6 +333,9 @@ extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
   return DP_EINVAL;
 }
 
+int dp_stem1_mfma(const float* image, int batch, int h, int w, const float* weight, const float* bias, int cout,
+                  int has_lab, float ls, float lb, void* out, int64_t obs, int ops, hipStream_t s);
+
 extern "C" int dp_stem_conv(const float* image, int32_t batch, int32_t h, int32_t w, const float* weight,
                             const float* bias, int32_t cout, int32_t has_lab, float lab_scale, float lab_bias,
                             void* out, int64_t out_bstride, int32_t out_pstride, int32_t dtype, void* stream) {
@@ -342,6 +345,11 @@ extern "C" int dp_stem_conv(const float* image, int32_t batch, int32_t h, int32_
   DP_REQUIRE(total < (1ll << 31), "dp_stem_conv: batch too large");
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
   hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16) {   // bf16 storage: MFMA kernel (stem.hip), image rounded to bf16 like every activation
+    const int r = dp_stem1_mfma(image, batch, h, w, weight, bias, cout, has_lab, lab_scale, lab_bias, out, out_bstride,
+                                out_pstride, s);
+    if (r >= 0) return r;
+  }
 #define DP_STEM(T_, N_)                                                                                     \
   if (cout == N_) {                                                                                        \
     hipLaunchKernelGGL((stem_conv_kernel<T_, N_>), grid, block, 0, s, image, batch, h, w, weight, bias,     \

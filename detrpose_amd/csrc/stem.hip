@@ -18,6 +18,98 @@
 
 namespace {
 
+// StemBlock.stem1 (hgnetv2.py:171-177): 3x3 stride-2 pad-1 conv over the f32 NCHW image,
+// 3 -> COUT channels, folded BN + ReLU (+ LAB), NHWC bf16 out. K = 27 taps (c, ky, kx) fit
+// one 32-wide MFMA slab: lane (q, g) gathers k = 8g .. 8g+7 of output pixel x0 + q straight
+// from the image (f32 -> bf16 in registers; k >= 27 is zero), the f32 weights are converted
+// into the A fragments once per wave. 864 FMAs per pixel become 2 MFMAs per 16 pixels, so
+// the kernel is a stream: 12 image bytes in (L1/L2 absorb the 3x3/stride-2 overlap) and
+// 2*COUT bytes out per pixel.
+template <int COUT>
+__global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict__ img, int batch, int H, int W,
+                                                         const float* __restrict__ wt, const float* __restrict__ bias,
+                                                         int has_lab, float ls, float lb, bf16_t* __restrict__ out,
+                                                         int64_t obs, int ops) {
+  constexpr int NT = COUT / 16;
+  constexpr int G = 4;                          // 16-pixel groups in flight per wave
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;
+  bf16x8 wa[NT];
+  int tc[8], tky[8], tkx[8];
+  bool tok[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * g + e;
+    const int c = k / 9, t = k - 9 * c;
+    tok[e] = k < 27;
+    tky[e] = t / 3, tkx[e] = t - 3 * (t / 3);
+    tc[e] = k < 27 ? c : 0;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) wa[j][e] = (bf16_t)(k < 27 ? wt[(16 * j + q) * 27 + k] : 0.f);
+  }
+  float bsum[NT][4];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bsum[j][r] = bias[16 * j + 4 * g + r];
+
+  const int gx = (OW + 15) >> 4;
+  const int ngroups = batch * OH * gx;
+  const int nw = gridDim.x * 4;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // lane-constant part of each gather offset: plane c, row ky, column kx, and this lane's
+  // pixel 2q; the per-group part (image, row 2oy-1, column 2*ox0-1) is wave-uniform
+  int loff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) loff[e] = (tc[e] * H + tky[e]) * W + tkx[e] + 2 * q;
+  for (int base = wid * G; base < ngroups; base += nw * G) {
+    bf16x8 xb[G];
+    int pb[G], py[G], px0[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      // the group (image, output row, 16-pixel column block) is wave-uniform: scalar math,
+      // an SGPR image base and 32-bit lane offsets for the loads
+      const int grp = __builtin_amdgcn_readfirstlane(base + i);
+      const int gc = grp < ngroups ? grp : 0;
+      const int bb = gc / (OH * gx), rem = gc - bb * (OH * gx);
+      const int oy = rem / gx, ox0 = (rem - oy * gx) * 16;
+      pb[i] = grp < ngroups ? bb : -1, py[i] = oy, px0[i] = ox0;
+      // buffer loads from the image's base (SGPRs) with 32-bit byte offsets; an out-of-range
+      // offset returns 0 = the conv zero padding, so the gather has no branches (loads under
+      // divergent ifs would make the compiler drain vmcnt between them)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(img + (int64_t)bb * 3 * H * W), (short)0, 0x7ffffff0, 0x00020000);
+      const int u = (2 * oy - 1) * W + 2 * ox0 - 1;
+      const int ix0 = 2 * (ox0 + q) - 1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int iy = 2 * oy - 1 + tky[e], ix = ix0 + tkx[e];
+        const bool ok = tok[e] && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        const unsigned bits = __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? 4 * (u + loff[e]) : 0x7ffffff0, 0, 0);
+        xb[i][e] = (bf16_t)__builtin_bit_cast(float, bits);   // the builtin returns the raw dword
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int ox = px0[i] + q;
+      if (pb[i] < 0 || ox >= OW) continue;
+      bf16_t* op = out + (int64_t)pb[i] * obs + ((int64_t)py[i] * OW + ox) * ops;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j], xb[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = fmaxf(acc[r] + bsum[j][r], 0.f);
+          if (has_lab) v = ls * v + lb;
+          o[r] = (bf16_t)v;
+        }
+        *reinterpret_cast<bf16x4*>(op + 16 * j + 4 * g) = o;
+      }
+    }
+  }
+}
+
 template <int CIN, int COUT, bool POOL, int ACT>
 __global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __restrict__ in, int64_t ibs, int ips,
                                                              int H, int W, int batch, const bf16_t* __restrict__ wt,
@@ -72,14 +164,15 @@ __global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __res
       const int y = rem / gx, x = (rem - y * gx) * 16 + q;
       pb[i] = bb, py[i] = y, px[i] = x;
       pv[i] = grp < ngroups && x < W;
-      const bf16_t* ib = in + (int64_t)bb * ibs;
+      const bf16_t* ib = in + (int64_t)(grp < ngroups ? bb : 0) * ibs;
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
+        // branch-free: clamped (always legal) address, then select the F.pad zero
         const int iy = y + tap_dy[s], ix = x + tap_dx[s];
-        bf16x8 v = {};
-        if (grp < ngroups && tap_ok[s] && iy < H && ix < W)
-          v = *reinterpret_cast<const bf16x8*>(ib + (int64_t)(iy * W + ix) * ips + tap_ci[s]);
-        xb[i][s] = v;
+        const bool ok = grp < ngroups && tap_ok[s] && iy < H && ix < W;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(ib + (ok ? (int64_t)(iy * W + ix) * ips + tap_ci[s] : 0));
+        const bf16x8 z = {};
+        xb[i][s] = ok ? v : z;
       }
     }
 #pragma unroll
@@ -181,4 +274,19 @@ int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t 
   if (d.cin == 16 && d.cout == 32) return launch_direct<16, 32, false>(d, s, nullptr, 0, 0);
   if (d.cin == 8 && d.cout == 16) return launch_direct<8, 16, false>(d, s, nullptr, 0, 0);
   return -1;
+}
+
+// bf16 stem1 on MFMA (dp_stem_conv's bf16 path); -1 when cout has no instantiation
+int dp_stem1_mfma(const float* image, int batch, int h, int w, const float* weight, const float* bias, int cout,
+                  int has_lab, float ls, float lb, void* out, int64_t obs, int ops, hipStream_t s) {
+  if ((cout != 16 && cout != 32) || ops % 4 || obs % 4 || (reinterpret_cast<uintptr_t>(out) & 7)) return -1;
+  const int oh = (h + 1) / 2, ow = (w + 1) / 2;
+  const int64_t ngroups = (int64_t)batch * oh * ((ow + 15) / 16);
+  if (ngroups >= (1ll << 31) || (int64_t)batch * 3 * h * w >= (1ll << 31)) return -1;
+  int blocks = (int)((ngroups + 15) / 16);
+  if (blocks > 256 * 8) blocks = 256 * 8;
+  auto kern = cout == 16 ? stem1_mfma_kernel<16> : stem1_mfma_kernel<32>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, image, batch, h, w, weight, bias, has_lab, ls, lb,
+                     reinterpret_cast<bf16_t*>(out), obs, ops);
+  return dp_check_launch("dp_stem_conv(mfma)");
 }
