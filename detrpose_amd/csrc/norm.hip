@@ -83,7 +83,12 @@ __device__ __forceinline__ void ln_apply(float* v, const float* __restrict__ g, 
   for (int t = 0; t < E; ++t) v[t] = (v[t] - mean) * rstd * g[c0 + t] + bta[c0 + t];
 }
 
-template <typename T, int E>
+// R rows per wave, all of their loads issued before the first reduction: one row per wave
+// left a single 512-byte load in flight per wave, far too few bytes in flight for HBM
+// (Little's law), and the row statistics of R rows now overlap in the shuffle chains. Rows
+// past the end are clamped for the loads (legal addresses, no divergent branches around
+// them) and skipped at the store; masked rows are selected at the end.
+template <typename T, int E, int R>
 __global__ __launch_bounds__(256) void layernorm_kernel(T* out, dp_rowmap om, const T* x, dp_rowmap xm, const T* res,
                                                         dp_rowmap rm, const float* __restrict__ g,
                                                         const float* __restrict__ bta, float eps, int rows,
@@ -91,37 +96,49 @@ __global__ __launch_bounds__(256) void layernorm_kernel(T* out, dp_rowmap om, co
                                                         const uint8_t* mask, int mask_period, const float* masked_row) {
   constexpr int c = 64 * E;
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (r0 >= rows) return;
   const int c0 = lane * E;
-  float v[E];
-  T* o = out + rowmap_off(om, r) + c0;
-  if (mask && mask[(unsigned)r % (unsigned)mask_period]) {
+  float v[R][E];
 #pragma unroll
-    for (int t = 0; t < E; ++t) v[t] = masked_row[c0 + t];
-    vstore<T, E>(o, v);
-    return;
-  }
-  vload<T, E>(x + rowmap_off(xm, r) + c0, v);
+  for (int i = 0; i < R; ++i) vload<T, E>(x + rowmap_off(xm, min(r0 + i, rows - 1)) + c0, v[i]);
   if (res) {
-    float rv[E];
-    vload<T, E>(res + rowmap_off(rm, r) + c0, rv);
 #pragma unroll
-    for (int t = 0; t < E; ++t) v[t] += rv[t];
-  }
-  ln_apply<E>(v, g, bta, c0, c, eps);
-  if (post) {
-    const int grp = (unsigned)r / (unsigned)post_group;
-    const int w = r - grp * post_group;
-    if (w >= post_skip) {
-      const int pr = grp * (post_group - post_skip) + (w - post_skip);
-      float pv[E];
-      vload<T, E>(post + rowmap_off(pm, pr) + c0, pv);
+    for (int i = 0; i < R; ++i) {
+      float rv[E];
+      vload<T, E>(res + rowmap_off(rm, min(r0 + i, rows - 1)) + c0, rv);
 #pragma unroll
-      for (int t = 0; t < E; ++t) v[t] += pv[t];
+      for (int t = 0; t < E; ++t) v[i][t] += rv[t];
     }
   }
-  vstore<T, E>(o, v);
+#pragma unroll
+  for (int i = 0; i < R; ++i) ln_apply<E>(v[i], g, bta, c0, c, eps);
+  if (post) {
+    // every row's post-add is read before the first store (out may alias the post rows)
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int r = min(r0 + i, rows - 1);
+      const int grp = (unsigned)r / (unsigned)post_group;
+      const int w = r - grp * post_group;
+      if (w >= post_skip) {
+        const int pr = grp * (post_group - post_skip) + (w - post_skip);
+        float pv[E];
+        vload<T, E>(post + rowmap_off(pm, pr) + c0, pv);
+#pragma unroll
+        for (int t = 0; t < E; ++t) v[i][t] += pv[t];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int r = r0 + i;
+    if (r >= rows) break;
+    if (mask && mask[(unsigned)r % (unsigned)mask_period]) {
+#pragma unroll
+      for (int t = 0; t < E; ++t) v[i][t] = masked_row[c0 + t];
+    }
+    vstore<T, E>(out + rowmap_off(om, r) + c0, v[i]);
+  }
 }
 
 template <typename T, int E>
@@ -146,14 +163,17 @@ __global__ __launch_bounds__(256) void gate_ln_kernel(T* out, int out_ld, const 
   vstore<T, E>(out + (int64_t)r * out_ld + c0, v);
 }
 
+constexpr int LN_ROWS = 4;   // rows per wave of layernorm_kernel
+
 template <typename T>
 int launch_ln(int e, dim3 grid, hipStream_t s, T* out, dp_rowmap om, const T* x, dp_rowmap xm, const T* res,
               dp_rowmap rm, const float* g, const float* b, float eps, int rows, const T* post, dp_rowmap pm, int pg,
               int ps, const uint8_t* mask, int mp, const float* mrow) {
 #define DP_LN(E_)                                                                                                   \
   case E_:                                                                                                          \
-    hipLaunchKernelGGL((layernorm_kernel<T, E_>), grid, dim3(256), 0, s, out, om, x, xm, res, rm, g, b, eps, rows, \
-                       post, pm, pg, ps, mask, mp, mrow);                                                           \
+    hipLaunchKernelGGL((layernorm_kernel<T, E_, LN_ROWS>), grid, dim3(256), 0, s, out, om, x, xm, res, rm, g, b, eps, \
+                       rows,                                                                                        \
+                       post, pm, pg, ps, mask, mp, mrow);                                                            \
     break;
   switch (e) {
     DP_LN(2) DP_LN(4) DP_LN(6) DP_LN(8)
@@ -212,7 +232,7 @@ extern "C" int dp_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm
   DP_REQUIRE(!post || (post_group > post_skip && pm.group > 0), "dp_layernorm: bad post map");
   DP_REQUIRE(!row_mask || (mask_period > 0 && masked_row), "dp_layernorm: bad mask");
   const int e = c / 64;
-  dim3 grid((unsigned)((rows + 3) / 4));
+  dim3 grid((unsigned)((rows + 4 * LN_ROWS - 1) / (4 * LN_ROWS)));
   hipStream_t s = as_stream(stream);
   if (dtype == DP_BF16)
     return launch_ln<bf16_t>(e, grid, s, (bf16_t*)out, om, (const bf16_t*)x, xm, (const bf16_t*)res, rm, gamma, beta,
