@@ -18,6 +18,44 @@
 
 namespace {
 
+// Output channel of MFMA C element (tile j, lane group g, row r). With two 16-row tiles the
+// weight rows are permuted (A row 16j + q holds channel stem_chan(j, q>>2, q&3)) so lane g
+// ends with channels 8g..8g+7 contiguous: one 16-byte store per pixel and lane instead of
+// two 8-byte pieces 32 bytes apart. One tile: the natural order, 8-byte stores.
+template <int NT>
+__device__ __forceinline__ constexpr int stem_chan(int j, int g, int r) {
+  return NT == 2 ? 8 * g + 4 * j + r : 16 * j + 4 * g + r;
+}
+
+// bias + ReLU/none + LAB of the lane's 4*NT channels, stored as one 16-byte (NT = 2) or
+// one 8-byte (NT = 1) chunk at channel stem_chan(0, g, 0)
+template <int NT, int ACT>
+__device__ __forceinline__ void stem_store(bf16_t* op, const f32x4 (&acc)[NT], const float (&bsum)[NT][4], int g,
+                                           int cout, int has_lab, float ls, float lb) {
+  float v[4 * NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = acc[j][r] + bsum[j][r];
+      if (ACT == DP_ACT_RELU) x = fmaxf(x, 0.f);
+      if (has_lab) x = ls * x + lb;
+      v[4 * j + r] = x;
+    }
+  if constexpr (NT == 2) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16_t)v[e];
+    *reinterpret_cast<bf16x8*>(op + 8 * g) = o;
+  } else {
+    if (4 * g >= cout) return;
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (bf16_t)v[e];
+    *reinterpret_cast<bf16x4*>(op + 4 * g) = o;
+  }
+}
+
 // StemBlock.stem1 (hgnetv2.py:171-177): 3x3 stride-2 pad-1 conv over the f32 NCHW image,
 // 3 -> COUT channels, folded BN + ReLU (+ LAB), NHWC bf16 out. K = 27 taps (c, ky, kx) fit
 // one 32-wide MFMA slab: lane (q, g) gathers k = 8g .. 8g+7 of output pixel x0 + q straight
@@ -45,13 +83,13 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
     tky[e] = t / 3, tkx[e] = t - 3 * (t / 3);
     tc[e] = k < 27 ? c : 0;
 #pragma unroll
-    for (int j = 0; j < NT; ++j) wa[j][e] = (bf16_t)(k < 27 ? wt[(16 * j + q) * 27 + k] : 0.f);
+    for (int j = 0; j < NT; ++j) wa[j][e] = (bf16_t)(k < 27 ? wt[stem_chan<NT>(j, q >> 2, q & 3) * 27 + k] : 0.f);
   }
   float bsum[NT][4];
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bsum[j][r] = bias[16 * j + 4 * g + r];
+    for (int r = 0; r < 4; ++r) bsum[j][r] = bias[stem_chan<NT>(j, g, r)];
 
   const int gx = (OW + 15) >> 4;
   const int ngroups = batch * OH * gx;
@@ -94,18 +132,11 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
       const int ox = px0[i] + q;
       if (pb[i] < 0 || ox >= OW) continue;
       bf16_t* op = out + (int64_t)pb[i] * obs + ((int64_t)py[i] * OW + ox) * ops;
+      f32x4 acc[NT];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j], xb[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = fmaxf(acc[r] + bsum[j][r], 0.f);
-          if (has_lab) v = ls * v + lb;
-          o[r] = (bf16_t)v;
-        }
-        *reinterpret_cast<bf16x4*>(op + 16 * j + 4 * g) = o;
-      }
+      for (int j = 0; j < NT; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j], xb[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      stem_store<NT, DP_ACT_RELU>(op, acc, bsum, g, COUT, has_lab, ls, lb);
     }
   }
 }
@@ -134,7 +165,7 @@ __global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __res
     tap_dy[s] = t >> 1, tap_dx[s] = t & 1, tap_ci[s] = k - t * CIN;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int row = 16 * j + q;
+      const int row = stem_chan<NT>(j, q >> 2, q & 3);
       bf16x8 w = {};
       if (row < COUT && tap_ok[s]) w = *reinterpret_cast<const bf16x8*>(wt + (int64_t)row * kpad + k);
       wa[j][s] = w;
@@ -145,7 +176,7 @@ __global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __res
   for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int c = 16 * j + 4 * g + r;
+      const int c = stem_chan<NT>(j, g, r);
       bsum[j][r] = (bias && c < COUT) ? bias[c] : 0.f;
     }
 
@@ -184,24 +215,9 @@ __global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __res
 #pragma unroll
         for (int s = 0; s < NKS; ++s) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][s], xb[i][s], acc[j], 0, 0, 0);
       }
-      // C layout: lane (q, g) holds channels 16 j + 4 g + r of pixel x0 + q
+      // C layout: lane (q, g) holds channels stem_chan(j, g, r) of pixel x0 + q
       const int64_t pix = (int64_t)py[i] * W + px[i];
-      if (pv[i]) {
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const int c = 16 * j + 4 * g;
-          if (c >= COUT) continue;
-          bf16x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[j][r] + bsum[j][r];
-            if (ACT == DP_ACT_RELU) v = fmaxf(v, 0.f);
-            if (has_lab) v = ls * v + lb;
-            o[r] = (bf16_t)v;
-          }
-          *reinterpret_cast<bf16x4*>(out + (int64_t)pb[i] * obs + pix * ops + c) = o;
-        }
-      }
+      if (pv[i]) stem_store<NT, ACT>(out + (int64_t)pb[i] * obs + pix * ops, acc, bsum, g, COUT, has_lab, ls, lb);
       if constexpr (POOL) {
         bf16x8 m;
         if constexpr (CIN == 32) {
@@ -259,6 +275,7 @@ int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t 
       d.in_bstride % 8)
     return -1;
   if ((int64_t)d.batch * d.in_h * ((d.in_w + 15) / 16) >= (1ll << 31)) return -1;
+  if (d.cout > 16 && (!a16(d.out) || d.out_pstride % 8 || d.out_bstride % 8)) return -1;   // 16-byte stores
   bf16_t* pl = reinterpret_cast<bf16_t*>(pool);
   if (pool && (!a16(pool) || pps % 8 || pbs % 8)) return -1;
 #define DP_DIRECT(CI, CO)                                                          \
@@ -279,7 +296,7 @@ int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t 
 // bf16 stem1 on MFMA (dp_stem_conv's bf16 path); -1 when cout has no instantiation
 int dp_stem1_mfma(const float* image, int batch, int h, int w, const float* weight, const float* bias, int cout,
                   int has_lab, float ls, float lb, void* out, int64_t obs, int ops, hipStream_t s) {
-  if ((cout != 16 && cout != 32) || ops % 4 || obs % 4 || (reinterpret_cast<uintptr_t>(out) & 7)) return -1;
+  if ((cout != 16 && cout != 32) || ops % 8 || obs % 8 || (reinterpret_cast<uintptr_t>(out) & 15)) return -1;
   const int oh = (h + 1) / 2, ow = (w + 1) / 2;
   const int64_t ngroups = (int64_t)batch * oh * ((ow + 15) / 16);
   if (ngroups >= (1ll << 31) || (int64_t)batch * 3 * h * w >= (1ll << 31)) return -1;
