@@ -19,8 +19,14 @@ def family(name):
     # every implicit-GEMM conv variant (conv_stream/halo/gemm_kernel) is one family
     if re.search(r"conv_(stream|halo|gemm)_kernel", name):
         return "conv"
+    # stem 2x2 register-direct kernel: the plain instantiation is a dp_conv2d launch (stem2b),
+    # the POOL one is dp_conv2d_pool (stem2a + max-pool)
+    m = re.search(r"conv2x2_direct_kernel(?:ILi\d+ELi\d+ELb([01])E|<\d+, \d+, (true|false))", name)
+    if m:
+        return "conv2x2_pool" if (m.group(1) == "1" or m.group(2) == "true") else "conv"
     for key in ("dwconv_kernel", "dwconv_lds_kernel", "layernorm_kernel", "attn_mfma_kernel", "attn_short_kernel",
-                "msda_kernel", "msda_wave_kernel", "add_rows_kernel", "stem_conv_kernel", "maxpool_kernel", "class_max_kernel",
+                "msda_kernel", "msda_wave_kernel", "add_rows_kernel", "stem_conv_kernel", "stem1_mfma_kernel",
+                "maxpool_kernel", "class_max_kernel",
                 "topk_kernel", "gate_ln_kernel", "sine_embed_kernel", "lqe_kernel", "pose_refine_kernel"):
         if key in name:
             return key
