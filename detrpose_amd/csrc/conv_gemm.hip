@@ -235,7 +235,7 @@ int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
 }  // namespace
 int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok);
 int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok);
-int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps);
+int dp_conv2d_stem_direct(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps);
 namespace {
 
 template <typename T, typename TO>
@@ -249,10 +249,12 @@ int dispatch(const dp_conv_desc& d, hipStream_t s) {
   const int M = d.batch * d.out_h * d.out_w;
   if constexpr (sizeof(T) == 2) {
     // bf16: LDS halo-tile kernel for the KxK convs it covers, persistent LDS-DMA GEMM otherwise
-    if (d.kh * d.kw > 1) {
-      int r = d.kh == 2 ? dp_conv2d_stem2x2(d, s, nullptr, 0, 0) : -1;   // stem 2x2: register-direct
+    if (d.kh <= 2 && d.cin <= 32) {   // the stem's 2x2 / 1x1 convs: register-direct kernels
+      const int r = dp_conv2d_stem_direct(d, s, nullptr, 0, 0);
       if (r >= 0) return r;
-      r = dp_conv2d_halo(d, s, vec_ok);
+    }
+    if (d.kh * d.kw > 1) {
+      const int r = dp_conv2d_halo(d, s, vec_ok);
       if (r >= 0) return r;
     }
     return dp_conv2d_stream(d, s, vec_ok);

@@ -333,7 +333,7 @@ int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   return -1;
 }
 
-int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps);
+int dp_conv2d_stem_direct(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps);
 
 // dp_conv2d of a 2x2 s1 bf16 conv (pad 0, zero read past the right/bottom edge) that also
 // writes MaxPool2d(2, 1) of the same zero-padded input: StemBlock's stem2a + pool
@@ -361,7 +361,7 @@ extern "C" int dp_conv2d_pool(const dp_conv_desc* dp, void* pool_out, int64_t po
   DP_REQUIRE(lds <= 80 * 1024, "dp_conv2d_pool: weights do not fit LDS");
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int vec_ok = (d.out_pstride % 8 == 0) && (d.out_bstride % 8 == 0) && al(d.out);
-  const int r = dp_conv2d_stem2x2(d, as_stream(stream), pool_out, pool_bstride, pool_pstride);
+  const int r = dp_conv2d_stem_direct(d, as_stream(stream), pool_out, pool_bstride, pool_pstride);
   if (r >= 0) return r;   // stem shapes: register-direct kernel (stem.hip)
   const HaloPool pool{reinterpret_cast<bf16_t*>(pool_out), pool_bstride, pool_pstride};
   return launch_halo_act<8, 4, 2, 2, 1, 32, true, false, true>(d, as_stream(stream), vec_ok, lds, pool);

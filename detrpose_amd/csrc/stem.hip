@@ -27,8 +27,8 @@ __device__ __forceinline__ constexpr int stem_chan(int j, int g, int r) {
   return NT == 2 ? 8 * g + 4 * j + r : 16 * j + 4 * g + r;
 }
 
-// bias + ReLU/none + LAB of the lane's 4*NT channels, stored as one 16-byte (NT = 2) or
-// one 8-byte (NT = 1) chunk at channel stem_chan(0, g, 0)
+// bias + ReLU/none + LAB of the lane's 4*NT channels: one 16-byte chunk at channel 8g
+// (NT = 2, permuted rows) or NT 8-byte chunks at 16j + 4g (natural order)
 template <int NT, int ACT>
 __device__ __forceinline__ void stem_store(bf16_t* op, const f32x4 (&acc)[NT], const float (&bsum)[NT][4], int g,
                                            int cout, int has_lab, float ls, float lb) {
@@ -48,11 +48,14 @@ __device__ __forceinline__ void stem_store(bf16_t* op, const f32x4 (&acc)[NT], c
     for (int e = 0; e < 8; ++e) o[e] = (bf16_t)v[e];
     *reinterpret_cast<bf16x8*>(op + 8 * g) = o;
   } else {
-    if (4 * g >= cout) return;
-    bf16x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (bf16_t)v[e];
-    *reinterpret_cast<bf16x4*>(op + 4 * g) = o;
+    for (int j = 0; j < NT; ++j) {
+      if (16 * j + 4 * g >= cout) continue;
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16_t)v[4 * j + e];
+      *reinterpret_cast<bf16x4*>(op + 16 * j + 4 * g) = o;
+    }
   }
 }
 
@@ -141,17 +144,19 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
   }
 }
 
-template <int CIN, int COUT, bool POOL, int ACT>
-__global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __restrict__ in, int64_t ibs, int ips,
+// KS x KS (1 or 2) stride-1 conv, right/bottom zero padding: the stem's 2x2 convs and its
+// 1x1 stem4 (cin <= 32: one or two K slabs, output of up to 4 16-channel tiles)
+template <int KS, int CIN, int COUT, bool POOL, int ACT>
+__global__ __launch_bounds__(256) void conv_direct_kernel(const bf16_t* __restrict__ in, int64_t ibs, int ips,
                                                              int H, int W, int batch, const bf16_t* __restrict__ wt,
                                                              int kpad, const float* __restrict__ bias, int has_lab,
                                                              float ls, float lb, bf16_t* __restrict__ out, int64_t obs,
                                                              int ops, bf16_t* __restrict__ pool, int64_t pbs, int pps) {
-  constexpr int NKS = (4 * CIN + 31) / 32;   // K slabs of 32
-  constexpr int NT = (COUT + 15) / 16;       // 16-channel output tiles
-  constexpr int G = 4;                       // pixel groups (16 px each) in flight per wave
-  static_assert(CIN % 8 == 0 && COUT % 4 == 0 && CIN <= 32 && COUT <= 32, "stem 2x2 shapes");
-  static_assert(!POOL || CIN == 32 || CIN == 16, "pool: cin 16 or 32");
+  constexpr int NKS = (KS * KS * CIN + 31) / 32;   // K slabs of 32
+  constexpr int NT = (COUT + 15) / 16;             // 16-channel output tiles
+  constexpr int G = 4;                             // pixel groups (16 px each) in flight per wave
+  static_assert((KS == 1 || KS == 2) && CIN % 8 == 0 && COUT % 4 == 0 && CIN <= 32 && NT <= 4, "stem shapes");
+  static_assert(!POOL || (KS == 2 && (CIN == 32 || CIN == 16)), "pool: 2x2 window, cin 16 or 32");
   const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
 
   bf16x8 wa[NT][NKS];
@@ -161,8 +166,8 @@ __global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __res
   for (int s = 0; s < NKS; ++s) {
     const int k = 32 * s + 8 * g;
     const int t = k / CIN;
-    tap_ok[s] = t < 4;
-    tap_dy[s] = t >> 1, tap_dx[s] = t & 1, tap_ci[s] = k - t * CIN;
+    tap_ok[s] = t < KS * KS;
+    tap_dy[s] = t / KS, tap_dx[s] = t % KS, tap_ci[s] = k - t * CIN;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int row = stem_chan<NT>(j, q >> 2, q & 3);
@@ -245,29 +250,30 @@ __global__ __launch_bounds__(256) void conv2x2_direct_kernel(const bf16_t* __res
   }
 }
 
-template <int CIN, int COUT, bool POOL>
+template <int KS, int CIN, int COUT, bool POOL>
 int launch_direct(const dp_conv_desc& d, hipStream_t s, bf16_t* pool, int64_t pbs, int pps) {
   const int gx = (d.in_w + 15) / 16;
   const int64_t ngroups = (int64_t)d.batch * d.in_h * gx;
   int blocks = (int)((ngroups + 4 * 4 - 1) / (4 * 4));   // 4 waves x G = 4 groups per block pass
   if (blocks > 256 * 8) blocks = 256 * 8;   // about one resident pass of the chip
-  auto kern = d.act == DP_ACT_RELU ? conv2x2_direct_kernel<CIN, COUT, POOL, DP_ACT_RELU>
-                                   : conv2x2_direct_kernel<CIN, COUT, POOL, DP_ACT_NONE>;
+  auto kern = d.act == DP_ACT_RELU ? conv_direct_kernel<KS, CIN, COUT, POOL, DP_ACT_RELU>
+                                   : conv_direct_kernel<KS, CIN, COUT, POOL, DP_ACT_NONE>;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const bf16_t*>(d.in), d.in_bstride,
                      d.in_pstride, d.in_h, d.in_w, d.batch, reinterpret_cast<const bf16_t*>(d.weight), d.kpad, d.bias,
                      d.has_lab, d.lab_scale, d.lab_bias, reinterpret_cast<bf16_t*>(d.out), d.out_bstride, d.out_pstride,
                      pool, pbs, pps);
-  return dp_check_launch("dp_conv2d(stem 2x2 direct)");
+  return dp_check_launch("dp_conv2d(stem direct)");
 }
 
 }  // namespace
 
-// bf16 2x2 stride-1 conv with right/bottom zero padding (StemBlock stem2a / stem2b), optionally
-// with the fused stem max-pool. Returns -1 when the shape has no instantiation (the caller
-// then uses the LDS halo kernel).
-int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps) {
-  if (d.dtype != DP_BF16 || d.out_f32 || d.res || d.up || d.kh != 2 || d.kw != 2 || d.stride != 1 || d.pad_t ||
-      d.pad_l || d.out_h != d.in_h || d.out_w != d.in_w || (d.act != DP_ACT_RELU && d.act != DP_ACT_NONE))
+// bf16 stem convs as register-direct kernels: 2x2 stride 1 with right/bottom zero padding
+// (stem2a / stem2b, optionally with the fused stem max-pool) and the 1x1 stem4. Returns -1
+// when the shape has no instantiation (the caller then uses the LDS halo / GEMM kernels).
+int dp_conv2d_stem_direct(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t pbs, int pps) {
+  const int ks = d.kh;
+  if (d.dtype != DP_BF16 || d.out_f32 || d.res || d.up || (ks != 1 && ks != 2) || d.kw != ks || d.stride != 1 ||
+      d.pad_t || d.pad_l || d.out_h != d.in_h || d.out_w != d.in_w || (d.act != DP_ACT_RELU && d.act != DP_ACT_NONE))
     return -1;
   auto a8 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; };
   auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -275,21 +281,29 @@ int dp_conv2d_stem2x2(const dp_conv_desc& d, hipStream_t s, void* pool, int64_t 
       d.in_bstride % 8)
     return -1;
   if ((int64_t)d.batch * d.in_h * ((d.in_w + 15) / 16) >= (1ll << 31)) return -1;
-  if (d.cout > 16 && (!a16(d.out) || d.out_pstride % 8 || d.out_bstride % 8)) return -1;   // 16-byte stores
+  const bool nt2 = d.cout > 16 && d.cout <= 32;   // permuted rows, 16-byte stores
+  if (nt2 && (!a16(d.out) || d.out_pstride % 8 || d.out_bstride % 8)) return -1;
   bf16_t* pl = reinterpret_cast<bf16_t*>(pool);
-  if (pool && (!a16(pool) || pps % 8 || pbs % 8)) return -1;
-#define DP_DIRECT(CI, CO)                                                          \
-  if (d.cin == CI && d.cout == CO) {                                               \
-    if (pool) return launch_direct<CI, CO, true>(d, s, pl, pbs, pps);              \
-    return launch_direct<CI, CO, false>(d, s, nullptr, 0, 0);                      \
-  }
+  if (pool && (ks != 2 || !a16(pool) || pps % 8 || pbs % 8)) return -1;
   // HGNetv2 stems: B0 [3,16,16], B4 (L) [3,32,48], B5 (X) [3,32,64]
-  DP_DIRECT(32, 16)
-  DP_DIRECT(16, 8)
+  if (ks == 2) {
+#define DP_DIRECT(CI, CO)                                                          \
+    if (d.cin == CI && d.cout == CO) {                                             \
+      if (pool) return launch_direct<2, CI, CO, true>(d, s, pl, pbs, pps);         \
+      return launch_direct<2, CI, CO, false>(d, s, nullptr, 0, 0);                 \
+    }
+    DP_DIRECT(32, 16)
+    DP_DIRECT(16, 8)
 #undef DP_DIRECT
-  if (pool) return -1;
-  if (d.cin == 16 && d.cout == 32) return launch_direct<16, 32, false>(d, s, nullptr, 0, 0);
-  if (d.cin == 8 && d.cout == 16) return launch_direct<8, 16, false>(d, s, nullptr, 0, 0);
+    if (pool) return -1;
+    if (d.cin == 16 && d.cout == 32) return launch_direct<2, 16, 32, false>(d, s, nullptr, 0, 0);
+    if (d.cin == 8 && d.cout == 16) return launch_direct<2, 8, 16, false>(d, s, nullptr, 0, 0);
+    return -1;
+  }
+  // stem4 (1x1)
+  if (d.cin == 32 && d.cout == 48) return launch_direct<1, 32, 48, false>(d, s, nullptr, 0, 0);
+  if (d.cin == 32 && d.cout == 64) return launch_direct<1, 32, 64, false>(d, s, nullptr, 0, 0);
+  if (d.cin == 16 && d.cout == 16) return launch_direct<1, 16, 16, false>(d, s, nullptr, 0, 0);
   return -1;
 }
 

@@ -19,7 +19,7 @@ from pmc_traffic import family  # noqa: E402
 
 
 def kfamily(name):
-    for k in ("conv_stream_kernel", "conv_halo_kernel", "conv_gemm_kernel", "conv2x2_direct_kernel"):
+    for k in ("conv_stream_kernel", "conv_halo_kernel", "conv_gemm_kernel", "conv_direct_kernel"):
         if k in name:
             return k
     return family(name)

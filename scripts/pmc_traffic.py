@@ -19,9 +19,9 @@ def family(name):
     # every implicit-GEMM conv variant (conv_stream/halo/gemm_kernel) is one family
     if re.search(r"conv_(stream|halo|gemm)_kernel", name):
         return "conv"
-    # stem 2x2 register-direct kernel: the plain instantiation is a dp_conv2d launch (stem2b),
+    # stem register-direct kernel: the plain instantiations are dp_conv2d launches (stem2b, stem4),
     # the POOL one is dp_conv2d_pool (stem2a + max-pool)
-    m = re.search(r"conv2x2_direct_kernel(?:ILi\d+ELi\d+ELb([01])E|<\d+, \d+, (true|false))", name)
+    m = re.search(r"conv_direct_kernel(?:ILi\d+ELi\d+ELi\d+ELb([01])E|<\d+, \d+, \d+, (true|false))", name)
     if m:
         return "conv2x2_pool" if (m.group(1) == "1" or m.group(2) == "true") else "conv"
     for key in ("dwconv_kernel", "dwconv_lds_kernel", "layernorm_kernel", "attn_mfma_kernel", "attn_short_kernel",

@@ -216,18 +216,21 @@ def test_conv2d_pool_fused(cin, cout, H, W, lab):
     assert (cat[..., cin:] == 7.0).all(), "fused pool wrote outside its channel slice"
 
 
-@pytest.mark.parametrize("cin,cout,lab", [(16, 32, None), (8, 16, (0.9, 0.1)), (32, 16, None), (16, 8, None)])
-def test_conv2d_stem2x2_direct(cin, cout, lab):
-    """The stem's register-direct 2x2 kernel through dp_conv2d (stem2b writes a channel slice
-    of the concat buffer): vs torch fp32 on the bf16-rounded input, ragged 16-pixel groups."""
-    torch.manual_seed(cin * cout)
+@pytest.mark.parametrize("k,cin,cout,lab", [(2, 16, 32, None), (2, 8, 16, (0.9, 0.1)), (2, 32, 16, None),
+                                            (2, 16, 8, None), (1, 32, 48, None), (1, 32, 64, (1.1, -0.1)),
+                                            (1, 16, 16, None)])
+def test_conv2d_stem_direct(k, cin, cout, lab):
+    """The stem's register-direct kernels through dp_conv2d: 2x2 over F.pad(0,1,0,1) (stem2b
+    writes a channel slice of the concat buffer) and the 1x1 stem4 (1-4 output tiles) vs torch
+    fp32 on the bf16-rounded input, ragged 16-pixel groups."""
+    torch.manual_seed(k * cin * cout)
     pk = Packer({}, "bf16", torch.device("cuda"))
     B, H, W = 2, 23, 37
     x = torch.randn(B, cin, H, W).bfloat16().float()
-    w = torch.randn(cout, cin, 2, 2) / (2 * cin ** 0.5)
+    w = torch.randn(cout, cin, k, k) / (k * cin ** 0.5)
     b = torch.randn(cout) * 0.1
     pc = pk.conv(w.double(), b.double(), act="relu", pad=0, lab=lab)
-    ref = F.relu(F.conv2d(F.pad(x, (0, 1, 0, 1)), w, b))
+    ref = F.relu(F.conv2d(F.pad(x, (0, 1, 0, 1)) if k == 2 else x, w, b))
     if lab:
         ref = lab[0] * ref + lab[1]
     wide = torch.full((B, H, W, 2 * cout), 5.0, device="cuda", dtype=torch.bfloat16)
@@ -235,7 +238,7 @@ def test_conv2d_stem2x2_direct(cin, cout, lab):
     d = ConvDesc()
     d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = xi.data_ptr(), H * W * cin, cin, H, W, cin
     d.weight, d.kpad, d.bias = pc.w.data_ptr(), pc.kpad, pc.b.data_ptr()
-    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = 2, 2, 1, 0, 0
+    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = k, k, 1, 0, 0
     d.out, d.out_bstride, d.out_pstride = wide.data_ptr() + 2 * cout, H * W * 2 * cout, 2 * cout
     d.out_h, d.out_w, d.cout = H, W, cout
     d.batch, d.act, d.dtype = B, pc.act, _lib.DP_BF16
@@ -243,7 +246,7 @@ def test_conv2d_stem2x2_direct(cin, cout, lab):
         d.has_lab, d.lab_scale, d.lab_bias = 1, lab[0], lab[1]
     _lib.check(_lib.load().dp_conv2d(C.byref(d), _s()), "conv2x2")
     torch.cuda.synchronize()
-    _close(wide[..., cout:], ref.permute(0, 2, 3, 1), "bf16", f"stem 2x2 {cin}->{cout}")
+    _close(wide[..., cout:], ref.permute(0, 2, 3, 1), "bf16", f"stem {k}x{k} {cin}->{cout}")
     assert (wide[..., :cout] == 5.0).all(), "wrote outside the channel slice"
 
 
