@@ -408,8 +408,14 @@ int occupancy(K kern, int threads) {
 // and with them the second wave per SIMD of the 128x128 kernel
 // A-ring depth: DP_STREAM_SA where it keeps the blocks per CU of a 2-deep ring (the narrow
 // tiles get their bytes in flight from more resident blocks instead)
+#ifndef DP_NARROW_SA
+#define DP_NARROW_SA 4   // A-ring depth of the narrow-cout (BN <= 64) streaming tiles: more bytes in flight
+                         // beat a third resident block (s0 squeeze 285 -> 265 us); 0: the rule below
+#endif
+
 template <int BM, int BN, int NW>
 constexpr int ring_a() {
+  if (DP_NARROW_SA && BN <= 64) return DP_NARROW_SA;
   constexpr int want = BM == 192 ? 3 : DP_STREAM_SA;   // the 192-row tile has LDS for a 3rd A stage
   constexpr int blocks2 = (160 * 1024) / ((2 * BM + 2 * BN) * 128 + 2048);     // + the 2 KB bias slots
   constexpr int blocksw = (160 * 1024) / ((want * BM + 2 * BN) * 128 + 2048);

@@ -26,6 +26,8 @@ SHAPES = {
         ("s2.sq", 64, 40, 40, 2176, 512, 1, 1, 1, False),
         ("fpn1.cv4", 64, 80, 80, 768, 256, 1, 1, 2, False),
         ("s1.sq", 64, 80, 80, 704, 256, 1, 1, 1, False),
+        ("s0.sq", 64, 160, 160, 336, 64, 1, 1, 1, False),
+        ("s0.ex", 64, 160, 160, 64, 128, 1, 1, 1, False),
         ("s1.ex", 64, 80, 80, 256, 512, 1, 1, 1, False),
         ("s2.ex+res", 64, 40, 40, 512, 1024, 1, 1, 1, True),
         ("enc_output", 64, 1, 8400, 256, 256, 1, 1, 0, False),
