@@ -60,7 +60,12 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   constexpr int TW = Gm::TW;
   constexpr int BM = TH * TW, WM = BM / NW, TM = WM / 16, TN = BN / 16, NPL = 4 * TN;
   constexpr int GB = BN / (8 * NW);                 // weight DMA instructions per wave per K-step (ring)
-  static_assert(TM >= 1 && WM % 16 == 0 && BN % 32 == 0 && (RESW || GB >= 1) && (RESW || !DBUF), "tile");
+  // NAT (BN = 48, the 48-channel stage-0 convs): natural weight-row order, lane g holds channels
+  // 16j + 4g .. +3 of tile j, 8-byte stores; otherwise the lane_chan permutation (16-byte stores)
+  constexpr bool NAT = NPL % 8 != 0;
+  static_assert(TM >= 1 && WM % 16 == 0 && BN % 16 == 0 && (RESW || (GB >= 1 && BN % 32 == 0)) && (RESW || !DBUF),
+                "tile");
+  static_assert(!NAT || (RESW && !POOL), "natural-order tiles: resident weights, plain epilogue");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -82,7 +87,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   // weight row -> LDS row R permuted for the register epilogue (single wave column)
   auto w_off = [&](int R) {
     const int j = R / 16, p = R % 16;
-    const int n = lane_chan<8>(p >> 2, 4 * j + (p & 3));
+    const int n = NAT ? R : lane_chan<8>(p >> 2, 4 * j + (p & 3));
     return n < d.cout ? n * d.kpad + ((lane & 7) ^ (R & 7)) * 8 : OOB;
   };
   if (RESW) {
@@ -223,7 +228,37 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
     step(0, std::true_type{});
     for (int kt = 1; kt < nk; ++kt) step(kt, std::false_type{});
     // epilogue: lane owns pixel (oy0 + yq, ox0 + q), channels lane_chan(g, 0 .. NPL-1)
-    {
+    if constexpr (NAT) {
+      // channels 16j + 4g + r: bias + act + LAB, one 8-byte store per tile j (no res / up:
+      // the dispatcher routes only plain convs here)
+      float bias[TN][4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cc = 16 * j + 4 * g + r;
+          bias[j][r] = (d.bias && cc < d.cout) ? d.bias[cc] : 0.f;
+        }
+      bf16_t* outp = reinterpret_cast<bf16_t*>(d.out) + (int64_t)b * d.out_bstride;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int oy = oy0 + wm * TM + i, ox = ox0 + q;
+        if (oy >= d.out_h || ox >= d.out_w) continue;
+        bf16_t* op = outp + (int64_t)(oy * d.out_w + ox) * d.out_pstride;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (16 * j + 4 * g >= d.cout) continue;
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = act_t<ACT>(acc[i][j][r] + bias[j][r]);
+            if (d.has_lab) v = d.lab_scale * v + d.lab_bias;
+            o[r] = (bf16_t)v;
+          }
+          *reinterpret_cast<bf16x4*>(op + 16 * j + 4 * g) = o;
+        }
+      }
+    } else {
       float bias[NPL];
       load_bias<bf16_t, NPL>(d, 0, g, bias);
       const bool full = lane_full<bf16_t, NPL>(d, 0, g, vec_ok);
@@ -314,8 +349,13 @@ int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   if (nk * 8 * 4 > TAB_BYTES && DP_HALO_TAB) return -1;
   auto lds_res = [&](int plane, int nbuf) { return TAB_BYTES + nk * bn * 128 + nbuf * nkc * plane; };  // resident W
   auto lds_str = [&](int plane) { return TAB_BYTES + 2 * bn * 128 + nkc * plane; };                     // W ring, 1 patch
+  auto lds_res48 = [&](int plane, int nbuf) { return TAB_BYTES + nk * 48 * 128 + nbuf * nkc * plane; };
   if (d.kh == 3 && d.kw == 3 && d.stride == 1) {
     constexpr int P16 = HaloGeom<16, 3, 3, 1>::PLANE, P8 = HaloGeom<8, 3, 3, 1>::PLANE;
+    // 48 output channels (HG stage 0 of L/X): a 48-wide tile, 25% fewer MFMAs than 64
+    if (d.cout == 48 && !d.res && !d.up && d.out_pstride % 4 == 0 && d.out_bstride % 4 == 0 &&
+        (reinterpret_cast<uintptr_t>(d.out) & 7) == 0 && lds_res48(P16, 2) <= LMAX)
+      return launch_halo_act<16, 8, 3, 3, 1, 48, true, true>(d, s, vec_ok, lds_res48(P16, 2));
     if (bn == 64 && lds_res(P16, 2) <= LMAX)
       return launch_halo_act<16, 8, 3, 3, 1, 64, true, true>(d, s, vec_ok, lds_res(P16, 2));
     if (bn == 32 && lds_res(P8, 1) <= 80 * 1024) return launch_halo_act<8, 4, 3, 3, 1, 32, true>(d, s, vec_ok, lds_res(P8, 1));

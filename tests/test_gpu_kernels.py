@@ -105,6 +105,34 @@ def test_conv2d(dt, k, s, cin, cout, H, act):
     _close(out[..., :cout], ref.permute(0, 2, 3, 1) + resid[..., :cout], dt, f"conv k{k}s{s} {cin}->{cout}")
 
 
+@pytest.mark.parametrize("H,W,act", [(50, 53, "relu"), (160, 160, "silu"), (17, 9, None)])
+def test_conv2d_halo_48(H, W, act):
+    """The 48-wide natural-order halo tile (HG stage-0 3x3 48->48 convs, no residual) writing a
+    channel slice of a wider concat buffer, as the HG_Block layers do; ragged 16x16 tiles and
+    the model's 160x160 map."""
+    torch.manual_seed(H * W)
+    pk = Packer({}, "bf16", torch.device("cuda"))
+    B, cin, cout, ld = 2, 48, 48, 336
+    x = torch.randn(B, cin, H, W).bfloat16().float()
+    w = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pk.conv(w.double(), b.double(), act=act)
+    ref = {"relu": F.relu, "silu": F.silu, None: lambda t: t}[act](F.conv2d(x, w, b, 1, 1))
+    wide = torch.full((B, H, W, ld), 3.0, device="cuda", dtype=torch.bfloat16)
+    xi = _nhwc(x, "bf16")
+    d = ConvDesc()
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = xi.data_ptr(), H * W * cin, cin, H, W, cin
+    d.weight, d.kpad, d.bias = pc.w.data_ptr(), pc.kpad, pc.b.data_ptr()
+    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = 3, 3, 1, 1, 1
+    d.out, d.out_bstride, d.out_pstride = wide.data_ptr() + 2 * 96, H * W * ld, ld
+    d.out_h, d.out_w, d.cout = H, W, cout
+    d.batch, d.act, d.dtype = B, pc.act, _lib.DP_BF16
+    _lib.check(_lib.load().dp_conv2d(C.byref(d), _s()), "conv halo48")
+    torch.cuda.synchronize()
+    _close(wide[..., 96:96 + cout], ref.permute(0, 2, 3, 1), "bf16", "halo 48")
+    assert (wide[..., :96] == 3.0).all() and (wide[..., 96 + cout:] == 3.0).all(), "wrote outside its slice"
+
+
 @pytest.mark.parametrize("dt", DT)
 def test_conv2d_stem_pad_and_upsample(dt):
     """2x2 conv over F.pad(0,1,0,1) (StemBlock) and the x2 nearest upsample epilogue."""
