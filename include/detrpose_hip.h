@@ -146,6 +146,15 @@ int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, const int32_t*
                      int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value,
                      float* grad_loc, float* grad_attn, int32_t dtype, void* stream);
 
+/* Input pipeline of the reference benchmark (tools/benchmark/dataset.py:56-61) for one image
+ * decoded to uint8 RGB (3, h, w) on the device: T.Resize to (new_h, new_w) (bilinear with
+ * antialias, round + clamp to uint8, as torchvision's tensor resize), PadToSize(out_h, out_w)
+ * with `fill` on the right / bottom, ConvertImageDtype(float) (/255) into out f32
+ * (3, out_h, out_w), i.e. one slot of the model's input batch. The resize size is the
+ * caller's (T.Resize(639, max_size=640) rule: detrpose_amd.preprocess.resized_size). */
+int dp_resize_pad(const uint8_t* img, int32_t h, int32_t w, int32_t new_h, int32_t new_w,
+                  float* out, int32_t out_h, int32_t out_w, float fill, void* stream);
+
 /* Per-row top-k of f32 scores, sorted descending, ties to the lower index:
  * torch.topk over the two-stage class score (transformer.py:1240) and in PostProcess
  * (postprocesses.py:19).  k <= 256, n <= 16384. idx is int64. */
