@@ -294,6 +294,13 @@ int launch_dw_lds(const dp_conv_desc& d, hipStream_t s) {
 
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+#ifndef DP_DW5_TH
+#define DP_DW5_TH 8    // output rows per 5x5 tile
+#endif
+#ifndef DP_DWS2_TH
+#define DP_DWS2_TH 2   // output rows per 3x3 stride-2 tile (2: more, smaller blocks in flight; 2-3% over 4)
+#endif
+
 }  // namespace
 
 extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
@@ -308,9 +315,9 @@ extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
   hipStream_t s = as_stream(stream);
   static const bool no_lds = getenv("DETRPOSE_DW_NO_LDS") != nullptr;
   if (d.dtype == DP_BF16 && d.cin % 64 == 0 && !no_lds) {
-    if (d.kh == 5 && d.kw == 5 && d.stride == 1) return launch_dw_lds<5, 1, 8, 20, 5>(d, s);
+    if (d.kh == 5 && d.kw == 5 && d.stride == 1) return launch_dw_lds<5, 1, DP_DW5_TH, 20, 5>(d, s);
     if (d.kh == 3 && d.kw == 3 && d.stride == 1) return launch_dw_lds<3, 1, 8, 20, 5>(d, s);
-    if (d.kh == 3 && d.kw == 3 && d.stride == 2) return launch_dw_lds<3, 2, 4, 16, 2>(d, s);
+    if (d.kh == 3 && d.kw == 3 && d.stride == 2) return launch_dw_lds<3, 2, DP_DWS2_TH, 16, 2>(d, s);
   }
   const int nchunk = d.cin / VEC;
   constexpr int PX = 4;

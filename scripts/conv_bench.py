@@ -35,6 +35,12 @@ SHAPES = {
         ("dec.ffn2", 64, 1, 1080, 1024, 256, 1, 1, 0, False),
         ("dec.gate", 64, 1, 1080, 512, 512, 1, 1, 0, False),
     ],
+    "dw": [
+        ("s1.down dw3s2", 64, 160, 160, 128, 128, 3, 2, 0, False),
+        ("s2.down dw3s2", 64, 80, 80, 512, 512, 3, 2, 0, False),
+        ("s2.l dw5", 64, 40, 40, 192, 192, 5, 1, 0, False),
+        ("s3.l dw5", 64, 20, 20, 384, 384, 5, 1, 0, False),
+    ],
     "conv3": [
         ("s0.l (48ch)", 64, 160, 160, 48, 48, 3, 1, 1, False),
         ("s1.l (96ch)", 64, 80, 80, 96, 96, 3, 1, 1, False),
@@ -46,18 +52,22 @@ SHAPES = {
 
 def load(path):
     lib = C.CDLL(path)
-    lib.dp_conv2d.restype = C.c_int32
-    lib.dp_conv2d.argtypes = [C.POINTER(ConvDesc), C.c_void_p]
+    for fn in (lib.dp_conv2d, lib.dp_dwconv2d):
+        fn.restype = C.c_int32
+        fn.argtypes = [C.POINTER(ConvDesc), C.c_void_p]
     return lib
 
 
 def make(shape, dev):
     name, B, H, W, cin, cout, k, s, act, res = shape
+    dw = " dw" in name
     kpad = (k * k * cin + 63) // 64 * 64
     pad = (k - 1) // 2
     oh, ow = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
     x = torch.randn(B * H * W * cin, device=dev).to(torch.bfloat16)
     w = (torch.randn(cout, kpad, device=dev) / (k * k * cin) ** 0.5).to(torch.bfloat16)
+    if dw:   # depthwise: f32 [k][k][C] weights
+        w = torch.randn(k * k * cin, device=dev) / k
     b = torch.randn(cout, device=dev) * 0.05
     y = torch.empty(B * oh * ow * cout, device=dev, dtype=torch.bfloat16)
     r = torch.randn(B * oh * ow * cout, device=dev).to(torch.bfloat16) if res else None
@@ -70,8 +80,8 @@ def make(shape, dev):
         d.res, d.res_bstride, d.res_pstride = r.data_ptr(), oh * ow * cout, cout
     d.batch, d.act, d.dtype = B, act, DP_BF16
     M = B * oh * ow
-    flops = 2.0 * M * cout * k * k * cin
-    byts = 2.0 * (B * H * W * cin + cout * k * k * cin + M * cout * (2 if res else 1))
+    flops = 2.0 * M * cout * k * k * (1 if dw else cin)
+    byts = 2.0 * (B * H * W * cin + (2 * k * k * cin if dw else cout * k * k * cin) + M * cout * (2 if res else 1))
     return d, (x, w, b, y, r), flops, byts, (M, cout, k * k * cin)
 
 
@@ -117,7 +127,7 @@ def main():
         for _ in range(a.rounds):
             for n, lib in libs:
                 def f(lib=lib):
-                    rc = lib.dp_conv2d(C.byref(d), s)
+                    rc = (lib.dp_dwconv2d if " dw" in sh[0] else lib.dp_conv2d)(C.byref(d), s)
                     assert rc == 0, rc
                 res[n].append(time_it(f, a.reps))
                 if a.check and n not in outs:
