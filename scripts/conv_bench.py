@@ -45,6 +45,7 @@ SHAPES = {
         ("s0.l (48ch)", 64, 160, 160, 48, 48, 3, 1, 1, False),
         ("s1.l (96ch)", 64, 80, 80, 96, 96, 3, 1, 1, False),
         ("fpn1.vgg (128ch)", 64, 80, 80, 128, 128, 3, 1, 2, False),
+        ("fpn0.vgg (128ch)", 64, 40, 40, 128, 128, 3, 1, 2, False),
         ("stem3 s2", 64, 320, 320, 64, 32, 3, 2, 1, False),
     ],
 }
