@@ -62,6 +62,7 @@ _SIGS = {
     "dp_gate_layernorm": (i32, [vp, i32, vp, vp, vp, vp, f32, i32, i32, i32, vp]),
     "dp_attention": (i32, [vp, i32, vp, vp, i32, vp, i32, i32, i32, i64, i64, i64, i32, i32, i32, i32, vp]),
     "dp_msda": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "dp_layernorm_classmax": (i32, [vp, vp, vp, vp, f32, i32, i32, vp, i32, vp, vp, vp, i32, vp, i32, vp]),
     "dp_resize_pad": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, f32, vp]),
     "dp_msda_core_fwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "dp_msda_core_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, i32, vp]),

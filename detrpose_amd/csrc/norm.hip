@@ -141,6 +141,48 @@ __global__ __launch_bounds__(256) void layernorm_kernel(T* out, dp_rowmap om, co
   }
 }
 
+// Two-stage selection head in one pass (transformer.py:1232-1240): LayerNorm of contiguous
+// rows (+ border mask: masked rows take masked_row), the row stored in T, and
+// cls_out[r] = max_j (y . w_j + b_j) over the STORED (T-rounded) row y, so the class scores
+// equal what dp_class_max would compute from the written rows, without reading them again.
+template <typename T, int E, int R>
+__global__ __launch_bounds__(256) void ln_classmax_kernel(T* out, const T* x, const float* __restrict__ g,
+                                                          const float* __restrict__ bta, float eps, int rows,
+                                                          const uint8_t* mask, int mask_period,
+                                                          const float* masked_row, const float* __restrict__ cw,
+                                                          const float* __restrict__ cb, int ncls, float* cls_out) {
+  constexpr int c = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (r0 >= rows) return;
+  const int c0 = lane * E;
+  float v[R][E];
+#pragma unroll
+  for (int i = 0; i < R; ++i) vload<T, E>(x + (int64_t)min(r0 + i, rows - 1) * c + c0, v[i]);
+#pragma unroll
+  for (int i = 0; i < R; ++i) ln_apply<E>(v[i], g, bta, c0, c, eps);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int r = r0 + i;
+    if (r >= rows) break;
+    if (mask && mask[(unsigned)r % (unsigned)mask_period]) {
+#pragma unroll
+      for (int t = 0; t < E; ++t) v[i][t] = masked_row[c0 + t];
+    }
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[i][t] = to_f32(from_f32<T>(v[i][t]));   // the stored value
+    vstore<T, E>(out + (int64_t)r * c + c0, v[i]);
+    float best = -INFINITY;
+    for (int j = 0; j < ncls; ++j) {
+      float sj = 0.f;
+#pragma unroll
+      for (int t = 0; t < E; ++t) sj = fmaf(v[i][t], cw[j * c + c0 + t], sj);
+      best = fmaxf(best, wave_sum(sj) + cb[j]);
+    }
+    if (lane == 0) cls_out[r] = best;
+  }
+}
+
 template <typename T, int E>
 __global__ __launch_bounds__(256) void gate_ln_kernel(T* out, int out_ld, const T* gates, const T* xcat,
                                                       const float* __restrict__ g, const float* __restrict__ bta,
@@ -240,6 +282,32 @@ extern "C" int dp_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm
                              masked_row);
   return launch_ln<float>(e, grid, s, (float*)out, om, (const float*)x, xm, (const float*)res, rm, gamma, beta, eps,
                           rows, (const float*)post, pm, post_group, post_skip, row_mask, mask_period, masked_row);
+}
+
+extern "C" int dp_layernorm_classmax(void* out, const void* x, const float* gamma, const float* beta, float eps,
+                                     int32_t rows, int32_t c, const uint8_t* row_mask, int32_t mask_period,
+                                     const float* masked_row, const float* cls_w, const float* cls_b, int32_t nclass,
+                                     float* cls_out, int32_t dtype, void* stream) {
+  DP_REQUIRE(out && x && gamma && beta && cls_w && cls_b && cls_out, "dp_layernorm_classmax: null pointer");
+  DP_REQUIRE(c % 64 == 0 && c / 64 <= 8 && nclass >= 1 && nclass <= 4,
+             "dp_layernorm_classmax: c=%d (multiple of 64, <= 512), nclass=%d (1..4)", c, nclass);
+  DP_REQUIRE(!row_mask || (mask_period > 0 && masked_row), "dp_layernorm_classmax: bad mask");
+  DP_REQUIRE((int64_t)rows * c < (1ll << 40), "dp_layernorm_classmax: too many rows");
+  const int e = c / 64;
+  dim3 grid((unsigned)((rows + 4 * LN_ROWS - 1) / (4 * LN_ROWS)));
+  hipStream_t s = as_stream(stream);
+#define DP_LNC(T_, E_)                                                                                          \
+  case E_:                                                                                                      \
+    hipLaunchKernelGGL((ln_classmax_kernel<T_, E_, LN_ROWS>), grid, dim3(256), 0, s, (T_*)out, (const T_*)x,    \
+                       gamma, beta, eps, rows, row_mask, mask_period, masked_row, cls_w, cls_b, nclass, cls_out); \
+    break;
+  if (dtype == DP_BF16) {
+    switch (e) { DP_LNC(bf16_t, 2) DP_LNC(bf16_t, 4) DP_LNC(bf16_t, 6) DP_LNC(bf16_t, 8) default: return DP_EINVAL; }
+  } else {
+    switch (e) { DP_LNC(float, 2) DP_LNC(float, 4) DP_LNC(float, 6) DP_LNC(float, 8) default: return DP_EINVAL; }
+  }
+#undef DP_LNC
+  return dp_check_launch("dp_layernorm_classmax");
 }
 
 extern "C" int dp_gate_layernorm(void* out, int32_t out_ld, const void* gates, const void* xcat, const float* gamma,

@@ -727,12 +727,19 @@ class Engine:
         eo = self._fmap(1, 1, rows_m, Cc)
         self._conv(plan, "ts.enc_output", mem_rows, P["enc_output"], eo)
         om = self._fmap(1, 1, rows_m, Cc)
-        self._ln(plan, "ts.enc_norm", om.ptr, contiguous_rows(Cc), eo.ptr, contiguous_rows(Cc), None, None,
-                 P["enc_norm"], rows_m, Cc, mask=(P["mask"], S, P["masked_row"]))
         score = self._empty(rows_m, dtype=torch.float32)
         wc, bc = P["enc_cls"]
-        plan._op("ts.class_max", lib.dp_class_max, om.ptr, rows_m, Cc, wc.data_ptr(), bc.data_ptr(), wc.shape[0],
-                 score.data_ptr(), self.code)
+        if self.code == _lib.DP_BF16 and wc.shape[0] <= 4:
+            # LN + class-score max in one pass over the rows (dp_layernorm_classmax)
+            g_, b_ = P["enc_norm"]
+            plan._op("ts.enc_norm", lib.dp_layernorm_classmax, om.ptr, eo.ptr, g_.data_ptr(), b_.data_ptr(),
+                     C.c_float(1e-5), rows_m, Cc, P["mask"].data_ptr(), S, P["masked_row"].data_ptr(), wc.data_ptr(),
+                     bc.data_ptr(), wc.shape[0], score.data_ptr(), self.code)
+        else:
+            self._ln(plan, "ts.enc_norm", om.ptr, contiguous_rows(Cc), eo.ptr, contiguous_rows(Cc), None, None,
+                     P["enc_norm"], rows_m, Cc, mask=(P["mask"], S, P["masked_row"]))
+            plan._op("ts.class_max", lib.dp_class_max, om.ptr, rows_m, Cc, wc.data_ptr(), bc.data_ptr(), wc.shape[0],
+                     score.data_ptr(), self.code)
         topv = self._empty(B, nq, dtype=torch.float32)
         topi = self._empty(B, nq, dtype=torch.int64)
         plan._op("ts.topk", lib.dp_topk, score.data_ptr(), B, S, S, nq, topv.data_ptr(), topi.data_ptr())

@@ -155,6 +155,15 @@ int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, const int32_t*
 int dp_resize_pad(const uint8_t* img, int32_t h, int32_t w, int32_t new_h, int32_t new_w,
                   float* out, int32_t out_h, int32_t out_w, float fill, void* stream);
 
+/* dp_layernorm over contiguous rows (+ border mask) that also writes
+ * cls_out[r] = max_j (y[r] . w[j] + b[j]), j < nclass, of the STORED (dtype-rounded) row y:
+ * the two-stage enc_output_norm + enc_out_class_embed + .max(-1) (transformer.py:1232-1240)
+ * in one pass (= dp_layernorm then dp_class_max, without re-reading the rows). */
+int dp_layernorm_classmax(void* out, const void* x, const float* gamma, const float* beta, float eps,
+                          int32_t rows, int32_t c, const uint8_t* row_mask, int32_t mask_period,
+                          const float* masked_row, const float* cls_w, const float* cls_b, int32_t nclass,
+                          float* cls_out, int32_t dtype, void* stream);
+
 /* Per-row top-k of f32 scores, sorted descending, ties to the lower index:
  * torch.topk over the two-stage class score (transformer.py:1240) and in PostProcess
  * (postprocesses.py:19).  k <= 256, n <= 16384. idx is int64. */

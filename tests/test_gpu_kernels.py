@@ -279,6 +279,40 @@ def test_conv2d_stem_direct(k, cin, cout, lab):
 
 
 @pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("rows,ncls", [(1000, 2), (8400 * 2 + 37, 3)])
+def test_layernorm_classmax(dt, rows, ncls):
+    """dp_layernorm_classmax (enc_output_norm + enc_out_class_embed + max, one pass): the rows
+    vs torch LayerNorm with the border mask, the scores vs max_j(y . w_j + b_j) over the
+    STORED rows (what dp_class_max would read), fp32 CPU reference."""
+    lib = _lib.load()
+    torch.manual_seed(rows + ncls)
+    c, period = 256, 8400
+    x = torch.randn(rows, c) * 2 + 0.3
+    g = torch.rand(c) + 0.5
+    b = torch.randn(c) * 0.1
+    mask = (torch.rand(period) < 0.05).to(torch.uint8)
+    mrow = torch.randn(c)
+    w = torch.randn(ncls, c) / 16
+    wb = torch.randn(ncls) * 0.1
+    tdt = DTYPES[dt][0]
+    xi = x.to("cuda", tdt)
+    out = torch.empty(rows, c, device="cuda", dtype=tdt)
+    score = torch.empty(rows, device="cuda")
+    _lib.check(lib.dp_layernorm_classmax(out.data_ptr(), xi.data_ptr(), _d(g), _d(b), C.c_float(1e-5), rows, c,
+                                         _d(mask), period, _d(mrow), _d(w), _d(wb), ncls, score.data_ptr(),
+                                         DTYPES[dt][1], _s()), "ln_classmax")
+    torch.cuda.synchronize()
+    ref = F.layer_norm(xi.float().cpu(), (c,), g, b, 1e-5)
+    m = mask[torch.arange(rows) % period].bool()
+    ref[m] = mrow
+    _close(out, ref, dt, "ln rows")
+    y = out.float().cpu()
+    sref = (y @ w.t() + wb).max(-1).values
+    err = (score.cpu() - sref).abs().max().item()
+    assert err <= 1e-4 * max(1.0, sref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("c", [128, 256, 384])
 def test_layernorm_variants(dt, c):
     lib = _lib.load()
