@@ -270,6 +270,8 @@ __global__ __launch_bounds__(256) void linear_small_kernel(const T* __restrict__
 }
 
 // one wave per query row: lane j < 2*nkp owns (keypoint j/2, coordinate j&1)
+constexpr int POSE_MAXZ = 1280;   // 2 * nkp * (reg_max + 1) floats per row staged in LDS
+
 __global__ __launch_bounds__(256) void pose_refine_kernel(const float* __restrict__ corners,
                                                           const float* __restrict__ project, int reg_max,
                                                           const float* __restrict__ ref_init, float reg_scale,
@@ -282,8 +284,19 @@ __global__ __launch_bounds__(256) void pose_refine_kernel(const float* __restric
   const bool act = lane < 2 * nkp;
   const int kp = lane >> 1, c = lane & 1;
   float val = 0.f;
+  // the row's 2*nkp*nb distribution logits are contiguous: stage them through LDS with
+  // coalesced loads (one lane per (keypoint, coordinate) walking its nb bins straight from
+  // global memory was a serial chain of 2*nb scattered loads per lane)
+  __shared__ float zs[4][POSE_MAXZ];
+  const int nz = 2 * nkp * nb;
+  const float* zrow = corners + (int64_t)r * nz;
+  float* zw = zs[threadIdx.x >> 6];
+  for (int i = lane; i < nz; i += 64) zw[i] = zrow[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (act) {
-    const float* z = corners + ((int64_t)(r * nkp + kp) * 2 + c) * nb;
+    const float* z = zw + (kp * 2 + c) * nb;
     float mx = -INFINITY;
     for (int i = 0; i < nb; ++i) mx = fmaxf(mx, z[i]);
     float se = 0.f, acc = 0.f;
@@ -499,7 +512,8 @@ extern "C" int dp_linear_small(const void* x, dp_rowmap xm, int32_t x_dtype, int
 
 extern "C" int dp_pose_refine(const float* corners, const float* project, int32_t reg_max, const float* ref_init,
                               float reg_scale, int32_t rows, int32_t nkp, float* kps, float* ref, void* stream) {
-  DP_REQUIRE(2 * nkp <= 64, "dp_pose_refine: nkp=%d (max 32)", nkp);
+  DP_REQUIRE(2 * nkp <= 64 && 2 * nkp * (reg_max + 1) <= POSE_MAXZ, "dp_pose_refine: nkp=%d reg_max=%d too large",
+             nkp, reg_max);
   hipLaunchKernelGGL(pose_refine_kernel, dim3(nblk(rows, 4)), dim3(256), 0, as_stream(stream), corners, project,
                      reg_max, ref_init, reg_scale, rows, nkp, kps, ref);
   return dp_check_launch("dp_pose_refine");
