@@ -34,6 +34,8 @@ SHAPES = {
         ("dec.ffn1", 64, 1, 1080, 256, 1024, 1, 1, 1, False),
         ("dec.ffn2", 64, 1, 1080, 1024, 256, 1, 1, 0, False),
         ("dec.gate", 64, 1, 1080, 512, 512, 1, 1, 0, False),
+        ("dec.out256", 64, 1, 1080, 256, 256, 1, 1, 0, False),
+        ("dec.pose0", 64, 1, 1020, 256, 256, 1, 1, 1, False),
     ],
     "dw": [
         ("s1.down dw3s2", 64, 160, 160, 128, 128, 3, 2, 0, False),
