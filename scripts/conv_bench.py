@@ -36,6 +36,8 @@ SHAPES = {
         ("dec.gate", 64, 1, 1080, 512, 512, 1, 1, 0, False),
         ("dec.out256", 64, 1, 1080, 256, 256, 1, 1, 0, False),
         ("dec.pose0", 64, 1, 1020, 256, 256, 1, 1, 1, False),
+        ("dec.offattn", 64, 1, 1080, 256, 288, 1, 1, 0, False),
+        ("dec.pose2", 64, 1, 1020, 256, 66, 1, 1, 0, False),
     ],
     "dw": [
         ("s1.down dw3s2", 64, 160, 160, 128, 128, 3, 2, 0, False),
