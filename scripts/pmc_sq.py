@@ -1,5 +1,6 @@
 """Per-kernel-family SQ counters from one rocprofv3 --pmc pass (scripts/gpu_round.sh):
-MFMA busy fraction, LDS bank-conflict fraction and wave-state split.
+MFMA busy fraction, LDS bank-conflict fraction and wave-state split; plus the three conv
+kernel instantiations with the most GPU time ("top3: <kernel name>").
 
     python scripts/pmc_sq.py <pmc_sq counter_collection.csv> [out.json]
 
@@ -27,18 +28,27 @@ def kfamily(name):
 
 def main():
     per = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = {}
+    disp, name = {}, {}
     for r in csv.DictReader(open(sys.argv[1])):
         key = r["Dispatch_Id"]
         disp[key] = kfamily(r["Kernel_Name"])
+        name[key] = r["Kernel_Name"]
         per[key][r["Counter_Name"]] += float(r["Counter_Value"])
     fam = collections.defaultdict(lambda: collections.defaultdict(float))
+    inst = collections.defaultdict(lambda: collections.defaultdict(float))   # per kernel instantiation
     for k, cs in per.items():
         for c, v in cs.items():
             fam[disp[k]][c] += v
+            if disp[k].startswith("conv_"):
+                inst[name[k]][c] += v
         fam[disp[k]]["dispatches"] += 1
+        if disp[k].startswith("conv_"):
+            inst[name[k]]["dispatches"] += 1
     out = {}
-    for f, cs in sorted(fam.items(), key=lambda kv: -kv[1]["GRBM_GUI_ACTIVE"]):
+    # the three conv instantiations with the most GPU time get their own rows
+    top = sorted(inst.items(), key=lambda kv: -kv[1]["GRBM_GUI_ACTIVE"])[:3]
+    groups = sorted(fam.items(), key=lambda kv: -kv[1]["GRBM_GUI_ACTIVE"]) + [("top3: " + n, cs) for n, cs in top]
+    for f, cs in groups:
         gui = cs["GRBM_GUI_ACTIVE"] / 8.0
         if gui <= 0 or f == "other":
             continue
@@ -49,7 +59,7 @@ def main():
                "wait_any": cs["SQ_WAIT_ANY"] / wc, "wait_inst": cs["SQ_WAIT_INST_ANY"] / wc,
                "active": 1.0 - (cs["SQ_WAIT_ANY"] + cs["SQ_WAIT_INST_ANY"]) / wc}
         out[f] = row
-        print(f"{f:22s} n={row['dispatches']:4d} mfma_busy {row['mfma_busy']:.3f} lds_conflict "
+        print(f"{f[:60]:22s} n={row['dispatches']:4d} mfma_busy {row['mfma_busy']:.3f} lds_conflict "
               f"{row['lds_conflict']:.4f} wait_any {row['wait_any']:.2f} wait_inst {row['wait_inst']:.2f} "
               f"active {row['active']:.2f}")
     if len(sys.argv) > 2:
