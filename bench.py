@@ -25,7 +25,8 @@ Also reported (rank 0):
   latency_bs1   the reference's latency protocol (torch_benchmark.py:29-51): batch 1,
                 400 warm-up and 1000 timed Model(images, sizes) calls (hipGraph replay,
                 synchronised each), mean of the fastest 100 and the median;
-  secondary     DETRPose-N bf16 batch 32 throughput (BASELINE configs[1]);
+  secondary     DETRPose-N bf16 batch 32 (BASELINE configs[1]) and DETRPose-X bf16 batch 32
+                (the per-GPU shard of configs[3]) throughput;
   cpu_baseline  the CPU oracle restatement (oracle/detrpose_cpu.py, kind "port") at
                 batch 1 and 8 (2 warm-up + 5 timed) on the host cores (N=1 only).
 """
@@ -357,12 +358,17 @@ def main():
         if world == 1 and not a.no_latency:
             out["latency_bs1"] = latency_bs1(model, pp, dev, a.latency_runs, a.latency_warmup)
         if world == 1 and not a.no_secondary:
-            mn, _ = build_model("n", dtype=a.dtype)
-            load_synthetic(mn, 0)
-            mn.deploy()
-            v, fin = throughput(mn, dev, 32, max(20, a.steps // 2), 5)
-            out["secondary"] = [{"workload": "DETRPose-N bf16 batch 32 640x640 (BASELINE configs[1])",
-                                 "value": round(v, 2), "unit": "images/sec", "outputs_finite": fin}]
+            out["secondary"] = []
+            for sz, bs, what in (("n", 32, "BASELINE configs[1]"),
+                                 ("x", 32, "the per-GPU shard of BASELINE configs[3], X b256 over 8 GPUs")):
+                ms, _ = build_model(sz, dtype=a.dtype)
+                load_synthetic(ms, 0)
+                ms.deploy()
+                v, fin = throughput(ms, dev, bs, max(20, a.steps // 2), 5)
+                out["secondary"].append({"workload": f"DETRPose-{sz.upper()} {a.dtype} batch {bs} 640x640 ({what})",
+                                         "value": round(v, 2), "unit": "images/sec", "outputs_finite": fin})
+                del ms
+                torch.cuda.empty_cache()
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.size, a.cpu_baseline_seconds)
         if not finite:

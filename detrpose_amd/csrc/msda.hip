@@ -201,8 +201,8 @@ __global__ __launch_bounds__(256) void msda_wave_kernel(const bf16_t* __restrict
     *reinterpret_cast<int4*>(ent + j * 32) = id;
     *reinterpret_cast<float4*>(ent + j * 32 + 16) = wv;
   }
-  __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
   // ---- gather

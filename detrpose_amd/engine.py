@@ -187,15 +187,18 @@ class Plan:
         self.input = None
         self.outputs = {}
         self.post = None         # PostProcess buffers once add_postprocess() appended it
+        self.post_ops = []       # its launch (kept apart: eager forwards do not rerun it)
         self._graph = None
 
     # -- recording
     def _op(self, name, fn, *args):
         self.ops.append((name, fn, args))
 
-    def run(self, stream=None, debug=None):
+    def run(self, stream=None, debug=None, post=False):
+        """Replay the forward launches; with post=True also the appended PostProcess (the
+        hipGraph always includes it; an eager forward leaves its buffers alone)."""
         s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.engine.device).cuda_stream)
-        for name, fn, args in self.ops:
+        for name, fn, args in self.ops + (self.post_ops if post else []):
             rc = fn(*args, s)
             if rc:
                 _lib.check(rc, name)
@@ -224,7 +227,10 @@ class Plan:
         return {k: sorted(v)[len(v) // 2] for k, v in times.items()}
 
     def add_postprocess(self, num_select=60, target_size=(640.0, 640.0)):
-        """Append PostProcess (deploy) to the plan: outputs scores / labels / keypoints."""
+        """Append PostProcess (deploy) to the plan: outputs scores / labels / keypoints.
+        Idempotent per num_select; a different num_select replaces the previous one."""
+        if self.post is not None and self.post["num_select"] == num_select:
+            return self.post
         eng = self.engine
         logits, kps = self.outputs["pred_logits"], self.outputs["pred_keypoints"]
         B, Q, NC = logits.shape
@@ -235,9 +241,10 @@ class Plan:
         sc = eng._empty(B, num_select, dtype=torch.float32)
         lb = eng._empty(B, num_select, dtype=torch.int64)
         ok = eng._empty(B, num_select, K, 2, dtype=torch.float32)
-        self._op("postprocess", eng.lib.dp_postprocess, logits.data_ptr(), kps.data_ptr(), ts.data_ptr(), B, Q, NC, K,
-                 num_select, sc.data_ptr(), lb.data_ptr(), ok.data_ptr())
-        self.post = {"scores": sc, "labels": lb, "keypoints": ok, "target_sizes": ts}
+        self.post_ops = [("postprocess", eng.lib.dp_postprocess, (logits.data_ptr(), kps.data_ptr(), ts.data_ptr(), B,
+                                                                  Q, NC, K, num_select, sc.data_ptr(), lb.data_ptr(),
+                                                                  ok.data_ptr()))]
+        self.post = {"scores": sc, "labels": lb, "keypoints": ok, "target_sizes": ts, "num_select": num_select}
         self._graph = None
         return self.post
 
@@ -250,12 +257,12 @@ class Plan:
                 side = torch.cuda.Stream(dev)
                 side.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(side):
-                    self.run()  # warm-up on the capture stream outside capture
+                    self.run(post=True)  # warm-up on the capture stream outside capture
                 torch.cuda.current_stream(dev).wait_stream(side)
                 torch.cuda.synchronize(dev)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self.run()
+                    self.run(post=True)
             self._graph = g
         return self._graph
 

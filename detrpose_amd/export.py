@@ -13,7 +13,9 @@ batch 1 only) any N works.
 
 `DeployModel.replay(images, orig_target_sizes)` is the same computation as one hipGraph
 launch of the recorded plan with PostProcess appended (what bench.py's latency mode
-times); outputs alias the plan's buffers until the next replay of that batch size.
+times); outputs alias the plan's buffers until the next replay of that batch size (an
+eager `model(images)` forward does not touch them: the plan keeps PostProcess out of its
+eager launch list).
 ONNX export itself is out of scope (onnx is not in this image; the kernels are the
 deployment artifact), so this module carries the contract, not an exporter.
 """
@@ -49,12 +51,12 @@ class DeployModel(nn.Module):
             raise ValueError(f"expected images (N, 3, {hw[0]}, {hw[1]}), got {tuple(images.shape)}")
         n = images.shape[0]
         eng = self.model.engine(images.device)
-        key = (n, eng.device)
+        ns = self.postprocessor.num_select
+        key = (n, eng.device, ns)
         entry = self._graphs.get(key)
-        if entry is None or entry[0] is not eng:
+        if entry is None or entry[0] is not eng or entry[1].post is not entry[2]:
             plan = eng.plan(n)
-            post = plan.post if getattr(plan, "post", None) is not None else plan.add_postprocess(
-                self.postprocessor.num_select)
+            post = plan.add_postprocess(ns)     # rebuilt (and the graph recaptured) when num_select changed
             entry = (eng, plan, post, plan.graph())
             self._graphs[key] = entry
         _, plan, post, g = entry

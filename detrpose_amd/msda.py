@@ -40,6 +40,9 @@ def _check(value, shapes, loc, attn):
         raise TypeError(f"msda core: value dtype {value.dtype} (f32 / bf16)")
     if not value.is_cuda:
         raise RuntimeError("msda core: tensors must be on the GPU (no CPU path)")
+    if loc.device != value.device or attn.device != value.device:
+        raise RuntimeError(f"msda core: value on {value.device}, loc on {loc.device}, attn on {attn.device}: "
+                           "all three must be on the same GPU")
     return N, S, Cc, Lq, nH, L, P
 
 

@@ -42,12 +42,16 @@ def preprocess(images, size: int = 639, max_size: int = 640, pad_to=(640, 640), 
         out = torch.empty(len(images), 3, ph, pw, device=dev, dtype=torch.float32)
     if out.shape != (len(images), 3, ph, pw) or out.dtype != torch.float32 or not out.is_contiguous():
         raise ValueError(f"preprocess: out must be contiguous f32 {(len(images), 3, ph, pw)}")
+    if out.device != dev:
+        raise ValueError(f"preprocess: out is on {out.device}, images on {dev}")
     lib = _lib.load()
     s = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     sizes = []
     for b, im in enumerate(images):
         if im.dtype != torch.uint8 or im.dim() != 3 or im.shape[0] != 3:
             raise ValueError(f"preprocess: image {b} must be uint8 (3, h, w), got {im.dtype} {tuple(im.shape)}")
+        if im.device != dev:
+            raise ValueError(f"preprocess: image {b} is on {im.device}, image 0 on {dev}: one GPU per call")
         im = im.contiguous()
         h, w = int(im.shape[1]), int(im.shape[2])
         nh, nw = resized_size(h, w, size, max_size)

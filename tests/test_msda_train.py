@@ -139,3 +139,18 @@ def test_msda_core_bwd_atomic_hotspot():
     for name, r, o in zip(("grad_value", "grad_loc", "grad_attn"), ref[1:], (v.grad, lc.grad, a.grad)):
         err = (r - o.cpu()).abs().max().item()
         assert err <= 1e-4 * max(1.0, r.abs().max().item()), (name, err)
+
+
+@pytest.mark.gpu
+def test_msda_core_rejects_mixed_devices():
+    """A CPU loc / attn next to a GPU value must raise before any pointer reaches the kernel."""
+    from detrpose_amd.msda import ms_deform_attn_core
+    N, nH, Dh, L, P, Lq = 1, 2, 8, 1, 2, 4
+    shapes = [(4, 4)]
+    value = torch.randn(N, 16, nH * Dh, device="cuda")
+    loc = torch.rand(N, Lq, nH, L, P, 2)
+    attn = torch.rand(N, Lq, nH, L, P)
+    with pytest.raises(RuntimeError, match="same GPU"):
+        ms_deform_attn_core(value, shapes, loc, attn.cuda())
+    with pytest.raises(RuntimeError, match="same GPU"):
+        ms_deform_attn_core(value, shapes, loc.cuda(), attn)

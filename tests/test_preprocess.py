@@ -36,3 +36,14 @@ def test_resize_pad_gpu(h, w):
         assert d.max().item() <= 1.0 + 1e-3, f"max {d.max().item()} levels"
         assert (d < 1e-3).float().mean().item() >= 0.999
         assert (out[b, :, nh:, :].cpu() == 114 / 255).all() and (out[b, :, :, nw:].cpu() == 114 / 255).all()
+
+
+@pytest.mark.gpu
+def test_resize_pad_rejects_mixed_devices():
+    """Every image (not just the first) and `out` must sit on the first image's GPU."""
+    from detrpose_amd.preprocess import preprocess
+    img = torch.zeros(3, 40, 50, dtype=torch.uint8)
+    with pytest.raises(ValueError, match="image 1"):
+        preprocess([img.cuda(), img])
+    with pytest.raises(ValueError, match="out is on"):
+        preprocess([img.cuda()], out=torch.empty(1, 3, 640, 640))
