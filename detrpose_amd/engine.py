@@ -791,6 +791,7 @@ class Engine:
         ph2 = self._fmap(1, 1, krows, Cc)
         nb = 2 * (tr.reg_max + 1)
         corners = [self._empty(krows, nb, dtype=torch.float32) for _ in range(2)]
+        plan.bufs["corners"] = corners        # layer l writes corners[l % 2] (pred_corners, f32)
         pre = self._empty(krows, 2, dtype=torch.float32)
         ref_init = self._empty(krows, 2, dtype=torch.float32)
         # outputs share one contiguous f32 buffer [logits (B,nq,ncls) | keypoints (B,nq,K,2)]

@@ -424,7 +424,7 @@ def transformer(feats, sd, cfg, force_topk=None):
     out = tgt
     prev_pose = 0
     prev_corners = 0
-    res = {"topk_idx": topk_idx, "layers": []}
+    res = {"topk_idx": topk_idx, "layers": [], "corners": []}
     for l in range(nlayers):
         ref_kp = ref[:, :, 1:]
         pos = _mlp(sine_embedding(ref_kp, dim_t), sd, "transformer.decoder.half_pose_ref_point_head", 2)
@@ -442,6 +442,7 @@ def transformer(feats, sd, cfg, force_topk=None):
             pre = torch.sigmoid(_mlp(pose, sd, "transformer.pre_pose_embed", 3) + inverse_sigmoid(ref_kp))
             ref_init = pre
         corners = _mlp(pose + prev_pose, sd, f"transformer.pose_embed.{l}", 3) + prev_corners
+        res["corners"].append(corners)
         # Integral (transformer.py:253-260) + distance2pose (198-219)
         prob = torch.softmax(corners.reshape(-1, reg_max + 1), 1)
         d = F.linear(prob, project[None]).reshape(B, nq, K, 2)
@@ -475,7 +476,7 @@ class OracleDETRPose:
         tr = transformer(en, self.sd, tcfg, force_topk=force_topk)
         out = {"pred_logits": tr["pred_logits"], "pred_keypoints": tr["pred_keypoints"]}
         if intermediates:
-            out.update(backbone=bb, encoder=en, topk_idx=tr["topk_idx"], layers=tr["layers"])
+            out.update(backbone=bb, encoder=en, topk_idx=tr["topk_idx"], layers=tr["layers"], corners=tr["corners"])
         return out
 
     __call__ = forward

@@ -64,10 +64,10 @@ def test_fp32_matches_reference(golden_dir, size, batch):
 
 # bf16 storage (8 mantissa bits) through ~110 conv/linear layers, 3-6 decoder layers and an
 # fp32 head, vs the fp32 oracle on the SAME selection ("Parity of the bf16
-# path"). Keypoints are normalised image coordinates in [0, 1]. Measured on MI355X
-# (profiles/r2a_pytest_gpu.txt): max|dkp| 0.009 / 0.012 / 0.008 and mean 1.3-1.6e-3 for
-# N / L / X; max|dlogit| 0.037 / 0.016 / 0.017, mean 5-8e-3. Bounds: ~1.5x the worst max,
-# 2x the worst mean.
+# path" and "Where the bf16 error comes from"). Keypoints are normalised image coordinates
+# in [0, 1]. Measured on MI355X at HEAD (profiles/r3a_pytest_gpu.txt, stem1 on bf16-rounded
+# pixels): max|dkp| 0.011 / 0.013 / 0.007 and mean 1.3-1.6e-3 for N / L / X; max|dlogit|
+# 0.041 / 0.014 / 0.027, mean 4-7e-3. Bounds: ~1.5x the worst max, ~2x the worst mean.
 BF16_TOL_KP, BF16_TOL_KP_MEAN = 2e-2, 3.5e-3
 BF16_TOL_LOGIT, BF16_TOL_LOGIT_MEAN = 5e-2, 1.6e-2
 
@@ -128,6 +128,56 @@ def test_bf16_b64_headline_batch_is_batch_invariant(golden_dir):
         assert dk <= 1e-4 and dl <= 1e-4, (r, dk, dl)
     # the other 62 images are different, so their outputs are too
     assert (o64["pred_keypoints"][1] - o64["pred_keypoints"][0]).abs().max() > 1e-3
+
+
+# loose per-stage bounds on the bf16 path's relative error (max|d| / max|ref|); the measured
+# table is printed and kept in DESIGN.md ("Where the bf16 error comes from")
+STAGE_REL_TOL = {"backbone": 0.05, "encoder": 0.08, "layer": 0.08, "corners": 0.08}
+
+
+@pytest.mark.parametrize("size,batch", CASES)
+def test_bf16_stage_errors(golden_dir, size, batch):
+    """Attribute the bf16 path's end-to-end error: every stage's output (backbone levels,
+    encoder levels = the MSDA memory, each decoder layer's token rows, each layer's
+    pred_corners) against the fp32 oracle's on the SAME selection."""
+    g = np.load(os.path.join(golden_dir, f"detrpose_{size}_b{batch}.npz"))
+    model, _ = _model(golden_dir, size, g, "bf16")
+    images = synthetic_images(batch, seed=int(g["meta"][2]))
+    model(images.cuda())
+    plan = model.engine().plan(batch)
+    nl = len(plan.bufs["layers"])
+    got = {}
+
+    def grab(name, _out):
+        for l in range(nl):
+            if name == f"dec{l}.norm2":
+                got[f"layer{l}"] = plan.bufs["layers"][l].float().cpu()
+            if name == f"dec{l}.pose2":
+                got[f"corners{l}"] = plan.bufs["corners"][l % 2].float().cpu()
+
+    plan.run(debug=grab)
+    torch.cuda.synchronize()
+    idx = plan.bufs["topk_idx"].cpu()
+    ref = _oracle(size, model)(images, intermediates=True, force_topk=idx)
+    rows = []
+
+    def rel(stage, a, b):
+        a, b = a.float().reshape(-1), b.float().reshape(-1)
+        d = (a - b).abs()
+        r = (d.max() / b.abs().max()).item()
+        rows.append((stage, d.max().item(), d.mean().item(), r))
+        return r
+
+    for i, fm in enumerate(plan.bufs["backbone"]):
+        assert rel(f"backbone{i}", fm.view().permute(0, 3, 1, 2).cpu(), ref["backbone"][i]) <= STAGE_REL_TOL["backbone"]
+    for i, fm in enumerate(plan.bufs["encoder"]):
+        assert rel(f"encoder{i}", fm.view().permute(0, 3, 1, 2).cpu(), ref["encoder"][i]) <= STAGE_REL_TOL["encoder"]
+    for l in range(nl):
+        assert rel(f"layer{l}", got[f"layer{l}"], ref["layers"][l]) <= STAGE_REL_TOL["layer"]
+        assert rel(f"corners{l}", got[f"corners{l}"], ref["corners"][l]) <= STAGE_REL_TOL["corners"]
+    print(f"\n{size} bf16 per-stage error vs fp32 oracle (forced selection): stage max|d| mean|d| max|d|/max|ref|")
+    for st, mx, mn, r in rows:
+        print(f"  {st:10s} {mx:.3e} {mn:.3e} {r:.3e}")
 
 
 @pytest.mark.parametrize("size,gbatch,big,rows", [
