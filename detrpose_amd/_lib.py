@@ -77,6 +77,12 @@ _SIGS = {
     "dp_pre_pose": (i32, [vp, vp, i32, i32, vp, vp]),
     "dp_lqe_stats": (i32, [vp, i64, i32, i32, i32, vp, i32, i32, i32, vp, i32, vp]),
     "dp_postprocess": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+    "dp_linear_layernorm": (i32, [vp, RowMap, vp, RowMap, i32, vp, vp, vp, RowMap, vp, vp, f32, i32, i32, vp, RowMap,
+                                  i32, i32, vp]),
+    "dp_gate_linear_layernorm": (i32, [vp, RowMap, vp, RowMap, vp, vp, vp, vp, f32, i32, i32, vp]),
+    "dp_ffn_layernorm": (i32, [vp, RowMap, vp, RowMap, vp, vp, i32, vp, vp, vp, vp, f32, i32, i32, vp]),
+    "dp_query_pos": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, RowMap, i32, vp]),
+    "dp_pose_mlp": (i32, [vp, RowMap, vp, RowMap, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, vp]),
 }
 
 EXPORTED = tuple(k for k in _SIGS)

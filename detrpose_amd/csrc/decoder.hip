@@ -1,0 +1,793 @@
+// Row-block fused kernels of the decoder layer (gfx950, bf16 storage, f32 accumulation).
+//
+// The decoder's token GEMMs have N = C (128 / 256 / 384) or a few C: one block can own
+// every output channel of its rows, so whatever follows a GEMM row-wise (bias, residual,
+// LayerNorm, the Gate's sigmoid mix, the in-place pos add, a second or third GEMM of an
+// MLP) finishes inside the block instead of round-tripping through HBM:
+//   dp_linear_layernorm       out_proj + residual + LN (+ pos re-add)   transformer.py:403-422
+//   dp_gate_linear_layernorm  Gate: Linear(2C->2C), sigmoid mix, LN     transformer.py:222-235
+//   dp_ffn_layernorm          Linear-ReLU-Linear + residual + LN        transformer.py:371-385
+//   dp_query_pos              sine embedding -> MLP(C,C,C,2) -> pos, tgt += pos
+//                                                                        transformer.py:360-370, 518-540, 588-592
+//   dp_pose_mlp               pose_embed MLP(C,C,66,3) (+ previous corners)  transformer.py:705-719
+//
+// Block = BM token rows (64 / 96 / 128) and NW = C/32 waves; wave w owns output channels
+// [32w, 32w+32) of EVERY row of the block (TM = BM/16 row tiles x 2 column tiles of
+// 16x16), so each weight fragment it loads feeds TM MFMAs: the weights are re-read from
+// L2 once per BM rows (flop per L2 weight byte = BM), which is what bounds these K = C
+// GEMMs. The row tile is staged once into LDS (16-byte chunks XOR-swizzled by row:
+// conflict-free ds_read_b128 of 16 rows x one chunk); weight fragments go straight from
+// L2 into registers (no other wave needs them), prefetched D k-steps ahead; the weights
+// are pre-packed in MFMA-fragment order (include/detrpose_hip.h, "fragment layout"), so
+// each fragment load is one contiguous 1 KB wave access instead of 16 rows x 64 B. MFMA
+// 16x16x32 with the weights as the A operand and the rows as B, so a lane ends with 8
+// CONTIGUOUS channels of one row (the A-row -> channel map below): bias, LN and stores
+// work on whole 16-byte chunks. Hidden activations of an MLP go back to LDS as bf16
+// (they are the next GEMM's B operand). LayerNorm statistics: shuffles across the lane
+// groups, then NW partial sums per row through LDS, two passes (mean, then centred
+// variance) as nn.LayerNorm computes them.
+#include "common.h"
+#include <stdlib.h>
+
+namespace {
+
+constexpr int TN = 2;          // 16-column tiles per wave: 32 channels
+constexpr int NV = 4 * TN;     // channels per lane per row (contiguous)
+
+// byte offset of 16-byte chunk c of row m in a [rows][K] bf16 LDS image (K % 128 == 0)
+template <int K>
+__device__ __forceinline__ int sw(int m, int c) {
+  return m * (K * 2) + (((c & ~15) | ((c ^ m) & 15)) << 4);
+}
+
+__device__ __forceinline__ bf16x8 lds16(const char* base, int off) {
+  return *reinterpret_cast<const bf16x8*>(base + off);
+}
+__device__ __forceinline__ void sts16(char* base, int off, const bf16x8& v) {
+  *reinterpret_cast<bf16x8*>(base + off) = v;
+}
+__device__ __forceinline__ bf16x8 gld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// Stage rows [row0, row0+BM) of a row-mapped bf16 matrix (K columns) into LDS in two
+// halves, so a kernel can issue its weight prefetch between them: stage_load issues the
+// global loads, stage_store writes the LDS image (rows past `rows` are zero). With ADD,
+// the element-wise sum of two row-mapped sources rounded to bf16.
+template <int K, int BM, int NTH, bool ADD>
+struct Stage {
+  static constexpr int CH = K / 8;
+  static constexpr int PER = BM * CH / NTH;   // chunks per thread
+  static_assert((BM * CH) % NTH == 0, "stage");
+  bf16x8 v[PER], v2[ADD ? PER : 1];
+
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ x, dp_rowmap xm, const bf16_t* __restrict__ x2,
+                                       dp_rowmap x2m, int row0, int rows) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int e = threadIdx.x + NTH * t;
+      const int m = e / CH, c = e - m * CH;
+      const int r = min(row0 + m, rows - 1);
+      v[t] = gld16(x + rowmap_off(xm, r) + c * 8);
+      if constexpr (ADD) v2[t] = gld16(x2 + rowmap_off(x2m, r) + c * 8);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int row0, int rows) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int e = threadIdx.x + NTH * t;
+      const int m = e / CH, c = e - m * CH;
+      bf16x8 o = v[t];
+      if constexpr (ADD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16_t)((float)v[t][j] + (float)v2[t][j]);
+      }
+      if (row0 + m >= rows) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16_t)0.f;
+      }
+      sts16(lds, sw<K>(m, c), o);
+    }
+  }
+};
+
+// Block barrier for LDS hand-offs only: LDS writes retired, then s_barrier. Unlike
+// __syncthreads() it does not wait for outstanding global loads, so the weight-fragment
+// prefetch of the next GEMM stays in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// channel (within the wave's 32) of A-operand row a (0..15) of column tile j: lane group
+// g of the C tile then holds channels 8g + 4j + r (r = 0..3) = 8 contiguous channels
+__device__ __forceinline__ int a_chan(int j, int a) { return (a >> 2) * NV + 4 * j + (a & 3); }
+
+// Weight-fragment ring of one wave: the fragments of k-step s of the running GEMM sit in
+// f[s % D]; D k-steps are in flight.
+constexpr int D = 4;
+struct WPipe {
+  bf16x8 f[D][TN];
+};
+
+// Fragment-layout weights: for output-channel block nb (32 channels) and k-step s, the
+// TN fragments of the 64 lanes are 1 KB each, contiguous: frag(nb, s, j) at
+// ((nb * NS + s) * TN + j) * 512 elements, lane l's 8 elements at + 8 l. `wb` below is a
+// lane's pointer to its fragment of (nb, s0, 0).
+__device__ __forceinline__ const bf16_t* frag_base(const bf16_t* w, int nb, int ksteps, int s0 = 0) {
+  const int lane = threadIdx.x & 63;
+  return w + ((int64_t)(nb * ksteps + s0) * TN * 64 + lane) * 8;
+}
+
+__device__ __forceinline__ void pipe_start(WPipe& p, const bf16_t* wb) {
+#pragma unroll
+  for (int s = 0; s < D; ++s)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) p.f[s][j] = gld16(wb + (s * TN + j) * 512);
+}
+
+// acc[i][j] += sum_k X[16i + q][k] * W[chan_j][k] over K, X from the LDS image, W as
+// fragments from global. The pipe holds this GEMM's first D k-steps on entry; as its own
+// steps run out it loads the first D k-steps of the NEXT GEMM (fragment base nx), so the
+// ring never drains between the GEMMs of a kernel. The X fragments of k-step s+1 are read
+// from LDS while the MFMAs of step s run.
+template <int K, int TM>
+__device__ __forceinline__ void wave_gemm(f32x4 (&acc)[TM][TN], const char* xl, const bf16_t* wb, WPipe& p,
+                                          const bf16_t* nx) {
+  constexpr int NS = K / 32;
+  static_assert(NS % D == 0, "k-steps must fill the ring");
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
+  bf16x8 xf[2][TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) xf[0][i] = lds16(xl, sw<K>(16 * i + q, g));
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    bf16x8 w[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) w[j] = p.f[s % D][j];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      p.f[s % D][j] = gld16(s + D < NS ? wb + ((s + D) * TN + j) * 512 : nx + ((s + D - NS) * TN + j) * 512);
+    if (s + 1 < NS) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) xf[(s + 1) & 1][i] = lds16(xl, sw<K>(16 * i + q, 4 * (s + 1) + g));
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j], xf[s & 1][i], acc[i][j], 0, 0, 0);
+  }
+}
+
+template <int TM>
+__device__ __forceinline__ void zero_acc(f32x4 (&acc)[TM][TN]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// the lane's 8 contiguous channel values of row tile i
+template <int TM>
+__device__ __forceinline__ void lane_vals(const f32x4 (&acc)[TM][TN], int i, float (&v)[NV]) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[4 * j + r] = acc[i][j][r];
+}
+
+// per-row sum over the block's channels (lane: 8 values of row 16i+q); result broadcast to
+// every lane holding that row. red: NW x BM floats of LDS.
+template <int TM, int NW>
+__device__ __forceinline__ void row_sums(const float (&x)[TM][NV], float (&out)[TM], float* red) {
+  constexpr int BM = 16 * TM;
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) s += x[i][e];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (g == 0) red[w * BM + 16 * i + q] = s;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = 16 * i + q;
+    float s = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) s += red[ww * BM + m];
+    out[i] = s;
+  }
+  lds_barrier();
+}
+
+// in-place LayerNorm of the block's rows: x[i][e] is channel cb + e of row 16i+q; gg/bb are
+// the lane's gamma/beta (fetched at kernel start with everything else)
+template <int TM, int NW>
+__device__ __forceinline__ void layernorm_rows(float (&x)[TM][NV], const float (&gg)[NV], const float (&bb)[NV],
+                                               float eps, float* red) {
+  constexpr float invc = 1.f / (32 * NW);
+  float mean[TM], var[TM];
+  row_sums<TM, NW>(x, mean, red);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) mean[i] *= invc;
+  float d[TM][NV];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      const float t = x[i][e] - mean[i];
+      d[i][e] = t * t;
+    }
+  row_sums<TM, NW>(d, var, red);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const float rstd = rsqrtf(var[i] * invc + eps);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) x[i][e] = (x[i][e] - mean[i]) * rstd * gg[e] + bb[e];
+  }
+}
+
+__device__ __forceinline__ void load_bias(const float* __restrict__ b, int cb, float (&v)[NV]) {
+#pragma unroll
+  for (int e = 0; e < NV; e += 4) {
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(b + cb + e);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[e + t] = b4[t];
+  }
+}
+
+__device__ __forceinline__ void load_row_vals(const bf16_t* p, float (&v)[NV]) {
+  const bf16x8 c = gld16(p);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) v[t] = (float)c[t];
+}
+
+__device__ __forceinline__ void store_row_vals(bf16_t* p, const float (&v)[NV]) {
+  bf16x8 c;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) c[t] = (bf16_t)v[t];
+  *reinterpret_cast<bf16x8*>(p) = c;
+}
+
+// the lane's 8 channels (chunk cb/8) of row m as bf16 into an LDS image with KH columns
+template <int KH>
+__device__ __forceinline__ void put_lds_row(char* lds, int m, int cb, const float (&v)[NV]) {
+  bf16x8 c;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) c[t] = (bf16_t)v[t];
+  sts16(lds, sw<KH>(m, cb >> 3), c);
+}
+
+
+// ------------------------------------------------------------------ out_proj + res + LN
+template <int C, int BM, bool POST>
+__global__ __launch_bounds__(C * 2) void linear_ln_kernel(bf16_t* out, dp_rowmap om, const bf16_t* x, dp_rowmap xm,
+                                                          const bf16_t* __restrict__ w, const float* __restrict__ b,
+                                                          const bf16_t* res, dp_rowmap rm,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, int rows,
+                                                          const bf16_t* post, dp_rowmap pm, int post_group,
+                                                          int post_skip) {
+  constexpr int NW = C / 32, NTH = 64 * NW, TM = BM / 16, K = C;
+  __shared__ __attribute__((aligned(16))) char smem[BM * K * 2 + NW * BM * 4];
+  char* xl = smem;
+  float* red = reinterpret_cast<float*>(smem + BM * K * 2);
+  const int row0 = blockIdx.x * BM;
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const int wbase = wv * 32, cb = wbase + g * NV;
+  // every global load of the block goes out before the first wait: rows, weights, residual
+  Stage<K, BM, NTH, false> st;
+  st.load(x, xm, nullptr, xm, row0, rows);
+  const bf16_t* wb = frag_base(w, wv, K / 32);
+  WPipe p;
+  pipe_start(p, wb);
+  bf16x8 rv[TM], pv[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = min(row0 + 16 * i + q, rows - 1);
+    rv[i] = gld16(res + rowmap_off(rm, r) + cb);
+    if (POST) {
+      const int grp = r / post_group, wi = r - grp * post_group;
+      pv[i] = gld16(post + rowmap_off(pm, (int64_t)grp * (post_group - post_skip) + max(wi - post_skip, 0)) + cb);
+    }
+  }
+  float bias[NV], gg[NV], bb[NV];
+  load_bias(b, cb, bias);
+  load_bias(gamma, cb, gg);
+  load_bias(beta, cb, bb);
+  st.store(xl, row0, rows);
+  lds_barrier();
+  f32x4 acc[TM][TN];
+  zero_acc<TM>(acc);
+  wave_gemm<K, TM>(acc, xl, wb, p, wb);
+  float v[TM][NV];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float a[NV];
+    lane_vals<TM>(acc, i, a);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[i][e] = a[e] + bias[e] + (float)rv[i][e];
+  }
+  layernorm_rows<TM, NW>(v, gg, bb, eps, red);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = row0 + 16 * i + q;
+    if (r >= rows) continue;
+    if (POST) {
+      const int grp = r / post_group, wi = r - grp * post_group;
+      if (wi >= post_skip) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) v[i][e] += (float)pv[i][e];
+      }
+    }
+    store_row_vals(out + rowmap_off(om, r) + cb, v[i]);
+  }
+}
+
+// ------------------------------------------------------------------ Gate: Linear + sigmoid mix + LN
+// xcat = [x1 | x2] (K = 2C); gate rows n < C -> g1, n >= C -> g2. Wave w computes g1 AND
+// g2 of its 32 channels, so the mix sigmoid(g1) x1 + sigmoid(g2) x2 is lane-local.
+template <int C, int BM>
+__global__ __launch_bounds__(C * 2) void gate_ln_kernel(bf16_t* out, dp_rowmap om, const bf16_t* x, dp_rowmap xm,
+                                                        const bf16_t* __restrict__ w, const float* __restrict__ b,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps, int rows) {
+  constexpr int NW = C / 32, NTH = 64 * NW, TM = BM / 16, K = 2 * C;
+  __shared__ __attribute__((aligned(16))) char smem[BM * K * 2 + NW * BM * 4];
+  char* xl = smem;
+  float* red = reinterpret_cast<float*>(smem + BM * K * 2);
+  const int row0 = blockIdx.x * BM;
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const int wbase = wv * 32, cb = wbase + g * NV;
+  Stage<K, BM, NTH, false> st;
+  st.load(x, xm, nullptr, xm, row0, rows);
+  const bf16_t* wb1 = frag_base(w, wv, K / 32);        // gate rows [32w, 32w+32): g1
+  const bf16_t* wb2 = frag_base(w, NW + wv, K / 32);   // gate rows C + [32w, 32w+32): g2
+  WPipe p;
+  pipe_start(p, wb1);
+  float b1[NV], b2[NV], gg[NV], bb[NV];
+  load_bias(b, cb, b1);
+  load_bias(b + C, cb, b2);
+  load_bias(gamma, cb, gg);
+  load_bias(beta, cb, bb);
+  st.store(xl, row0, rows);
+  lds_barrier();
+  f32x4 a1[TM][TN], a2[TM][TN];
+  zero_acc<TM>(a1);
+  zero_acc<TM>(a2);
+  wave_gemm<K, TM>(a1, xl, wb1, p, wb2);
+  wave_gemm<K, TM>(a2, xl, wb2, p, wb2);
+  float v[TM][NV];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = 16 * i + q;
+    float g1[NV], g2[NV];
+    lane_vals<TM>(a1, i, g1);
+    lane_vals<TM>(a2, i, g2);
+    const bf16x8 x1 = lds16(xl, sw<K>(m, cb >> 3));
+    const bf16x8 x2 = lds16(xl, sw<K>(m, (C + cb) >> 3));
+#pragma unroll
+    for (int t = 0; t < NV; ++t)
+      v[i][t] = sigmoidf_(g1[t] + b1[t]) * (float)x1[t] + sigmoidf_(g2[t] + b2[t]) * (float)x2[t];
+  }
+  layernorm_rows<TM, NW>(v, gg, bb, eps, red);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = row0 + 16 * i + q;
+    if (r < rows) store_row_vals(out + rowmap_off(om, r) + cb, v[i]);
+  }
+}
+
+// ------------------------------------------------------------------ FFN + residual + LN
+// hidden in chunks of HC = min(256, C) columns, computed by the first HC/32 waves:
+// H = relu(X W1[chunk]^T + b1) -> LDS (bf16); then every wave Y += H W2[:, chunk]^T.
+// One weight ring runs through the whole chain W1[0] -> W2[0] -> W1[1] -> ... The block's
+// own staged rows are the residual.
+template <int C, int BM, int F>
+__global__ __launch_bounds__(C * 2) void ffn_ln_kernel(bf16_t* out, dp_rowmap om, const bf16_t* x, dp_rowmap xm,
+                                                       const bf16_t* __restrict__ w1, const float* __restrict__ b1,
+                                                       const bf16_t* __restrict__ w2, const float* __restrict__ b2,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps, int rows) {
+  constexpr int NW = C / 32, NTH = 64 * NW, TM = BM / 16;
+  constexpr int HC = C < 256 ? C : 256, HW = HC / 32, NCH = F / HC;
+  static_assert(F % HC == 0, "ffn hidden");
+  __shared__ __attribute__((aligned(16))) char smem[BM * C * 2 + BM * HC * 2 + NW * BM * 4];
+  char* xl = smem;
+  char* hl = smem + BM * C * 2;
+  float* red = reinterpret_cast<float*>(smem + BM * C * 2 + BM * HC * 2);
+  const int row0 = blockIdx.x * BM;
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const int wbase = wv * 32, cb = wbase + g * NV;
+  const bool g1w = wv < HW;   // wave-uniform: this wave computes hidden columns
+  Stage<C, BM, NTH, false> st;
+  st.load(x, xm, nullptr, xm, row0, rows);
+  // W1 [F][C]: this wave's hidden block of chunk h is nb = h*HW + wv (C/32 k-steps);
+  // W2 [C][F]: output block nb = wv, chunk h covers k-steps [h*HC/32, (h+1)*HC/32)
+  auto w1b = [&](int h) { return frag_base(w1, h * HW + (g1w ? wv : 0), C / 32); };
+  auto w2b = [&](int h) { return frag_base(w2, wv, F / 32, h * (HC / 32)); };
+  WPipe p;
+  pipe_start(p, g1w ? w1b(0) : w2b(0));
+  float bias[NV], gg[NV], bb[NV], bh[NV];
+  load_bias(b2, cb, bias);
+  load_bias(gamma, cb, gg);
+  load_bias(beta, cb, bb);
+  load_bias(b1, g1w ? cb : 0, bh);
+  st.store(xl, row0, rows);
+  lds_barrier();
+  f32x4 acc[TM][TN];
+  zero_acc<TM>(acc);
+#pragma unroll 1
+  for (int h = 0; h < NCH; ++h) {
+    const int h0 = h * HC;
+    float bn[NV];   // next chunk's hidden bias, in flight during this chunk
+    load_bias(b1 + (h + 1 < NCH ? h0 + HC : 0), g1w ? cb : 0, bn);
+    const bf16_t* c1 = w1b(h);
+    const bf16_t* c2 = w2b(h);
+    const bf16_t* n1 = h + 1 < NCH ? (g1w ? w1b(h + 1) : w2b(h + 1)) : c2;
+    if (g1w) {
+      f32x4 ah[TM][TN];
+      zero_acc<TM>(ah);
+      wave_gemm<C, TM>(ah, xl, c1, p, c2);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float hv[NV];
+        lane_vals<TM>(ah, i, hv);
+#pragma unroll
+        for (int e = 0; e < NV; ++e) hv[e] = fmaxf(hv[e] + bh[e], 0.f);
+        put_lds_row<HC>(hl, 16 * i + q, cb, hv);
+      }
+    }
+    lds_barrier();
+    wave_gemm<HC, TM>(acc, hl, c2, p, n1);
+    lds_barrier();   // every wave done reading this chunk's H before the next one lands
+#pragma unroll
+    for (int e = 0; e < NV; ++e) bh[e] = bn[e];
+  }
+  float v[TM][NV];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = 16 * i + q;
+    float a[NV];
+    lane_vals<TM>(acc, i, a);
+    const bf16x8 xr = lds16(xl, sw<C>(m, cb >> 3));
+#pragma unroll
+    for (int t = 0; t < NV; ++t) v[i][t] = a[t] + bias[t] + (float)xr[t];
+  }
+  layernorm_rows<TM, NW>(v, gg, bb, eps, red);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = row0 + 16 * i + q;
+    if (r < rows) store_row_vals(out + rowmap_off(om, r) + cb, v[i]);
+  }
+}
+
+// ------------------------------------------------------------------ query pos of the keypoint tokens
+// row r = (query row qr = r / nkp, keypoint kp = r % nkp): sine embedding of ref[qr][1+kp]
+// (cat(pos_y, pos_x), sin on even / cos on odd dims), MLP(C, C, C, 2) -> pos[r] (bf16) and
+// tgt keypoint row r += pos (in place, the reference's with_pos_embed).
+template <int C, int BM>
+__global__ __launch_bounds__(C * 2) void query_pos_kernel(const float* __restrict__ ref, int rows, int nkp,
+                                                          const float* __restrict__ dim_t,
+                                                          const bf16_t* __restrict__ w0, const float* __restrict__ b0,
+                                                          const bf16_t* __restrict__ w1, const float* __restrict__ b1,
+                                                          bf16_t* pos, bf16_t* tgt, dp_rowmap tm) {
+  constexpr int NW = C / 32, NTH = 64 * NW, TM = BM / 16, CH = C / 8, PER = BM * CH / NTH;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BM * C * 2];
+  char* xl = smem;
+  char* hl = smem + BM * C * 2;
+  const int row0 = blockIdx.x * BM;
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const int wbase = wv * 32, cb = wbase + g * NV;
+  const bf16_t* wb0 = frag_base(w0, wv, C / 32);
+  const bf16_t* wb1 = frag_base(w1, wv, C / 32);
+  WPipe p;
+  pipe_start(p, wb0);
+  bf16x8 tv[TM];   // the tgt keypoint rows this lane updates at the end
+#pragma unroll
+  for (int i = 0; i < TM; ++i) tv[i] = gld16(tgt + rowmap_off(tm, min(row0 + 16 * i + q, rows - 1)) + cb);
+  float bias0[NV], bias1[NV];
+  load_bias(b0, cb, bias0);
+  load_bias(b1, cb, bias1);
+  constexpr int half = C / 2;
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const int e = threadIdx.x + NTH * t;
+    const int m = e / CH, c0 = (e - m * CH) * 8;
+    const int r = min(row0 + m, rows - 1);
+    const int qr = r / nkp, kp = r - qr * nkp;
+    const float* pp = ref + ((int64_t)qr * (nkp + 1) + 1 + kp) * 2;
+    const bool ylow = c0 < half;
+    const int i0 = ylow ? c0 : c0 - half;
+    const float coord = (ylow ? pp[1] : pp[0]) * 6.283185307179586f;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = coord / dim_t[i0 + j];
+      o[j] = (bf16_t)(((i0 + j) & 1) ? __cosf(a) : __sinf(a));
+    }
+    sts16(xl, sw<C>(m, c0 >> 3), o);
+  }
+  lds_barrier();
+  f32x4 acc[TM][TN];
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, xl, wb0, p, wb1);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float hv[NV];
+    lane_vals<TM>(acc, i, hv);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) hv[e] = fmaxf(hv[e] + bias0[e], 0.f);
+    put_lds_row<C>(hl, 16 * i + q, cb, hv);
+  }
+  lds_barrier();
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, hl, wb1, p, wb1);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = row0 + 16 * i + q;
+    if (r >= rows) continue;
+    float pv[NV], t2[NV];
+    lane_vals<TM>(acc, i, pv);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      pv[e] = (float)(bf16_t)(pv[e] + bias1[e]);   // pos as stored
+      t2[e] = (float)tv[i][e] + pv[e];
+    }
+    store_row_vals(pos + (int64_t)r * C + cb, pv);
+    store_row_vals(tgt + rowmap_off(tm, r) + cb, t2);
+  }
+}
+
+// ------------------------------------------------------------------ pose head MLP(C, C, nout, 3)
+// x (+ x2) -> relu(W0) -> relu(W1) -> W2 (+ b2) (+ prev) -> out f32 [rows][nout]. The last
+// layer's nout (66) columns are computed by the first ceil(nout/32) waves; columns past
+// nout use clamped weight rows and are never stored.
+template <int C, int BM, bool ADD, bool PREV>
+__global__ __launch_bounds__(C * 2) void pose_mlp_kernel(const bf16_t* x, dp_rowmap xm, const bf16_t* x2,
+                                                         dp_rowmap x2m, int rows, const bf16_t* __restrict__ w0,
+                                                         const float* __restrict__ b0, const bf16_t* __restrict__ w1,
+                                                         const float* __restrict__ b1, const bf16_t* __restrict__ w2,
+                                                         const float* __restrict__ b2, int nout,
+                                                         const float* __restrict__ prev, float* __restrict__ out) {
+  constexpr int NW = C / 32, NTH = 64 * NW, TM = BM / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BM * C * 2];
+  char* xl = smem;
+  char* hl = smem + BM * C * 2;
+  const int row0 = blockIdx.x * BM;
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const int wbase = wv * 32, cb = wbase + g * NV;
+  Stage<C, BM, NTH, ADD> st;
+  st.load(x, xm, x2, x2m, row0, rows);
+  const bf16_t* wb0 = frag_base(w0, wv, C / 32);
+  const bf16_t* wb1 = frag_base(w1, wv, C / 32);
+  // w2 is packed with its rows padded to a multiple of 32: waves past nout read block 0
+  const bf16_t* wb2 = frag_base(w2, wbase < nout ? wv : 0, C / 32);
+  WPipe p;
+  pipe_start(p, wb0);
+  float bias0[NV], bias1[NV], bias2[NV];
+  load_bias(b0, cb, bias0);
+  load_bias(b1, cb, bias1);
+#pragma unroll
+  for (int e = 0; e < NV; ++e) bias2[e] = b2[min(cb + e, nout - 1)];
+  st.store(xl, row0, rows);
+  lds_barrier();
+  f32x4 acc[TM][TN];
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, xl, wb0, p, wb1);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float hv[NV];
+    lane_vals<TM>(acc, i, hv);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) hv[e] = fmaxf(hv[e] + bias0[e], 0.f);
+    put_lds_row<C>(hl, 16 * i + q, cb, hv);
+  }
+  lds_barrier();
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, hl, wb1, p, wb2);
+  lds_barrier();   // every wave done reading xl (GEMM 0) before H2 overwrites it
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float hv[NV];
+    lane_vals<TM>(acc, i, hv);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) hv[e] = fmaxf(hv[e] + bias1[e], 0.f);
+    put_lds_row<C>(xl, 16 * i + q, cb, hv);
+  }
+  lds_barrier();
+  if (wbase >= nout) return;   // wave-uniform: no barrier after this point
+  // the previous corners of the lane's rows, in flight during the last GEMM
+  float pr[TM][NV];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < NV; ++e)
+      pr[i][e] = PREV ? prev[(int64_t)min(row0 + 16 * i + q, rows - 1) * nout + min(cb + e, nout - 1)] : 0.f;
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, xl, wb2, p, wb2);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = row0 + 16 * i + q;
+    if (r >= rows) continue;
+    float v[NV];
+    lane_vals<TM>(acc, i, v);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      const int n = cb + e;
+      if (n < nout) out[(int64_t)r * nout + n] = v[e] + bias2[e] + pr[i][e];
+    }
+  }
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+bool map16(const dp_rowmap& m) { return m.base % 8 == 0 && m.stride_g % 8 == 0 && m.stride_r % 8 == 0 && m.group > 0; }
+
+// Rows per block: every kernel here runs one block per CU (LDS / registers), so a launch
+// takes ceil(blocks / CUs) rounds of equal length; pick the row tile with the least total
+// rows x rounds (ties: the larger tile, fewer weight re-reads). DETRPOSE_DEC_BM overrides.
+int pick_bm(int rows, int c, int max_bm = 128) {
+  static const int forced = [] {
+    const char* e = getenv("DETRPOSE_DEC_BM");
+    return e ? atoi(e) : 0;
+  }();
+  if (c != 256) return 64;
+  if ((forced == 64 || forced == 96 || forced == 128) && forced <= max_bm) return forced;
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess)
+    cus = 256;
+  int best = 64;
+  int64_t best_cost = INT64_MAX;
+  for (int bm : {128, 96, 64}) {
+    if (bm > max_bm) continue;
+    const int64_t blocks = (rows + bm - 1) / bm;
+    const int64_t cost = (blocks + cus - 1) / cus * bm;
+    if (cost < best_cost) best_cost = cost, best = bm;
+  }
+  return best;
+}
+
+}  // namespace
+
+// Instantiation table: C in {128, 256, 384}; BM in {64, 96, 128} for C = 256, 64 otherwise.
+#define DP_FOR_BM64(C_, X) \
+  if (c == C_ && bm == 64) X(C_, 64);
+#define DP_FOR_BM256(X)                \
+  if (c == 256 && bm == 64) X(256, 64);  \
+  if (c == 256 && bm == 96) X(256, 96);  \
+  if (c == 256 && bm == 128) X(256, 128);
+#define DP_FOR_BM(X) DP_FOR_BM64(128, X) DP_FOR_BM256(X) DP_FOR_BM64(384, X)
+
+extern "C" int dp_linear_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, int32_t k, const void* w,
+                                   const float* b, const void* res, dp_rowmap rm, const float* gamma,
+                                   const float* beta, float eps, int32_t rows, int32_t c, const void* post,
+                                   dp_rowmap pm, int32_t post_group, int32_t post_skip, void* stream) {
+  DP_REQUIRE(out && x && w && b && res && gamma && beta && rows > 0, "dp_linear_layernorm: bad args");
+  DP_REQUIRE(al16(out) && al16(x) && al16(w) && al16(res) && map16(om) && map16(xm) && map16(rm) &&
+                 (!post || (al16(post) && map16(pm) && post_group > post_skip)),
+             "dp_linear_layernorm: rows must be 16-byte aligned");
+  DP_REQUIRE(k == c, "dp_linear_layernorm: k=%d != c=%d (out_proj only)", k, c);
+  hipStream_t s = as_stream(stream);
+  const int bm = pick_bm(rows, c);
+  dim3 grid((rows + bm - 1) / bm);
+#define DP_LLN(C_, BM_)                                                                                            \
+  do {                                                                                                             \
+    if (post)                                                                                                      \
+      hipLaunchKernelGGL((linear_ln_kernel<C_, BM_, true>), grid, dim3(2 * C_), 0, s, (bf16_t*)out, om,              \
+                         (const bf16_t*)x, xm, (const bf16_t*)w, b, (const bf16_t*)res, rm, gamma, beta, eps, rows,    \
+                         (const bf16_t*)post, pm, post_group, post_skip);                                           \
+    else                                                                                                           \
+      hipLaunchKernelGGL((linear_ln_kernel<C_, BM_, false>), grid, dim3(2 * C_), 0, s, (bf16_t*)out, om,             \
+                         (const bf16_t*)x, xm, (const bf16_t*)w, b, (const bf16_t*)res, rm, gamma, beta, eps, rows,    \
+                         (const bf16_t*)nullptr, pm, 1, 0);                                                         \
+    return dp_check_launch("dp_linear_layernorm");                                                                 \
+  } while (0)
+  DP_FOR_BM(DP_LLN)
+#undef DP_LLN
+  dp_set_error("dp_linear_layernorm: c=%d unsupported (128/256/384)", c);
+  return DP_EINVAL;
+}
+
+extern "C" int dp_gate_linear_layernorm(void* out, dp_rowmap om, const void* xcat, dp_rowmap xm, const void* w,
+                                        const float* b, const float* gamma, const float* beta, float eps,
+                                        int32_t rows, int32_t c, void* stream) {
+  DP_REQUIRE(out && xcat && w && b && gamma && beta && rows > 0, "dp_gate_linear_layernorm: bad args");
+  DP_REQUIRE(al16(out) && al16(xcat) && al16(w) && map16(om) && map16(xm),
+             "dp_gate_linear_layernorm: rows must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int bm = pick_bm(rows, c, 64);   // two accumulator sets: larger row tiles spill
+  dim3 grid((rows + bm - 1) / bm);
+#define DP_GLN(C_, BM_)                                                                                           \
+  do {                                                                                                            \
+    hipLaunchKernelGGL((gate_ln_kernel<C_, BM_>), grid, dim3(2 * C_), 0, s, (bf16_t*)out, om, (const bf16_t*)xcat, \
+                       xm, (const bf16_t*)w, b, gamma, beta, eps, rows);                                           \
+    return dp_check_launch("dp_gate_linear_layernorm");                                                           \
+  } while (0)
+  DP_FOR_BM64(128, DP_GLN) DP_FOR_BM64(256, DP_GLN) DP_FOR_BM64(384, DP_GLN)
+#undef DP_GLN
+  dp_set_error("dp_gate_linear_layernorm: c=%d unsupported (128/256/384)", c);
+  return DP_EINVAL;
+}
+
+extern "C" int dp_ffn_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, const void* w1, const float* b1,
+                                int32_t f, const void* w2, const float* b2, const float* gamma, const float* beta,
+                                float eps, int32_t rows, int32_t c, void* stream) {
+  DP_REQUIRE(out && x && w1 && b1 && w2 && b2 && gamma && beta && rows > 0, "dp_ffn_layernorm: bad args");
+  DP_REQUIRE(al16(out) && al16(x) && al16(w1) && al16(w2) && map16(om) && map16(xm),
+             "dp_ffn_layernorm: rows must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int bm = pick_bm(rows, c, 64);   // larger row tiles spill
+  dim3 grid((rows + bm - 1) / bm);
+#define DP_FLN(C_, BM_, F_)                                                                                        \
+  do {                                                                                                             \
+    hipLaunchKernelGGL((ffn_ln_kernel<C_, BM_, F_>), grid, dim3(2 * C_), 0, s, (bf16_t*)out, om, (const bf16_t*)x,   \
+                       xm, (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, gamma, beta, eps, rows);                  \
+    return dp_check_launch("dp_ffn_layernorm");                                                                    \
+  } while (0)
+#define DP_FLN_N(C_, BM_) if (f == 512) DP_FLN(C_, BM_, 512)
+#define DP_FLN_X(C_, BM_)                   \
+  if (f == 1024) DP_FLN(C_, BM_, 1024);     \
+  if (f == 2048) DP_FLN(C_, BM_, 2048)
+  DP_FOR_BM64(128, DP_FLN_N)
+  if (c == 256 && f == 1024 && bm == 64) DP_FLN(256, 64, 1024);
+  if (c == 256 && f == 1024 && bm == 96) DP_FLN(256, 96, 1024);
+  DP_FOR_BM64(384, DP_FLN_X)
+#undef DP_FLN_N
+#undef DP_FLN_X
+#undef DP_FLN
+  dp_set_error("dp_ffn_layernorm: c=%d, f=%d unsupported (128/512, 256/1024, 384/1024 or 2048)", c, f);
+  return DP_EINVAL;
+}
+
+extern "C" int dp_query_pos(const float* ref, int32_t rows, int32_t nkp, const float* dim_t, const void* w0,
+                            const float* b0, const void* w1, const float* b1, void* pos, void* tgt, dp_rowmap tm,
+                            int32_t c, void* stream) {
+  DP_REQUIRE(ref && dim_t && w0 && b0 && w1 && b1 && pos && tgt && rows > 0 && nkp > 0, "dp_query_pos: bad args");
+  DP_REQUIRE(al16(pos) && al16(tgt) && al16(w0) && al16(w1) && map16(tm), "dp_query_pos: rows must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int bm = pick_bm(rows, c);
+  dim3 grid((rows + bm - 1) / bm);
+#define DP_QP(C_, BM_)                                                                                           \
+  do {                                                                                                           \
+    hipLaunchKernelGGL((query_pos_kernel<C_, BM_>), grid, dim3(2 * C_), 0, s, ref, rows, nkp, dim_t,              \
+                       (const bf16_t*)w0, b0, (const bf16_t*)w1, b1, (bf16_t*)pos, (bf16_t*)tgt, tm);            \
+    return dp_check_launch("dp_query_pos");                                                                      \
+  } while (0)
+  DP_FOR_BM(DP_QP)
+#undef DP_QP
+  dp_set_error("dp_query_pos: c=%d unsupported (128/256/384)", c);
+  return DP_EINVAL;
+}
+
+extern "C" int dp_pose_mlp(const void* x, dp_rowmap xm, const void* x2, dp_rowmap x2m, int32_t rows, const void* w0,
+                           const float* b0, const void* w1, const float* b1, const void* w2, const float* b2,
+                           int32_t nout, const float* prev, float* out, int32_t c, void* stream) {
+  DP_REQUIRE(x && w0 && b0 && w1 && b1 && w2 && b2 && out && rows > 0 && nout > 0 && nout <= c,
+             "dp_pose_mlp: bad args (nout 1..c)");
+  DP_REQUIRE((x2 != nullptr) == (prev != nullptr), "dp_pose_mlp: x2 and prev come together (layers > 0)");
+  DP_REQUIRE(al16(x) && al16(w0) && al16(w1) && al16(w2) && map16(xm) && (!x2 || (al16(x2) && map16(x2m))),
+             "dp_pose_mlp: rows must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int bm = pick_bm(rows, c);
+  dim3 grid((rows + bm - 1) / bm);
+#define DP_PM(C_, BM_)                                                                                            \
+  do {                                                                                                            \
+    if (x2)                                                                                                       \
+      hipLaunchKernelGGL((pose_mlp_kernel<C_, BM_, true, true>), grid, dim3(2 * C_), 0, s, (const bf16_t*)x, xm,    \
+                         (const bf16_t*)x2, x2m, rows, (const bf16_t*)w0, b0, (const bf16_t*)w1, b1,                \
+                         (const bf16_t*)w2, b2, nout, prev, out);                                                  \
+    else                                                                                                          \
+      hipLaunchKernelGGL((pose_mlp_kernel<C_, BM_, false, false>), grid, dim3(2 * C_), 0, s, (const bf16_t*)x, xm,  \
+                         (const bf16_t*)x2, x2m, rows, (const bf16_t*)w0, b0, (const bf16_t*)w1, b1,                \
+                         (const bf16_t*)w2, b2, nout, prev, out);                                                  \
+    return dp_check_launch("dp_pose_mlp");                                                                        \
+  } while (0)
+  DP_FOR_BM(DP_PM)
+#undef DP_PM
+  dp_set_error("dp_pose_mlp: c=%d unsupported (128/256/384)", c);
+  return DP_EINVAL;
+}

@@ -24,6 +24,7 @@ import torch
 
 from . import _lib
 from ._lib import ACT, DP_BF16, DP_F32, ConvDesc, contiguous_rows, rowmap
+from .fragments import frag_pack
 from .hybrid_encoder import sine_pos_embed_2d
 from .transformer import weighting_function
 
@@ -418,6 +419,8 @@ class Engine:
         hp = t + "decoder.half_pose_ref_point_head.layers."
         P["pos_head"] = [pk.linear(sd[hp + "0.weight"], sd[hp + "0.bias"], act="relu"),
                          pk.linear(sd[hp + "1.weight"], sd[hp + "1.bias"])]
+        if self.code == _lib.DP_BF16:
+            P["pos_head_frag"] = [frag_pack(pc.w) for pc in P["pos_head"]]
         P["project"] = pk.t(weighting_function(tr.reg_max, float(sd[t + "up"]), float(sd[t + "reg_scale"])))
         P["reg_scale"] = abs(float(sd[t + "reg_scale"]))
         pp = t + "pre_pose_embed.layers."
@@ -448,6 +451,10 @@ class Engine:
                          pk.linear(sd[pe + "1.weight"], sd[pe + "1.bias"], act="relu"),
                          pk.linear(sd[pe + "2.weight"], sd[pe + "2.bias"], exact=True)],
             }
+            if self.code == _lib.DP_BF16:
+                # MFMA-fragment copies for the row-block fused kernels (detrpose_amd/fragments.py)
+                L["frag"] = {k: frag_pack(L[k].w) for k in ("within_out", "across_out", "gate", "ffn1", "ffn2")}
+                L["frag"]["pose"] = [frag_pack(pc.w) for pc in L["pose"]]
             if l == tr.num_decoder_layers - 1:
                 qp = f"{t}lqe_embed.{l}.reg_conf.layers."
                 L["cls"] = pk.small(sd[f"{t}class_embed.{l}.weight"], sd[f"{t}class_embed.{l}.bias"])
@@ -773,22 +780,27 @@ class Engine:
         tmpl = P["tgt_tmpl"]
         plan._op("dec.tgt", lib.dp_broadcast, tmpl.data_ptr(), tmpl.numel() * tmpl.element_size(), tgtA.data_ptr(), B)
         kp_map = rowmap(Cc, K, T * Cc, Cc)       # keypoint token rows of a [rows][C] tensor
-        se = self._fmap(1, 1, krows, Cc)
-        h1 = self._fmap(1, 1, krows, Cc)
+        # bf16: the row-block fused decoder kernels (csrc/decoder.hip); fp32 parity mode keeps
+        # one launch per reference op
+        fused = self.code == _lib.DP_BF16 and Cc in (128, 256, 384)
+        plan.decoder_fused = fused
         pos = self._fmap(1, 1, krows, Cc)
         qkv = self._empty(rows * 3 * Cc, dtype=dt)
         att = self._fmap(1, 1, rows, Cc)
-        ao = self._fmap(1, 1, rows, Cc)
         gx = self._empty(rows * 2 * Cc, dtype=dt)   # [x1 | msda]
-        gt = self._fmap(1, 1, rows, 2 * Cc)
         nl_, npnt = tr.num_feature_levels, tr.dec_n_points
         assert (nh * nl_ * npnt * 3) % 8 == 0, "offsets|logits row must be 16-byte aligned"
         oa = self._fmap(1, 1, rows, nh * nl_ * npnt * 3)
-        f1 = self._fmap(1, 1, rows, tr.dim_feedforward)
-        f2 = self._fmap(1, 1, rows, Cc)
-        pin = self._fmap(1, 1, krows, Cc)
         ph1 = self._fmap(1, 1, krows, Cc)
         ph2 = self._fmap(1, 1, krows, Cc)
+        if not fused:
+            se = self._fmap(1, 1, krows, Cc)
+            h1 = self._fmap(1, 1, krows, Cc)
+            ao = self._fmap(1, 1, rows, Cc)
+            gt = self._fmap(1, 1, rows, 2 * Cc)
+            f1 = self._fmap(1, 1, rows, tr.dim_feedforward)
+            f2 = self._fmap(1, 1, rows, Cc)
+            pin = self._fmap(1, 1, krows, Cc)
         nb = 2 * (tr.reg_max + 1)
         corners = [self._empty(krows, nb, dtype=torch.float32) for _ in range(2)]
         plan.bufs["corners"] = corners        # layer l writes corners[l % 2] (pred_corners, f32)
@@ -806,53 +818,95 @@ class Engine:
         qkv_f = FMap(qkv, 0, 1, 1, rows, 3 * Cc, 3 * Cc, rows * 3 * Cc)
         gx_f = FMap(gx, 0, 1, 1, rows, 2 * Cc, 2 * Cc, rows * 2 * Cc)
         plan.bufs["layers"] = []
+        plan.bufs["layer_ops"] = []           # per layer: (op that finishes its token rows, op writing its corners)
         src, dst = tgtA, tgtB
         nlayers = tr.num_decoder_layers
+        cr = contiguous_rows
+        eps = C.c_float(1e-5)
+
+        def lin(pc, frag, k):
+            """(fragment-layout weight, f32 bias) of a fused-kernel GEMM with k inputs"""
+            assert pc.kpad == k and frag.shape[1] * 32 == k, (pc.kpad, k, tuple(frag.shape))
+            return frag.data_ptr(), pc.b.data_ptr()
+
         for l, L in enumerate(P["layers"]):
             n = f"dec{l}"
-            # query pos from the current reference points (transformer.py:588-592)
-            plan._op(n + ".sine", lib.dp_sine_embed, ref.data_ptr(), B * nq, K, Cc, P["dim_t"].data_ptr(), se.ptr,
-                     self.code)
-            self._conv(plan, n + ".pos0", se, P["pos_head"][0], h1)
-            self._conv(plan, n + ".pos1", h1, P["pos_head"][1], pos)
-            # in-place with_pos_embed on the layer input (transformer.py:369): also turns the previous
-            # layer's output_pose into output_pose_detach + pos (aliasing kept on purpose)
-            plan._op(n + ".addpos", lib.dp_add_rows, src.data_ptr(), kp_map, src.data_ptr(), kp_map, pos.ptr,
-                     contiguous_rows(Cc), krows, Cc, self.code)
             src_f = FMap(src, 0, 1, 1, rows, Cc, Cc, rows * Cc)
             dst_f = FMap(dst, 0, 1, 1, rows, Cc, Cc, rows * Cc)
+            if fused:
+                # sine embedding -> pos MLP -> pos, and the in-place with_pos_embed of the layer
+                # input (transformer.py:369, 588-592): also turns the previous layer's output_pose
+                # into output_pose_detach + pos (aliasing kept on purpose)
+                ph = P["pos_head"]
+                phf = P["pos_head_frag"]
+                plan._op(n + ".pos", lib.dp_query_pos, ref.data_ptr(), krows, K, P["dim_t"].data_ptr(),
+                         *lin(ph[0], phf[0], Cc), *lin(ph[1], phf[1], Cc), pos.ptr, src.data_ptr(), kp_map, Cc)
+            else:
+                # query pos from the current reference points (transformer.py:588-592)
+                plan._op(n + ".sine", lib.dp_sine_embed, ref.data_ptr(), B * nq, K, Cc, P["dim_t"].data_ptr(),
+                         se.ptr, self.code)
+                self._conv(plan, n + ".pos0", se, P["pos_head"][0], h1)
+                self._conv(plan, n + ".pos1", h1, P["pos_head"][1], pos)
+                # in-place with_pos_embed on the layer input (transformer.py:369): also turns the previous
+                # layer's output_pose into output_pose_detach + pos (aliasing kept on purpose)
+                plan._op(n + ".addpos", lib.dp_add_rows, src.data_ptr(), kp_map, src.data_ptr(), kp_map, pos.ptr,
+                         contiguous_rows(Cc), krows, Cc, self.code)
             # within-instance MHA over the T tokens of a query (transformer.py:403-406)
             self._conv(plan, n + ".w_qkv", src_f, L["within_qkv"], qkv_f)
             plan._op(n + ".w_attn", lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
                      qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B * nq, 1, T, 0, 1, T, nh, Cc // nh, self.code)
-            self._conv(plan, n + ".w_out", att, L["within_out"], ao)
-            self._ln(plan, n + ".w_norm", dst.data_ptr(), contiguous_rows(Cc), src.data_ptr(), contiguous_rows(Cc),
-                     ao.ptr, contiguous_rows(Cc), L["within_norm"], rows, Cc)
+            if fused:
+                wn, fr = L["within_norm"], L["frag"]
+                plan._op(n + ".w_out_ln", lib.dp_linear_layernorm, dst.data_ptr(), cr(Cc), att.ptr, cr(Cc), Cc,
+                         *lin(L["within_out"], fr["within_out"], Cc), src.data_ptr(), cr(Cc), wn[0].data_ptr(),
+                         wn[1].data_ptr(), eps, rows, Cc, None, rowmap(group=1), 1, 0)
+            else:
+                self._conv(plan, n + ".w_out", att, L["within_out"], ao)
+                self._ln(plan, n + ".w_norm", dst.data_ptr(), contiguous_rows(Cc), src.data_ptr(), contiguous_rows(Cc),
+                         ao.ptr, contiguous_rows(Cc), L["within_norm"], rows, Cc)
             # across-instance MHA over the nq queries of a token slot (transformer.py:409-419)
             self._conv(plan, n + ".a_qkv", dst_f, L["across_qkv"], qkv_f)
             plan._op(n + ".a_attn", lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
                      qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B, T, nq * T, 1, T, nq, nh, Cc // nh,
                      self.code)
-            self._conv(plan, n + ".a_out", att, L["across_out"], ao)
-            # LN + second in-place pos add -> x1 = gx[:, :C]   (transformer.py:419-422)
-            self._ln(plan, n + ".a_norm", gx.data_ptr(), contiguous_rows(2 * Cc), dst.data_ptr(),
-                     contiguous_rows(Cc), ao.ptr, contiguous_rows(Cc), L["across_norm"], rows, Cc,
-                     post=(pos.ptr, contiguous_rows(Cc)), post_group=T, post_skip=1)
+            # out_proj + LN + second in-place pos add -> x1 = gx[:, :C]   (transformer.py:419-422)
+            if fused:
+                an, fr = L["across_norm"], L["frag"]
+                plan._op(n + ".a_out_ln", lib.dp_linear_layernorm, gx.data_ptr(), cr(2 * Cc), att.ptr, cr(Cc), Cc,
+                         *lin(L["across_out"], fr["across_out"], Cc), dst.data_ptr(), cr(Cc), an[0].data_ptr(),
+                         an[1].data_ptr(), eps, rows, Cc, pos.ptr, cr(Cc), T, 1)
+            else:
+                self._conv(plan, n + ".a_out", att, L["across_out"], ao)
+                self._ln(plan, n + ".a_norm", gx.data_ptr(), contiguous_rows(2 * Cc), dst.data_ptr(),
+                         contiguous_rows(Cc), ao.ptr, contiguous_rows(Cc), L["across_norm"], rows, Cc,
+                         post=(pos.ptr, contiguous_rows(Cc)), post_group=T, post_skip=1)
             # MSDA (ms_deform_attn.py:384-444) -> gx[:, C:]
             self._conv(plan, n + ".offattn", gx_f.ch(0, Cc), L["offattn"], oa)
             plan._op(n + ".msda", lib.dp_msda, memory.data_ptr(), B, S, lvl_hw, len(shapes), oa.ptr, ref.data_ptr(),
                      gx.data_ptr() + Cc * e, 2 * Cc, nq * T, nh, Cc // nh, npnt, self.code)
             # SURVEY.md §8d algorithmic bytes: value once + offsets/logits + ref + output
             plan.op_bytes[n + ".msda"] = e * (B * S * Cc + rows * oa.C + rows * Cc) + 4 * rows * 2
-            # Gate (transformer.py:222-235)
-            self._conv(plan, n + ".gate", gx_f, L["gate"], gt)
-            plan._op(n + ".gate_ln", lib.dp_gate_layernorm, dst.data_ptr(), Cc, gt.ptr, gx.data_ptr(),
-                     L["gate_norm"][0].data_ptr(), L["gate_norm"][1].data_ptr(), C.c_float(1e-5), rows, Cc, self.code)
-            # FFN (transformer.py:380-385)
-            self._conv(plan, n + ".ffn1", dst_f, L["ffn1"], f1)
-            self._conv(plan, n + ".ffn2", f1, L["ffn2"], f2)
-            self._ln(plan, n + ".norm2", dst.data_ptr(), contiguous_rows(Cc), dst.data_ptr(), contiguous_rows(Cc),
-                     f2.ptr, contiguous_rows(Cc), L["norm2"], rows, Cc)
+            # Gate (transformer.py:222-235), FFN (transformer.py:380-385)
+            if fused:
+                gn, n2, fr = L["gate_norm"], L["norm2"], L["frag"]
+                plan._op(n + ".gate_ln", lib.dp_gate_linear_layernorm, dst.data_ptr(), cr(Cc), gx.data_ptr(),
+                         cr(2 * Cc), *lin(L["gate"], fr["gate"], 2 * Cc), gn[0].data_ptr(), gn[1].data_ptr(), eps,
+                         rows, Cc)
+                fd = tr.dim_feedforward
+                plan._op(n + ".ffn_ln", lib.dp_ffn_layernorm, dst.data_ptr(), cr(Cc), dst.data_ptr(), cr(Cc),
+                         *lin(L["ffn1"], fr["ffn1"], Cc), fd, *lin(L["ffn2"], fr["ffn2"], fd), n2[0].data_ptr(),
+                         n2[1].data_ptr(), eps, rows, Cc)
+                last_op = n + ".ffn_ln"
+            else:
+                self._conv(plan, n + ".gate", gx_f, L["gate"], gt)
+                plan._op(n + ".gate_ln", lib.dp_gate_layernorm, dst.data_ptr(), Cc, gt.ptr, gx.data_ptr(),
+                         L["gate_norm"][0].data_ptr(), L["gate_norm"][1].data_ptr(), C.c_float(1e-5), rows, Cc,
+                         self.code)
+                self._conv(plan, n + ".ffn1", dst_f, L["ffn1"], f1)
+                self._conv(plan, n + ".ffn2", f1, L["ffn2"], f2)
+                self._ln(plan, n + ".norm2", dst.data_ptr(), contiguous_rows(Cc), dst.data_ptr(), contiguous_rows(Cc),
+                         f2.ptr, contiguous_rows(Cc), L["norm2"], rows, Cc)
+                last_op = n + ".norm2"
             plan.bufs["layers"].append(dst)
             # ---- heads (transformer.py:701-728)
             pose_f = FMap(dst, Cc, B * nq, 1, K, Cc, Cc, T * Cc)       # output[:, :, 1:]
@@ -863,20 +917,31 @@ class Engine:
                 self._conv(plan, n + ".pre2", ph2, pp[2], FMap(pre, 0, 1, 1, krows, 2, 2, pre.numel()), out_f32=True)
                 plan._op(n + ".pre_pose", lib.dp_pre_pose, pre.data_ptr(), ref.data_ptr(), B * nq, K,
                          ref_init.data_ptr())
-                x_in = pose_f
-            else:
-                # pose_head(output_pose + output_pose_detach): src keypoint rows hold the previous
-                # output_pose + this layer's pos (in-place aliasing, transformer.py:369/716/922)
-                plan._op(n + ".pin", lib.dp_add_rows, pin.ptr, contiguous_rows(Cc), dst.data_ptr(), kp_map,
-                         src.data_ptr(), kp_map, krows, Cc, self.code)
-                x_in = pin
             ph = L["pose"]
-            self._conv(plan, n + ".pose0", x_in, ph[0], ph1)
-            self._conv(plan, n + ".pose1", ph1, ph[1], ph2)
             cur, prev = corners[l % 2], corners[(l + 1) % 2]
-            # pred_corners = pose_head(...) + pred_corners_undetach (transformer.py:712), f32 out + f32 residual
-            self._conv(plan, n + ".pose2", ph2, ph[2], FMap(cur, 0, 1, 1, krows, nb, nb, cur.numel()),
-                       res=FMap(prev, 0, 1, 1, krows, nb, nb, prev.numel()) if l > 0 else None, out_f32=True)
+            if fused:
+                # pred_corners = pose_head(output_pose [+ output_pose_detach]) [+ pred_corners_undetach]
+                # (transformer.py:712): src keypoint rows hold the previous output_pose + this layer's
+                # pos (in-place aliasing, transformer.py:369/716/922)
+                pw = [v for i in range(3) for v in lin(ph[i], L["frag"]["pose"][i], Cc)]
+                plan._op(n + ".pose", lib.dp_pose_mlp, dst.data_ptr(), kp_map, src.data_ptr() if l > 0 else None,
+                         kp_map, krows, *pw, nb, prev.data_ptr() if l > 0 else None, cur.data_ptr(), Cc)
+                plan.bufs["layer_ops"].append((last_op, n + ".pose"))
+            else:
+                if l == 0:
+                    x_in = pose_f
+                else:
+                    # pose_head(output_pose + output_pose_detach): src keypoint rows hold the previous
+                    # output_pose + this layer's pos (in-place aliasing, transformer.py:369/716/922)
+                    plan._op(n + ".pin", lib.dp_add_rows, pin.ptr, contiguous_rows(Cc), dst.data_ptr(), kp_map,
+                             src.data_ptr(), kp_map, krows, Cc, self.code)
+                    x_in = pin
+                self._conv(plan, n + ".pose0", x_in, ph[0], ph1)
+                self._conv(plan, n + ".pose1", ph1, ph[1], ph2)
+                # pred_corners = pose_head(...) + pred_corners_undetach (transformer.py:712), f32 out + f32 residual
+                self._conv(plan, n + ".pose2", ph2, ph[2], FMap(cur, 0, 1, 1, krows, nb, nb, cur.numel()),
+                           res=FMap(prev, 0, 1, 1, krows, nb, nb, prev.numel()) if l > 0 else None, out_f32=True)
+                plan.bufs["layer_ops"].append((last_op, n + ".pose2"))
             plan._op(n + ".refine", lib.dp_pose_refine, cur.data_ptr(), P["project"].data_ptr(), tr.reg_max,
                      ref_init.data_ptr(), C.c_float(P["reg_scale"]), B * nq, K, kps.data_ptr(), ref.data_ptr())
             if l == nlayers - 1:

@@ -221,6 +221,50 @@ int dp_postprocess(const float* logits, const float* kps, const float* target_si
                    int32_t nq, int32_t nclass, int32_t nkp, int32_t num_select,
                    float* scores, int64_t* labels, float* out_kps, void* stream);
 
+/* ---- Row-block fused decoder-layer kernels (bf16 only; c = hidden dim 128 / 256 / 384).
+ * A block owns 64 token rows and all c channels, so the row-wise op after each GEMM runs
+ * in its epilogue. Weights bf16 [n][k] (nn.Linear layout), biases f32. */
+
+/* out = LayerNorm(x . w^T + b + res) (+ post on the rows the post map selects, as in
+ * dp_layernorm). MultiheadAttention.out_proj + residual + LayerNorm of the decoder layer:
+ * within_attn -> within_norm, across_attn -> across_norm + the second in-place pos add
+ * (transformer.py:403-422, 360-370). k == c. out may not alias x. */
+int dp_linear_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, int32_t k,
+                        const void* w, const float* b, const void* res, dp_rowmap rm,
+                        const float* gamma, const float* beta, float eps, int32_t rows, int32_t c,
+                        const void* post, dp_rowmap pm, int32_t post_group, int32_t post_skip,
+                        void* stream);
+
+/* Gate.forward (transformer.py:222-235) including its Linear: xcat rows [x1 | x2] (2c),
+ * w [2c][2c]; out = LayerNorm(sigmoid(g1) * x1 + sigmoid(g2) * x2). */
+int dp_gate_linear_layernorm(void* out, dp_rowmap om, const void* xcat, dp_rowmap xm,
+                             const void* w, const float* b, const float* gamma, const float* beta,
+                             float eps, int32_t rows, int32_t c, void* stream);
+
+/* forward_ffn (transformer.py:371-385): out = LayerNorm(x + w2 . relu(w1 . x + b1) + b2),
+ * w1 [f][c], w2 [c][f]; the hidden activations never leave the block. out may alias x. */
+int dp_ffn_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, const void* w1,
+                     const float* b1, int32_t f, const void* w2, const float* b2,
+                     const float* gamma, const float* beta, float eps, int32_t rows, int32_t c,
+                     void* stream);
+
+/* Query position of the keypoint tokens: sine_embedding of the keypoint reference points
+ * (transformer.py:518-540) -> half_pose_ref_point_head MLP(c, c, c, 2) (588-592) ->
+ * pos [rows][c], and the in-place with_pos_embed of the layer input (360-370):
+ * tgt keypoint row r += pos[r]. rows = nq_rows * nkp keypoint tokens; ref f32
+ * [nq_rows][nkp + 1][2] (row 0 of a query = its centre). */
+int dp_query_pos(const float* ref, int32_t rows, int32_t nkp, const float* dim_t,
+                 const void* w0, const float* b0, const void* w1, const float* b1,
+                 void* pos, void* tgt, dp_rowmap tm, int32_t c, void* stream);
+
+/* pose_embed[l] MLP(c, c, nout, 3) (utils.py:75-87) on x (+ x2, the reference's
+ * output_pose + output_pose_detach) (+ prev: pred_corners + pred_corners_undetach):
+ * transformer.py:705-719. out f32 [rows][nout], nout <= 128. */
+int dp_pose_mlp(const void* x, dp_rowmap xm, const void* x2, dp_rowmap x2m, int32_t rows,
+                const void* w0, const float* b0, const void* w1, const float* b1,
+                const void* w2, const float* b2, int32_t nout, const float* prev, float* out,
+                int32_t c, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

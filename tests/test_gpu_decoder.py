@@ -1,0 +1,172 @@
+"""The row-block fused decoder kernels (csrc/decoder.hip) against plain PyTorch fp32 on
+the same bf16-rounded inputs and weights (weights passed in the MFMA-fragment layout,
+detrpose_amd.fragments.frag_pack): out_proj + residual + LayerNorm (+ pos re-add),
+the Gate with its Linear, the FFN + LayerNorm (also in place), the query-pos MLP with the
+in-place pos add, and the pose MLP (with the previous corners). Row counts are not
+multiples of the 64-row block, so the tail block is exercised too.
+
+Tolerance: outputs are stored in bf16 (half-ulp 2^-9 relative); LayerNorm outputs are
+O(1), so 2.5e-2 absolute covers the rounding of the output plus the f32 accumulation-order
+differences; f32-output pose corners 5e-3 of their scale.
+"""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from detrpose_amd import _lib
+from detrpose_amd._lib import contiguous_rows, rowmap
+from detrpose_amd.fragments import frag_pack
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2.5e-2
+
+
+def _bf(*shape, scale=1.0, g=None):
+    return (torch.randn(*shape, generator=g) * scale).bfloat16()
+
+
+def _s():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ln(x, gamma, beta):
+    return F.layer_norm(x, (x.shape[-1],), gamma, beta, 1e-5)
+
+
+@pytest.mark.parametrize("c", [128, 256, 384])
+@pytest.mark.parametrize("post", [False, True])
+def test_linear_layernorm(c, post):
+    g = torch.Generator().manual_seed(c + post)
+    T, rows = 18, 18 * 61   # 1098 rows: 17 full blocks + a tail
+    x, res = _bf(rows, c, g=g), _bf(rows, c, g=g)
+    w = _bf(c, c, scale=c ** -0.5, g=g)
+    b, gamma, beta = torch.randn(c, generator=g) * 0.1, 1 + 0.1 * torch.randn(c, generator=g), 0.1 * torch.randn(c, generator=g)
+    krows = rows // T * (T - 1)
+    pos = _bf(krows, c, g=g)
+    ld = 2 * c   # written into the first half of a wider row, as the decoder does
+    out = torch.zeros(rows, ld, dtype=torch.bfloat16, device="cuda")
+    dx, dres, dw, dpos = x.cuda(), res.cuda(), frag_pack(w).cuda(), pos.cuda()
+    db, dg, dbe = b.cuda(), gamma.cuda(), beta.cuda()
+    lib = _lib.load()
+    _lib.check(lib.dp_linear_layernorm(out.data_ptr(), contiguous_rows(ld), dx.data_ptr(), contiguous_rows(c), c,
+                                       dw.data_ptr(), db.data_ptr(), dres.data_ptr(), contiguous_rows(c),
+                                       dg.data_ptr(), dbe.data_ptr(), C.c_float(1e-5), rows, c,
+                                       dpos.data_ptr() if post else None, contiguous_rows(c), T, 1, _s()))
+    torch.cuda.synchronize()
+    ref = _ln(x.float() @ w.float().t() + b + res.float(), gamma, beta)
+    if post:
+        ref = ref.reshape(rows // T, T, c)
+        ref[:, 1:] += pos.float().reshape(rows // T, T - 1, c)
+        ref = ref.reshape(rows, c)
+    got = out[:, :c].float().cpu()
+    assert (got - ref).abs().max().item() <= TOL
+    assert (out[:, c:] == 0).all()
+
+
+@pytest.mark.parametrize("c", [128, 256, 384])
+def test_gate_linear_layernorm(c):
+    g = torch.Generator().manual_seed(7 + c)
+    rows = 1000
+    x = _bf(rows, 2 * c, g=g)
+    w = _bf(2 * c, 2 * c, scale=(2 * c) ** -0.5, g=g)
+    b, gamma, beta = torch.randn(2 * c, generator=g) * 0.1, 1 + 0.1 * torch.randn(c, generator=g), 0.1 * torch.randn(c, generator=g)
+    out = torch.empty(rows, c, dtype=torch.bfloat16, device="cuda")
+    dx, dw, db, dg, dbe = x.cuda(), frag_pack(w).cuda(), b.cuda(), gamma.cuda(), beta.cuda()
+    lib = _lib.load()
+    _lib.check(lib.dp_gate_linear_layernorm(out.data_ptr(), contiguous_rows(c), dx.data_ptr(), contiguous_rows(2 * c),
+                                            dw.data_ptr(), db.data_ptr(), dg.data_ptr(), dbe.data_ptr(),
+                                            C.c_float(1e-5), rows, c, _s()))
+    torch.cuda.synchronize()
+    xf = x.float()
+    gates = torch.sigmoid(xf @ w.float().t() + b)
+    ref = _ln(gates[:, :c] * xf[:, :c] + gates[:, c:] * xf[:, c:], gamma, beta)
+    assert (out.float().cpu() - ref).abs().max().item() <= TOL
+
+
+@pytest.mark.parametrize("c,f", [(128, 512), (256, 1024), (384, 1024), (384, 2048)])
+def test_ffn_layernorm_in_place(c, f):
+    g = torch.Generator().manual_seed(c + f)
+    rows = 1000
+    x = _bf(rows, c, g=g)
+    w1, w2 = _bf(f, c, scale=c ** -0.5, g=g), _bf(c, f, scale=f ** -0.5, g=g)
+    b1, b2 = 0.1 * torch.randn(f, generator=g), 0.1 * torch.randn(c, generator=g)
+    gamma, beta = 1 + 0.1 * torch.randn(c, generator=g), 0.1 * torch.randn(c, generator=g)
+    dx = x.cuda()
+    d = [t.cuda() for t in (frag_pack(w1), b1, frag_pack(w2), b2, gamma, beta)]   # kept alive across the launch
+    lib = _lib.load()
+    _lib.check(lib.dp_ffn_layernorm(dx.data_ptr(), contiguous_rows(c), dx.data_ptr(), contiguous_rows(c),
+                                    d[0].data_ptr(), d[1].data_ptr(), f, d[2].data_ptr(), d[3].data_ptr(),
+                                    d[4].data_ptr(), d[5].data_ptr(), C.c_float(1e-5), rows, c, _s()))
+    torch.cuda.synchronize()
+    h = torch.relu(x.float() @ w1.float().t() + b1).bfloat16().float()   # the hidden layer is a bf16 operand
+    ref = _ln(x.float() + h @ w2.float().t() + b2, gamma, beta)
+    assert (dx.float().cpu() - ref).abs().max().item() <= TOL
+
+
+def _sine(ref_kp, dim_t):
+    """TransformerDecoder.sine_embedding (transformer.py:518-540), the oracle's restatement."""
+    from oracle.detrpose_cpu import sine_embedding
+    return sine_embedding(ref_kp, dim_t)
+
+
+@pytest.mark.parametrize("c", [128, 256, 384])
+def test_query_pos(c):
+    g = torch.Generator().manual_seed(11 + c)
+    nq_rows, K, T = 61, 17, 18
+    krows = nq_rows * K
+    ref = torch.rand(nq_rows, T, 2, generator=g)
+    dim_t = 10000 ** (2 * (torch.arange(c // 2) // 2) / (c // 2)).float()
+    w0, w1 = _bf(c, c, scale=c ** -0.5, g=g), _bf(c, c, scale=c ** -0.5, g=g)
+    b0, b1 = 0.1 * torch.randn(c, generator=g), 0.1 * torch.randn(c, generator=g)
+    tgt = _bf(nq_rows * T, c, g=g)
+    dtgt = tgt.cuda()
+    pos = torch.empty(krows, c, dtype=torch.bfloat16, device="cuda")
+    d = [t.cuda() for t in (ref, dim_t, frag_pack(w0), b0, frag_pack(w1), b1)]   # kept alive across the launch
+    lib = _lib.load()
+    _lib.check(lib.dp_query_pos(d[0].data_ptr(), krows, K, d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(),
+                                d[4].data_ptr(), d[5].data_ptr(), pos.data_ptr(), dtgt.data_ptr(),
+                                rowmap(c, K, T * c, c), c, _s()))
+    torch.cuda.synchronize()
+    se = _sine(ref[None, :, 1:], dim_t).reshape(krows, c).bfloat16().float()
+    h = torch.relu(se @ w0.float().t() + b0).bfloat16().float()
+    p_ref = h @ w1.float().t() + b1
+    assert (pos.float().cpu() - p_ref).abs().max().item() <= TOL
+    t_ref = tgt.float().reshape(nq_rows, T, c).clone()
+    t_ref[:, 1:] += pos.float().cpu().reshape(nq_rows, K, c)
+    got = dtgt.float().cpu().reshape(nq_rows, T, c)
+    assert (got[:, 0] == tgt.float().reshape(nq_rows, T, c)[:, 0]).all()   # instance rows untouched
+    assert (got - t_ref).abs().max().item() <= 2e-2
+
+
+@pytest.mark.parametrize("c", [128, 256, 384])
+@pytest.mark.parametrize("add", [False, True])
+def test_pose_mlp(c, add):
+    g = torch.Generator().manual_seed(13 + c + add)
+    nq_rows, K, T, nout = 61, 17, 18, 66
+    krows = nq_rows * K
+    a, b = _bf(nq_rows * T, c, g=g), _bf(nq_rows * T, c, g=g)
+    w0, w1 = _bf(c, c, scale=c ** -0.5, g=g), _bf(c, c, scale=c ** -0.5, g=g)
+    w2 = _bf(nout, c, scale=c ** -0.5, g=g)
+    b0, b1, b2 = (0.1 * torch.randn(n, generator=g) for n in (c, c, nout))
+    prev = torch.randn(krows, nout, generator=g)
+    out = torch.empty(krows, nout, device="cuda")
+    kp = rowmap(c, K, T * c, c)
+    da, db_ = a.cuda(), b.cuda()
+    d = [t.cuda() for t in (frag_pack(w0), b0, frag_pack(w1), b1, frag_pack(w2), b2, prev)]   # kept alive
+    lib = _lib.load()
+    _lib.check(lib.dp_pose_mlp(da.data_ptr(), kp, db_.data_ptr() if add else None, kp, krows, d[0].data_ptr(),
+                               d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), d[4].data_ptr(), d[5].data_ptr(),
+                               nout, d[6].data_ptr() if add else None, out.data_ptr(), c, _s()))
+    torch.cuda.synchronize()
+    x = a.float().reshape(nq_rows, T, c)[:, 1:]
+    if add:
+        x = (x + b.float().reshape(nq_rows, T, c)[:, 1:]).bfloat16().float()
+    x = x.reshape(krows, c)
+    h1 = torch.relu(x @ w0.float().t() + b0).bfloat16().float()
+    h2 = torch.relu(h1 @ w1.float().t() + b1).bfloat16().float()
+    ref = h2 @ w2.float().t() + b2 + (prev if add else 0)
+    err = (out.cpu() - ref).abs().max().item()
+    assert err <= 5e-3 * max(1.0, ref.abs().max().item()), err

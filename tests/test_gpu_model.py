@@ -149,10 +149,10 @@ def test_bf16_stage_errors(golden_dir, size, batch):
     got = {}
 
     def grab(name, _out):
-        for l in range(nl):
-            if name == f"dec{l}.norm2":
+        for l, (layer_op, corners_op) in enumerate(plan.bufs["layer_ops"]):
+            if name == layer_op:
                 got[f"layer{l}"] = plan.bufs["layers"][l].float().cpu()
-            if name == f"dec{l}.pose2":
+            if name == corners_op:
                 got[f"corners{l}"] = plan.bufs["corners"][l % 2].float().cpu()
 
     plan.run(debug=grab)

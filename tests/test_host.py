@@ -98,3 +98,18 @@ def test_forward_refuses_cpu_tensors():
     model, _ = build_model("n")
     with pytest.raises(RuntimeError):
         model.deploy()(torch.rand(1, 3, 640, 640))
+
+
+def test_frag_pack_layout():
+    """The MFMA-fragment weight layout (include/detrpose_hip.h): lane l = 16 g + q of
+    fragment j of block (nb, s) holds W[32 nb + (q//4)*8 + 4j + q%4][32 s + 8 g : +8]."""
+    from detrpose_amd.fragments import frag_pack, frag_unpack
+    w = torch.randn(66, 128).bfloat16().float()
+    f = frag_pack(w)
+    assert f.shape == (3, 4, 2, 64, 8) and f.dtype == torch.bfloat16
+    assert torch.equal(frag_unpack(f, 66), w)
+    for nb, s, j, g, q in ((0, 0, 0, 0, 0), (1, 3, 1, 2, 13), (2, 1, 0, 3, 7)):
+        c = 32 * nb + (q // 4) * 8 + 4 * j + q % 4
+        if c < 66:
+            assert torch.equal(f[nb, s, j, 16 * g + q].float(), w[c, 32 * s + 8 * g: 32 * s + 8 * g + 8])
+    assert (frag_unpack(f, 96)[66:] == 0).all()
