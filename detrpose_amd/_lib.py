@@ -40,6 +40,12 @@ class RowMap(C.Structure):
     _fields_ = [("base", i64), ("group", i32), ("stride_g", i64), ("stride_r", i64)]
 
 
+class LossHead(C.Structure):
+    """Mirror of dp_loss_head."""
+    _fields_ = [("logits", vp), ("lg_b", i64), ("lg_q", i32), ("kps", vp), ("kp_b", i64), ("kp_q", i32),
+                ("match", vp)]
+
+
 def rowmap(base=0, group=1, stride_g=0, stride_r=0) -> RowMap:
     return RowMap(int(base), int(group), int(stride_g), int(stride_r))
 
@@ -83,6 +89,11 @@ _SIGS = {
     "dp_ffn_layernorm": (i32, [vp, RowMap, vp, RowMap, vp, vp, i32, vp, vp, vp, vp, f32, i32, i32, vp]),
     "dp_query_pos": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, RowMap, i32, vp]),
     "dp_pose_mlp": (i32, [vp, RowMap, vp, RowMap, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, vp]),
+    "dp_hungarian_match": (i32, [vp, i64, i64, i32, i32, vp, i64, i64, i32, i32, vp, vp, vp, vp, i32, i32, i32, i32,
+                                 f32, f32, f32, f32, vp, vp, vp, vp]),
+    "dp_match_union": (i32, [vp, i32, i32, i32, vp, vp, vp]),
+    "dp_pose_loss": (i32, [C.POINTER(LossHead), i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp,
+                           f32, f32, f32, f32, vp, vp, vp, vp, vp]),
 }
 
 EXPORTED = tuple(k for k in _SIGS)

@@ -265,6 +265,53 @@ int dp_pose_mlp(const void* x, dp_rowmap xm, const void* x2, dp_rowmap x2m, int3
                 const void* w2, const float* b2, int32_t nout, const float* prev, float* out,
                 int32_t c, void* stream);
 
+/* ---- Training criterion: matching + the default losses of the L/N/X
+ * configs (criterion losses ['vfl', 'keypoints'], configs/detrpose/include/detrpose_hgnetv2.py).
+ * Heads are the decoder outputs the reference matches: final, aux 0..L-2, pre, interm.
+ * Targets are packed per batch: tgt_off [B+1] prefix offsets (int32), tgt_label [T] (int32),
+ * tgt_kps [T][3K] f32 = K (x, y) pairs then K visibilities, tgt_area [T] f32. */
+
+/* HungarianMatcher.forward (src/models/detrpose/matcher.py:47-112) for H heads at once:
+ * logits (H, B, Q, ncls) and keypoints (H, B, Q, 2K) f32 at the given element strides;
+ * cost = cost_class * focal + cost_kp * L1 + cost_oks * (1 - OKS) per image, solved by
+ * scipy's shortest augmenting path (linear_sum_assignment, matcher.py:97) in f64 on the
+ * GPU. match (H, B, Q) int32 = the image-local target index of query q, or -1.
+ * max_t = the most targets of any image (LDS sizing). cost_out (H, B, Q, max_t) or NULL. */
+int dp_hungarian_match(const float* logits, int64_t lg_h, int64_t lg_b, int32_t lg_q, int32_t ncls,
+                       const float* kps, int64_t kp_h, int64_t kp_b, int32_t kp_q, int32_t nkp,
+                       const int32_t* tgt_off, const int32_t* tgt_label, const float* tgt_kps,
+                       const float* tgt_area, int32_t H, int32_t B, int32_t Q, int32_t max_t,
+                       float cost_class, float cost_kp, float cost_oks, float alpha,
+                       const float* sigmas, int32_t* match, float* cost_out, void* stream);
+
+/* Criterion._get_go_indices (criterion.py:247-268): go (B, Q) = per query the target the
+ * most of the H matchings chose (ties: the smallest target index), -1 if none;
+ * n_go = number of matched queries (f32 scalar, before the all-reduce of criterion.py:306-312). */
+int dp_match_union(const int32_t* match, int32_t H, int32_t B, int32_t Q, int32_t* go, float* n_go,
+                   void* stream);
+
+#define DP_LOSS_MAX_HEADS 16
+/* One decoder head for dp_pose_loss: its logits (B, Q, ncls) and keypoints (B, Q, 2K) f32
+ * at element strides, and its own matching (B, Q) from dp_hungarian_match. */
+typedef struct dp_loss_head {
+  const float* logits;  int64_t lg_b;  int32_t lg_q;
+  const float* kps;     int64_t kp_b;  int32_t kp_q;
+  const int32_t* match;
+} dp_loss_head;
+
+/* Criterion.loss_vfl (criterion.py:58-93) with the head's matching and loss_keypoints
+ * (criterion.py:200-229: L1 + OKS, keypoint_loss.py) with the union matching go, for H heads:
+ * losses (H, 3) = [loss_vfl * w_vfl, loss_keypoints * w_kp, loss_oks * w_oks], normalised by
+ * max(n_boxes / world, 1) and max(n_boxes_go / world, 1) (device scalars, all-reduced by the
+ * caller); and the gradients of those three weighted losses: g_logits (H, B, Q, ncls) of
+ * loss_vfl, g_kp_l1 / g_kp_oks (H, B, Q, 2K) of loss_keypoints / loss_oks. */
+int dp_pose_loss(const dp_loss_head* heads /* host array of H */, int32_t H, int32_t B, int32_t Q,
+                 int32_t ncls, int32_t nkp, const int32_t* go, const int32_t* tgt_off,
+                 const int32_t* tgt_label, const float* tgt_kps, const float* tgt_area,
+                 const float* sigmas, float alpha, float gamma, const float* n_boxes,
+                 const float* n_boxes_go, float world, float w_vfl, float w_kp, float w_oks,
+                 float* losses, float* g_logits, float* g_kp_l1, float* g_kp_oks, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

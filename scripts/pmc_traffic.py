@@ -27,7 +27,8 @@ def family(name):
     for key in ("dwconv_kernel", "dwconv_lds_kernel", "layernorm_kernel", "attn_mfma_kernel", "attn_short_kernel",
                 "msda_kernel", "msda_wave_kernel", "add_rows_kernel", "stem_conv_kernel", "stem1_mfma_kernel",
                 "maxpool_kernel", "class_max_kernel",
-                "topk_kernel", "gate_ln_kernel", "sine_embed_kernel", "lqe_kernel", "pose_refine_kernel"):
+                "topk_kernel", "gate_ln_kernel", "sine_embed_kernel", "lqe_kernel", "pose_refine_kernel",
+                "linear_ln_kernel", "ffn_ln_kernel", "query_pos_kernel", "pose_mlp_kernel", "ln_classmax_kernel"):
         if key in name:
             return key
     return "other"

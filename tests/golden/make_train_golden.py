@@ -1,0 +1,184 @@
+"""Generate the training-criterion fixtures under tests/golden/ by running the REFERENCE
+HungarianMatcher + Criterion (read-only at /root/reference) on CPU-constructed decoder
+outputs (training parity is pinned on the criterion with such inputs; the
+DN path needs .cuda()).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_train_golden.py
+
+Import recipe: make_golden._import_reference() plus two bare namespaces the criterion's
+import chain needs: `src.data` (its __init__ pulls cv2) and `src.data.dataloader` (imported by
+src/misc/dist_utils.py for a DataLoader class the criterion never uses; torchvision's
+transforms are absent), stubbed as an empty module.
+
+One deliberate change to the reference's behaviour: Criterion._get_go_indices orders the
+(query, target) pair counts with torch.argsort(descending=True) (criterion.py:258), whose
+order among EQUAL counts is unspecified (on CPU it is not stable: it differs from
+torch.sort(stable=True) on ties). While the criterion runs here torch.argsort is replaced by
+the stable sort, so that among tied counts the smaller target index wins: the rule
+detrpose_amd (dp_match_union) and the oracle implement. Without it the chosen target of a
+tied query is an artefact of the sort kernel. Everything else runs unmodified.
+
+Output: criterion_{a,b,c}.npz with inputs (per-head logits / keypoints, targets), the
+reference's per-head matchings, the final head's cost matrix, the union matching, the loss
+dict and the gradients of sum(losses) and of the vfl losses w.r.t. every head's outputs.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import make_golden  # noqa: E402
+
+CASES = {
+    # name: (B, Q, ncls, K, n_aux, target sizes, seed)
+    "a": (4, 60, 2, 17, 5, [3, 0, 7, 1], 11),
+    "b": (2, 20, 2, 17, 3, [25, 4], 12),     # an image with more targets than queries
+    "c": (3, 30, 2, 14, 5, [5, 2, 9], 13),   # CrowdPose keypoints (14, other sigmas)
+}
+
+
+def _import_criterion():
+    make_golden._import_reference()
+    ref = make_golden.REF
+    m = types.ModuleType("src.data")
+    m.__path__ = [os.path.join(ref, "src", "data")]
+    sys.modules["src.data"] = m
+    dl = types.ModuleType("src.data.dataloader")
+    dl.DataLoader = None
+    sys.modules["src.data.dataloader"] = dl
+    from src.models.detrpose.criterion import Criterion
+    from src.models.detrpose.matcher import HungarianMatcher
+    return Criterion, HungarianMatcher
+
+
+def make_case(Criterion, HungarianMatcher, B, Q, ncls, K, n_aux, sizes, seed):
+    g = torch.Generator().manual_seed(seed)
+    r = np.random.default_rng(seed)
+    targets = []
+    for n in sizes:
+        xy = torch.rand(n, K, 2, generator=g)
+        vis = (torch.rand(n, K, generator=g) > 0.3).float()
+        if n >= 3:
+            vis[1] = 0.0                      # an instance with no visible keypoint
+        kps = torch.cat([xy.flatten(1), vis], 1)
+        targets.append({"labels": torch.as_tensor(r.integers(0, ncls, n), dtype=torch.int64),
+                        "keypoints": kps, "area": torch.rand(n, generator=g) * 0.3 + 0.002,
+                        "boxes": torch.zeros(n, 4)})
+    heads = 1 + n_aux + 2   # final, aux, pre, interm
+    lg, kp = [], []
+    for h in range(heads):
+        logit = torch.randn(B, Q, ncls, generator=g) * 2
+        k = torch.sigmoid(torch.randn(B, Q, 2 * K, generator=g) * 2)
+        # some queries near their image's targets, so matchings are not arbitrary
+        for b, t in enumerate(targets):
+            for i in range(len(t["labels"])):
+                q = int(r.integers(0, Q))
+                k[b, q] = (t["keypoints"][i, :2 * K] + 0.03 * torch.randn(2 * K, generator=g)).clamp(0, 1)
+        lg.append(logit.requires_grad_(True))
+        kp.append(k.requires_grad_(True))
+
+    def head(i):
+        return {"pred_logits": lg[i], "pred_keypoints": kp[i]}
+
+    outputs = {**head(0), "pred_corners": torch.zeros(1), "ref_points": torch.zeros(1), "up": torch.tensor(0.5),
+               "reg_scale": torch.tensor(4.0), "reg_max": 32,
+               "aux_outputs": [head(1 + i) for i in range(n_aux)],
+               "aux_pre_outputs": head(1 + n_aux), "aux_interm_outputs": [head(2 + n_aux)]}
+    matcher = HungarianMatcher(cost_class=2.0, cost_keypoints=10.0, cost_oks=4.0, focal_alpha=0.25,
+                               num_body_points=K)
+    crit = Criterion(num_classes=ncls, matcher=matcher,
+                     weight_dict={"loss_vfl": 2.0, "loss_keypoints": 10.0, "loss_oks": 4.0},
+                     losses=["vfl", "keypoints"], num_body_points=K, focal_alpha=0.25)
+    store = {"B": np.array(B), "Q": np.array(Q), "ncls": np.array(ncls), "K": np.array(K), "n_aux": np.array(n_aux),
+             "sizes": np.array(sizes, np.int64)}
+    for i in range(heads):
+        store[f"logits{i}"] = lg[i].detach().numpy()
+        store[f"kps{i}"] = kp[i].detach().numpy()
+    T = sum(sizes)
+    store["tgt_labels"] = torch.cat([t["labels"] for t in targets]).numpy() if T else np.zeros(0, np.int64)
+    store["tgt_kps"] = torch.cat([t["keypoints"] for t in targets]).numpy() if T else np.zeros((0, 3 * K), np.float32)
+    store["tgt_area"] = torch.cat([t["area"] for t in targets]).numpy() if T else np.zeros(0, np.float32)
+    # per-head matchings of the reference matcher (matcher.py:47-112)
+    match = np.full((heads, B, Q), -1, np.int64)
+    with torch.no_grad():
+        for i in range(heads):
+            for b, (I, J) in enumerate(matcher(head(i), targets)):
+                match[i, b, I.numpy()] = J.numpy()
+    store["match"] = match
+    # the final head's cost matrix (matcher.py:87), all targets of the batch as columns
+    cap = {}
+    orig_split = torch.Tensor.split
+
+    def split_spy(self, sizes_, dim=0):
+        if dim == -1 and self.dim() == 3 and "C" not in cap:
+            cap["C"] = self.clone()
+        return orig_split(self, sizes_, dim)
+
+    torch.Tensor.split = split_spy
+    try:
+        with torch.no_grad():
+            matcher(head(0), targets)
+    finally:
+        torch.Tensor.split = orig_split
+    store["cost_final"] = cap["C"].numpy()
+    # criterion with a stable argsort in _get_go_indices (module docstring)
+    orig_argsort = torch.argsort
+
+    def stable_argsort(x, dim=-1, descending=False, **kw):
+        return torch.sort(x, dim=dim, descending=descending, stable=True)[1]
+
+    go_cap = {}
+    orig_go = Criterion._get_go_indices
+
+    def go_spy(self, indices, indices_aux_list):
+        res = orig_go(self, indices, indices_aux_list)
+        go_cap["go"] = res
+        return res
+
+    torch.argsort = stable_argsort
+    Criterion._get_go_indices = go_spy
+    try:
+        losses = crit(outputs, targets)
+    finally:
+        torch.argsort = orig_argsort
+        Criterion._get_go_indices = orig_go
+    go = np.full((B, Q), -1, np.int64)
+    for b, (I, J) in enumerate(go_cap["go"]):
+        go[b, I.numpy()] = J.numpy()
+    store["go"] = go
+    keys = sorted(losses)
+    store["loss_keys"] = np.array(keys)
+    store["loss_vals"] = np.array([float(losses[k]) for k in keys], np.float64)
+    total = sum(losses.values())
+    grads = torch.autograd.grad(total, lg + kp, retain_graph=True)
+    for i in range(heads):
+        store[f"grad_logits{i}"] = grads[i].numpy()
+        store[f"grad_kps{i}"] = grads[heads + i].numpy()
+    vfl = sum(v for k, v in losses.items() if k.startswith("loss_vfl"))
+    gv = torch.autograd.grad(vfl, lg)
+    for i in range(heads):
+        store[f"grad_vfl_logits{i}"] = gv[i].numpy()
+    print(f"  B={B} Q={Q} K={K} heads={heads} sizes={sizes}: {len(keys)} losses, "
+          f"go pairs={int((go >= 0).sum())}, total={float(total):.6f}")
+    return store
+
+
+def main():
+    torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
+    Criterion, HungarianMatcher = _import_criterion()
+    for name, (B, Q, ncls, K, n_aux, sizes, seed) in CASES.items():
+        st = make_case(Criterion, HungarianMatcher, B, Q, ncls, K, n_aux, sizes, seed)
+        np.savez_compressed(os.path.join(HERE, f"criterion_{name}.npz"), **st)
+        print("wrote", f"criterion_{name}.npz")
+
+
+if __name__ == "__main__":
+    main()
