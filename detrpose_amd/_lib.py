@@ -72,6 +72,7 @@ _SIGS = {
     "dp_resize_pad": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, f32, vp]),
     "dp_msda_core_fwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "dp_msda_core_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, i32, vp]),
+    "dp_msda_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, i32, vp]),
     "dp_topk": (i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
     "dp_class_max": (i32, [vp, i32, i32, vp, vp, i32, vp, i32, vp]),
     "dp_gather_rows": (i32, [vp, i64, vp, i32, i32, i32, vp, i32, vp]),

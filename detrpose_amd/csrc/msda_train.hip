@@ -125,6 +125,112 @@ __global__ __launch_bounds__(256) void msda_core_kernel(const T* __restrict__ va
   }
 }
 
+// Backward of the fused inference op dp_msda (MSDeformAttn.forward's default branch,
+// ms_deform_attn.py:384-441): from the raw sampling offsets | attention logits row of each
+// token (the two Linear outputs) and its reference point. Per (token, head): softmax over the
+// L*P logits and loc = ref + off / (W, H) recomputed in registers, then the core backward
+// above, then the chain rule through them in the same pass:
+//   d off_x = d loc_x / W,  d off_y = d loc_y / H,  d ref += d loc (atomics over heads),
+//   d logit_j = a_j (d a_j - sum_k a_k d a_k).
+// grad_oa has the offattn layout [rows][nH*L*P*2 | nH*L*P]; grad_ref [rows][2] or NULL.
+template <typename T>
+__global__ __launch_bounds__(256) void msda_fused_bwd_kernel(const T* __restrict__ value, int S, TLevels lv, int L,
+                                                             int P, const float* __restrict__ oa,
+                                                             const float* __restrict__ ref, const T* __restrict__ gout,
+                                                             float* __restrict__ gvalue, float* __restrict__ goa,
+                                                             float* __restrict__ gref, int lq, int pairs, int nh,
+                                                             int dh) {
+  constexpr int VEC = Vec16<T>::N;
+  const int cpt = dh / VEC;
+  const int ppw = 64 / cpt;
+  const int lane = threadIdx.x & 63;
+  const int slot = lane / cpt, c = lane - slot * cpt;
+  const int pair = (blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw + slot;
+  if (slot >= ppw || pair >= pairs) return;
+  const int g0 = lane - c;
+  const int r = pair / nh, h = pair - r * nh;
+  const int b = r / lq;
+  const int C = nh * dh;
+  const int LP = L * P;
+  const int ncol = nh * LP * 3;
+  const int ch = h * dh + c * VEC;
+  const T* vb = value + (int64_t)b * S * C + ch;
+  const float* orow = oa + (int64_t)r * ncol;
+  float* grow = goa + (int64_t)r * ncol;
+  const float* lg = orow + nh * LP * 2 + h * LP;
+  float go[VEC];
+  load_vec(gout + (int64_t)r * C + ch, go);
+  float mx = -INFINITY;
+  for (int j = 0; j < LP; ++j) mx = fmaxf(mx, lg[j]);
+  float den = 0.f;
+  for (int j = 0; j < LP; ++j) den += expf(lg[j] - mx);
+  const float inv = 1.f / den;
+  const float rx = ref[2 * r], ry = ref[2 * r + 1];
+  float dot = 0.f, grx = 0.f, gry = 0.f;
+  for (int j = 0; j < LP; ++j) {
+    const int l = j / P;
+    const int H = lv.h[l], W = lv.w[l];
+    const float ox = orow[(h * LP + j) * 2], oy = orow[(h * LP + j) * 2 + 1];
+    const float x = (rx + ox / W) * W - 0.5f, y = (ry + oy / H) * H - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float fx = x - fx0, fy = y - fy0;
+    const float a = expf(lg[j] - mx) * inv;
+    const float wk[4] = {(1.f - fx) * (1.f - fy), fx * (1.f - fy), (1.f - fx) * fy, fx * fy};
+    float v[4][VEC];
+    int row[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int xi = x0 + (k & 1), yi = y0 + (k >> 1);
+      const bool ok = xi >= 0 && xi < W && yi >= 0 && yi < H;
+      row[k] = ok ? lv.start[l] + yi * W + xi : -1;
+      if (ok) load_vec(vb + (int64_t)row[k] * C, v[k]);
+      else
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) v[k][e] = 0.f;
+    }
+    float ga = 0.f, gx = 0.f, gy = 0.f;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float s = wk[0] * v[0][e] + wk[1] * v[1][e] + wk[2] * v[2][e] + wk[3] * v[3][e];
+      ga += go[e] * s;
+      gx += go[e] * ((v[1][e] - v[0][e]) * (1.f - fy) + (v[3][e] - v[2][e]) * fy);
+      gy += go[e] * ((v[2][e] - v[0][e]) * (1.f - fx) + (v[3][e] - v[1][e]) * fx);
+    }
+    ga = group_sum(ga, g0, cpt);
+    gx = group_sum(gx, g0, cpt);
+    gy = group_sum(gy, g0, cpt);
+    dot += a * ga;
+    if (c == 0) {
+      // d loc = a * g * (W, H); d off = d loc / (W, H)
+      grow[(h * LP + j) * 2] = a * gx;
+      grow[(h * LP + j) * 2 + 1] = a * gy;
+      grow[nh * LP * 2 + h * LP + j] = ga;   // d attn for now; the softmax pass below finishes it
+      grx += a * gx * W;
+      gry += a * gy * H;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (row[k] < 0) continue;
+      float* gp = gvalue + ((int64_t)b * S + row[k]) * C + ch;
+      const float sc = a * wk[k];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) unsafeAtomicAdd(gp + e, sc * go[e]);
+    }
+  }
+  if (c == 0) {
+    float* gl = grow + nh * LP * 2 + h * LP;
+    for (int j = 0; j < LP; ++j) {
+      const float a = expf(lg[j] - mx) * inv;
+      gl[j] = a * (gl[j] - dot);
+    }
+    if (gref) {
+      unsafeAtomicAdd(gref + 2 * r, grx);
+      unsafeAtomicAdd(gref + 2 * r + 1, gry);
+    }
+  }
+}
+
 template <typename T, bool BWD>
 int launch_core(const void* value, int batch, int S, const TLevels& lv, int L, int P, const float* loc,
                 const float* attn, const void* gout, void* out, float* gvalue, float* gloc, float* gattn, int lq, int nh,
@@ -198,4 +304,33 @@ extern "C" int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, con
                                      grad_loc, grad_attn, lq, nhead, dh, s);
   return launch_core<float, true>(value, batch, S, lv, nlevels, npoints, loc, attn, grad_out, nullptr, grad_value,
                                   grad_loc, grad_attn, lq, nhead, dh, s);
+}
+
+extern "C" int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
+                           const float* offattn, const float* ref, const void* grad_out, int32_t lq, int32_t nhead,
+                           int32_t dh, int32_t npoints, float* grad_value, float* grad_offattn, float* grad_ref,
+                           int32_t dtype, void* stream) {
+  TLevels lv;
+  const int rc = check_core(value, batch, S, lvl_hw, nlevels, offattn, ref, lq, nhead, dh, npoints, dtype, &lv);
+  if (rc) return rc;
+  DP_REQUIRE(grad_out && grad_value && grad_offattn, "dp_msda_bwd: null gradient pointer");
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0, "dp_msda_bwd: grad_out must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  // grad_value (and grad_ref) are accumulated by atomics: clear them on the stream first
+  if (hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess ||
+      (grad_ref && hipMemsetAsync(grad_ref, 0, (size_t)batch * lq * 2 * sizeof(float), s) != hipSuccess))
+    return dp_check_launch("dp_msda_bwd(memset)");
+  const int VEC = dtype == DP_BF16 ? 8 : 4;
+  const int ppw = 64 / (dh / VEC);
+  const int pairs = batch * lq * nhead;
+  const int grid = ((pairs + ppw - 1) / ppw + 3) / 4;
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(msda_fused_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)value, S, lv,
+                       nlevels, npoints, offattn, ref, (const bf16_t*)grad_out, grad_value, grad_offattn, grad_ref, lq,
+                       pairs, nhead, dh);
+  else
+    hipLaunchKernelGGL(msda_fused_bwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)value, S, lv, nlevels,
+                       npoints, offattn, ref, (const float*)grad_out, grad_value, grad_offattn, grad_ref, lq, pairs,
+                       nhead, dh);
+  return dp_check_launch("dp_msda_bwd");
 }

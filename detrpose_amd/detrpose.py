@@ -69,8 +69,7 @@ class DETRPose(nn.Module):
     @torch.no_grad()
     def forward(self, samples, targets=None):
         if self.training:
-            raise NotImplementedError("training forward (DN queries, aux outputs) is outside the inference hot path; "
-                                      "call .eval() or .deploy() first")
+            return self._forward_train(samples, targets)
         if not samples.is_cuda:
             raise RuntimeError("DETRPose (MI355X) runs on the GPU only: move the images to a HIP device")
         hw = tuple(self.encoder.eval_spatial_size)
@@ -87,6 +86,51 @@ class DETRPose(nn.Module):
             out = {k: v.clone() for k, v in plan.outputs.items()}
         if not self.deploy_mode:
             out["pred_keypoints"] = out["pred_keypoints"].flatten(-2)
+        return out
+
+    def _check_input(self, samples):
+        if not samples.is_cuda:
+            raise RuntimeError("DETRPose (MI355X) runs on the GPU only: move the images to a HIP device")
+        hw = tuple(self.encoder.eval_spatial_size)
+        if samples.dim() != 4 or tuple(samples.shape[1:]) != (3, *hw):
+            raise ValueError(f"DETRPose expects images (B, 3, {hw[0]}, {hw[1]}), got {tuple(samples.shape)}")
+
+    def _forward_train(self, samples, targets):
+        """The training-mode forward's outputs (transformer.py:1219-1385) without denoising:
+        every decoder layer's logits / keypoints / corners (aux_outputs), the first layer's
+        pre head (aux_pre_outputs) and the two-stage selection (aux_interm_outputs), in the
+        reference's dict layout, for Criterion. Values only: there is no backward through the
+        network on this path. Supported: targets=None (the reference's prepare_for_cdn needs
+        targets and .cuda(), dn_component.py:115) and BatchNorm layers in eval mode (frozen
+        BN; train-mode batch statistics / SyncBN are not built)."""
+        if targets is not None:
+            raise NotImplementedError("training forward with targets = OKS-denoising queries (prepare_for_cdn, "
+                                      "dn_component.py:39-183): not built; call with targets=None")
+        bn = [n for n, m in self.named_modules() if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.training]
+        if bn:
+            raise NotImplementedError(f"{len(bn)} BatchNorm layers are in train mode (batch statistics / SyncBN are not "
+                                      f"built, e.g. {bn[0]}): put them in eval mode (frozen-BN training)")
+        self._check_input(samples)
+        eng = self.engine(samples.device)
+        plan = eng.plan(samples.shape[0], aux=True)
+        with torch.cuda.device(samples.device):
+            if samples.data_ptr() != plan.input.data_ptr():
+                plan.input.copy_(samples.to(torch.float32), non_blocking=True)
+            plan.run()
+            ao = plan.aux_outputs
+            logits = [t.clone() for t in ao["logits"]]
+            poses = [t.clone().flatten(-2) for t in ao["keypoints"]]
+            corners = [t.clone() for t in ao["corners"]]
+            refs = ao["ref_init"].clone()
+            tr = self.transformer
+            out = {"pred_logits": logits[-1], "pred_keypoints": poses[-1], "pred_corners": corners[-1],
+                   "ref_points": refs, "up": tr.up, "reg_scale": tr.reg_scale, "reg_max": tr.reg_max}
+            out["aux_outputs"] = [{"pred_logits": logits[l], "pred_keypoints": poses[l], "pred_corners": corners[l],
+                                   "ref_points": refs, "teacher_corners": corners[-1], "teacher_logits": logits[-1]}
+                                  for l in range(len(logits) - 1)]
+            out["aux_interm_outputs"] = [{"pred_logits": ao["interm_logits"].clone(),
+                                          "pred_keypoints": ao["interm_ref"][:, :, 1:].clone().flatten(-2)}]
+            out["aux_pre_outputs"] = {"pred_logits": ao["pre_logits"].clone(), "pred_keypoints": refs.clone()}
         return out
 
 

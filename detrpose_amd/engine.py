@@ -189,6 +189,8 @@ class Plan:
         self.outputs = {}
         self.post = None         # PostProcess buffers once add_postprocess() appended it
         self.post_ops = []       # its launch (kept apart: eager forwards do not rerun it)
+        self.aux = False         # training-mode outputs recorded (Engine.plan(aux=True))
+        self.aux_outputs = None  # their buffers (see Engine._plan_transformer)
         self._graph = None
 
     # -- recording
@@ -407,6 +409,7 @@ class Engine:
         P["mask"] = pk.t(sd[t + "valid_mask"].reshape(-1), torch.uint8)
         P["anchors"] = pk.t(sd[t + "anchors"].reshape(-1, 2))
         P["enc_cls"] = (pk.t(sd[t + "enc_out_class_embed.weight"]), pk.t(sd[t + "enc_out_class_embed.bias"]))
+        P["enc_cls_small"] = pk.small(sd[t + "enc_out_class_embed.weight"], sd[t + "enc_out_class_embed.bias"])
         ep = t + "enc_pose_embed.layers."
         P["enc_pose"] = [pk.linear(sd[ep + f"{i}.weight"], sd[ep + f"{i}.bias"], act="relu") for i in range(3)]
         P["enc_pose_last"] = pk.linear(sd[ep + "3.weight"], sd[ep + "3.bias"], exact=True)
@@ -455,9 +458,11 @@ class Engine:
                 # MFMA-fragment copies for the row-block fused kernels (detrpose_amd/fragments.py)
                 L["frag"] = {k: frag_pack(L[k].w) for k in ("within_out", "across_out", "gate", "ffn1", "ffn2")}
                 L["frag"]["pose"] = [frag_pack(pc.w) for pc in L["pose"]]
-            if l == tr.num_decoder_layers - 1:
-                qp = f"{t}lqe_embed.{l}.reg_conf.layers."
-                L["cls"] = pk.small(sd[f"{t}class_embed.{l}.weight"], sd[f"{t}class_embed.{l}.bias"])
+            # class / LQE heads of every layer: the inference plan runs the last layer's
+            # (eval_idx), the training-mode plan all of them (transformer.py:726-728)
+            qp = f"{t}lqe_embed.{l}.reg_conf.layers."
+            L["cls"] = pk.small(sd[f"{t}class_embed.{l}.weight"], sd[f"{t}class_embed.{l}.bias"])
+            if qp + "0.weight" in sd:
                 L["lqe"] = [pk.small(sd[qp + "0.weight"], sd[qp + "0.bias"], act="relu"),
                             pk.small(sd[qp + "1.weight"], sd[qp + "1.bias"])]
             P["layers"].append(L)
@@ -538,17 +543,21 @@ class Engine:
                  post_group, post_skip, mask_ptr, period, mrow, self.code)
 
     # ------------------------------------------------------------------ planning
-    def plan(self, batch: int) -> Plan:
-        if batch in self.plans:
-            return self.plans[batch]
+    def plan(self, batch: int, aux: bool = False) -> Plan:
+        """aux=True: the training-mode forward's extra outputs too (every decoder layer's
+        logits / keypoints / corners, the pre and interm heads: transformer.py:1348-1385)."""
+        key = (batch, True) if aux else batch
+        if key in self.plans:
+            return self.plans[key]
         plan = Plan(self, batch)
+        plan.aux = aux
         self._cur = plan
         img = self._empty(batch, 3, *self._img_hw(), dtype=torch.float32)
         plan.input = img
         feats = self._plan_backbone(plan, img)
         memory, shapes = self._plan_encoder(plan, feats)
         self._plan_transformer(plan, memory, shapes)
-        self.plans[batch] = plan
+        self.plans[key] = plan
         return plan
 
     def _img_hw(self):
@@ -772,6 +781,16 @@ class Engine:
         plan._op("ts.refpoints", lib.dp_refpoint_init, delta.data_ptr(), P["anchors"].data_ptr(), topi.data_ptr(), B,
                  nq, K, ref.data_ptr())
         plan.bufs.update(topk_idx=topi, topk_val=topv, enc_output_norm=om, score=score)
+        aux = plan.aux
+        if aux:
+            # aux_interm_outputs (transformer.py:1248-1250, 1372): every class score of the selected
+            # rows, and the initial keypoint coordinates (the decoder refines ref in place)
+            ecs = P["enc_cls_small"]
+            interm_logits = self._empty(B, nq, ecs.n, dtype=torch.float32)
+            plan._op("aux.interm_cls", lib.dp_linear_small, tm.ptr, contiguous_rows(Cc), self.code, B * nq, ecs.k,
+                     ecs.wt.data_ptr(), ecs.b.data_ptr(), ecs.n, ecs.n, 0, None, interm_logits.data_ptr())
+            interm_ref = self._empty(B, nq, T, 2, dtype=torch.float32)
+            plan._op("aux.interm_ref", lib.dp_broadcast, ref.data_ptr(), ref.numel() * 4, interm_ref.data_ptr(), 1)
         # ---- decoder (transformer.py:558-925)
         rows = B * nq * T               # all tokens
         krows = B * nq * K              # keypoint tokens
@@ -802,8 +821,10 @@ class Engine:
             f2 = self._fmap(1, 1, rows, Cc)
             pin = self._fmap(1, 1, krows, Cc)
         nb = 2 * (tr.reg_max + 1)
-        corners = [self._empty(krows, nb, dtype=torch.float32) for _ in range(2)]
-        plan.bufs["corners"] = corners        # layer l writes corners[l % 2] (pred_corners, f32)
+        nlayers = tr.num_decoder_layers
+        ncorn = nlayers if aux else 2
+        corners = [self._empty(krows, nb, dtype=torch.float32) for _ in range(ncorn)]
+        plan.bufs["corners"] = corners        # layer l writes corners[l % ncorn] (pred_corners, f32)
         pre = self._empty(krows, 2, dtype=torch.float32)
         ref_init = self._empty(krows, 2, dtype=torch.float32)
         # outputs share one contiguous f32 buffer [logits (B,nq,ncls) | keypoints (B,nq,K,2)]
@@ -820,8 +841,32 @@ class Engine:
         plan.bufs["layers"] = []
         plan.bufs["layer_ops"] = []           # per layer: (op that finishes its token rows, op writing its corners)
         src, dst = tgtA, tgtB
-        nlayers = tr.num_decoder_layers
         cr = contiguous_rows
+        # training mode: each layer's keypoints / logits in buffers of their own (the last
+        # layer's are the outputs in out_flat)
+        layer_kps = [self._empty(B, nq, K, 2, dtype=torch.float32) if aux and l < nlayers - 1 else kps
+                     for l in range(nlayers)]
+        layer_logits = [self._empty(B, nq, ncls, dtype=torch.float32) if aux and l < nlayers - 1 else
+                        out_flat[:B * nq * ncls].view(B, nq, ncls) for l in range(nlayers)]
+        pre_logits = self._empty(B, nq, ncls, dtype=torch.float32) if aux else None
+
+        def class_lqe(n, L, x_rows, kps_l, logits_l):
+            """class_embed[l] on the instance tokens + LQE (transformer.py:726-728)"""
+            cls, lqe = L["cls"], L["lqe"]
+            score2 = self._empty(B * nq, cls.n, dtype=torch.float32)
+            plan._op(n + ".cls", lib.dp_linear_small, x_rows, rowmap(0, 1, T * Cc, 0), self.code, B * nq,
+                     cls.k, cls.wt.data_ptr(), cls.b.data_ptr(), cls.n, cls.n, 0, None, score2.data_ptr())
+            lv0 = plan.bufs["encoder"][0]
+            st = self._empty(B * nq, K * 5, dtype=torch.float32)
+            plan._op(n + ".lqe_stats", lib.dp_lqe_stats, lv0.ptr, lv0.bs, lv0.H, lv0.W, Cc, kps_l.data_ptr(), B, nq,
+                     K, st.data_ptr(), self.code)
+            hid = self._empty(B * nq, lqe[0].n, dtype=torch.float32)
+            plan._op(n + ".lqe0", lib.dp_linear_small, st.data_ptr(), contiguous_rows(K * 5), DP_F32, B * nq,
+                     lqe[0].k, lqe[0].wt.data_ptr(), lqe[0].b.data_ptr(), lqe[0].n, lqe[0].n, lqe[0].act, None,
+                     hid.data_ptr())
+            plan._op(n + ".lqe1", lib.dp_linear_small, hid.data_ptr(), contiguous_rows(lqe[0].n), DP_F32, B * nq,
+                     lqe[1].k, lqe[1].wt.data_ptr(), lqe[1].b.data_ptr(), lqe[1].n, cls.n, 0,
+                     score2.data_ptr(), logits_l.data_ptr())
         eps = C.c_float(1e-5)
 
         def lin(pc, frag, k):
@@ -917,8 +962,14 @@ class Engine:
                 self._conv(plan, n + ".pre2", ph2, pp[2], FMap(pre, 0, 1, 1, krows, 2, 2, pre.numel()), out_f32=True)
                 plan._op(n + ".pre_pose", lib.dp_pre_pose, pre.data_ptr(), ref.data_ptr(), B * nq, K,
                          ref_init.data_ptr())
+                if aux:
+                    # pre_scores = class_head[0](output_instance) (transformer.py:708)
+                    c0 = P["layers"][0]["cls"]
+                    plan._op(n + ".pre_cls", lib.dp_linear_small, dst.data_ptr(), rowmap(0, 1, T * Cc, 0), self.code,
+                             B * nq, c0.k, c0.wt.data_ptr(), c0.b.data_ptr(), c0.n, c0.n, 0, None,
+                             pre_logits.data_ptr())
             ph = L["pose"]
-            cur, prev = corners[l % 2], corners[(l + 1) % 2]
+            cur, prev = corners[l % ncorn], corners[(l - 1) % ncorn]
             if fused:
                 # pred_corners = pose_head(output_pose [+ output_pose_detach]) [+ pred_corners_undetach]
                 # (transformer.py:712): src keypoint rows hold the previous output_pose + this layer's
@@ -943,24 +994,15 @@ class Engine:
                            res=FMap(prev, 0, 1, 1, krows, nb, nb, prev.numel()) if l > 0 else None, out_f32=True)
                 plan.bufs["layer_ops"].append((last_op, n + ".pose2"))
             plan._op(n + ".refine", lib.dp_pose_refine, cur.data_ptr(), P["project"].data_ptr(), tr.reg_max,
-                     ref_init.data_ptr(), C.c_float(P["reg_scale"]), B * nq, K, kps.data_ptr(), ref.data_ptr())
+                     ref_init.data_ptr(), C.c_float(P["reg_scale"]), B * nq, K, layer_kps[l].data_ptr(), ref.data_ptr())
+            if l == nlayers - 1 or aux:
+                class_lqe(n, L, dst.data_ptr(), layer_kps[l], layer_logits[l])
             if l == nlayers - 1:
-                cls, lqe = L["cls"], L["lqe"]
-                score2 = self._empty(B * nq, cls.n, dtype=torch.float32)
-                plan._op(n + ".cls", lib.dp_linear_small, dst.data_ptr(), rowmap(0, 1, T * Cc, 0), self.code, B * nq,
-                         cls.k, cls.wt.data_ptr(), cls.b.data_ptr(), cls.n, cls.n, 0, None, score2.data_ptr())
-                lv0 = plan.bufs["encoder"][0]
-                st = self._empty(B * nq, K * 5, dtype=torch.float32)
-                plan._op(n + ".lqe_stats", lib.dp_lqe_stats, lv0.ptr, lv0.bs, lv0.H, lv0.W, Cc, kps.data_ptr(), B, nq,
-                         K, st.data_ptr(), self.code)
-                hid = self._empty(B * nq, lqe[0].n, dtype=torch.float32)
-                plan._op(n + ".lqe0", lib.dp_linear_small, st.data_ptr(), contiguous_rows(K * 5), DP_F32, B * nq,
-                         lqe[0].k, lqe[0].wt.data_ptr(), lqe[0].b.data_ptr(), lqe[0].n, lqe[0].n, lqe[0].act, None,
-                         hid.data_ptr())
-                logits = out_flat[:B * nq * ncls].view(B, nq, ncls)
-                plan._op(n + ".lqe1", lib.dp_linear_small, hid.data_ptr(), contiguous_rows(lqe[0].n), DP_F32, B * nq,
-                         lqe[1].k, lqe[1].wt.data_ptr(), lqe[1].b.data_ptr(), lqe[1].n, cls.n, 0,
-                         score2.data_ptr(), logits.data_ptr())
-                plan.outputs = {"pred_logits": logits, "pred_keypoints": kps}
+                plan.outputs = {"pred_logits": layer_logits[l], "pred_keypoints": kps}
             src, dst = dst, src
         plan.bufs["ref"] = ref
+        if aux:
+            plan.aux_outputs = {"logits": layer_logits, "keypoints": layer_kps,
+                                "corners": [corners[l % ncorn].view(B, nq, K, nb) for l in range(nlayers)],
+                                "ref_init": ref_init.view(B, nq, K, 2), "pre_logits": pre_logits,
+                                "interm_logits": interm_logits, "interm_ref": interm_ref}

@@ -87,6 +87,69 @@ def ms_deform_attn_core(value, value_spatial_shapes, sampling_locations, attenti
     return MSDeformAttnCoreFunction.apply(value, value_spatial_shapes, sampling_locations, attention_weights)
 
 
+class MSDeformAttnFunction(torch.autograd.Function):
+    """The fused op of MSDeformAttn.forward's default branch (ms_deform_attn.py:384-441):
+    raw offsets | attention logits + reference points -> softmax, sampling locations,
+    bilinear gather, weighted sum. Forward `dp_msda` (the inference kernel), backward
+    `dp_msda_bwd` (softmax and location chain rule fused into the gather backward)."""
+
+    @staticmethod
+    def forward(ctx, value, shapes, offattn, ref, n_heads, n_points):
+        N, S, Cc = value.shape
+        rows, ncol = offattn.shape
+        L = len(shapes)
+        if value.dtype not in _DT:
+            raise TypeError(f"msda: value dtype {value.dtype} (f32 / bf16)")
+        if not (value.is_cuda and offattn.device == value.device and ref.device == value.device):
+            raise RuntimeError("msda: value, offattn and ref must be on the same GPU (no CPU path)")
+        if ncol != n_heads * L * n_points * 3 or rows % N or ref.shape != (rows, 2) or Cc % n_heads:
+            raise ValueError(f"msda: offattn {tuple(offattn.shape)} / ref {tuple(ref.shape)} do not match value "
+                             f"{tuple(value.shape)} with {n_heads} heads, {L} levels, {n_points} points")
+        if sum(int(h) * int(w) for h, w in shapes) != S:
+            raise ValueError("msda: spatial shapes do not match value")
+        lq = rows // N
+        value = value.contiguous()
+        # the forward reads offattn in value's dtype: the backward differentiates at those values
+        oa = offattn.detach().to(value.dtype).contiguous()
+        ref = ref.detach().float().contiguous()
+        out = torch.empty(N, lq, Cc, device=value.device, dtype=value.dtype)
+        hw, nl = _shapes_arg(shapes)
+        lib = _lib.load()
+        s = torch.cuda.current_stream(value.device).cuda_stream
+        _lib.check(lib.dp_msda(value.data_ptr(), N, S, hw, nl, oa.data_ptr(), ref.data_ptr(), out.data_ptr(), Cc, lq,
+                               n_heads, Cc // n_heads, n_points, _DT[value.dtype], C.c_void_p(s)), "dp_msda")
+        ctx.save_for_backward(value, oa, ref)
+        ctx.shapes = [tuple(int(v) for v in hw_) for hw_ in shapes]
+        ctx.n_heads, ctx.n_points = n_heads, n_points
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        value, oa, ref = ctx.saved_tensors
+        N, S, Cc = value.shape
+        rows = oa.shape[0]
+        go = grad_out.contiguous().to(value.dtype)
+        gv = torch.empty(N, S, Cc, device=value.device, dtype=torch.float32)
+        goa = torch.empty(oa.shape, device=value.device, dtype=torch.float32)
+        gref = torch.empty(rows, 2, device=value.device, dtype=torch.float32) if ctx.needs_input_grad[3] else None
+        oa32 = oa.float()
+        hw, nl = _shapes_arg(ctx.shapes)
+        lib = _lib.load()
+        s = torch.cuda.current_stream(value.device).cuda_stream
+        _lib.check(lib.dp_msda_bwd(value.data_ptr(), N, S, hw, nl, oa32.data_ptr(), ref.data_ptr(), go.data_ptr(),
+                                   rows // N, ctx.n_heads, Cc // ctx.n_heads, ctx.n_points, gv.data_ptr(),
+                                   goa.data_ptr(), gref.data_ptr() if gref is not None else None,
+                                   _DT[value.dtype], C.c_void_p(s)), "dp_msda_bwd")
+        return gv.to(value.dtype), None, goa, gref, None, None
+
+
+def msdeform_attn(value, shapes, offattn, ref, n_heads, n_points):
+    """value (N, S, C); offattn (N*Lq, nH*L*P*3) = [sampling_offsets | attention_weights]
+    Linear outputs; ref (N*Lq, 2) one point per query shared by the levels -> (N, Lq, C).
+    Differentiable in value, offattn and ref."""
+    return MSDeformAttnFunction.apply(value, shapes, offattn, ref, n_heads, n_points)
+
+
 def value_from_levels(value_list, n_heads):
     """The reference's per-level value list [(N*nH, Dh, H*W)] -> (N, S, nH*Dh)."""
     parts = []

@@ -41,6 +41,28 @@ class MSDeformAttn(nn.Module):
         self.sampling_offsets = nn.Linear(d_model, n_heads * n_levels * n_points * 2)
         self.attention_weights = nn.Linear(d_model, n_heads * n_levels * n_points)
 
+    def forward(self, query, reference_points, value, input_spatial_shapes):
+        """ms_deform_attn.py:359-444 (default branch), differentiable: the two Linear layers
+        (torch), then one fused HIP op for softmax + sampling locations + bilinear gather +
+        weighted sum (dp_msda; backward dp_msda_bwd). query (N, Lq, C); reference_points with
+        one 2-D point per query, shaped as the decoder passes it ((N, Q, 1, T, 2), transposed
+        and flattened to (N, Lq, 1, 2) as at :412); value: the reference's per-level list
+        [(N*nH, Dh, H*W)] or the encoder memory (N, S, C)."""
+        from .msda import msdeform_attn, value_from_levels
+        N, Lq, _ = query.shape
+        ref = torch.transpose(reference_points, 2, 3).flatten(1, 2) if reference_points.dim() == 5 else reference_points
+        if ref.shape[-1] != 2 or ref.shape[1] != Lq:
+            raise ValueError(f"reference_points {tuple(reference_points.shape)}: one 2-D point per query expected")
+        if ref.dim() == 4:
+            if ref.shape[2] != 1:
+                raise NotImplementedError("per-level reference points (n_levels > 1 in dim 2) are not used by DETRPose")
+            ref = ref[:, :, 0]
+        if isinstance(value, (list, tuple)):
+            value = value_from_levels(value, self.n_heads)
+        oa = torch.cat([self.sampling_offsets(query), self.attention_weights(query)], -1)
+        return msdeform_attn(value, [tuple(int(v) for v in hw) for hw in input_spatial_shapes],
+                             oa.reshape(N * Lq, -1), ref.reshape(N * Lq, 2), self.n_heads, self.n_points)
+
 
 class Gate(nn.Module):
     """transformer.py:222-235."""

@@ -146,6 +146,17 @@ int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, const int32_t*
                      int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value,
                      float* grad_loc, float* grad_attn, int32_t dtype, void* stream);
 
+/* Backward of dp_msda (MSDeformAttn.forward's default branch, ms_deform_attn.py:384-441,
+ * the module-level training op): offattn f32 [batch*lq][nhead*L*P*2 | nhead*L*P] = the raw
+ * sampling_offsets | attention_weights Linear outputs, ref f32 [batch*lq][2]. Recomputes the
+ * softmax and the sampling locations and applies the chain rule through them in the same pass:
+ * grad_value f32 (zeroed here, f32 atomics), grad_offattn f32 (offattn layout), grad_ref f32
+ * [batch*lq][2] or NULL (zeroed here; atomics over the heads). value / grad_out of dtype. */
+int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */,
+                int32_t nlevels, const float* offattn, const float* ref, const void* grad_out, int32_t lq,
+                int32_t nhead, int32_t dh, int32_t npoints, float* grad_value, float* grad_offattn,
+                float* grad_ref, int32_t dtype, void* stream);
+
 /* Input pipeline of the reference benchmark (tools/benchmark/dataset.py:56-61) for one image
  * decoded to uint8 RGB (3, h, w) on the device: T.Resize to (new_h, new_w) (bilinear with
  * antialias, round + clamp to uint8, as torchvision's tensor resize), PadToSize(out_h, out_w)

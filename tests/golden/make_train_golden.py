@@ -171,9 +171,67 @@ def make_case(Criterion, HungarianMatcher, B, Q, ncls, K, n_aux, sizes, seed):
     return store
 
 
+def golden_train_forward(ref, size, batch, wseed=0):
+    """The reference's training-mode forward without denoising (targets=None) on the golden
+    images, BatchNorm layers in eval mode (frozen BN: the path detrpose_amd builds).
+
+    The reference itself cannot finish this call: without DN, Transformer.forward raises
+    UnboundLocalError at transformer.py:1353 (`out_refs` is only bound on the DN branch,
+    1339). Everything it computes before that line is captured by hooks: the decoder's
+    return value (per-layer poses / logits / corners / references, pre poses / scores,
+    transformer.py:1293-1316), its refpoints_sigmoid input (= enc_outputs_pose_coord) and the
+    two-stage class scores gathered at the top-k (interm_class, 1248-1250). The dict that
+    1348-1385 would assemble from them is rebuilt here the same way."""
+    from detrpose_amd.synthetic import load_synthetic, synthetic_images
+    torch.manual_seed(0)
+    model, _ = make_golden.build_reference(ref, size)
+    load_synthetic(model, seed=wseed)
+    model.train()
+    for m in model.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.eval()
+    images = synthetic_images(batch, seed=1)
+    tr = model.transformer
+    cap = {}
+    h1 = tr.decoder.register_forward_hook(lambda mod, a, out: cap.__setitem__("dec", out))
+    h2 = tr.decoder.register_forward_pre_hook(
+        lambda mod, a, kw: cap.__setitem__("ref0", kw["refpoints_sigmoid"].clone()), with_kwargs=True)
+    h3 = tr.enc_out_class_embed.register_forward_hook(lambda mod, a, out: cap.__setitem__("cls", out))
+    err = None
+    try:
+        with torch.no_grad():
+            model(images)
+    except UnboundLocalError as e:
+        err = str(e)
+    finally:
+        h1.remove(), h2.remove(), h3.remove()
+    assert err is not None and "out_refs" in err, "the reference's non-DN training forward was expected to fail"
+    poses, logits, corners, refs, pre_poses, pre_scores = cap["dec"]
+    topk = torch.topk(cap["cls"].max(-1)[0], tr.num_queries, dim=1)[1]
+    interm_cls = torch.gather(cap["cls"], 1, topk.unsqueeze(-1).repeat(1, 1, cap["cls"].shape[-1]))
+    st = {"meta": np.array([batch, wseed, 1], np.int64)}
+    nl = poses.shape[0]
+    for l in range(nl):
+        name = "out" if l == nl - 1 else f"aux{l}"
+        st[f"{name}.pred_logits"] = logits[l].numpy()
+        st[f"{name}.pred_keypoints"] = poses[l].flatten(-2).numpy()
+        st[f"{name}.pred_corners"] = corners[l].numpy()
+        st[f"{name}.ref_points"] = refs[l].numpy()
+    st["pre.pred_logits"] = pre_scores.numpy()
+    st["pre.pred_keypoints"] = pre_poses.numpy()
+    st["interm.pred_logits"] = interm_cls.numpy()
+    st["interm.pred_keypoints"] = cap["ref0"][:, :, 1:].flatten(-2).numpy()
+    print(f"  [{size}] train forward b{batch}: {nl} layers (reference stopped at: {err})")
+    return st
+
+
 def main():
     torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
     Criterion, HungarianMatcher = _import_criterion()
+    ref = make_golden._import_reference()
+    st = golden_train_forward(ref, "n", 2)
+    np.savez_compressed(os.path.join(HERE, "train_forward_n_b2.npz"), **st)
+    print("wrote train_forward_n_b2.npz")
     for name, (B, Q, ncls, K, n_aux, sizes, seed) in CASES.items():
         st = make_case(Criterion, HungarianMatcher, B, Q, ncls, K, n_aux, sizes, seed)
         np.savez_compressed(os.path.join(HERE, f"criterion_{name}.npz"), **st)

@@ -1,0 +1,98 @@
+"""Training-mode forward (no denoising, frozen BN) and the criterion on its outputs.
+
+The reference's own non-DN training forward stops with UnboundLocalError at
+transformer.py:1353; tests/golden/make_train_golden.py captures every value it computes
+before that line (decoder return, two-stage tensors) from the reference on the N golden
+images (b2), BatchNorm in eval mode: tests/golden/train_forward_n_b2.npz. The HIP path in
+fp32 parity mode must match every output of every layer within the north-star gate
+(1e-3 abs on logits / keypoints; pred_corners, distribution logits of scale ~10, within
+1e-3 of their scale). In bf16 the training plan's final outputs must equal the inference
+plan's bit for bit (same kernels), and the criterion must consume the dict as the
+reference's would.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from detrpose_amd import build_model
+from detrpose_amd.synthetic import synthetic_images, synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(golden_dir, size, seed, dtype):
+    with open(os.path.join(golden_dir, "manifest.json")) as f:
+        man = json.load(f)
+    model, _ = build_model(size, dtype=dtype)
+    model.load_state_dict(synthetic_state_dict(man[size], seed=seed), strict=False)
+    return model
+
+
+def _frozen_bn_train(model):
+    model.train()
+    for m in model.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.eval()
+    return model
+
+
+def test_train_forward_matches_reference(golden_dir):
+    g = np.load(os.path.join(golden_dir, "train_forward_n_b2.npz"))
+    batch, wseed, iseed = (int(v) for v in g["meta"])
+    model = _frozen_bn_train(_model(golden_dir, "n", wseed, "fp32"))
+    out = model(synthetic_images(batch, seed=iseed).cuda())
+    torch.cuda.synchronize()
+    heads = {"out": out, "pre": out["aux_pre_outputs"], "interm": out["aux_interm_outputs"][0]}
+    heads.update({f"aux{i}": a for i, a in enumerate(out["aux_outputs"])})
+    n = 0
+    for key in g.files:
+        if key == "meta":
+            continue
+        name, field = key.split(".")
+        got = heads[name][field].float().cpu().numpy()
+        ref = g[key]
+        assert got.shape == ref.shape, (key, got.shape, ref.shape)
+        tol = 1e-3 * max(1.0, float(np.abs(ref).max())) if field == "pred_corners" else 1e-3
+        np.testing.assert_allclose(got, ref, atol=tol, rtol=0, err_msg=key)
+        n += 1
+    assert n == 4 * len(out["aux_outputs"]) + 4 + 2 + 2
+    assert out["aux_outputs"][0]["teacher_corners"] is out["pred_corners"]
+    assert float(out["reg_scale"]) == 4.0 and out["reg_max"] == 32
+
+
+def test_train_forward_refusals(golden_dir):
+    model = _model(golden_dir, "n", 0, "fp32")
+    img = synthetic_images(1, seed=1).cuda()
+    model.train()   # encoder BatchNorm in train mode: batch statistics are not built
+    with pytest.raises(NotImplementedError):
+        model(img)
+    _frozen_bn_train(model)
+    with pytest.raises(NotImplementedError):   # targets -> denoising queries
+        model(img, [{"labels": torch.zeros(1, dtype=torch.int64), "keypoints": torch.rand(1, 51)}])
+
+
+def test_train_forward_bf16_and_criterion(golden_dir):
+    from detrpose_amd.criterion import Criterion, HungarianMatcher
+    batch = 4
+    model = _model(golden_dir, "l", 0, "bf16")
+    img = synthetic_images(batch, seed=1).cuda()
+    ev = model.eval()(img)
+    out = _frozen_bn_train(model)(img)
+    assert torch.equal(out["pred_logits"], ev["pred_logits"])
+    assert torch.equal(out["pred_keypoints"], ev["pred_keypoints"])
+    assert len(out["aux_outputs"]) == 5
+    gen = torch.Generator().manual_seed(3)
+    targets = []
+    for n in (3, 0, 5, 1):
+        kp = torch.cat([torch.rand(n, 34, generator=gen), (torch.rand(n, 17, generator=gen) > 0.3).float()], 1)
+        targets.append({"labels": torch.zeros(n, dtype=torch.int64).cuda(), "keypoints": kp.cuda(),
+                        "area": (torch.rand(n, generator=gen) * 0.2 + 0.01).cuda()})
+    crit = Criterion(2, HungarianMatcher(2.0, 0.25, 10.0, 4.0), {"loss_vfl": 2.0, "loss_keypoints": 10.0,
+                                                                 "loss_oks": 4.0}, ["vfl", "keypoints"], 17)
+    losses = crit(out, targets)
+    assert len(losses) == 3 * (1 + 5 + 1 + 1)
+    vals = torch.stack(list(losses.values()))
+    assert torch.isfinite(vals).all() and (vals >= 0).all()
