@@ -505,6 +505,16 @@ int dp_conv2d_stream(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   if (d.cout <= 64) return f32o ? launch<128, 64, 4, float>(d, s, vec_ok) : launch<128, 64, 4, bf16_t>(d, s, vec_ok);
   if (M <= 8192) return f32o ? launch<64, 128, 2, float>(d, s, vec_ok) : launch<64, 128, 2, bf16_t>(d, s, vec_ok);
   if (f32o) return launch<128, 128, 2, float>(d, s, vec_ok);
+  static const int forced = [] {   // A/B experiments only (scripts/conv_bench.py)
+    const char* e = getenv("DETRPOSE_CONV_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced && M >= 32768) {
+    if (forced == 1) return launch<256, 256, 2, bf16_t, 8>(d, s, vec_ok);
+    if (forced == 2) return launch<192, 256, 2, bf16_t, 8>(d, s, vec_ok);
+    if (forced == 3) return launch<256, 128, 4, bf16_t, 8>(d, s, vec_ok);
+    if (forced == 4) return launch<128, 128, 2, bf16_t>(d, s, vec_ok);
+  }
   // large GEMMs: 256-row tiles with 8 waves halve the LDS-DMA bytes per MFMA flop
   if (DP_BIG_TILES && M >= 32768 && d.kpad >= 256) {
     if (d.cout > 128) {

@@ -105,6 +105,53 @@ def test_conv2d(dt, k, s, cin, cout, H, act):
     _close(out[..., :cout], ref.permute(0, 2, 3, 1) + resid[..., :cout], dt, f"conv k{k}s{s} {cin}->{cout}")
 
 
+@pytest.mark.parametrize("cin,cout,H,W,ld,off,mode,act", [
+    (336, 64, 64, 67, 400, 32, "plain", "relu"),    # K tail (kpad 384), input = concat slice
+    (512, 256, 48, 47, 512, 0, "up", "silu"),       # nearest-x2 epilogue
+    (256, 256, 70, 71, 256, 0, "f32", None),        # f32 output (linear heads)
+    (576, 192, 40, 43, 640, 64, "res", "gelu"),     # N tail, residual
+    (64, 48, 130, 129, 64, 0, "plain", "relu")])    # narrow cout (48 of a 64 tile)
+def test_conv2d_1x1_large_m(cin, cout, H, W, ld, off, mode, act):
+    """1x1 convs at M >= 16K (the persistent conv_stream tiles) with every epilogue mode
+    (plain, nearest-x2 copy, f32 output, residual), K / M / cout tails and input rows that are
+    a channel slice of a wider concat buffer, vs torch fp32 on the same bf16-rounded operands."""
+    torch.manual_seed(cin + cout + H)
+    B = 2
+    pk = Packer({}, "bf16", torch.device("cuda"))
+    x = torch.randn(B, cin, H, W).bfloat16().float()
+    w = torch.randn(cout, cin, 1, 1) / cin ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pk.conv(w.double(), b.double(), act=act)
+    ref = {"relu": F.relu, "silu": F.silu, "gelu": F.gelu, None: lambda t: t}[act](F.conv2d(x, w, b))
+    wide = torch.zeros(B, H, W, ld, device="cuda", dtype=torch.bfloat16)
+    wide[..., off:off + cin] = x.permute(0, 2, 3, 1).to("cuda", torch.bfloat16)
+    _KEEP.append(wide)
+    odt = torch.float32 if mode == "f32" else torch.bfloat16
+    out = torch.empty(B, H, W, cout, device="cuda", dtype=odt)
+    d = ConvDesc()
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = wide.data_ptr() + 2 * off, H * W * ld, ld, H, W, cin
+    d.weight, d.kpad, d.bias = pc.w.data_ptr(), pc.kpad, pc.b.data_ptr()
+    d.kh, d.kw, d.stride = 1, 1, 1
+    d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out.data_ptr(), H * W * cout, cout, H, W, cout
+    d.batch, d.act, d.dtype = B, pc.act, _lib.DP_BF16
+    d.out_f32 = 1 if mode == "f32" else 0
+    want = ref.permute(0, 2, 3, 1)
+    if mode == "res":
+        r = torch.randn(B, H, W, cout).bfloat16()
+        rd = r.to("cuda")
+        _KEEP.append(rd)
+        d.res, d.res_bstride, d.res_pstride = rd.data_ptr(), H * W * cout, cout
+        want = want + r.float()
+    if mode == "up":
+        up = torch.empty(B, 2 * H, 2 * W, cout, device="cuda", dtype=torch.bfloat16)
+        d.up, d.up_bstride, d.up_pstride = up.data_ptr(), 4 * H * W * cout, cout
+    _lib.check(_lib.load().dp_conv2d(C.byref(d), _s()), "conv 1x1")
+    torch.cuda.synchronize()
+    _close(out, want, "bf16", f"1x1 {cin}->{cout} {mode}")
+    if mode == "up":
+        _close(up, F.interpolate(ref, scale_factor=2.0, mode="nearest").permute(0, 2, 3, 1), "bf16", "1x1 up")
+
+
 @pytest.mark.parametrize("H,W,act", [(50, 53, "relu"), (160, 160, "silu"), (17, 9, None)])
 def test_conv2d_halo_48(H, W, act):
     """The 48-wide natural-order halo tile (HG stage-0 3x3 48->48 convs, no residual) writing a
