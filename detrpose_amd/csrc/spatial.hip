@@ -166,16 +166,179 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ in, 
 }
 
 
-// Depthwise k x k, bf16, LDS-tiled (production path for channels % 64 == 0): a block owns
-// a TH x TW tile of output pixels x 64 channels. The ((TH-1)S+KS) x ((TW-1)S+KS) input
-// patch is read ONCE with whole 128-byte pixel lines (8 lanes per pixel) into LDS (zeros
-// outside the map = the conv padding), then each thread computes PX consecutive outputs of
-// one 16-byte channel chunk from LDS with a register sliding window per kernel row. Block
-// order is XCD-sliced (logical = (blockIdx % 8) * (G / 8) + blockIdx / 8, channel chunk
-// fastest), so the tiles that share a halo row run on one XCD and re-read it from its L2,
-// not from HBM (the per-thread kernel above re-fetched each input row from up to KS XCDs).
-template <int KS, int S, int TH, int TW, int PX, int ACT>
+// Depthwise k x k, bf16, LDS-tiled (production path for channels % 64 == 0): a tile is TH x
+// TW output pixels x 64 channels. The ((TH-1)S+KS) x ((TW-1)S+KS) input patch is read ONCE
+// with whole 128-byte pixel lines (8 lanes per pixel) into LDS by LDS-DMA (zeros outside the
+// map = the conv padding), then each thread computes PX consecutive outputs of one 16-byte
+// channel chunk from LDS with a register sliding window per kernel row.
+// Persistent blocks, double-buffered patches: a block keeps ONE 64-channel chunk (its tap
+// weights and biases stay in LDS / registers) and walks that chunk's tiles; the next tile's
+// patch is DMA'd while the current one computes, so the patch latency (the whole cost of a
+// one-tile block on the 40x40 5x5 convs) overlaps the FMAs. Block order is XCD-sliced
+// (logical = (blockIdx % 8) * (G / 8) + blockIdx / 8): the tiles sharing halo rows run on one
+// XCD at about the same time and re-read the halo from its L2.
+template <int KS, int S, int TH, int TW, int PX, bool PERSIST, int ACT>
 __global__ __launch_bounds__(256) void dwconv_lds_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int nchk,
+                                                         int ntiles) {
+  constexpr int PH = (TH - 1) * S + KS, PW = (TW - 1) * S + KS;
+  constexpr int NIN = (PX - 1) * S + KS;
+  constexpr int GX = TW / PX;
+  constexpr int PBYTES = (PH * PW * 128 + 1023) / 1024 * 1024;   // DMA groups are whole 1 KB
+  // (a one-tile-per-block launch allocates one buffer: the prefetch below never fires there)
+  static_assert(TW % PX == 0, "tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];     // [2][patch] + weights
+  const int G = gridDim.x;                                        // multiple of 8 * nchk
+  const int L = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int ck = L % nchk;
+  const int spatial = ntiles / nchk;                              // tiles of this chunk
+  const int first = L / nchk, step = G / nchk;
+  if (first >= spatial) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  float* wl = reinterpret_cast<float*>(smem + (PERSIST ? 2 : 1) * PBYTES);
+
+  auto issue_patch = [&](int t, char* patch) {
+    int rest = t;
+    const int tx = rest % tiles_x;
+    rest /= tiles_x;
+    const int ty = rest % tiles_y, b = rest / tiles_y;
+    const int iy0 = ty * TH * S - d.pad_t, ix0 = tx * TW * S - d.pad_l;
+    const dpconv::i32x4 rs =
+        dpconv::make_rsrc(reinterpret_cast<const bf16_t*>(d.in) + (int64_t)b * d.in_bstride + ck * 64);
+    constexpr int NE = PH * PW * 8;
+    for (int e0 = wave * 64; e0 < NE; e0 += 256) {
+      const int e = e0 + lane;
+      const int px = e >> 3, c = e & 7;
+      const int py = px / PW, pxx = px - py * PW;
+      const int iy = iy0 + py, ix = ix0 + pxx;
+      const bool ok = e < NE && (unsigned)iy < (unsigned)d.in_h && (unsigned)ix < (unsigned)d.in_w;
+      const int o = ok ? ((iy * d.in_w + ix) * d.in_pstride + c * 8) * 2 : dpconv::OOB;
+      dpconv::dma16(rs, patch + e0 * 16, o);
+    }
+  };
+
+  issue_patch(first, smem);
+  // the chunk's 64 channels of the KS*KS tap weights (f32), and this thread's 8 biases
+  for (int e = tid; e < KS * KS * 16; e += 256) {
+    const int tap = e >> 4, q = e & 15;
+    *reinterpret_cast<f32x4*>(wl + tap * 64 + 4 * q) =
+        *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(d.weight) + tap * d.cin + ck * 64 + 4 * q);
+  }
+  const int c = tid & 7, c0 = c * 8;   // items it = tid + 256 k all have chunk tid & 7
+  float bias[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) bias[t] = d.bias ? d.bias[ck * 64 + c0 + t] : 0.f;
+  dpconv::wait_vmcnt<0>();
+  __syncthreads();
+
+  int u = 0;
+  for (int t = first; t < spatial; t += step, ++u) {
+    // next tile's patch into the other buffer (its previous readers passed the barrier below)
+    if (PERSIST && t + step < spatial) issue_patch(t + step, smem + ((u + 1) & 1) * PBYTES);
+    const char* patch = smem + (PERSIST ? (u & 1) * PBYTES : 0);
+    int rest = t;
+    const int tx = rest % tiles_x;
+    rest /= tiles_x;
+    const int ty = rest % tiles_y, b = rest / tiles_y;
+    const int oy0 = ty * TH, ox0 = tx * TW;
+    for (int it = tid; it < TH * GX * 8; it += 256) {
+      const int pg = it >> 3;
+      const int row = pg / GX, xg = pg - row * GX;
+      const int oy = oy0 + row, oxb = ox0 + xg * PX;
+      if (oy >= d.out_h || oxb >= d.out_w) continue;
+      float acc[PX][8];
+#pragma unroll
+      for (int tt = 0; tt < 8; ++tt)
+#pragma unroll
+        for (int p = 0; p < PX; ++p) acc[p][tt] = bias[tt];
+      // kernel rows double-buffered in registers: row ky+1's LDS reads are in flight while
+      // row ky's FMAs run (a fully unrolled 5x5 needs more than 256 VGPRs)
+      auto load_row = [&](int ky, bf16x8 (&x)[NIN]) __attribute__((always_inline)) {
+        const char* prow = patch + ((row * S + ky) * PW + xg * PX * S) * 128 + c * 16;
+#pragma unroll
+        for (int j = 0; j < NIN; ++j) x[j] = *reinterpret_cast<const bf16x8*>(prow + j * 128);
+      };
+      auto fma_row = [&](int ky, const bf16x8 (&x)[NIN]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) {
+          const float* wk = wl + (ky * KS + kx) * 64 + c0;
+          const f32x4 w0 = *reinterpret_cast<const f32x4*>(wk), w1 = *reinterpret_cast<const f32x4*>(wk + 4);
+          const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+          for (int p = 0; p < PX; ++p)
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) acc[p][tt] = fmaf((float)x[p * S + kx][tt], wv[tt], acc[p][tt]);
+        }
+      };
+      bf16x8 xa[NIN], xb[NIN];
+      load_row(0, xa);
+#pragma unroll 1
+      for (int ky = 0; ky < KS; ky += 2) {
+        if (ky + 1 < KS) load_row(ky + 1, xb);
+        fma_row(ky, xa);
+        if (ky + 1 < KS) {
+          if (ky + 2 < KS) load_row(ky + 2, xa);
+          fma_row(ky + 1, xb);
+        }
+      }
+      bf16_t* out = reinterpret_cast<bf16_t*>(d.out) + (int64_t)b * d.out_bstride + ck * 64 + c0;
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        const int ox = oxb + p;
+        if (ox >= d.out_w) break;
+        bf16x8 o;
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+          float v = dpconv::act_t<ACT>(acc[p][tt]);
+          if (d.has_lab) v = d.lab_scale * v + d.lab_bias;
+          o[tt] = (bf16_t)v;
+        }
+        *reinterpret_cast<bf16x8*>(out + ((int64_t)oy * d.out_w + ox) * d.out_pstride) = o;
+      }
+    }
+    // the next patch has landed (and this tile's stores are out); every wave is done with
+    // this buffer before the following iteration DMAs into it
+    dpconv::wait_vmcnt<0>();
+    __syncthreads();
+  }
+}
+
+// PERSIST: persistent blocks with double-buffered patches (the compute-heavy 5x5 / 3x3 s1
+// convs); otherwise one tile per block and a single patch buffer, i.e. twice as many
+// resident blocks (the HBM-bound stride-2 downsamples want the bytes in flight)
+template <int KS, int S, int TH, int TW, int PX, bool PERSIST>
+int launch_dw_lds(const dp_conv_desc& d, hipStream_t s) {
+  constexpr int PH = (TH - 1) * S + KS, PW = (TW - 1) * S + KS;
+  constexpr int lds = (PERSIST ? 2 : 1) * ((PH * PW * 128 + 1023) / 1024 * 1024) + KS * KS * 64 * 4;
+  static_assert(lds <= 160 * 1024, "patch");
+  const int tiles_x = (d.out_w + TW - 1) / TW, tiles_y = (d.out_h + TH - 1) / TH, nchk = d.cin / 64;
+  const int64_t ntiles = (int64_t)d.batch * tiles_y * tiles_x * nchk;
+  DP_REQUIRE(ntiles < (1ll << 30), "dp_dwconv2d: too many tiles");
+  // whole groups of 8 * nchk blocks (one channel chunk per block); persistent: about the LDS
+  // occupancy per CU, never more blocks than tiles
+  const int per_cu = (160 * 1024) / lds;
+  const int unit = 8 * nchk;
+  const int64_t need = (ntiles + unit - 1) / unit * unit;
+  int64_t grid = PERSIST ? (int64_t)per_cu * dpconv::num_cus() / unit * unit : need;
+  if (grid > need) grid = need;
+  if (grid < unit) grid = unit;
+#define DP_DWL(A_)                                                                                          \
+  hipLaunchKernelGGL((dwconv_lds_kernel<KS, S, TH, TW, PX, PERSIST, A_>), dim3((unsigned)grid), dim3(256), lds, s, d, \
+                     tiles_x, tiles_y, nchk, (int)ntiles)
+  switch (d.act) {
+    case DP_ACT_RELU: DP_DWL(DP_ACT_RELU); break;
+    case DP_ACT_SILU: DP_DWL(DP_ACT_SILU); break;
+    case DP_ACT_GELU: DP_DWL(DP_ACT_GELU); break;
+    default: DP_DWL(DP_ACT_NONE); break;
+  }
+#undef DP_DWL
+  return dp_check_launch("dp_dwconv2d(lds)");
+}
+
+// One tile per block (the original form): the HBM-bound stride-2 downsamples, where many
+// small resident blocks keep more bytes in flight than persistent double-buffered ones
+// (A/B: s2.down 0.133 ms one-tile vs 0.148-0.170 persistent).
+template <int KS, int S, int TH, int TW, int PX, int ACT>
+__global__ __launch_bounds__(256) void dwconv_tile_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int nchk,
                                                          int ntiles) {
   constexpr int PH = (TH - 1) * S + KS, PW = (TW - 1) * S + KS;
   constexpr int NIN = (PX - 1) * S + KS;
@@ -271,7 +434,7 @@ __global__ __launch_bounds__(256) void dwconv_lds_kernel(dp_conv_desc d, int til
 }
 
 template <int KS, int S, int TH, int TW, int PX>
-int launch_dw_lds(const dp_conv_desc& d, hipStream_t s) {
+int launch_dw_tile(const dp_conv_desc& d, hipStream_t s) {
   constexpr int PH = (TH - 1) * S + KS, PW = (TW - 1) * S + KS;
   constexpr int lds = (PH * PW * 128 + 1023) / 1024 * 1024 + KS * KS * 64 * 4;   // DMA groups are whole 1 KB
   static_assert(lds <= 64 * 1024, "patch");
@@ -280,7 +443,7 @@ int launch_dw_lds(const dp_conv_desc& d, hipStream_t s) {
   DP_REQUIRE(ntiles < (1ll << 30), "dp_dwconv2d: too many tiles");
   const int grid = (int)((ntiles + 7) / 8 * 8);
 #define DP_DWL(A_)                                                                                          \
-  hipLaunchKernelGGL((dwconv_lds_kernel<KS, S, TH, TW, PX, A_>), dim3(grid), dim3(256), lds, s, d, tiles_x, \
+  hipLaunchKernelGGL((dwconv_tile_kernel<KS, S, TH, TW, PX, A_>), dim3(grid), dim3(256), lds, s, d, tiles_x, \
                      tiles_y, nchk, (int)ntiles)
   switch (d.act) {
     case DP_ACT_RELU: DP_DWL(DP_ACT_RELU); break;
@@ -315,9 +478,9 @@ extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
   hipStream_t s = as_stream(stream);
   static const bool no_lds = getenv("DETRPOSE_DW_NO_LDS") != nullptr;
   if (d.dtype == DP_BF16 && d.cin % 64 == 0 && !no_lds) {
-    if (d.kh == 5 && d.kw == 5 && d.stride == 1) return launch_dw_lds<5, 1, DP_DW5_TH, 20, 5>(d, s);
-    if (d.kh == 3 && d.kw == 3 && d.stride == 1) return launch_dw_lds<3, 1, 8, 20, 5>(d, s);
-    if (d.kh == 3 && d.kw == 3 && d.stride == 2) return launch_dw_lds<3, 2, DP_DWS2_TH, 16, 2>(d, s);
+    if (d.kh == 5 && d.kw == 5 && d.stride == 1) return launch_dw_lds<5, 1, DP_DW5_TH, 20, 5, true>(d, s);
+    if (d.kh == 3 && d.kw == 3 && d.stride == 1) return launch_dw_lds<3, 1, 8, 20, 5, true>(d, s);
+    if (d.kh == 3 && d.kw == 3 && d.stride == 2) return launch_dw_tile<3, 2, DP_DWS2_TH, 16, 2>(d, s);
   }
   const int nchunk = d.cin / VEC;
   constexpr int PX = 4;
