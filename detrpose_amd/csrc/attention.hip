@@ -430,6 +430,208 @@ __global__ __launch_bounds__(256) void attn_short_kernel(const bf16_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------
+// bf16 long-sequence path (AIFI's 400 tokens): attn_short_kernel's register scheme with an
+// online softmax over 64-key blocks. One wave = one (sequence, head, 64-query block).
+//  * S^T = K Q^T per key block (K rows as the A operand straight from the projection rows),
+//    so the lane holds S^T[key 16j+4lg+r][query 16i+lr]: the running max / sum of query
+//    column (i, lr) reduce over its registers and 2 xor-shuffles (16, 32); no LDS for P.
+//  * O^T += V^T P^T: P (bf16) from registers is the B operand; V^T fragments come from the
+//    block's V rows staged row-major in the wave's LDS slice with 16-byte stores and read
+//    back transposed by ds_read_b64_tr_b16 (the previous kernel transposed V with 2-byte
+//    scalar LDS stores: 24 % of its LDS cycles were bank conflicts).
+//  * The 64-query block's O^T accumulators are rescaled by exp(m_old - m_new) per block.
+template <int DH>
+__global__ __launch_bounds__(256) void attn_long_kernel(const bf16_t* __restrict__ q, int ld_q,
+                                                        const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                        int ld_kv, bf16_t* __restrict__ out, int ld_o, int n_inner,
+                                                        int64_t so, int64_t si, int64_t st, int seqlen, int nhead,
+                                                        int npairs, int nqb, float scale) {
+  constexpr int KT = 4;                          // 16-row tiles per 64 queries / 64 keys
+  constexpr int KS = (DH + 31) / 32;
+  constexpr int ND = DH / 16;
+  constexpr int DHP = DH == 16 ? 16 : 48;        // V row pitch (elements): conflict-free tr reads
+  constexpr int VCH = DH / 8;
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) bf16_t vl[4][64 * DHP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int item = blockIdx.x * 4 + wave;
+  if (item >= npairs * nqb) return;              // wave-uniform: EXEC stays full below
+  const int pair = item / nqb, qb = item - pair * nqb;
+  const int h = pair % nhead, sq = pair / nhead;
+  const int o = sq / n_inner, ii = sq - o * n_inner;
+  const int64_t base = (int64_t)o * so + (int64_t)ii * si;
+  const int lr = lane & 15, lg = lane >> 4;
+  bf16_t* V = vl[wave];
+
+  bf16x8 qf[KT][KS];   // B operand: query columns
+#pragma unroll
+  for (int i = 0; i < KT; ++i)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int row = qb * 64 + 16 * i + lr, d0 = 32 * ks + 8 * lg;
+      qf[i][ks] = (row < seqlen && d0 < DH)
+                      ? *reinterpret_cast<const bf16x8*>(q + (base + (int64_t)row * st) * ld_q + h * DH + d0)
+                      : bf16x8{};
+    }
+  f32x4 oacc[ND][KT];
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int i = 0; i < KT; ++i) oacc[d][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrow[KT], lrow[KT];
+#pragma unroll
+  for (int i = 0; i < KT; ++i) mrow[i] = -INFINITY, lrow[i] = 0.f;
+  const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int nkb = (seqlen + 63) / 64;
+  constexpr int VT = (64 * VCH + 63) / 64;       // V chunks per lane per key block
+  // K fragments and V chunks of one key block
+  struct Blk {
+    bf16x8 kf[KT][KS];
+    bf16x8 vv[VT];
+  };
+  auto load_blk = [&](int kb, Blk& bk) __attribute__((always_inline)) {
+    const int k0 = kb * 64;
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+      const int row = k0 + 16 * j + lr;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int d0 = 32 * ks + 8 * lg;
+        bk.kf[j][ks] = (row < seqlen && d0 < DH)
+                           ? *reinterpret_cast<const bf16x8*>(k + (base + (int64_t)row * st) * ld_kv + h * DH + d0)
+                           : bf16x8{};
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < VT; ++t) {
+      const int c = lane + 64 * t;
+      const int key = c / VCH, dc = c - key * VCH;
+      bk.vv[t] = (c < 64 * VCH && k0 + key < seqlen)
+                     ? *reinterpret_cast<const bf16x8*>(v + (base + (int64_t)(k0 + key) * st) * ld_kv + h * DH + dc * 8)
+                     : bf16x8{};
+    }
+  };
+  auto run_blk = [&](int kb, const Blk& bk) __attribute__((always_inline)) {
+    const int k0 = kb * 64;
+    // V rows -> LDS (the previous block's tr reads are done: wave barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+    for (int t = 0; t < VT; ++t) {
+      const int c = lane + 64 * t;
+      const int key = c / VCH, dc = c - key * VCH;
+      if (c < 64 * VCH) *reinterpret_cast<bf16x8*>(V + key * DHP + dc * 8) = bk.vv[t];
+    }
+    f32x4 sv[KT][KT];   // S^T: [j key tile][i query tile]
+#pragma unroll
+    for (int j = 0; j < KT; ++j)
+#pragma unroll
+      for (int i = 0; i < KT; ++i) {
+        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bk.kf[j][ks], qf[i][ks], a, 0, 0, 0);
+        sv[j][i] = a;
+      }
+    // online softmax per query column
+#pragma unroll
+    for (int i = 0; i < KT; ++i) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < KT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * j + 4 * lg + r;
+          const float x = key < seqlen ? sv[j][i][r] * scale : -INFINITY;
+          sv[j][i][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(mrow[i], mx);
+      const float corr = __expf(mrow[i] - mn);
+      mrow[i] = mn;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < KT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __expf(sv[j][i][r] - mn);
+          sv[j][i][r] = pv;
+          sum += pv;
+        }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      lrow[i] = lrow[i] * corr + sum;
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) oacc[d][i][r] *= corr;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // O^T += V^T P^T over the block's two 32-key steps
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      bf16x8 pf[KT];
+#pragma unroll
+      for (int i = 0; i < KT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pf[i][r] = (bf16_t)sv[2 * m][i][r];
+          pf[i][4 + r] = (bf16_t)sv[2 * m + 1][i][r];
+        }
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const bf16_t* a0 = V + (32 * m + 4 * lg + q4) * DHP + 16 * d + 4 * p4;
+        const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0));
+        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0 + 16 * DHP));
+        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(tmp);
+#pragma unroll
+        for (int i = 0; i < KT; ++i) oacc[d][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[i], oacc[d][i], 0, 0, 0);
+      }
+    }
+  };
+  // one key block at a time: prefetching the next block's K/V into registers (two Blk
+  // buffers, kb loop unrolled by two) pushed the kernel to 255 VGPRs and measured slower
+  // (74 -> 82 us at L b64); the 3-4 waves per SIMD hide the load latency instead
+  Blk bk;
+  for (int kb = 0; kb < nkb; ++kb) {
+    load_blk(kb, bk);
+    run_blk(kb, bk);
+  }
+  // store: query 16i+lr of the block, channels 16d + 4lg .. +3 (8 bytes)
+#pragma unroll
+  for (int i = 0; i < KT; ++i) {
+    const int qi = qb * 64 + 16 * i + lr;
+    if (qi >= seqlen) continue;
+    const float inv = 1.f / lrow[i];
+    bf16_t* op = out + (base + (int64_t)qi * st) * ld_o + h * DH;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16_t)(oacc[d][i][r] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * d + 4 * lg) = w;
+    }
+  }
+}
+
+template <int DH>
+int launch_long(const void* q, int ld_q, const void* k, const void* v, int ld_kv, void* out, int ld_o, int n_outer,
+                int n_inner, int64_t so, int64_t si, int64_t st, int seqlen, int nhead, hipStream_t s) {
+  const int npairs = n_outer * n_inner * nhead;
+  const int nqb = (seqlen + 63) / 64;
+  const int64_t items = (int64_t)npairs * nqb;
+  hipLaunchKernelGGL((attn_long_kernel<DH>), dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, (const bf16_t*)q,
+                     ld_q, (const bf16_t*)k, (const bf16_t*)v, ld_kv, (bf16_t*)out, ld_o, n_inner, so, si, st, seqlen,
+                     nhead, npairs, nqb, 1.f / sqrtf((float)DH));
+  return dp_check_launch("dp_attention(long)");
+}
+
 template <int DH, int KT>
 int launch_short(const void* q, int ld_q, const void* k, const void* v, int ld_kv, void* out, int ld_o, int n_outer,
                  int n_inner, int64_t so, int64_t si, int64_t st, int seqlen, int nhead, hipStream_t s) {
@@ -479,6 +681,12 @@ extern "C" int dp_attention(const void* q, int32_t ld_q, const void* k, const vo
     if (dh == 16) return launch_short_any<16>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
     if (dh == 32) return launch_short_any<32>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
     if (dh == 48) return launch_short_any<48>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+  }
+  static const bool no_long = getenv("DETRPOSE_ATTN_NO_LONG") != nullptr;   // A/B: the LDS-P kernel
+  if (dtype == DP_BF16 && al && al8 && !no_long) {
+    if (dh == 16) return launch_long<16>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+    if (dh == 32) return launch_long<32>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
+    if (dh == 48) return launch_long<48>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);
   }
   if (dtype == DP_BF16 && al) {
     if (dh == 16) return launch_mfma<16>(q, ld_q, k, v, ld_kv, out, ld_o, n_outer, n_inner, so, si, st, seqlen, nhead, s);

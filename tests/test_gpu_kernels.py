@@ -420,14 +420,18 @@ def _attn_ref(q, k, v, nh):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("geom", ["within", "across", "aifi", "aifi_x", "within_n", "across_n", "within_x", "across_x"])
+@pytest.mark.parametrize("geom", ["within", "across", "aifi", "aifi_x", "aifi_n", "aifi_ragged", "within_n",
+                                  "across_n", "within_x", "across_x"])
 def test_attention(dt, geom):
+    """Decoder within / across attention (short kernel) and AIFI (long kernel, online softmax
+    over 64-key blocks; a ragged 250-token sequence exercises the masked tail block)."""
     lib = _lib.load()
     torch.manual_seed(len(geom))
     B, nq, T = 2, 60, 18
-    Cc = {"aifi_x": 384, "within_n": 128, "across_n": 128, "within_x": 384, "across_x": 384}.get(geom, 256)
+    Cc = {"aifi_x": 384, "aifi_n": 128, "within_n": 128, "across_n": 128, "within_x": 384, "across_x": 384}.get(geom, 256)
     nh = 8
-    rows = B * 400 if geom.startswith("aifi") else B * nq * T
+    S = 250 if geom == "aifi_ragged" else 400
+    rows = B * S if geom.startswith("aifi") else B * nq * T
     qkv = torch.randn(rows, 3 * Cc)
     td = DTYPES[dt][0]
     qd = qkv.to("cuda", td)
@@ -441,8 +445,8 @@ def test_attention(dt, geom):
         args = (B, T, nq * T, 1, T, nq)
         seqs = q32.reshape(B, nq, T, 3 * Cc).transpose(1, 2).reshape(B * T, nq, 3 * Cc)
     else:
-        args = (B, 1, 400, 0, 1, 400)
-        seqs = q32.reshape(B, 400, 3 * Cc)
+        args = (B, 1, S, 0, 1, S)
+        seqs = q32.reshape(B, S, 3 * Cc)
     _lib.check(lib.dp_attention(qd.data_ptr(), 3 * Cc, qd.data_ptr() + Cc * e, qd.data_ptr() + 2 * Cc * e, 3 * Cc,
                                 out.data_ptr(), Cc, *args, nh, Cc // nh, DTYPES[dt][1], _s()))
     ref = _attn_ref(seqs[..., :Cc], seqs[..., Cc:2 * Cc], seqs[..., 2 * Cc:], nh)
