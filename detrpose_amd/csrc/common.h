@@ -59,16 +59,21 @@ __device__ __forceinline__ void store16(T* p, const Vec16<T>& r) {
 }
 
 // ---------------------------------------------------------------- activations
+// sigmoid / SiLU through v_exp_f32 + v_rcp_f32 (1 ulp): a plain `/` compiles to the IEEE
+// division sequence (div_scale x2, div_fmas, div_fixup + Newton steps), which made SiLU the
+// most expensive part of the conv epilogues
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float silu_f(float x) { return x * sigmoidf_(x); }
+
 __device__ __forceinline__ float apply_act(float x, int act) {
   switch (act) {
     case DP_ACT_RELU: return fmaxf(x, 0.f);
-    case DP_ACT_SILU: return x / (1.f + __expf(-x));
+    case DP_ACT_SILU: return silu_f(x);
     case DP_ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
     default: return x;
   }
 }
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // ---------------------------------------------------------------- wave reductions (64 lanes)
 __device__ __forceinline__ float wave_sum(float v) {

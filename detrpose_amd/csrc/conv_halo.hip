@@ -21,6 +21,9 @@
 #include <stdlib.h>
 #include <type_traits>
 
+#ifndef DP_HALO_ABL
+#define DP_HALO_ABL 0   // ablation builds only: 1 no K-step vmcnt wait, 2 no K-step barrier, 4 no epilogue
+#endif
 #ifndef DP_HALO_TAB
 #define DP_HALO_TAB 1   // per-K-step tap table in LDS (0: recompute tap / channel per step, A/B only)
 #endif
@@ -30,7 +33,9 @@ namespace {
 using namespace dpconv;
 
 // LDS bytes in front of the weights: the K-step -> (tap offset, channel chunk, plane) table
-constexpr int TAB_BYTES = DP_HALO_TAB ? 2048 : 0;
+// (TAB_ENTRY_BYTES), then the conv's f32 biases (cout <= 128), loaded once per block
+constexpr int TAB_BYTES = 2048;
+constexpr int TAB_ENTRY_BYTES = 1536;
 
 template <int TH, int KH, int KW, int S>
 struct HaloGeom {
@@ -79,6 +84,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   const int pbytes = nkc * Gm::PLANE;                // one patch buffer
   const int ktaps = KH * KW;
   int* const tab = reinterpret_cast<int*>(smem);
+  float* const bias_l = reinterpret_cast<float*>(smem + TAB_ENTRY_BYTES);
   char* const wbase = smem + TAB_BYTES;
   char* const pbase0 = wbase + (RESW ? nk : 2) * BN * 128;
   const int r8 = lane >> 3;
@@ -128,6 +134,8 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
     }
   };
 
+  // biases of every output channel (0 past cout), published with the table by the first barrier
+  for (int e = tid; e < 128; e += NW * 64) bias_l[e] = (d.bias && e < d.cout) ? d.bias[e] : 0.f;
 #if DP_HALO_TAB
   // K-step table: entry kt*8 + cc (k = 64 kt + 8 cc -> tap = k / cin, ci = k % cin) holds the
   // tap's patch-pixel offset ky*PW + kx, the 16-byte chunk (ci/8)%8 and the 64-channel plane
@@ -145,22 +153,41 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   const int wm = wave;
   const int cin = d.cin;
 
-  if (DBUF) issue_patch(L, pbase0);
+  // EARLY (single patch buffer, no pool epilogue): the next tile's patch (and first weight
+  // K-step) is issued as soon as every wave is done reading this tile's, so its latency
+  // hides behind this tile's epilogue instead of stalling the next tile's start
+  constexpr bool EARLY = !DBUF && !POOL;
+  if (DBUF || EARLY) issue_patch(L, pbase0);
+  if (EARLY && !RESW) issue_w(0, wbase);
   f32x4 acc[TM][TN];
+  // stores one wave issues in the epilogue of a whole tile (plain epilogue, vector path): the
+  // next tile's wait may leave them in flight, since VMEM ops retire in issue order and the
+  // patch / weight DMAs it waits for were issued before them
+  constexpr int NSTORE = NAT ? TM * TN : TM * (NPL / 8);
+  const bool plain_full = !d.res && !d.up && (NAT || (vec_ok && d.cout == BN));
+  bool prev_full = false;
   int u = 0;
   for (int tile = L; tile < ntiles; tile += G, ++u) {
     const int tx = tile % tiles_x, rest = tile / tiles_x;
     const int ty = rest % tiles_y, b = rest / tiles_y;
     const int oy0 = ty * TH, ox0 = tx * TW;
+    const bool tile_full = plain_full && oy0 + TH <= d.out_h && ox0 + TW <= d.out_w;
     const char* pbase;
     if (DBUF) {
       // this tile's patch (prefetched during the previous tile) has landed; every wave is
       // past the previous tile, so the other buffer is free for the next tile's patch
-      wait_vmcnt<0>();
+      if (prev_full) wait_vmcnt<NSTORE>();
+      else wait_vmcnt<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (tile + G < ntiles) issue_patch(tile + G, pbase0 + ((u + 1) & 1) * pbytes);
       pbase = pbase0 + (u & 1) * pbytes;
+    } else if (EARLY) {
+      if (prev_full) wait_vmcnt<NSTORE>();
+      else wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      pbase = pbase0;
     } else {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -179,9 +206,9 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
         wsl = wbase + kt * BN * 128;
       } else {
         if (!FIRST) {
-          wait_vmcnt<0>();
+          if (!(DP_HALO_ABL & 1)) wait_vmcnt<0>();
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
+          if (!(DP_HALO_ABL & 2)) __builtin_amdgcn_s_barrier();
         }
         if (kt + 1 < nk) issue_w(kt + 1, wbase + ((kt + 1) & 1) * BN * 128);
         wsl = wbase + (kt & 1) * BN * 128;
@@ -227,18 +254,26 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
     };
     step(0, std::true_type{});
     for (int kt = 1; kt < nk; ++kt) step(kt, std::false_type{});
+    if constexpr (EARLY) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (tile + G < ntiles) {
+        issue_patch(tile + G, pbase0);
+        if (!RESW) issue_w(0, wbase);
+      }
+    }
     // epilogue: lane owns pixel (oy0 + yq, ox0 + q), channels lane_chan(g, 0 .. NPL-1)
-    if constexpr (NAT) {
+    if constexpr ((DP_HALO_ABL & 4) != 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else if constexpr (NAT) {
       // channels 16j + 4g + r: bias + act + LAB, one 8-byte store per tile j (no res / up:
       // the dispatcher routes only plain convs here)
-      float bias[TN][4];
+      f32x4 bias[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int cc = 16 * j + 4 * g + r;
-          bias[j][r] = (d.bias && cc < d.cout) ? d.bias[cc] : 0.f;
-        }
+      for (int j = 0; j < TN; ++j) bias[j] = *reinterpret_cast<const f32x4*>(bias_l + 16 * j + 4 * g);
       bf16_t* outp = reinterpret_cast<bf16_t*>(d.out) + (int64_t)b * d.out_bstride;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -260,7 +295,11 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
       }
     } else {
       float bias[NPL];
-      load_bias<bf16_t, NPL>(d, 0, g, bias);
+#pragma unroll
+      for (int e = 0; e < NPL; e += 4) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_l + lane_chan<8>(g, e));
+        bias[e] = b4[0], bias[e + 1] = b4[1], bias[e + 2] = b4[2], bias[e + 3] = b4[3];
+      }
       const bool full = lane_full<bf16_t, NPL>(d, 0, g, vec_ok);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -293,6 +332,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
         }
       }
     }
+    prev_full = tile_full && !POOL && !(DP_HALO_ABL & 4);
   }
   wait_vmcnt<0>();
 }
@@ -346,7 +386,7 @@ int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   const int bn = (d.cout + 31) / 32 * 32;
   const int nk = d.kpad / 64, nkc = (d.cin + 63) / 64;
   constexpr int LMAX = 160 * 1024;
-  if (nk * 8 * 4 > TAB_BYTES && DP_HALO_TAB) return -1;
+  if (nk * 8 * 4 > TAB_ENTRY_BYTES) return -1;
   auto lds_res = [&](int plane, int nbuf) { return TAB_BYTES + nk * bn * 128 + nbuf * nkc * plane; };  // resident W
   auto lds_str = [&](int plane) { return TAB_BYTES + 2 * bn * 128 + nkc * plane; };                     // W ring, 1 patch
   auto lds_res48 = [&](int plane, int nbuf) { return TAB_BYTES + nk * 48 * 128 + nbuf * nkc * plane; };

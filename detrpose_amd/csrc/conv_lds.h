@@ -48,7 +48,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 template <int ACT>
 __device__ __forceinline__ float act_t(float x) {
   if constexpr (ACT == DP_ACT_RELU) return fmaxf(x, 0.f);
-  else if constexpr (ACT == DP_ACT_SILU) return x / (1.f + __expf(-x));
+  else if constexpr (ACT == DP_ACT_SILU) return silu_f(x);
   else if constexpr (ACT == DP_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
   else return x;
 }
