@@ -40,6 +40,13 @@ class RowMap(C.Structure):
     _fields_ = [("base", i64), ("group", i32), ("stride_g", i64), ("stride_r", i64)]
 
 
+class StemWeights(C.Structure):
+    """dp_stem_weights (include/detrpose_hip.h)."""
+    _fields_ = [("w1", vp), ("b1", vp), ("w2a", vp), ("b2a", vp), ("w2b", vp), ("b2b", vp), ("w3", vp), ("b3", vp),
+                ("w4", vp), ("b4", vp), ("k2a", i32), ("k2b", i32), ("k3", i32), ("k4", i32), ("mid", i32),
+                ("cout", i32), ("has_lab", i32), ("lab", (f32 * 2) * 5)]
+
+
 class LossHead(C.Structure):
     """Mirror of dp_loss_head."""
     _fields_ = [("logits", vp), ("lg_b", i64), ("lg_q", i32), ("kps", vp), ("kp_b", i64), ("kp_q", i32),
@@ -62,6 +69,7 @@ _SIGS = {
     "dp_stem_conv": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, f32, f32, vp, i64, i32, i32, vp]),
     "dp_maxpool2x2_pad_rb": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, vp]),
     "dp_conv2d_pool": (i32, [C.POINTER(ConvDesc), vp, i64, i32, vp]),
+    "dp_stem_fused": (i32, [vp, i32, i32, i32, C.POINTER(StemWeights), vp, i64, i32, vp]),
     "dp_add_rows": (i32, [vp, RowMap, vp, RowMap, vp, RowMap, i32, i32, i32, vp]),
     "dp_layernorm": (i32, [vp, RowMap, vp, RowMap, vp, RowMap, vp, vp, f32, i32, i32, vp, RowMap, i32, i32,
                            vp, i32, vp, i32, vp]),

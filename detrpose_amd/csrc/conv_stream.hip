@@ -30,6 +30,9 @@
 #ifndef DP_ABL_NODMA
 #define DP_ABL_NODMA 0     // ... drop the LDS-DMA loads
 #endif
+#ifndef DP_STREAM_PRIO
+#define DP_STREAM_PRIO 0   // A/B: s_setprio(1) around each K-step's fragment reads + MFMAs
+#endif
 #ifndef DP_ABL_NOMFMA
 #define DP_ABL_NOMFMA 0    // ... drop the MFMAs (fragment reads kept live)
 #endif
@@ -351,6 +354,7 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
     if (a_n < total) issue_a();
     const char* sbw = smem + (c % SB) * BBYTES;
     const char* sbp = sa_base + (c % SA) * ABYTES;
+    if (DP_STREAM_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int cc = 4 * ks + lg;
@@ -379,6 +383,7 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
               wf[j], pf[i], (FIRST && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
 #endif
     }
+    if (DP_STREAM_PRIO) __builtin_amdgcn_s_setprio(0);
     ++c;
   };
   int t_n = 0;

@@ -506,7 +506,7 @@ __global__ __launch_bounds__(C * 2) void query_pos_kernel(const float* __restric
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float a = coord / dim_t[i0 + j];
+      const float a = coord * __builtin_amdgcn_rcpf(dim_t[i0 + j]);   // 1 ulp; bf16 output
       o[j] = (bf16_t)(((i0 + j) & 1) ? __cosf(a) : __sinf(a));
     }
     sts16(xl, sw<C>(m, c0 >> 3), o);

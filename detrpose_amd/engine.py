@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -566,28 +567,14 @@ class Engine:
     def _plan_backbone(self, plan, img):
         B = img.shape[0]
         H, W = img.shape[2], img.shape[3]
-        mid, so = self.stem_mid, self.stem_out
         P = self.bbP
         h1, w1 = (H + 1) // 2, (W + 1) // 2
-        s1 = self._fmap(B, h1, w1, mid)
-        wst, bst, lab = P["stem1"]
-        plan._op("stem1", self.lib.dp_stem_conv, img.data_ptr(), B, H, W, wst.data_ptr(), bst.data_ptr(), mid,
-                 1 if lab else 0, C.c_float(lab[0] if lab else 1.0), C.c_float(lab[1] if lab else 0.0), s1.ptr, s1.bs,
-                 s1.ps, self.code)
-        s2a = self._fmap(B, h1, w1, P["stem2a"].cout)
-        cat = self._fmap(B, h1, w1, 2 * mid)
-        if self.code == _lib.DP_BF16 and mid % 8 == 0 and mid <= 64 and P["stem2a"].cout <= 32:
-            # stem2a and the stem max-pool read the same F.pad(0,1,0,1) windows of stem1: one pass
-            self._conv(plan, "stem2a", s1, P["stem2a"], s2a, pool=cat.ch(0, mid))
-        else:
-            self._conv(plan, "stem2a", s1, P["stem2a"], s2a)   # F.pad(0,1,0,1) == zero read past the edge
-            plan._op("stem_pool", self.lib.dp_maxpool2x2_pad_rb, s1.ptr, s1.bs, s1.ps, B, h1, w1, mid, cat.ptr,
-                     cat.bs, cat.ps, self.code)
-        self._conv(plan, "stem2b", s2a, P["stem2b"], cat.ch(mid, mid))
         h2, w2 = (h1 + 1) // 2, (w1 + 1) // 2
-        s3 = self._fmap(B, h2, w2, mid)
-        self._conv(plan, "stem3", cat, P["stem3"], s3)
-        x_src = s3
+        fused = self._stem_fusable()
+        if fused:
+            x_src = None   # the whole StemBlock runs as one launch into stage 0's concat slot
+        else:
+            x_src = self._plan_stem(plan, img, B, H, W, h1, w1)
         outs = []
         h, w = h2, w2
         for si, st in enumerate(self.stages):
@@ -599,7 +586,9 @@ class Engine:
                 bin_ = cin if bi == 0 else cout
                 blocks_in.append(self._fmap(B, h, w, bin_ + nl * midc))
             # stage input -> block 0 concat slot [0:cin]
-            if si == 0:
+            if si == 0 and fused:
+                self._stem_fused_op(plan, img, blocks_in[0].ch(0, cin))
+            elif si == 0:
                 self._conv(plan, "stem4", x_src, P["stem4"], blocks_in[0].ch(0, cin))
             else:
                 self._conv(plan, f"s{si}.down", x_src, st["down"], blocks_in[0].ch(0, cin))
@@ -632,6 +621,63 @@ class Engine:
                 outs.append(x_src)
         plan.bufs["backbone"] = outs
         return outs
+
+    def _stem_fusable(self):
+        """dp_stem_fused covers the bf16 32-channel stems (B4 / B5: DETRPose-L / X)."""
+        P = self.bbP
+        return (self.code == _lib.DP_BF16 and self.stem_mid == 32 and self.stem_out in (48, 64)
+                and not os.environ.get("DETRPOSE_NO_STEM_FUSE")
+                and P["stem2a"].cout == 16 and P["stem2b"].cout == 32 and P["stem3"].cin == 64
+                and P["stem3"].cout == 32 and P["stem3"].kpad >= 576 and P["stem4"].cin == 32
+                and P["stem4"].cout == self.stem_out)
+
+    def _stem_fused_op(self, plan, img, out: FMap):
+        """StemBlock.forward (hgnetv2.py:204-220) as one dp_stem_fused launch."""
+        P = self.bbP
+        B, H, W = img.shape[0], img.shape[2], img.shape[3]
+        w1, b1, lab1 = P["stem1"]
+        sw = _lib.StemWeights()
+        sw.w1, sw.b1 = w1.data_ptr(), b1.data_ptr()
+        convs = [P[n] for n in ("stem2a", "stem2b", "stem3", "stem4")]
+        (sw.w2a, sw.b2a, sw.k2a), (sw.w2b, sw.b2b, sw.k2b), (sw.w3, sw.b3, sw.k3), (sw.w4, sw.b4, sw.k4) = (
+            (pc.w.data_ptr(), pc.b.data_ptr(), pc.kpad) for pc in convs)
+        sw.mid, sw.cout = self.stem_mid, self.stem_out
+        labs = [lab1] + [pc.lab for pc in convs]
+        sw.has_lab = int(any(lb is not None for lb in labs))
+        for i, lb in enumerate(labs):
+            sw.lab[i][0], sw.lab[i][1] = (lb[0], lb[1]) if lb is not None else (1.0, 0.0)
+        plan.keep.append(sw)
+        assert (out.B, out.H, out.W, out.C) == (B, ((H + 1) // 2 + 1) // 2, ((W + 1) // 2 + 1) // 2, self.stem_out)
+        plan._op("stem", self.lib.dp_stem_fused, img.data_ptr(), B, H, W, C.byref(sw), out.ptr, out.bs, out.ps)
+        plan.op_out["stem"] = out
+        h1, w1_ = (H + 1) // 2, (W + 1) // 2
+        m1, m3 = B * h1 * w1_, B * out.H * out.W
+        plan.op_flops["stem"] = 2.0 * (m1 * 32 * 27 + m1 * 16 * 128 + m1 * 32 * 64 + m3 * 32 * 576 + m3 * out.C * 32)
+        plan.conv_bytes["stem"] = 4.0 * B * 3 * H * W + 2.0 * m3 * out.C
+
+    def _plan_stem(self, plan, img, B, H, W, h1, w1):
+        """StemBlock.forward (hgnetv2.py:204-220) as five launches; returns stem3's map."""
+        mid = self.stem_mid
+        P = self.bbP
+        s1 = self._fmap(B, h1, w1, mid)
+        wst, bst, lab = P["stem1"]
+        plan._op("stem1", self.lib.dp_stem_conv, img.data_ptr(), B, H, W, wst.data_ptr(), bst.data_ptr(), mid,
+                 1 if lab else 0, C.c_float(lab[0] if lab else 1.0), C.c_float(lab[1] if lab else 0.0), s1.ptr, s1.bs,
+                 s1.ps, self.code)
+        s2a = self._fmap(B, h1, w1, P["stem2a"].cout)
+        cat = self._fmap(B, h1, w1, 2 * mid)
+        if self.code == _lib.DP_BF16 and mid % 8 == 0 and mid <= 64 and P["stem2a"].cout <= 32:
+            # stem2a and the stem max-pool read the same F.pad(0,1,0,1) windows of stem1: one pass
+            self._conv(plan, "stem2a", s1, P["stem2a"], s2a, pool=cat.ch(0, mid))
+        else:
+            self._conv(plan, "stem2a", s1, P["stem2a"], s2a)   # F.pad(0,1,0,1) == zero read past the edge
+            plan._op("stem_pool", self.lib.dp_maxpool2x2_pad_rb, s1.ptr, s1.bs, s1.ps, B, h1, w1, mid, cat.ptr,
+                     cat.bs, cat.ps, self.code)
+        self._conv(plan, "stem2b", s2a, P["stem2b"], cat.ch(mid, mid))
+        h2, w2 = (h1 + 1) // 2, (w1 + 1) // 2
+        s3 = self._fmap(B, h2, w2, mid)
+        self._conv(plan, "stem3", cat, P["stem3"], s3)
+        return s3
 
     def _plan_elan(self, plan, name, x: FMap, E, out: FMap):
         """RepNCSPELAN4.forward (hybrid_encoder.py:210-212)."""

@@ -77,6 +77,34 @@ int dp_stem_conv(const float* image, int32_t batch, int32_t h, int32_t w,
                  int32_t has_lab, float lab_scale, float lab_bias,
                  void* out, int64_t out_bstride, int32_t out_pstride, int32_t dtype, void* stream);
 
+/* Packed StemBlock weights for dp_stem_fused: stem1 f32 [32][27] (OIHW flattening), the
+ * other convs bf16 [cout][k*] (k = tap * cin + ci, rows padded to k* elements) as dp_conv2d
+ * takes them; stem3's cin is the cat order [pool, stem2b]. f32 biases (folded BN). LAB
+ * (scale, bias) per conv in the order stem1, 2a, 2b, 3, 4 when has_lab. */
+typedef struct dp_stem_weights {
+  const float* w1;
+  const float* b1;
+  const void* w2a;
+  const float* b2a;
+  const void* w2b;
+  const float* b2b;
+  const void* w3;
+  const float* b3;
+  const void* w4;
+  const float* b4;
+  int32_t k2a, k2b, k3, k4;
+  int32_t mid, cout;
+  int32_t has_lab;
+  float lab[5][2];
+} dp_stem_weights;
+
+/* The whole StemBlock.forward (hgnetv2.py:204-220: stem1, stem2a, stem2b, max-pool, cat,
+ * stem3, stem4) in one bf16 launch: f32 NCHW image in, stem4's NHWC bf16 map out (into the
+ * first HG stage's concat slot). Stem channels [3, 32, 48|64] (B4 / B5). Same rounding points
+ * as the five-launch path (bit-identical output). */
+int dp_stem_fused(const float* image, int32_t batch, int32_t h, int32_t w, const dp_stem_weights* weights,
+                  void* out, int64_t out_bstride, int32_t out_pstride, void* stream);
+
 /* F.pad(x,(0,1,0,1)) + MaxPool2d(2, 1, ceil_mode=True) of StemBlock (hgnetv2.py:215,217). */
 int dp_maxpool2x2_pad_rb(const void* in, int64_t in_bstride, int32_t in_pstride,
                          int32_t batch, int32_t h, int32_t w, int32_t c,

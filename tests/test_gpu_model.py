@@ -273,3 +273,33 @@ def test_deploy_model_boundary(golden_dir):
         np.testing.assert_allclose(k.cpu().numpy(), g["pp_keypoints"], atol=640 * 1e-3)
     with pytest.raises(ValueError):
         model(torch.rand(1, 3, 320, 320, device="cuda"))
+
+
+@pytest.mark.parametrize("size,batch", [("l", 2), ("x", 1)])
+def test_stem_fused_bit_identical(golden_dir, size, batch, monkeypatch):
+    """dp_stem_fused (the whole StemBlock in one launch, hgnetv2.py:204-220) writes exactly
+    the map of the five-launch path (stem1, stem2a + pool, stem2b, stem3, stem4): same K
+    order, f32 accumulation sequence and bf16 rounding points. Also the end outputs."""
+    from detrpose_amd.engine import Engine
+    with open(os.path.join(golden_dir, "manifest.json")) as f:
+        man = json.load(f)
+    model, _ = build_model(size, dtype="bf16")
+    model.load_state_dict(synthetic_state_dict(man[size], seed=0), strict=False)
+    model.eval()
+    img = synthetic_images(batch, seed=5).cuda()
+    outs = {}
+    for fused in (True, False):
+        if fused:
+            monkeypatch.delenv("DETRPOSE_NO_STEM_FUSE", raising=False)
+        else:
+            monkeypatch.setenv("DETRPOSE_NO_STEM_FUSE", "1")
+        plan = Engine(model, "bf16", device="cuda").plan(batch)
+        names = [n for n, _, _ in plan.ops]
+        assert ("stem" in names) == fused and ("stem1" in names) != fused
+        plan.input.copy_(img)
+        plan.run()
+        torch.cuda.synchronize()
+        outs[fused] = (plan.op_out["stem" if fused else "stem4"].view().clone(),
+                       plan.outputs["pred_logits"].clone(), plan.outputs["pred_keypoints"].clone())
+    for a, b, what in zip(outs[True], outs[False], ("stem4 map", "logits", "keypoints")):
+        assert torch.equal(a, b), what
