@@ -327,6 +327,231 @@ __global__ __launch_bounds__(C * 2) void linear_ln_kernel(bf16_t* out, dp_rowmap
   }
 }
 
+// ------------------------------------------------------------------ fused MHA + out_proj + res + LN
+// nn.MultiheadAttention(q = k = v = x) + residual + LayerNorm of the decoder layer's two token
+// attentions (transformer.py:403-422): within-instance (the T tokens of a query, rows
+// contiguous) and across-instance (the nq queries of one token slot, rows T apart). One block
+// = GB sequences of SEQ tokens, block row m = g * SEQ + t (padded to TM tiles of 16), C = 256,
+// 8 heads of 32, 8 waves: wave h = head h.
+//   1. X rows -> LDS; wave h runs its head's Q, K, V projections (3 x [R x 32] GEMMs off the
+//      LDS image, weight fragments from L2): Q and K stay in registers as bf16 MFMA fragments
+//      (the projection's C layout -- 8 contiguous channels of one row per lane -- IS the A/B
+//      operand layout for K = dh = 32), V goes to the wave's own LDS slice (row-major).
+//   2. per 16-query tile: S^T = K Q^T over the key tiles of its sequences (one MFMA each,
+//      other sequences masked), softmax over registers + 2 xor-shuffles, O^T = V^T P^T with P
+//      from registers and V^T by ds_read_b64_tr_b16 (attention.hip's attn_long scheme); O (bf16)
+//      overwrites the X image in LDS (all waves are past their projections).
+//   3. out_proj off the O image, + bias + residual (x rows re-read, L2) -> LayerNorm (+ the
+//      across attention's pos re-add on keypoint rows) -> out.
+// HBM: x read once (+ the residual re-read from L2), out written once: the qkv (3C) and
+// attention-output (C) round trips of the unfused path are gone.
+template <int SEQ, int GB, bool POST>
+__global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, const bf16_t* x, dp_rowmap xm,
+                                                     int n_inner, int64_t so, int64_t si, int64_t st, int nseq,
+                                                     const bf16_t* __restrict__ wqkv, const float* __restrict__ bqkv,
+                                                     const bf16_t* __restrict__ wo, const float* __restrict__ bo,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float eps, float scale, const bf16_t* post, dp_rowmap pm,
+                                                     int post_group, int post_skip) {
+  constexpr int C = 256, NW = 8, NTH = 512, DH = 32;
+  constexpr int RR = SEQ * GB, TM = (RR + 15) / 16, R = 16 * TM;
+  constexpr int DHP = 48;                      // V row pitch (elements): conflict-free tr reads
+  constexpr int VR = R + 16;                   // + one zero tile: the last key pair's upper half
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) char smem[R * C * 2 + NW * VR * DHP * 2 + NW * R * 4];
+  char* xl = smem;
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  bf16_t* V = reinterpret_cast<bf16_t*>(smem + R * C * 2) + wv * VR * DHP;
+  float* red = reinterpret_cast<float*>(smem + R * C * 2 + NW * VR * DHP * 2);
+  const int sq0 = blockIdx.x * GB;
+  // block row m -> token row (o * so + ii * si + t * st < 2^31, checked by the launcher); -1
+  // past the last sequence / padding
+  auto row_of = [&](int m) -> int {
+    if (m >= RR) return -1;
+    const int gq = m / SEQ, t = m - gq * SEQ, sq = sq0 + gq;
+    if (sq >= nseq) return -1;
+    const int o = (int)((unsigned)sq / (unsigned)n_inner), ii = sq - o * n_inner;
+    return o * (int)so + ii * (int)si + t * (int)st;
+  };
+  const bf16_t* wq = frag_base(wqkv, wv, C / 32);
+  const bf16_t* wk = frag_base(wqkv, NW + wv, C / 32);
+  const bf16_t* wvv = frag_base(wqkv, 2 * NW + wv, C / 32);
+  const bf16_t* wob = frag_base(wo, wv, C / 32);
+  WPipe p;
+  pipe_start(p, wvv);
+  // ---- X rows -> LDS (zero rows past the block's tokens); the zero V tile
+  {
+    constexpr int CH = C / 8, PER = R * CH / NTH;
+    bf16x8 xv[PER];
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int e = threadIdx.x + NTH * t;
+      const int m = e / CH, c = e - m * CH;
+      const int r = row_of(m);
+      xv[t] = r >= 0 ? gld16(x + rowmap_off(xm, r) + c * 8) : bf16x8{};
+    }
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int e = threadIdx.x + NTH * t;
+      const int m = e / CH, c = e - m * CH;
+      sts16(xl, sw<C>(m, c), xv[t]);
+    }
+    for (int e = lane; e < 16 * DHP / 8; e += 64) sts16(reinterpret_cast<char*>(V + R * DHP), e * 16, bf16x8{});
+  }
+  const int cb = g * NV;   // the lane's 8 contiguous channels within a 32-channel block
+  lds_barrier();
+
+  // ---- 1. this head's projections
+  bf16x8 qf[TM], kf[TM];
+  f32x4 acc[TM][TN];
+  // + bias (channels 32 wv + cb .. of projection `part`), bf16: the MFMA fragment of row 16i + q
+  auto frag_of = [&](int i, int part) __attribute__((always_inline)) {
+    float b[NV];
+    load_bias(bqkv, part * C + 32 * wv + cb, b);
+    bf16x8 f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) f[4 * j + r] = (bf16_t)(acc[i][j][r] + b[4 * j + r]);
+    return f;
+  };
+  // V first (to LDS), then K, then Q: the fewest fragments live across a GEMM
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, xl, wvv, p, wk);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) *reinterpret_cast<bf16x8*>(V + (16 * i + q) * DHP + cb) = frag_of(i, 2);
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, xl, wk, p, wq);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) kf[i] = frag_of(i, 1);
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, xl, wq, p, wob);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) qf[i] = frag_of(i, 0);
+  lds_barrier();   // every wave is past its projections: the X image may be overwritten by O
+
+  // ---- 2. attention, one 16-query tile at a time
+  const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    // key tiles of the sequences this query tile touches (compile time)
+    const int glo = (16 * i) / SEQ, ghi = min((16 * i + 15) / SEQ, GB - 1);
+    const int klo = (glo * SEQ) / 16, khi = ((ghi + 1) * SEQ - 1) / 16;
+    constexpr int NKMAX = (SEQ + 15) / 16 + 2;
+    f32x4 sv[NKMAX];
+    const int qm = 16 * i + q;          // this lane's query row
+    const int qg = qm / SEQ;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kk = 0; kk < NKMAX; ++kk) {
+      const int kt = klo + kk;
+      if (kt > khi) break;
+      sv[kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt], qf[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int km = 16 * kt + 4 * g + r;   // key row of S^T element r
+        const float v = (km < RR && km / SEQ == qg) ? sv[kk][r] * scale : -INFINITY;
+        sv[kk][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < NKMAX; ++kk) {
+      if (klo + kk > khi) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(sv[kk][r] - mx);
+        sv[kk][r] = e;
+        sum += e;
+      }
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+    f32x4 oacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kk = 0; kk < NKMAX; kk += 2) {
+      const int kt = klo + kk;
+      if (kt > khi) break;
+      const bool two = kt + 1 <= khi;
+      bf16x8 pf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[r] = (bf16_t)sv[kk][r];
+        pf[4 + r] = (bf16_t)(two ? sv[kk + 1][r] : 0.f);
+      }
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const bf16_t* a0 = V + (16 * kt + 4 * g + q4) * DHP + 16 * d + 4 * p4;
+        const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0));
+        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0 + 16 * DHP));
+        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 vfr = *reinterpret_cast<const bf16x8*>(tmp);
+        oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfr, pf, oacc[d], 0, 0, 0);
+      }
+    }
+    // O^T[16d + 4g + r][query q] -> O image row qm, channels 32 wv + 16 d + 4 g .. +3
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16_t)(oacc[d][r] * inv);
+      const int ch = 32 * wv + 16 * d + 4 * g;
+      *reinterpret_cast<bf16x4*>(xl + sw<C>(qm, ch >> 3) + (ch & 7) * 2) = w;
+    }
+  }
+  // residual rows for the epilogue, in flight across the barrier and the out_proj GEMM
+  bf16x8 rv[TM], pv[TM];
+  float bias[NV], gg[NV], bb[NV];
+  {
+    const int ocb = 32 * wv + cb;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = max(row_of(16 * i + q), 0);
+      rv[i] = gld16(x + rowmap_off(xm, r) + ocb);
+      if (POST) {
+        const int grp = (int)((unsigned)r / (unsigned)post_group), wi = r - grp * post_group;
+        pv[i] = gld16(post + rowmap_off(pm, grp * (post_group - post_skip) + max(wi - post_skip, 0)) + ocb);
+      }
+    }
+    load_bias(bo, ocb, bias);
+    load_bias(gamma, ocb, gg);
+    load_bias(beta, ocb, bb);
+  }
+  lds_barrier();   // the O image is complete
+
+  // ---- 3. out_proj + bias + residual -> LayerNorm -> out
+  zero_acc<TM>(acc);
+  wave_gemm<C, TM>(acc, xl, wob, p, wob);
+  float v[TM][NV];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float a[NV];
+    lane_vals<TM>(acc, i, a);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[i][e] = a[e] + bias[e] + (float)rv[i][e];
+  }
+  layernorm_rows<TM, NW>(v, gg, bb, eps, red);
+  const int ocb = 32 * wv + cb;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = row_of(16 * i + q);
+    if (r < 0) continue;
+    if (POST) {
+      const int wi = (int)((unsigned)r % (unsigned)post_group);
+      if (wi >= post_skip) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) v[i][e] += (float)pv[i][e];
+      }
+    }
+    store_row_vals(out + rowmap_off(om, r) + ocb, v[i]);
+  }
+}
+
 // ------------------------------------------------------------------ Gate: Linear + sigmoid mix + LN
 // xcat = [x1 | x2] (K = 2C); gate rows n < C -> g1, n >= C -> g2. Wave w computes g1 AND
 // g2 of its 32 channels, so the mix sigmoid(g1) x1 + sigmoid(g2) x2 is lane-local.
@@ -789,5 +1014,41 @@ extern "C" int dp_pose_mlp(const void* x, dp_rowmap xm, const void* x2, dp_rowma
   DP_FOR_BM(DP_PM)
 #undef DP_PM
   dp_set_error("dp_pose_mlp: c=%d unsupported (128/256/384)", c);
+  return DP_EINVAL;
+}
+
+extern "C" int dp_mha_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, int32_t n_outer,
+                                int32_t n_inner, int64_t so, int64_t si, int64_t st, int32_t seqlen, const void* wqkv,
+                                const float* bqkv, const void* wo, const float* bo, const float* gamma,
+                                const float* beta, float eps, int32_t c, int32_t nhead, const void* post, dp_rowmap pm,
+                                int32_t post_group, int32_t post_skip, void* stream) {
+  DP_REQUIRE(out && x && wqkv && bqkv && wo && bo && gamma && beta && n_outer > 0 && n_inner > 0,
+             "dp_mha_layernorm: bad args");
+  DP_REQUIRE(al16(out) && al16(x) && al16(wqkv) && al16(wo) && map16(om) && map16(xm) &&
+                 (!post || (al16(post) && map16(pm) && post_group > post_skip)),
+             "dp_mha_layernorm: rows must be 16-byte aligned");
+  DP_REQUIRE(c == 256 && nhead == 8, "dp_mha_layernorm: C = 256 with 8 heads only (got %d / %d)", c, nhead);
+  const int64_t nseq = (int64_t)n_outer * n_inner;
+  DP_REQUIRE((int64_t)(n_outer - 1) * so + (int64_t)(n_inner - 1) * si + (int64_t)(seqlen - 1) * st < (1ll << 31),
+             "dp_mha_layernorm: token rows exceed 2^31");
+  hipStream_t s = as_stream(stream);
+  const float scale = 1.f / sqrtf(32.f);
+#define DP_MHA(SEQ_, GB_)                                                                                          \
+  do {                                                                                                             \
+    dim3 grid((unsigned)((nseq + GB_ - 1) / GB_));                                                                 \
+    if (post)                                                                                                      \
+      hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, true>), grid, dim3(512), 0, s, (bf16_t*)out, om, (const bf16_t*)x, \
+                         xm, n_inner, so, si, st, (int)nseq, (const bf16_t*)wqkv, bqkv, (const bf16_t*)wo, bo, gamma,  \
+                         beta, eps, scale, (const bf16_t*)post, pm, post_group, post_skip);                         \
+    else                                                                                                           \
+      hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, false>), grid, dim3(512), 0, s, (bf16_t*)out, om, (const bf16_t*)x, \
+                         xm, n_inner, so, si, st, (int)nseq, (const bf16_t*)wqkv, bqkv, (const bf16_t*)wo, bo, gamma,  \
+                         beta, eps, scale, (const bf16_t*)nullptr, pm, 1, 0);                                       \
+    return dp_check_launch("dp_mha_layernorm");                                                                    \
+  } while (0)
+  if (seqlen == 18) DP_MHA(18, 4);   // within-instance: the 1 + 17 tokens of a query
+  if (seqlen == 60) DP_MHA(60, 1);   // across-instance: the 60 queries of a token slot
+#undef DP_MHA
+  dp_set_error("dp_mha_layernorm: seqlen %d not instantiated (18 / 60)", seqlen);
   return DP_EINVAL;
 }

@@ -457,7 +457,8 @@ class Engine:
             }
             if self.code == _lib.DP_BF16:
                 # MFMA-fragment copies for the row-block fused kernels (detrpose_amd/fragments.py)
-                L["frag"] = {k: frag_pack(L[k].w) for k in ("within_out", "across_out", "gate", "ffn1", "ffn2")}
+                L["frag"] = {k: frag_pack(L[k].w) for k in ("within_out", "across_out", "gate", "ffn1", "ffn2",
+                                                             "within_qkv", "across_qkv")}
                 L["frag"]["pose"] = [frag_pack(pc.w) for pc in L["pose"]]
             # class / LQE heads of every layer: the inference plan runs the last layer's
             # (eval_idx), the training-mode plan all of them (transformer.py:726-728)
@@ -849,6 +850,9 @@ class Engine:
         # one launch per reference op
         fused = self.code == _lib.DP_BF16 and Cc in (128, 256, 384)
         plan.decoder_fused = fused
+        # the two token attentions as one launch each (dp_mha_layernorm: C = 256, 8 heads)
+        mha = (fused and Cc == 256 and nh == 8 and T == 18 and nq == 60
+               and not os.environ.get("DETRPOSE_NO_MHA_FUSE"))
         pos = self._fmap(1, 1, krows, Cc)
         qkv = self._empty(rows * 3 * Cc, dtype=dt)
         att = self._fmap(1, 1, rows, Cc)
@@ -942,35 +946,50 @@ class Engine:
                 # layer's output_pose into output_pose_detach + pos (aliasing kept on purpose)
                 plan._op(n + ".addpos", lib.dp_add_rows, src.data_ptr(), kp_map, src.data_ptr(), kp_map, pos.ptr,
                          contiguous_rows(Cc), krows, Cc, self.code)
-            # within-instance MHA over the T tokens of a query (transformer.py:403-406)
-            self._conv(plan, n + ".w_qkv", src_f, L["within_qkv"], qkv_f)
-            plan._op(n + ".w_attn", lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
-                     qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B * nq, 1, T, 0, 1, T, nh, Cc // nh, self.code)
-            if fused:
-                wn, fr = L["within_norm"], L["frag"]
-                plan._op(n + ".w_out_ln", lib.dp_linear_layernorm, dst.data_ptr(), cr(Cc), att.ptr, cr(Cc), Cc,
-                         *lin(L["within_out"], fr["within_out"], Cc), src.data_ptr(), cr(Cc), wn[0].data_ptr(),
-                         wn[1].data_ptr(), eps, rows, Cc, None, rowmap(group=1), 1, 0)
+            if mha:
+                # within-instance MHA + out_proj + residual + LN (transformer.py:403-406), then the
+                # across-instance one over the nq queries of a token slot (transformer.py:409-422)
+                fr, wn, an = L["frag"], L["within_norm"], L["across_norm"]
+                plan._op(n + ".w_mha", lib.dp_mha_layernorm, dst.data_ptr(), cr(Cc), src.data_ptr(), cr(Cc), B * nq, 1,
+                         T, 0, 1, T, *lin(L["within_qkv"], fr["within_qkv"], Cc),
+                         *lin(L["within_out"], fr["within_out"], Cc), wn[0].data_ptr(), wn[1].data_ptr(), eps, Cc, nh,
+                         None, rowmap(group=1), 1, 0)
+                plan._op(n + ".a_mha", lib.dp_mha_layernorm, gx.data_ptr(), cr(2 * Cc), dst.data_ptr(), cr(Cc), B, T,
+                         nq * T, 1, T, nq, *lin(L["across_qkv"], fr["across_qkv"], Cc),
+                         *lin(L["across_out"], fr["across_out"], Cc), an[0].data_ptr(), an[1].data_ptr(), eps, Cc, nh,
+                         pos.ptr, cr(Cc), T, 1)
+                mha_flops = 2.0 * rows * Cc * 4 * Cc
+                plan.op_flops[n + ".w_mha"] = plan.op_flops[n + ".a_mha"] = mha_flops
             else:
-                self._conv(plan, n + ".w_out", att, L["within_out"], ao)
-                self._ln(plan, n + ".w_norm", dst.data_ptr(), contiguous_rows(Cc), src.data_ptr(), contiguous_rows(Cc),
-                         ao.ptr, contiguous_rows(Cc), L["within_norm"], rows, Cc)
-            # across-instance MHA over the nq queries of a token slot (transformer.py:409-419)
-            self._conv(plan, n + ".a_qkv", dst_f, L["across_qkv"], qkv_f)
-            plan._op(n + ".a_attn", lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
-                     qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B, T, nq * T, 1, T, nq, nh, Cc // nh,
-                     self.code)
-            # out_proj + LN + second in-place pos add -> x1 = gx[:, :C]   (transformer.py:419-422)
-            if fused:
-                an, fr = L["across_norm"], L["frag"]
-                plan._op(n + ".a_out_ln", lib.dp_linear_layernorm, gx.data_ptr(), cr(2 * Cc), att.ptr, cr(Cc), Cc,
-                         *lin(L["across_out"], fr["across_out"], Cc), dst.data_ptr(), cr(Cc), an[0].data_ptr(),
-                         an[1].data_ptr(), eps, rows, Cc, pos.ptr, cr(Cc), T, 1)
-            else:
-                self._conv(plan, n + ".a_out", att, L["across_out"], ao)
-                self._ln(plan, n + ".a_norm", gx.data_ptr(), contiguous_rows(2 * Cc), dst.data_ptr(),
-                         contiguous_rows(Cc), ao.ptr, contiguous_rows(Cc), L["across_norm"], rows, Cc,
-                         post=(pos.ptr, contiguous_rows(Cc)), post_group=T, post_skip=1)
+                # within-instance MHA over the T tokens of a query (transformer.py:403-406)
+                self._conv(plan, n + ".w_qkv", src_f, L["within_qkv"], qkv_f)
+                plan._op(n + ".w_attn", lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
+                         qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B * nq, 1, T, 0, 1, T, nh, Cc // nh, self.code)
+                if fused:
+                    wn, fr = L["within_norm"], L["frag"]
+                    plan._op(n + ".w_out_ln", lib.dp_linear_layernorm, dst.data_ptr(), cr(Cc), att.ptr, cr(Cc), Cc,
+                             *lin(L["within_out"], fr["within_out"], Cc), src.data_ptr(), cr(Cc), wn[0].data_ptr(),
+                             wn[1].data_ptr(), eps, rows, Cc, None, rowmap(group=1), 1, 0)
+                else:
+                    self._conv(plan, n + ".w_out", att, L["within_out"], ao)
+                    self._ln(plan, n + ".w_norm", dst.data_ptr(), contiguous_rows(Cc), src.data_ptr(), contiguous_rows(Cc),
+                             ao.ptr, contiguous_rows(Cc), L["within_norm"], rows, Cc)
+                # across-instance MHA over the nq queries of a token slot (transformer.py:409-419)
+                self._conv(plan, n + ".a_qkv", dst_f, L["across_qkv"], qkv_f)
+                plan._op(n + ".a_attn", lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
+                         qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B, T, nq * T, 1, T, nq, nh, Cc // nh,
+                         self.code)
+                # out_proj + LN + second in-place pos add -> x1 = gx[:, :C]   (transformer.py:419-422)
+                if fused:
+                    an, fr = L["across_norm"], L["frag"]
+                    plan._op(n + ".a_out_ln", lib.dp_linear_layernorm, gx.data_ptr(), cr(2 * Cc), att.ptr, cr(Cc), Cc,
+                             *lin(L["across_out"], fr["across_out"], Cc), dst.data_ptr(), cr(Cc), an[0].data_ptr(),
+                             an[1].data_ptr(), eps, rows, Cc, pos.ptr, cr(Cc), T, 1)
+                else:
+                    self._conv(plan, n + ".a_out", att, L["across_out"], ao)
+                    self._ln(plan, n + ".a_norm", gx.data_ptr(), contiguous_rows(2 * Cc), dst.data_ptr(),
+                             contiguous_rows(Cc), ao.ptr, contiguous_rows(Cc), L["across_norm"], rows, Cc,
+                             post=(pos.ptr, contiguous_rows(Cc)), post_group=T, post_skip=1)
             # MSDA (ms_deform_attn.py:384-444) -> gx[:, C:]
             self._conv(plan, n + ".offattn", gx_f.ch(0, Cc), L["offattn"], oa)
             plan._op(n + ".msda", lib.dp_msda, memory.data_ptr(), B, S, lvl_hw, len(shapes), oa.ptr, ref.data_ptr(),

@@ -264,6 +264,20 @@ int dp_postprocess(const float* logits, const float* kps, const float* target_si
  * A block owns 64 token rows and all c channels, so the row-wise op after each GEMM runs
  * in its epilogue. Weights bf16 [n][k] (nn.Linear layout), biases f32. */
 
+/* The whole token self-attention block of the decoder layer in one launch:
+ * out = LayerNorm(x + MHA(x, x, x) . wo^T + bo) (+ post as dp_linear_layernorm), with
+ * MHA = nn.MultiheadAttention(C, nhead) (in_proj wqkv [3C][C] + bqkv, out_proj wo [C][C] + bo,
+ * both in the fragment layout). Replaces within_attn + within_norm and across_attn +
+ * across_norm + the second in-place pos add (transformer.py:403-422). Token t of sequence
+ * (o, ii) (o < n_outer, ii < n_inner, t < seqlen) is row o*so + ii*si + t*st of x and out.
+ * C = 256 with 8 heads; seqlen 18 (within: the 1 + 17 tokens of a query) or 60 (across:
+ * the queries of a token slot). out may not alias x. */
+int dp_mha_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, int32_t n_outer, int32_t n_inner,
+                     int64_t so, int64_t si, int64_t st, int32_t seqlen, const void* wqkv, const float* bqkv,
+                     const void* wo, const float* bo, const float* gamma, const float* beta, float eps, int32_t c,
+                     int32_t nhead, const void* post, dp_rowmap pm, int32_t post_group, int32_t post_skip,
+                     void* stream);
+
 /* out = LayerNorm(x . w^T + b + res) (+ post on the rows the post map selects, as in
  * dp_layernorm). MultiheadAttention.out_proj + residual + LayerNorm of the decoder layer:
  * within_attn -> within_norm, across_attn -> across_norm + the second in-place pos add

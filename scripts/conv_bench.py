@@ -47,6 +47,8 @@ SHAPES = {
     ],
     "conv3": [
         ("s0.l (48ch)", 64, 160, 160, 48, 48, 3, 1, 1, False),
+        ("s0.l@336", 64, 160, 160, 48, 48, 3, 1, 1, False),
+        ("s1.l@704", 64, 80, 80, 96, 96, 3, 1, 1, False),
         ("s1.l (96ch)", 64, 80, 80, 96, 96, 3, 1, 1, False),
         ("fpn1.vgg (128ch)", 64, 80, 80, 128, 128, 3, 1, 2, False),
         ("fpn0.vgg (128ch)", 64, 40, 40, 128, 128, 3, 1, 2, False),
@@ -66,10 +68,13 @@ def load(path):
 def make(shape, dev):
     name, B, H, W, cin, cout, k, s, act, res = shape
     dw = " dw" in name
+    # "name@P": input and output are channel slices of one concat buffer with P channels per
+    # pixel (the HG-block layout: read slot [0, cin), write slot [cin, cin + cout))
+    ps = int(name.split("@")[1]) if "@" in name else 0
     kpad = (k * k * cin + 63) // 64 * 64
     pad = (k - 1) // 2
     oh, ow = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
-    x = torch.randn(B * H * W * cin, device=dev).to(torch.bfloat16)
+    x = torch.randn(B * H * W * (ps or cin), device=dev).to(torch.bfloat16)
     w = (torch.randn(cout, kpad, device=dev) / (k * k * cin) ** 0.5).to(torch.bfloat16)
     if dw:   # depthwise: f32 [k][k][C] weights
         w = torch.randn(k * k * cin, device=dev) / k
@@ -81,6 +86,10 @@ def make(shape, dev):
     d.weight, d.kpad, d.bias = w.data_ptr(), kpad, b.data_ptr()
     d.kh, d.kw, d.stride, d.pad_t, d.pad_l = k, k, s, pad, pad
     d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = y.data_ptr(), oh * ow * cout, cout, oh, ow, cout
+    if ps:
+        assert (oh, ow) == (H, W)
+        d.in_bstride, d.in_pstride = H * W * ps, ps
+        d.out, d.out_bstride, d.out_pstride = x.data_ptr() + 2 * cin, H * W * ps, ps
     if r is not None:
         d.res, d.res_bstride, d.res_pstride = r.data_ptr(), oh * ow * cout, cout
     d.batch, d.act, d.dtype = B, act, DP_BF16

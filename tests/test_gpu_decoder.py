@@ -170,3 +170,70 @@ def test_pose_mlp(c, add):
     ref = h2 @ w2.float().t() + b2 + (prev if add else 0)
     err = (out.cpu() - ref).abs().max().item()
     assert err <= 5e-3 * max(1.0, ref.abs().max().item()), err
+
+
+def _mha_ref(x, wqkv, bqkv, wo, bo, nhead):
+    """nn.MultiheadAttention(q = k = v = x) in fp32 on the bf16 projections the kernel stores
+    (q, k, v rounded to bf16 as the unfused qkv buffer is); x: [nseq, L, C]."""
+    c = x.shape[-1]
+    dh = c // nhead
+    qkv = (x @ wqkv.t() + bqkv).bfloat16().float()
+    q, k, v = (t.reshape(*x.shape[:2], nhead, dh).transpose(1, 2) for t in qkv.split(c, -1))
+    a = torch.softmax(q @ k.transpose(-1, -2) / dh ** 0.5, -1)
+    o = (a @ v).transpose(1, 2).reshape(x.shape).bfloat16().float()
+    return o @ wo.t() + bo
+
+
+@pytest.mark.parametrize("mode", ["within", "across", "across_post", "within_tail"])
+def test_mha_layernorm(mode):
+    """dp_mha_layernorm (the decoder's within / across token attention + out_proj + residual +
+    LN, transformer.py:403-422) against torch fp32 on the same bf16 inputs: within = groups of
+    18 contiguous rows; across = the 60 queries of a token slot, rows 18 apart, with and
+    without the keypoint-row pos re-add; within_tail: a sequence count that leaves a partial
+    last block."""
+    g = torch.Generator().manual_seed(11 + len(mode))
+    c, nh, T, nq = 256, 8, 18, 60
+    B = 2
+    nseq_w = B * nq - (5 if mode == "within_tail" else 0)
+    rows = B * nq * T
+    x = _bf(rows, c, g=g)
+    wqkv = _bf(3 * c, c, scale=c ** -0.5, g=g)
+    wo = _bf(c, c, scale=c ** -0.5, g=g)
+    bqkv, bo = torch.randn(3 * c, generator=g) * 0.1, torch.randn(c, generator=g) * 0.1
+    gamma, beta = 1 + 0.1 * torch.randn(c, generator=g), 0.1 * torch.randn(c, generator=g)
+    krows = rows // T * (T - 1)
+    pos = _bf(krows, c, g=g)
+    post = mode == "across_post"
+    ld = 2 * c
+    out = torch.zeros(rows, ld, dtype=torch.bfloat16, device="cuda")
+    dx, dpos = x.cuda(), pos.cuda()
+    dq, dbq, dwo, dbo, dg, dbe = (t.cuda() for t in (frag_pack(wqkv), bqkv, frag_pack(wo), bo, gamma, beta))
+    if mode.startswith("within"):
+        geo = (nseq_w, 1, T, 0, 1, T)
+    else:
+        geo = (B, T, nq * T, 1, T, nq)
+    lib = _lib.load()
+    _lib.check(lib.dp_mha_layernorm(out.data_ptr(), contiguous_rows(ld), dx.data_ptr(), contiguous_rows(c), *geo,
+                                    dq.data_ptr(), dbq.data_ptr(), dwo.data_ptr(), dbo.data_ptr(), dg.data_ptr(),
+                                    dbe.data_ptr(), C.c_float(1e-5), c, nh, dpos.data_ptr() if post else None,
+                                    contiguous_rows(c), T, 1, _s()), "dp_mha_layernorm")
+    torch.cuda.synchronize()
+    xf = x.float()
+    if mode.startswith("within"):
+        seqs = xf[:nseq_w * T].reshape(nseq_w, T, c)
+        y = _mha_ref(seqs, wqkv.float(), bqkv, wo.float(), bo, nh)
+        ref = _ln(seqs + y, gamma, beta).reshape(-1, c)
+        got = out[:nseq_w * T, :c].float().cpu()
+        assert (out[nseq_w * T:] == 0).all()
+    else:
+        seqs = xf.reshape(B, nq, T, c).transpose(1, 2).reshape(B * T, nq, c)
+        y = _mha_ref(seqs, wqkv.float(), bqkv, wo.float(), bo, nh)
+        ref = _ln(seqs + y, gamma, beta).reshape(B, T, nq, c).transpose(1, 2).reshape(rows, c)
+        if post:
+            ref = ref.reshape(rows // T, T, c)
+            ref[:, 1:] += pos.float().reshape(rows // T, T - 1, c)
+            ref = ref.reshape(rows, c)
+        got = out[:, :c].float().cpu()
+    err = (got - ref).abs().max().item()
+    assert err <= TOL, f"{mode}: max err {err:.3g}"
+    assert (out[:, c:] == 0).all()
