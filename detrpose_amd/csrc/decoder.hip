@@ -345,7 +345,7 @@ __global__ __launch_bounds__(C * 2) void linear_ln_kernel(bf16_t* out, dp_rowmap
 //      across attention's pos re-add on keypoint rows) -> out.
 // HBM: x read once (+ the residual re-read from L2), out written once: the qkv (3C) and
 // attention-output (C) round trips of the unfused path are gone.
-template <int SEQ, int GB, bool POST>
+template <int SEQ, int GB, bool POST, int DHP>
 __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, const bf16_t* x, dp_rowmap xm,
                                                      int n_inner, int64_t so, int64_t si, int64_t st, int nseq,
                                                      const bf16_t* __restrict__ wqkv, const float* __restrict__ bqkv,
@@ -355,7 +355,8 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
                                                      int post_group, int post_skip) {
   constexpr int C = 256, NW = 8, NTH = 512, DH = 32;
   constexpr int RR = SEQ * GB, TM = (RR + 15) / 16, R = 16 * TM;
-  constexpr int DHP = 48;                      // V row pitch (elements): conflict-free tr reads
+  // DHP: V row pitch (elements). 48 makes the transposed reads conflict-free, 32 keeps the
+  // block under 80 KB of LDS (two blocks per CU)
   constexpr int VR = R + 16;                   // + one zero tile: the last key pair's upper half
   typedef short s4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) char smem[R * C * 2 + NW * VR * DHP * 2 + NW * R * 4];
@@ -1033,20 +1034,26 @@ extern "C" int dp_mha_layernorm(void* out, dp_rowmap om, const void* x, dp_rowma
              "dp_mha_layernorm: token rows exceed 2^31");
   hipStream_t s = as_stream(stream);
   const float scale = 1.f / sqrtf(32.f);
+#ifndef DP_MHA_DHP
+#define DP_MHA_DHP 48   // 32 (two blocks per CU by LDS, but not by registers): 86 -> 130 us within, spills
+#endif
+#ifndef DP_MHA_GBW
+#define DP_MHA_GBW 4
+#endif
 #define DP_MHA(SEQ_, GB_)                                                                                          \
   do {                                                                                                             \
     dim3 grid((unsigned)((nseq + GB_ - 1) / GB_));                                                                 \
     if (post)                                                                                                      \
-      hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, true>), grid, dim3(512), 0, s, (bf16_t*)out, om, (const bf16_t*)x, \
+      hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, true, DP_MHA_DHP>), grid, dim3(512), 0, s, (bf16_t*)out, om, (const bf16_t*)x, \
                          xm, n_inner, so, si, st, (int)nseq, (const bf16_t*)wqkv, bqkv, (const bf16_t*)wo, bo, gamma,  \
                          beta, eps, scale, (const bf16_t*)post, pm, post_group, post_skip);                         \
     else                                                                                                           \
-      hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, false>), grid, dim3(512), 0, s, (bf16_t*)out, om, (const bf16_t*)x, \
+      hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, false, DP_MHA_DHP>), grid, dim3(512), 0, s, (bf16_t*)out, om, (const bf16_t*)x, \
                          xm, n_inner, so, si, st, (int)nseq, (const bf16_t*)wqkv, bqkv, (const bf16_t*)wo, bo, gamma,  \
                          beta, eps, scale, (const bf16_t*)nullptr, pm, 1, 0);                                       \
     return dp_check_launch("dp_mha_layernorm");                                                                    \
   } while (0)
-  if (seqlen == 18) DP_MHA(18, 4);   // within-instance: the 1 + 17 tokens of a query
+  if (seqlen == 18) DP_MHA(18, DP_MHA_GBW);   // within-instance: the 1 + 17 tokens of a query
   if (seqlen == 60) DP_MHA(60, 1);   // across-instance: the 60 queries of a token slot
 #undef DP_MHA
   dp_set_error("dp_mha_layernorm: seqlen %d not instantiated (18 / 60)", seqlen);
