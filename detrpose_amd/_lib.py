@@ -95,8 +95,9 @@ _SIGS = {
     "dp_linear_layernorm": (i32, [vp, RowMap, vp, RowMap, i32, vp, vp, vp, RowMap, vp, vp, f32, i32, i32, vp, RowMap,
                                   i32, i32, vp]),
     "dp_gate_linear_layernorm": (i32, [vp, RowMap, vp, RowMap, vp, vp, vp, vp, f32, i32, i32, vp]),
+    "dp_linear_layernorm_classmax": (i32, [vp, vp, i32, i32, vp, vp, vp, vp, f32, vp, i32, vp, vp, vp, i32, vp, vp]),
     "dp_mha_layernorm": (i32, [vp, RowMap, vp, RowMap, i32, i32, i64, i64, i64, i32, vp, vp, vp, vp, vp, vp, f32, i32,
-                               i32, vp, RowMap, i32, i32, vp]),
+                               i32, vp, RowMap, i32, i32, vp, i32, vp, vp, i32, vp]),
     "dp_ffn_layernorm": (i32, [vp, RowMap, vp, RowMap, vp, vp, i32, vp, vp, vp, vp, f32, i32, i32, vp]),
     "dp_query_pos": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, RowMap, i32, vp]),
     "dp_pose_mlp": (i32, [vp, RowMap, vp, RowMap, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, vp]),

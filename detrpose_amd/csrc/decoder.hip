@@ -327,6 +327,95 @@ __global__ __launch_bounds__(C * 2) void linear_ln_kernel(bf16_t* out, dp_rowmap
   }
 }
 
+// ------------------------------------------------------------------ enc_output + LN + class max
+// The two-stage selection head (transformer.py:1232-1240) in one pass over memory's rows:
+// output_memory = LayerNorm(enc_output(memory)) with the border/invalid rows replaced by
+// masked_row (= LN(enc_output bias), the reference's masked_fill(0) then Linear), and the
+// class-score max over the STORED (bf16) row, as dp_layernorm_classmax computes it. The
+// enc_output GEMM runs as linear_ln_kernel's; the class dot products are reduced over the
+// lane groups by shuffles and over the waves through LDS.
+template <int C, int BM>
+__global__ __launch_bounds__(C * 2) void linear_ln_cls_kernel(bf16_t* out, const bf16_t* x,
+                                                              const bf16_t* __restrict__ w, const float* __restrict__ b,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps, int rows,
+                                                              const uint8_t* __restrict__ mask, int mask_period,
+                                                              const float* __restrict__ masked_row,
+                                                              const float* __restrict__ cw,
+                                                              const float* __restrict__ cbias, int ncls,
+                                                              float* __restrict__ cls_out) {
+  constexpr int NW = C / 32, NTH = 64 * NW, TM = BM / 16, K = C, MAXCLS = 4;
+  __shared__ __attribute__((aligned(16))) char smem[BM * K * 2 + MAXCLS * NW * BM * 4];
+  char* xl = smem;
+  float* red = reinterpret_cast<float*>(smem + BM * K * 2);
+  const int row0 = blockIdx.x * BM;
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const int wbase = wv * 32, cb = wbase + g * NV;
+  const dp_rowmap xm{0, 1, K, 0};   // contiguous rows
+  Stage<K, BM, NTH, false> st;
+  st.load(x, xm, nullptr, xm, row0, rows);
+  const bf16_t* wb = frag_base(w, wv, K / 32);
+  WPipe p;
+  pipe_start(p, wb);
+  float bias[NV], gg[NV], bb[NV];
+  load_bias(b, cb, bias);
+  load_bias(gamma, cb, gg);
+  load_bias(beta, cb, bb);
+  st.store(xl, row0, rows);
+  lds_barrier();
+  f32x4 acc[TM][TN];
+  zero_acc<TM>(acc);
+  wave_gemm<K, TM>(acc, xl, wb, p, wb);
+  float v[TM][NV];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float a[NV];
+    lane_vals<TM>(acc, i, a);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[i][e] = a[e] + bias[e];
+  }
+  layernorm_rows<TM, NW>(v, gg, bb, eps, red);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = row0 + 16 * i + q;
+    if (mask && r < rows && mask[(unsigned)r % (unsigned)mask_period]) {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) v[i][e] = masked_row[cb + e];
+    }
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[i][e] = (float)(bf16_t)v[i][e];   // the stored value
+    if (r < rows) store_row_vals(out + (int64_t)r * K + cb, v[i]);
+  }
+  // class scores: per-wave partial dot products of the lane's 8 channels, lane groups by
+  // shuffles, waves through LDS
+  for (int j = 0; j < ncls; ++j) {
+    float cwv[NV];
+    load_bias(cw + j * K, cb, cwv);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float sj = 0.f;
+#pragma unroll
+      for (int e = 0; e < NV; ++e) sj = fmaf(v[i][e], cwv[e], sj);
+      sj += __shfl_xor(sj, 16, 64);
+      sj += __shfl_xor(sj, 32, 64);
+      if (g == 0) red[(j * NW + wv) * BM + 16 * i + q] = sj;
+    }
+  }
+  lds_barrier();
+  for (int t = threadIdx.x; t < BM; t += NTH) {
+    const int r = row0 + t;
+    if (r >= rows) continue;
+    float best = -INFINITY;
+    for (int j = 0; j < ncls; ++j) {
+      float sj = cbias[j];
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) sj += red[(j * NW + ww) * BM + t];
+      best = fmaxf(best, sj);
+    }
+    cls_out[r] = best;
+  }
+}
+
 // ------------------------------------------------------------------ fused MHA + out_proj + res + LN
 // nn.MultiheadAttention(q = k = v = x) + residual + LayerNorm of the decoder layer's two token
 // attentions (transformer.py:403-422): within-instance (the T tokens of a query, rows
@@ -345,14 +434,16 @@ __global__ __launch_bounds__(C * 2) void linear_ln_kernel(bf16_t* out, dp_rowmap
 //      across attention's pos re-add on keypoint rows) -> out.
 // HBM: x read once (+ the residual re-read from L2), out written once: the qkv (3C) and
 // attention-output (C) round trips of the unfused path are gone.
-template <int SEQ, int GB, bool POST, int DHP>
+template <int SEQ, int GB, bool POST, int DHP, bool NEXT>
 __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, const bf16_t* x, dp_rowmap xm,
                                                      int n_inner, int64_t so, int64_t si, int64_t st, int nseq,
                                                      const bf16_t* __restrict__ wqkv, const float* __restrict__ bqkv,
                                                      const bf16_t* __restrict__ wo, const float* __restrict__ bo,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      float eps, float scale, const bf16_t* post, dp_rowmap pm,
-                                                     int post_group, int post_skip) {
+                                                     int post_group, int post_skip, bf16_t* __restrict__ nout,
+                                                     int nout_ld, const bf16_t* __restrict__ wn,
+                                                     const float* __restrict__ bn, int nn) {
   constexpr int C = 256, NW = 8, NTH = 512, DH = 32;
   constexpr int RR = SEQ * GB, TM = (RR + 15) / 16, R = 16 * TM;
   // DHP: V row pitch (elements). 48 makes the transposed reads conflict-free, 32 keeps the
@@ -550,6 +641,34 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
       }
     }
     store_row_vals(out + rowmap_off(om, r) + ocb, v[i]);
+  }
+  if constexpr (NEXT) {
+    // 4. the next Linear on the rows just stored (the across attention's output + pos is the
+    //    MSDA query: its sampling-offset / attention-logit projection, ms_deform_attn.py:
+    //    428-432), straight from registers: the stored bf16 rows -> the LDS image (every wave
+    //    is past the out_proj GEMM: layernorm_rows' barriers), nn / 32 channel blocks over the
+    //    waves, + bias, 16-byte stores.
+#pragma unroll
+    for (int i = 0; i < TM; ++i) put_lds_row<C>(xl, 16 * i + q, ocb, v[i]);
+    lds_barrier();
+    for (int nb = wv; nb < nn / 32; nb += NW) {
+      const bf16_t* wnb = frag_base(wn, nb, C / 32);
+      pipe_start(p, wnb);
+      zero_acc<TM>(acc);
+      wave_gemm<C, TM>(acc, xl, wnb, p, wnb);
+      float nbias[NV];
+      load_bias(bn, 32 * nb + cb, nbias);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = row_of(16 * i + q);
+        if (r < 0) continue;
+        float a[NV];
+        lane_vals<TM>(acc, i, a);
+#pragma unroll
+        for (int e = 0; e < NV; ++e) a[e] += nbias[e];
+        store_row_vals(nout + (int64_t)r * nout_ld + 32 * nb + cb, a);
+      }
+    }
   }
 }
 
@@ -1022,13 +1141,17 @@ extern "C" int dp_mha_layernorm(void* out, dp_rowmap om, const void* x, dp_rowma
                                 int32_t n_inner, int64_t so, int64_t si, int64_t st, int32_t seqlen, const void* wqkv,
                                 const float* bqkv, const void* wo, const float* bo, const float* gamma,
                                 const float* beta, float eps, int32_t c, int32_t nhead, const void* post, dp_rowmap pm,
-                                int32_t post_group, int32_t post_skip, void* stream) {
+                                int32_t post_group, int32_t post_skip, void* next_out, int32_t next_ld,
+                                const void* next_w, const float* next_b, int32_t next_n, void* stream) {
   DP_REQUIRE(out && x && wqkv && bqkv && wo && bo && gamma && beta && n_outer > 0 && n_inner > 0,
              "dp_mha_layernorm: bad args");
   DP_REQUIRE(al16(out) && al16(x) && al16(wqkv) && al16(wo) && map16(om) && map16(xm) &&
                  (!post || (al16(post) && map16(pm) && post_group > post_skip)),
              "dp_mha_layernorm: rows must be 16-byte aligned");
   DP_REQUIRE(c == 256 && nhead == 8, "dp_mha_layernorm: C = 256 with 8 heads only (got %d / %d)", c, nhead);
+  DP_REQUIRE(!next_out || (next_w && next_b && next_n > 0 && next_n % 32 == 0 && next_ld % 8 == 0 && next_ld >= next_n &&
+                           al16(next_out) && al16(next_w)),
+             "dp_mha_layernorm: next linear needs n %% 32 == 0, 16-byte aligned rows");
   const int64_t nseq = (int64_t)n_outer * n_inner;
   DP_REQUIRE((int64_t)(n_outer - 1) * so + (int64_t)(n_inner - 1) * si + (int64_t)(seqlen - 1) * st < (1ll << 31),
              "dp_mha_layernorm: token rows exceed 2^31");
@@ -1040,22 +1163,45 @@ extern "C" int dp_mha_layernorm(void* out, dp_rowmap om, const void* x, dp_rowma
 #ifndef DP_MHA_GBW
 #define DP_MHA_GBW 4
 #endif
+#define DP_MHA_L(SEQ_, GB_, POST_, NEXT_)                                                                          \
+  hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, POST_, DP_MHA_DHP, NEXT_>), grid, dim3(512), 0, s, (bf16_t*)out, om,   \
+                     (const bf16_t*)x, xm, n_inner, so, si, st, (int)nseq, (const bf16_t*)wqkv, bqkv,              \
+                     (const bf16_t*)wo, bo, gamma, beta, eps, scale, (const bf16_t*)post, pm, POST_ ? post_group : 1, \
+                     POST_ ? post_skip : 0, (bf16_t*)next_out, next_ld, (const bf16_t*)next_w, next_b, next_n)
 #define DP_MHA(SEQ_, GB_)                                                                                          \
   do {                                                                                                             \
     dim3 grid((unsigned)((nseq + GB_ - 1) / GB_));                                                                 \
-    if (post)                                                                                                      \
-      hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, true, DP_MHA_DHP>), grid, dim3(512), 0, s, (bf16_t*)out, om, (const bf16_t*)x, \
-                         xm, n_inner, so, si, st, (int)nseq, (const bf16_t*)wqkv, bqkv, (const bf16_t*)wo, bo, gamma,  \
-                         beta, eps, scale, (const bf16_t*)post, pm, post_group, post_skip);                         \
-    else                                                                                                           \
-      hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, false, DP_MHA_DHP>), grid, dim3(512), 0, s, (bf16_t*)out, om, (const bf16_t*)x, \
-                         xm, n_inner, so, si, st, (int)nseq, (const bf16_t*)wqkv, bqkv, (const bf16_t*)wo, bo, gamma,  \
-                         beta, eps, scale, (const bf16_t*)nullptr, pm, 1, 0);                                       \
+    if (post && next_out) DP_MHA_L(SEQ_, GB_, true, true);                                                         \
+    else if (post) DP_MHA_L(SEQ_, GB_, true, false);                                                               \
+    else if (next_out) DP_MHA_L(SEQ_, GB_, false, true);                                                           \
+    else DP_MHA_L(SEQ_, GB_, false, false);                                                                        \
     return dp_check_launch("dp_mha_layernorm");                                                                    \
   } while (0)
   if (seqlen == 18) DP_MHA(18, DP_MHA_GBW);   // within-instance: the 1 + 17 tokens of a query
   if (seqlen == 60) DP_MHA(60, 1);   // across-instance: the 60 queries of a token slot
 #undef DP_MHA
+#undef DP_MHA_L
   dp_set_error("dp_mha_layernorm: seqlen %d not instantiated (18 / 60)", seqlen);
   return DP_EINVAL;
+}
+
+extern "C" int dp_linear_layernorm_classmax(void* out, const void* x, int32_t rows, int32_t c, const void* w,
+                                            const float* b, const float* gamma, const float* beta, float eps,
+                                            const uint8_t* row_mask, int32_t mask_period, const float* masked_row,
+                                            const float* cls_w, const float* cls_b, int32_t nclass, float* cls_out,
+                                            void* stream) {
+  DP_REQUIRE(out && x && w && b && gamma && beta && cls_w && cls_b && cls_out && rows > 0,
+             "dp_linear_layernorm_classmax: bad args");
+  DP_REQUIRE(al16(out) && al16(x) && al16(w), "dp_linear_layernorm_classmax: rows must be 16-byte aligned");
+  DP_REQUIRE(c == 256 && nclass >= 1 && nclass <= 4, "dp_linear_layernorm_classmax: c=%d (256), nclass=%d (1..4)", c,
+             nclass);
+  DP_REQUIRE(!row_mask || (mask_period > 0 && masked_row), "dp_linear_layernorm_classmax: bad mask");
+  DP_REQUIRE((int64_t)rows * c < (1ll << 40), "dp_linear_layernorm_classmax: too many rows");
+  hipStream_t s = as_stream(stream);
+  constexpr int BM = 128;
+  dim3 grid((rows + BM - 1) / BM);
+  hipLaunchKernelGGL((linear_ln_cls_kernel<256, BM>), grid, dim3(512), 0, s, (bf16_t*)out, (const bf16_t*)x,
+                     (const bf16_t*)w, b, gamma, beta, eps, rows, row_mask, mask_period, masked_row, cls_w, cls_b,
+                     nclass, cls_out);
+  return dp_check_launch("dp_linear_layernorm_classmax");
 }

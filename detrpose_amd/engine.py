@@ -458,7 +458,7 @@ class Engine:
             if self.code == _lib.DP_BF16:
                 # MFMA-fragment copies for the row-block fused kernels (detrpose_amd/fragments.py)
                 L["frag"] = {k: frag_pack(L[k].w) for k in ("within_out", "across_out", "gate", "ffn1", "ffn2",
-                                                             "within_qkv", "across_qkv")}
+                                                             "within_qkv", "across_qkv", "offattn")}
                 L["frag"]["pose"] = [frag_pack(pc.w) for pc in L["pose"]]
             # class / LQE heads of every layer: the inference plan runs the last layer's
             # (eval_idx), the training-mode plan all of them (transformer.py:726-728)
@@ -794,12 +794,28 @@ class Engine:
         rows_m = B * S
         # ---- two-stage selection (transformer.py:1228-1254)
         mem_rows = FMap(memory, 0, 1, 1, rows_m, Cc, Cc, rows_m * Cc)
-        eo = self._fmap(1, 1, rows_m, Cc)
-        self._conv(plan, "ts.enc_output", mem_rows, P["enc_output"], eo)
         om = self._fmap(1, 1, rows_m, Cc)
         score = self._empty(rows_m, dtype=torch.float32)
         wc, bc = P["enc_cls"]
-        if self.code == _lib.DP_BF16 and wc.shape[0] <= 4:
+        if (self.code == _lib.DP_BF16 and wc.shape[0] <= 4 and Cc == 256
+                and not os.environ.get("DETRPOSE_NO_ENC_FUSE")):
+            # enc_output + LN + masked rows + class max in one row-block pass (no eo round trip)
+            g_, b_ = P["enc_norm"]
+            eof = P.get("enc_output_frag")
+            if eof is None:
+                eof = P["enc_output_frag"] = frag_pack(P["enc_output"].w)
+            plan._op("ts.enc_out_ln", lib.dp_linear_layernorm_classmax, om.ptr, memory.data_ptr(), rows_m, Cc,
+                     eof.data_ptr(), P["enc_output"].b.data_ptr(), g_.data_ptr(), b_.data_ptr(), C.c_float(1e-5),
+                     P["mask"].data_ptr(), S, P["masked_row"].data_ptr(), wc.data_ptr(), bc.data_ptr(), wc.shape[0],
+                     score.data_ptr())
+            plan.op_flops["ts.enc_out_ln"] = 2.0 * rows_m * Cc * Cc
+            eo = None
+        else:
+            eo = self._fmap(1, 1, rows_m, Cc)
+            self._conv(plan, "ts.enc_output", mem_rows, P["enc_output"], eo)
+        if eo is None:
+            pass
+        elif self.code == _lib.DP_BF16 and wc.shape[0] <= 4:
             # LN + class-score max in one pass over the rows (dp_layernorm_classmax)
             g_, b_ = P["enc_norm"]
             plan._op("ts.enc_norm", lib.dp_layernorm_classmax, om.ptr, eo.ptr, g_.data_ptr(), b_.data_ptr(),
@@ -953,11 +969,12 @@ class Engine:
                 plan._op(n + ".w_mha", lib.dp_mha_layernorm, dst.data_ptr(), cr(Cc), src.data_ptr(), cr(Cc), B * nq, 1,
                          T, 0, 1, T, *lin(L["within_qkv"], fr["within_qkv"], Cc),
                          *lin(L["within_out"], fr["within_out"], Cc), wn[0].data_ptr(), wn[1].data_ptr(), eps, Cc, nh,
-                         None, rowmap(group=1), 1, 0)
+                         None, rowmap(group=1), 1, 0, None, 0, None, None, 0)
+                # + the MSDA offsets/logits Linear on the rows it stores (ms_deform_attn.py:428-432)
                 plan._op(n + ".a_mha", lib.dp_mha_layernorm, gx.data_ptr(), cr(2 * Cc), dst.data_ptr(), cr(Cc), B, T,
                          nq * T, 1, T, nq, *lin(L["across_qkv"], fr["across_qkv"], Cc),
                          *lin(L["across_out"], fr["across_out"], Cc), an[0].data_ptr(), an[1].data_ptr(), eps, Cc, nh,
-                         pos.ptr, cr(Cc), T, 1)
+                         pos.ptr, cr(Cc), T, 1, oa.ptr, oa.ps, *lin(L["offattn"], fr["offattn"], Cc), oa.C)
                 mha_flops = 2.0 * rows * Cc * 4 * Cc
                 plan.op_flops[n + ".w_mha"] = plan.op_flops[n + ".a_mha"] = mha_flops
             else:
@@ -991,7 +1008,8 @@ class Engine:
                              contiguous_rows(Cc), ao.ptr, contiguous_rows(Cc), L["across_norm"], rows, Cc,
                              post=(pos.ptr, contiguous_rows(Cc)), post_group=T, post_skip=1)
             # MSDA (ms_deform_attn.py:384-444) -> gx[:, C:]
-            self._conv(plan, n + ".offattn", gx_f.ch(0, Cc), L["offattn"], oa)
+            if not mha:
+                self._conv(plan, n + ".offattn", gx_f.ch(0, Cc), L["offattn"], oa)
             plan._op(n + ".msda", lib.dp_msda, memory.data_ptr(), B, S, lvl_hw, len(shapes), oa.ptr, ref.data_ptr(),
                      gx.data_ptr() + Cc * e, 2 * Cc, nq * T, nh, Cc // nh, npnt, self.code)
             # SURVEY.md §8d algorithmic bytes: value once + offsets/logits + ref + output

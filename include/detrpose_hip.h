@@ -264,6 +264,16 @@ int dp_postprocess(const float* logits, const float* kps, const float* target_si
  * A block owns 64 token rows and all c channels, so the row-wise op after each GEMM runs
  * in its epilogue. Weights bf16 [n][k] (nn.Linear layout), biases f32. */
 
+/* enc_output Linear + LayerNorm + masked rows + class-score max of the two-stage selection
+ * (transformer.py:1232-1240) in one pass: out = LN(x . w^T + b) (rows with
+ * row_mask[r % mask_period] != 0 take masked_row), cls_out[r] = max_j (out[r] . cls_w[j] +
+ * cls_b[j]) over the stored bf16 row. bf16, contiguous rows of c = 256, w in the fragment
+ * layout; replaces the enc_output dp_conv2d + dp_layernorm_classmax pair. */
+int dp_linear_layernorm_classmax(void* out, const void* x, int32_t rows, int32_t c, const void* w, const float* b,
+                                 const float* gamma, const float* beta, float eps, const uint8_t* row_mask,
+                                 int32_t mask_period, const float* masked_row, const float* cls_w,
+                                 const float* cls_b, int32_t nclass, float* cls_out, void* stream);
+
 /* The whole token self-attention block of the decoder layer in one launch:
  * out = LayerNorm(x + MHA(x, x, x) . wo^T + bo) (+ post as dp_linear_layernorm), with
  * MHA = nn.MultiheadAttention(C, nhead) (in_proj wqkv [3C][C] + bqkv, out_proj wo [C][C] + bo,
@@ -271,11 +281,15 @@ int dp_postprocess(const float* logits, const float* kps, const float* target_si
  * across_norm + the second in-place pos add (transformer.py:403-422). Token t of sequence
  * (o, ii) (o < n_outer, ii < n_inner, t < seqlen) is row o*so + ii*si + t*st of x and out.
  * C = 256 with 8 heads; seqlen 18 (within: the 1 + 17 tokens of a query) or 60 (across:
- * the queries of a token slot). out may not alias x. */
+ * the queries of a token slot). out may not alias x. With next_out: also
+ * next_out[r] = out[r] . next_w^T + next_b (next_n outputs, fragment layout) from the stored
+ * rows -- the MSDA sampling-offset / attention-logit projection of the across attention's
+ * output (ms_deform_attn.py:428-432). */
 int dp_mha_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, int32_t n_outer, int32_t n_inner,
                      int64_t so, int64_t si, int64_t st, int32_t seqlen, const void* wqkv, const float* bqkv,
                      const void* wo, const float* bo, const float* gamma, const float* beta, float eps, int32_t c,
                      int32_t nhead, const void* post, dp_rowmap pm, int32_t post_group, int32_t post_skip,
+                     void* next_out, int32_t next_ld, const void* next_w, const float* next_b, int32_t next_n,
                      void* stream);
 
 /* out = LayerNorm(x . w^T + b + res) (+ post on the rows the post map selects, as in

@@ -73,12 +73,13 @@ def main():
             "mhaw": (lambda: lib.dp_mha_layernorm(out2.data_ptr(), cr(c), x.data_ptr(), cr(c), nq, 1, T, 0, 1, T,
                                                   W["qkv"].data_ptr(), B["qkv"].data_ptr(), W["wo"].data_ptr(),
                                                   B["wo"].data_ptr(), gam.data_ptr(), bet.data_ptr(), eps, c, 8, None,
-                                                  cr(c), 1, 0, s),
+                                                  cr(c), 1, 0, None, 0, None, None, 0, s),
                      2 * rows * c * 2, 2 * rows * c * 4 * c),
             "mhaa": (lambda: lib.dp_mha_layernorm(out2.data_ptr(), cr(2 * c), x.data_ptr(), cr(c), bimg, T, nqi * T,
                                                   1, T, nqi, W["qkv"].data_ptr(), B["qkv"].data_ptr(),
                                                   W["wo"].data_ptr(), B["wo"].data_ptr(), gam.data_ptr(),
-                                                  bet.data_ptr(), eps, c, 8, pos.data_ptr(), cr(c), T, 1, s),
+                                                  bet.data_ptr(), eps, c, 8, pos.data_ptr(), cr(c), T, 1, None, 0, None, None,
+                                                  0, s),
                      3 * rows * c * 2, 2 * rows * c * 4 * c),
             "ln": (lambda: lib.dp_linear_layernorm(out2.data_ptr(), cr(2 * c), x.data_ptr(), cr(c), c,
                                                    W["wo"].data_ptr(), B["wo"].data_ptr(), res.data_ptr(), cr(c),

@@ -184,13 +184,14 @@ def _mha_ref(x, wqkv, bqkv, wo, bo, nhead):
     return o @ wo.t() + bo
 
 
-@pytest.mark.parametrize("mode", ["within", "across", "across_post", "within_tail"])
+@pytest.mark.parametrize("mode", ["within", "across", "across_post", "within_tail", "across_post_next"])
 def test_mha_layernorm(mode):
     """dp_mha_layernorm (the decoder's within / across token attention + out_proj + residual +
     LN, transformer.py:403-422) against torch fp32 on the same bf16 inputs: within = groups of
     18 contiguous rows; across = the 60 queries of a token slot, rows 18 apart, with and
     without the keypoint-row pos re-add; within_tail: a sequence count that leaves a partial
-    last block."""
+    last block; across_post_next: plus the fused next Linear (the MSDA offsets / logits
+    projection, 288 outputs) on the stored rows."""
     g = torch.Generator().manual_seed(11 + len(mode))
     c, nh, T, nq = 256, 8, 18, 60
     B = 2
@@ -203,7 +204,13 @@ def test_mha_layernorm(mode):
     gamma, beta = 1 + 0.1 * torch.randn(c, generator=g), 0.1 * torch.randn(c, generator=g)
     krows = rows // T * (T - 1)
     pos = _bf(krows, c, g=g)
-    post = mode == "across_post"
+    post = mode.startswith("across_post")
+    nxt = mode.endswith("next")
+    nn_ = 288
+    wn = _bf(nn_, c, scale=c ** -0.5, g=g)
+    bn = torch.randn(nn_, generator=g) * 0.1
+    nout = torch.zeros(rows, nn_, dtype=torch.bfloat16, device="cuda")
+    dwn, dbn = frag_pack(wn).cuda(), bn.cuda()
     ld = 2 * c
     out = torch.zeros(rows, ld, dtype=torch.bfloat16, device="cuda")
     dx, dpos = x.cuda(), pos.cuda()
@@ -216,7 +223,9 @@ def test_mha_layernorm(mode):
     _lib.check(lib.dp_mha_layernorm(out.data_ptr(), contiguous_rows(ld), dx.data_ptr(), contiguous_rows(c), *geo,
                                     dq.data_ptr(), dbq.data_ptr(), dwo.data_ptr(), dbo.data_ptr(), dg.data_ptr(),
                                     dbe.data_ptr(), C.c_float(1e-5), c, nh, dpos.data_ptr() if post else None,
-                                    contiguous_rows(c), T, 1, _s()), "dp_mha_layernorm")
+                                    contiguous_rows(c), T, 1, nout.data_ptr() if nxt else None, nn_,
+                                    dwn.data_ptr() if nxt else None, dbn.data_ptr() if nxt else None,
+                                    nn_ if nxt else 0, _s()), "dp_mha_layernorm")
     torch.cuda.synchronize()
     xf = x.float()
     if mode.startswith("within"):
@@ -237,3 +246,39 @@ def test_mha_layernorm(mode):
     err = (got - ref).abs().max().item()
     assert err <= TOL, f"{mode}: max err {err:.3g}"
     assert (out[:, c:] == 0).all()
+    if nxt:   # the next Linear runs on the STORED rows
+        nref = out[:, :c].float().cpu() @ wn.float().t() + bn
+        nerr = (nout.float().cpu() - nref).abs().max().item()
+        assert nerr <= TOL * max(1.0, nref.abs().max().item()), f"next linear: max err {nerr:.3g}"
+
+
+def test_linear_layernorm_classmax():
+    """dp_linear_layernorm_classmax (enc_output + enc_output_norm + masked rows + class max,
+    transformer.py:1232-1240) against torch fp32 on the same bf16 inputs; rows not a multiple
+    of the 128-row block; the class max is taken over the stored bf16 row."""
+    g = torch.Generator().manual_seed(5)
+    c, ncls, period = 256, 2, 70
+    rows = 128 * 9 + 77
+    x = _bf(rows, c, g=g)
+    w = _bf(c, c, scale=c ** -0.5, g=g)
+    b, gamma, beta = torch.randn(c, generator=g) * 0.1, 1 + 0.1 * torch.randn(c, generator=g), 0.1 * torch.randn(c, generator=g)
+    mask = (torch.rand(period, generator=g) < 0.2).to(torch.uint8)
+    masked_row = torch.randn(c, generator=g)
+    cw, cb = torch.randn(ncls, c, generator=g) * 0.1, torch.randn(ncls, generator=g)
+    out = torch.empty(rows, c, dtype=torch.bfloat16, device="cuda")
+    score = torch.empty(rows, device="cuda")
+    dev = [t.cuda() for t in (x, frag_pack(w), b, gamma, beta, mask, masked_row, cw, cb)]
+    lib = _lib.load()
+    _lib.check(lib.dp_linear_layernorm_classmax(out.data_ptr(), dev[0].data_ptr(), rows, c, dev[1].data_ptr(),
+                                                dev[2].data_ptr(), dev[3].data_ptr(), dev[4].data_ptr(),
+                                                C.c_float(1e-5), dev[5].data_ptr(), period, dev[6].data_ptr(),
+                                                dev[7].data_ptr(), dev[8].data_ptr(), ncls, score.data_ptr(), _s()),
+               "dp_linear_layernorm_classmax")
+    torch.cuda.synchronize()
+    ref = _ln(x.float() @ w.float().t() + b, gamma, beta)
+    m = mask.bool()[torch.arange(rows) % period]
+    ref[m] = masked_row
+    got = out.float().cpu()
+    assert (got - ref).abs().max().item() <= TOL
+    sref = (got @ cw.t() + cb).max(1).values        # class max over the stored rows
+    assert (score.cpu() - sref).abs().max().item() <= 1e-4
