@@ -57,7 +57,12 @@ struct HaloPool {
   int pstride;
 };
 
-template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false>
+// NKC > 0 (resident weights only): the K-step count is a compile-time constant, the K loop is
+// unrolled and every pixel-fragment address is a lane constant computed once per block (the
+// tile geometry is the same for every tile): no tap-table reads or address arithmetic
+// between the fragment reads of the MFMA loop.
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false,
+          int NKC = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 2)))
 void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int vec_ok, HaloPool pool) {
   static_assert(!POOL || (KH == 2 && KW == 2 && S == 1 && !DBUF), "pool: 2x2 s1 window, single patch buffer");
@@ -152,6 +157,26 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   const int q = lane & 15, g = lane >> 4;
   const int wm = wave;
   const int cin = d.cin;
+  constexpr int NKA = NKC > 0 ? NKC : 1;
+  int pfa[NKA][2][TM];   // NKC: byte offset (from the patch base) of the lane's pixel fragments
+  if constexpr (NKC > 0) {
+    static_assert(RESW, "compile-time K loop: resident weights only");
+#pragma unroll
+    for (int kt = 0; kt < NKC; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int k = kt * 64 + (4 * ks + g) * 8;
+        int tap = k / cin, ci = k - tap * cin;
+        if (tap >= ktaps) tap = 0, ci = 0;           // kpad tail: the weights are zero there
+        const int ky = tap / KW, kx = tap - ky * KW;
+        const int toff = ky * Gm::PW + kx, c8 = (ci >> 3) & 7;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int pr = (wm * TM + i) * S * Gm::PW + q * S + toff;
+          pfa[kt][ks][i] = (ci >> 6) * Gm::PLANE + pr * 128 + ((c8 ^ (pr & 7)) << 4);
+        }
+      }
+  }
 
   // EARLY (single patch buffer, no pool epilogue): the next tile's patch (and first weight
   // K-step) is issued as soon as every wave is done reading this tile's, so its latency
@@ -252,8 +277,33 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
                 wf[j], pf[i], (FIRST && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
       }
     };
-    step(0, std::true_type{});
-    for (int kt = 1; kt < nk; ++kt) step(kt, std::false_type{});
+    if constexpr (NKC > 0) {
+#pragma unroll
+      for (int kt = 0; kt < NKC; ++kt) {
+        const char* wsl = wbase + kt * BN * 128;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int cc = 4 * ks + g;
+          bf16x8 wf[TN], pf[TM];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int r = 16 * j + (lane & 15);
+            wf[j] = *reinterpret_cast<const bf16x8*>(wsl + r * 128 + ((cc ^ (r & 7)) << 4));
+          }
+#pragma unroll
+          for (int i = 0; i < TM; ++i) pf[i] = *reinterpret_cast<const bf16x8*>(pbase + pfa[kt][ks][i]);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  wf[j], pf[i], (kt == 0 && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
+        }
+      }
+    } else {
+      step(0, std::true_type{});
+      for (int kt = 1; kt < nk; ++kt) step(kt, std::false_type{});
+    }
     if constexpr (EARLY) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -337,9 +387,9 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   wait_vmcnt<0>();
 }
 
-template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false>
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false, int NKC = 0>
 int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloPool pool = {}) {
-  auto kern = conv_halo_kernel<TH, NW, KH, KW, S, BN, RESW, DBUF, ACT, POOL>;
+  auto kern = conv_halo_kernel<TH, NW, KH, KW, S, BN, RESW, DBUF, ACT, POOL, NKC>;
   static const int occ = [&] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
@@ -366,12 +416,15 @@ int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloP
   return dp_check_launch("dp_conv2d(halo)");
 }
 
-template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF = false, bool POOL = false>
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF = false, bool POOL = false, int NKC = 0>
 int launch_halo_act(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloPool pool = {}) {
   switch (d.act) {
-    case DP_ACT_RELU: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_RELU, POOL>(d, s, vec_ok, lds, pool);
-    case DP_ACT_SILU: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_SILU, POOL>(d, s, vec_ok, lds, pool);
-    case DP_ACT_NONE: return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_NONE, POOL>(d, s, vec_ok, lds, pool);
+    case DP_ACT_RELU:
+      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_RELU, POOL, NKC>(d, s, vec_ok, lds, pool);
+    case DP_ACT_SILU:
+      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_SILU, POOL, NKC>(d, s, vec_ok, lds, pool);
+    case DP_ACT_NONE:
+      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_NONE, POOL, NKC>(d, s, vec_ok, lds, pool);
     default: return -1;
   }
 }
@@ -394,8 +447,12 @@ int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
     constexpr int P16 = HaloGeom<16, 3, 3, 1>::PLANE, P8 = HaloGeom<8, 3, 3, 1>::PLANE;
     // 48 output channels (HG stage 0 of L/X): a 48-wide tile, 25% fewer MFMAs than 64
     if (d.cout == 48 && !d.res && !d.up && d.out_pstride % 4 == 0 && d.out_bstride % 4 == 0 &&
-        (reinterpret_cast<uintptr_t>(d.out) & 7) == 0 && lds_res48(P16, 2) <= LMAX)
+        (reinterpret_cast<uintptr_t>(d.out) & 7) == 0 && lds_res48(P16, 2) <= LMAX) {
+      static const bool rt_k = getenv("DETRPOSE_HALO_RTK") != nullptr;   // A/B: the runtime K loop
+      if (nk == 7 && !rt_k)   // cin 48: 9 x 48 = 432 -> 7 K-steps
+        return launch_halo_act<16, 8, 3, 3, 1, 48, true, true, false, 7>(d, s, vec_ok, lds_res48(P16, 2));
       return launch_halo_act<16, 8, 3, 3, 1, 48, true, true>(d, s, vec_ok, lds_res48(P16, 2));
+    }
     if (bn == 64 && lds_res(P16, 2) <= LMAX)
       return launch_halo_act<16, 8, 3, 3, 1, 64, true, true>(d, s, vec_ok, lds_res(P16, 2));
     if (bn == 32 && lds_res(P8, 1) <= 80 * 1024) return launch_halo_act<8, 4, 3, 3, 1, 32, true>(d, s, vec_ok, lds_res(P8, 1));

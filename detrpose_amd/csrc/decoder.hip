@@ -1198,7 +1198,10 @@ extern "C" int dp_linear_layernorm_classmax(void* out, const void* x, int32_t ro
   DP_REQUIRE(!row_mask || (mask_period > 0 && masked_row), "dp_linear_layernorm_classmax: bad mask");
   DP_REQUIRE((int64_t)rows * c < (1ll << 40), "dp_linear_layernorm_classmax: too many rows");
   hipStream_t s = as_stream(stream);
-  constexpr int BM = 128;
+#ifndef DP_ENC_BM
+#define DP_ENC_BM 64   // 64 rows: 40 KB LDS and <= 128 VGPRs, two blocks per CU overlap their phases
+#endif
+  constexpr int BM = DP_ENC_BM;
   dim3 grid((rows + BM - 1) / BM);
   hipLaunchKernelGGL((linear_ln_cls_kernel<256, BM>), grid, dim3(512), 0, s, (bf16_t*)out, (const bf16_t*)x,
                      (const bf16_t*)w, b, gamma, beta, eps, rows, row_mask, mask_period, masked_row, cls_w, cls_b,
