@@ -974,7 +974,21 @@ bool map16(const dp_rowmap& m) { return m.base % 8 == 0 && m.stride_g % 8 == 0 &
 // Rows per block: every kernel here runs one block per CU (LDS / registers), so a launch
 // takes ceil(blocks / CUs) rounds of equal length; pick the row tile with the least total
 // rows x rounds (ties: the larger tile, fewer weight re-reads). DETRPOSE_DEC_BM overrides.
-int pick_bm(int rows, int c, int max_bm = 128) {
+template <typename K>
+int blocks_per_cu(K kern, int threads) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kern), threads, 0) !=
+          hipSuccess ||
+      n < 1)
+    n = 1;
+  return n;
+}
+
+// Rows per block: the candidate whose launch runs the fewest row-rounds, a round being one
+// block per resident slot (occ = blocks per CU of that instantiation, by registers and LDS:
+// a 64-row block that fits twice per CU overlaps its load / GEMM / epilogue phases with the
+// other's).
+int pick_bm(int rows, int c, int max_bm = 128, int occ128 = 1, int occ96 = 1, int occ64 = 1) {
   static const int forced = [] {
     const char* e = getenv("DETRPOSE_DEC_BM");
     return e ? atoi(e) : 0;
@@ -990,7 +1004,8 @@ int pick_bm(int rows, int c, int max_bm = 128) {
   for (int bm : {128, 96, 64}) {
     if (bm > max_bm) continue;
     const int64_t blocks = (rows + bm - 1) / bm;
-    const int64_t cost = (blocks + cus - 1) / cus * bm;
+    const int64_t slots = (int64_t)cus * (bm == 128 ? occ128 : bm == 96 ? occ96 : occ64);
+    const int64_t cost = (blocks + slots - 1) / slots * bm;
     if (cost < best_cost) best_cost = cost, best = bm;
   }
   return best;
@@ -1017,7 +1032,14 @@ extern "C" int dp_linear_layernorm(void* out, dp_rowmap om, const void* x, dp_ro
              "dp_linear_layernorm: rows must be 16-byte aligned");
   DP_REQUIRE(k == c, "dp_linear_layernorm: k=%d != c=%d (out_proj only)", k, c);
   hipStream_t s = as_stream(stream);
-  const int bm = pick_bm(rows, c);
+  static const int ol1[3] = {blocks_per_cu(linear_ln_kernel<256, 128, true>, 512),
+                             blocks_per_cu(linear_ln_kernel<256, 96, true>, 512),
+                             blocks_per_cu(linear_ln_kernel<256, 64, true>, 512)};
+  static const int ol0[3] = {blocks_per_cu(linear_ln_kernel<256, 128, false>, 512),
+                             blocks_per_cu(linear_ln_kernel<256, 96, false>, 512),
+                             blocks_per_cu(linear_ln_kernel<256, 64, false>, 512)};
+  const int* ol = post ? ol1 : ol0;
+  const int bm = pick_bm(rows, c, 128, ol[0], ol[1], ol[2]);
   dim3 grid((rows + bm - 1) / bm);
 #define DP_LLN(C_, BM_)                                                                                            \
   do {                                                                                                             \
@@ -1094,7 +1116,9 @@ extern "C" int dp_query_pos(const float* ref, int32_t rows, int32_t nkp, const f
   DP_REQUIRE(ref && dim_t && w0 && b0 && w1 && b1 && pos && tgt && rows > 0 && nkp > 0, "dp_query_pos: bad args");
   DP_REQUIRE(al16(pos) && al16(tgt) && al16(w0) && al16(w1) && map16(tm), "dp_query_pos: rows must be 16-byte aligned");
   hipStream_t s = as_stream(stream);
-  const int bm = pick_bm(rows, c);
+  static const int oq[3] = {blocks_per_cu(query_pos_kernel<256, 128>, 512), blocks_per_cu(query_pos_kernel<256, 96>, 512),
+                            blocks_per_cu(query_pos_kernel<256, 64>, 512)};
+  const int bm = pick_bm(rows, c, 128, oq[0], oq[1], oq[2]);
   dim3 grid((rows + bm - 1) / bm);
 #define DP_QP(C_, BM_)                                                                                           \
   do {                                                                                                           \
@@ -1117,7 +1141,14 @@ extern "C" int dp_pose_mlp(const void* x, dp_rowmap xm, const void* x2, dp_rowma
   DP_REQUIRE(al16(x) && al16(w0) && al16(w1) && al16(w2) && map16(xm) && (!x2 || (al16(x2) && map16(x2m))),
              "dp_pose_mlp: rows must be 16-byte aligned");
   hipStream_t s = as_stream(stream);
-  const int bm = pick_bm(rows, c);
+  static const int op1[3] = {blocks_per_cu(pose_mlp_kernel<256, 128, true, true>, 512),
+                             blocks_per_cu(pose_mlp_kernel<256, 96, true, true>, 512),
+                             blocks_per_cu(pose_mlp_kernel<256, 64, true, true>, 512)};
+  static const int op0[3] = {blocks_per_cu(pose_mlp_kernel<256, 128, false, false>, 512),
+                             blocks_per_cu(pose_mlp_kernel<256, 96, false, false>, 512),
+                             blocks_per_cu(pose_mlp_kernel<256, 64, false, false>, 512)};
+  const int* op = x2 ? op1 : op0;
+  const int bm = pick_bm(rows, c, 128, op[0], op[1], op[2]);
   dim3 grid((rows + bm - 1) / bm);
 #define DP_PM(C_, BM_)                                                                                            \
   do {                                                                                                            \
