@@ -32,6 +32,7 @@ class ConvDesc(C.Structure):
         ("dtype", i32),
         ("up", vp), ("up_bstride", i64), ("up_pstride", i32),
         ("out_f32", i32),
+        ("in_seg_ch", i32), ("in_seg_stride", i64),
     ]
 
 

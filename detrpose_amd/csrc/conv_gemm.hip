@@ -248,6 +248,7 @@ int dispatch(const dp_conv_desc& d, hipStream_t s) {
   if (d.up) vec_ok = vec_ok && (d.up_pstride % VO == 0) && (d.up_bstride % VO == 0) && al(d.up);
   const int M = d.batch * d.out_h * d.out_w;
   if constexpr (sizeof(T) == 2) {
+    if (d.in_seg_ch) return dp_conv2d_stream(d, s, vec_ok);   // segmented input: the 1x1 GEMM path
     // bf16: LDS halo-tile kernel for the KxK convs it covers, persistent LDS-DMA GEMM otherwise
     if (d.kh <= 2 && d.cin <= 32) {   // the stem's 2x2 / 1x1 convs: register-direct kernels
       const int r = dp_conv2d_stem_direct(d, s, nullptr, 0, 0);
@@ -296,6 +297,12 @@ extern "C" int dp_conv2d(const dp_conv_desc* dp, void* stream) {
              "dp_conv2d: per-block input span / weight exceeds 2 GB of 32-bit buffer offsets");
   DP_REQUIRE(!d.out_f32 || (d.kh == 1 && d.kw == 1 && d.pad_t == 0 && d.pad_l == 0 && !d.up),
              "dp_conv2d: out_f32 is supported for 1x1 / linear layers without upsample");
+  DP_REQUIRE(!d.in_seg_ch || (d.dtype == DP_BF16 && d.kh == 1 && d.kw == 1 && d.stride == 1 && d.pad_t == 0 &&
+                              d.pad_l == 0 && d.in_seg_ch % 8 == 0 && d.cin % d.in_seg_ch == 0 &&
+                              d.in_seg_stride % 8 == 0 &&
+                              span + (d.cin / d.in_seg_ch - 1) * d.in_seg_stride * es < 0x7ff00000ll),
+             "dp_conv2d: segmented input only for bf16 1x1 convs, in_seg_ch %% 8 == 0 dividing cin, "
+             "segments within 2 GB of 32-bit offsets");
   hipStream_t s = as_stream(stream);
   if (d.dtype == DP_BF16) return d.out_f32 ? dispatch<bf16_t, float>(d, s) : dispatch<bf16_t, bf16_t>(d, s);
   return dispatch<float, float>(d, s);

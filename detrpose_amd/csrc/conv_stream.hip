@@ -31,7 +31,7 @@
 #define DP_ABL_NODMA 0     // ... drop the LDS-DMA loads
 #endif
 #ifndef DP_STREAM_PRIO
-#define DP_STREAM_PRIO 0   // A/B: s_setprio(1) around each K-step's fragment reads + MFMAs
+#define DP_STREAM_PRIO 1   // s_setprio(1) around each K-step's fragment reads + MFMAs (fpn1.cv1 +3.5%, s2.sq +2.4%, others flat)
 #endif
 #ifndef DP_ABL_NOMFMA
 #define DP_ABL_NOMFMA 0    // ... drop the MFMAs (fragment reads kept live)
@@ -265,9 +265,14 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
     const int kk = a_kt * 64 + chunk * 8;
     if (K1X1) {
       const bool kv = kk < d.cin;
+      int kofs = kk;
+      if (d.in_seg_ch) {   // segmented input: channel kk lives in segment kk / in_seg_ch
+        const int sg = (int)((unsigned)kk / (unsigned)d.in_seg_ch);
+        kofs = sg * (int)d.in_seg_stride + (kk - sg * d.in_seg_ch);
+      }
 #pragma unroll
       for (int t = 0; t < GA; ++t) {
-        const int o = (a_off[t] != OOB && kv) ? (a_off[t] + kk) * 2 : OOB;
+        const int o = (a_off[t] != OOB && kv) ? (a_off[t] + kofs) * 2 : OOB;
         if (!DP_ABL_NODMA) dma16(ra_src, sb + (wave + NW * t) * 1024, o);
       }
     } else {

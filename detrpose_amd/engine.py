@@ -482,7 +482,9 @@ class Engine:
         return FMap(t, 0, B, H, W, Cc, Cc, H * W * Cc)
 
     def _conv(self, plan, name, x: FMap, pc: PConv, out: FMap, res: FMap | None = None, up: FMap | None = None,
-              out_f32: bool = False, pool: FMap | None = None):
+              out_f32: bool = False, pool: FMap | None = None, seg: tuple | None = None):
+        """seg = (channels per segment, elements between segments): x is a segmented input
+        (dp_conv_desc.in_seg_ch / in_seg_stride), x.ps / x.bs the per-segment strides."""
         if pc.depthwise:
             assert x.C == pc.cin == out.C, (name, x.C, pc.cin, out.C)
         else:
@@ -512,6 +514,8 @@ class Engine:
             d.out_f32 = 1
         if pc.lab is not None:
             d.has_lab, d.lab_scale, d.lab_bias = 1, pc.lab[0], pc.lab[1]
+        if seg is not None:
+            d.in_seg_ch, d.in_seg_stride = seg
         plan.keep.append(d)
         plan.op_out[name] = out
         if not pc.depthwise:
@@ -582,23 +586,36 @@ class Engine:
             cin, midc, cout, nblk, down, light, ks, nl = st["cfg"]
             if down:
                 h, w = (h + 1) // 2, (w + 1) // 2
-            blocks_in = []
+            # a one-block stage whose input and layers have the same width keeps its HG-block
+            # concat as one contiguous map per member (the 3x3 layers then read and write whole
+            # 128-byte lines instead of 96-byte slices of 672-byte rows); the squeeze conv reads
+            # the members as a segmented input (dp_conv_desc.in_seg_ch)
+            segmented = (self.code == _lib.DP_BF16 and nblk == 1 and not light and cin == midc
+                         and not os.environ.get("DETRPOSE_NO_SEG_CONCAT"))
+            blocks_in, segs = [], None
             for bi in range(nblk):
                 bin_ = cin if bi == 0 else cout
-                blocks_in.append(self._fmap(B, h, w, bin_ + nl * midc))
+                if segmented:
+                    selems = B * h * w * cin
+                    t = self._empty((1 + nl) * selems)
+                    segs = [FMap(t, i * selems, B, h, w, cin, cin, h * w * cin) for i in range(1 + nl)]
+                    blocks_in.append(FMap(t, 0, B, h, w, cin * (1 + nl), cin, h * w * cin))
+                else:
+                    blocks_in.append(self._fmap(B, h, w, bin_ + nl * midc))
             # stage input -> block 0 concat slot [0:cin]
+            slot0 = segs[0] if segs else blocks_in[0].ch(0, cin)
             if si == 0 and fused:
-                self._stem_fused_op(plan, img, blocks_in[0].ch(0, cin))
+                self._stem_fused_op(plan, img, slot0)
             elif si == 0:
-                self._conv(plan, "stem4", x_src, P["stem4"], blocks_in[0].ch(0, cin))
+                self._conv(plan, "stem4", x_src, P["stem4"], slot0)
             else:
-                self._conv(plan, f"s{si}.down", x_src, st["down"], blocks_in[0].ch(0, cin))
+                self._conv(plan, f"s{si}.down", x_src, st["down"], slot0)
             for bi, blk in enumerate(st["blocks"]):
                 cb = blocks_in[bi]
                 bin_ = cin if bi == 0 else cout
-                prev = cb.ch(0, bin_)
+                prev = segs[0] if segs else cb.ch(0, bin_)
                 for li, layer in enumerate(blk["layers"]):
-                    dst = cb.ch(bin_ + li * midc, midc)
+                    dst = segs[li + 1] if segs else cb.ch(bin_ + li * midc, midc)
                     if light:
                         tmp = plan.bufs.get(("light_tmp", si))
                         if tmp is None:
@@ -610,7 +627,8 @@ class Engine:
                         self._conv(plan, f"s{si}.b{bi}.l{li}", prev, layer[0], dst)
                     prev = dst
                 sq = self._fmap(B, h, w, blk["squeeze"].cout)
-                self._conv(plan, f"s{si}.b{bi}.sq", cb, blk["squeeze"], sq)
+                self._conv(plan, f"s{si}.b{bi}.sq", cb, blk["squeeze"], sq,
+                           seg=(cin, segs[1].off - segs[0].off) if segs else None)
                 if bi + 1 < nblk:
                     dst = blocks_in[bi + 1].ch(0, cout)
                 else:

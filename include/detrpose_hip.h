@@ -49,6 +49,11 @@ typedef struct dp_conv_desc {
   void* up;        int64_t up_bstride;  int32_t up_pstride;
   /* out_f32 != 0: out (and res) are f32 whatever dtype is (1x1 / linear layers only) */
   int32_t out_f32;
+  /* in_seg_ch != 0 (bf16 1x1 convs): the input's channels are cin / in_seg_ch segments of
+   * in_seg_ch channels, segment s a map of its own at in + s * in_seg_stride elements (each
+   * with in_pstride / in_bstride): the HG-block concat stored one contiguous map per layer */
+  int32_t in_seg_ch;
+  int64_t in_seg_stride;
 } dp_conv_desc;
 
 /* Row map: row r -> element offset  base + (r / group)*stride_g + (r % group)*stride_r. */

@@ -105,6 +105,39 @@ def test_conv2d(dt, k, s, cin, cout, H, act):
     _close(out[..., :cout], ref.permute(0, 2, 3, 1) + resid[..., :cout], dt, f"conv k{k}s{s} {cin}->{cout}")
 
 
+@pytest.mark.parametrize("seg,nseg,cout,H,W", [(48, 7, 64, 64, 67), (16, 7, 32, 40, 41), (64, 7, 64, 30, 33)])
+def test_conv2d_1x1_segmented_input(seg, nseg, cout, H, W):
+    """The squeeze conv over an HG-block concat stored as one contiguous map per member
+    (dp_conv_desc.in_seg_ch / in_seg_stride; segments not adjacent in memory) vs torch fp32 on
+    the concatenated channels."""
+    torch.manual_seed(seg + H)
+    B, cin = 2, seg * nseg
+    pk = Packer({}, "bf16", torch.device("cuda"))
+    x = torch.randn(B, cin, H, W).bfloat16().float()
+    w = torch.randn(cout, cin, 1, 1) / cin ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pk.conv(w.double(), b.double(), act="relu")
+    ref = F.relu(F.conv2d(x, w, b)).permute(0, 2, 3, 1)
+    gap = 4096                                       # elements between one segment's end and the next
+    sel = B * H * W * seg
+    arena = torch.zeros(nseg * (sel + gap), device="cuda", dtype=torch.bfloat16)
+    for i in range(nseg):
+        arena[i * (sel + gap):i * (sel + gap) + sel] = \
+            x[:, i * seg:(i + 1) * seg].permute(0, 2, 3, 1).reshape(-1).to("cuda", torch.bfloat16)
+    _KEEP.append(arena)
+    out = torch.empty(B, H, W, cout, device="cuda", dtype=torch.bfloat16)
+    d = ConvDesc()
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = arena.data_ptr(), H * W * seg, seg, H, W, cin
+    d.weight, d.kpad, d.bias = pc.w.data_ptr(), pc.kpad, pc.b.data_ptr()
+    d.kh, d.kw, d.stride = 1, 1, 1
+    d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out.data_ptr(), H * W * cout, cout, H, W, cout
+    d.batch, d.act, d.dtype = B, pc.act, _lib.DP_BF16
+    d.in_seg_ch, d.in_seg_stride = seg, sel + gap
+    _lib.check(_lib.load().dp_conv2d(C.byref(d), _s()), "conv 1x1 segmented")
+    torch.cuda.synchronize()
+    _close(out, ref, "bf16", f"1x1 segmented {seg}x{nseg}->{cout}")
+
+
 @pytest.mark.parametrize("cin,cout,H,W,ld,off,mode,act", [
     (336, 64, 64, 67, 400, 32, "plain", "relu"),    # K tail (kpad 384), input = concat slice
     (512, 256, 48, 47, 512, 0, "up", "silu"),       # nearest-x2 epilogue
