@@ -39,6 +39,11 @@ __device__ int block_excl_scan(int v, int* buf, int* total) {
 __global__ __launch_bounds__(TOPK_THREADS) void topk_kernel(const float* __restrict__ x, int n, int ld, int k,
                                                             float* __restrict__ ov, int64_t* __restrict__ oi) {
   extern __shared__ uint32_t keys[];           // [n]
+  // NH copies of the digit histogram, lane l adding into copy l % NH: the sigmoid scores share
+  // their top key bytes, so one shared histogram serialises every wave on one or two bins
+  // (70 % of the kernel's LDS cycles were bank conflicts); the copies are summed per pass
+  constexpr int NH = 16, HP = 257;
+  __shared__ int hcopy[NH * HP];
   __shared__ int hist[256];
   __shared__ int scan_buf[TOPK_THREADS];
   __shared__ uint32_t s_prefix;
@@ -54,13 +59,21 @@ __global__ __launch_bounds__(TOPK_THREADS) void topk_kernel(const float* __restr
   }
   __syncthreads();
   uint32_t mask = 0;
+  int* const hmine = hcopy + (t % NH) * HP;
   for (int shift = 24; shift >= 0; shift -= 8) {
-    hist[t] = 0;
+    for (int e = t; e < NH * HP; e += TOPK_THREADS) hcopy[e] = 0;
     __syncthreads();
     const uint32_t prefix = s_prefix;
     for (int i = t; i < n; i += TOPK_THREADS) {
       const uint32_t kv = keys[i];
-      if ((kv & mask) == prefix) atomicAdd(&hist[(kv >> shift) & 255], 1);
+      if ((kv & mask) == prefix) atomicAdd(&hmine[(kv >> shift) & 255], 1);
+    }
+    __syncthreads();
+    {
+      int sum = 0;
+#pragma unroll
+      for (int c = 0; c < NH; ++c) sum += hcopy[c * HP + t];
+      hist[t] = sum;
     }
     __syncthreads();
     if (t == 0) {
