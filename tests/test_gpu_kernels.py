@@ -88,7 +88,7 @@ def _run_conv(pc, x_nhwc, out, dt, res=None, up=None):
     # planes, resident weights, stride 2 with 64 outputs, ragged tile edges
     (3, 1, 128, 128, 37, "silu"), (3, 1, 96, 96, 33, "relu"), (3, 1, 48, 48, 50, "relu"), (3, 2, 64, 64, 45, None),
     (2, 1, 16, 32, 29, "relu"), (3, 1, 256, 64, 21, "silu"),
-    # the 128-wide halo tile's 2 x 2 wave grid with the second wave column partly past cout
+    # the 128-wide halo tile with its last 16-byte channel chunks partly / wholly past cout
     (3, 1, 64, 112, 23, "relu"), (3, 1, 96, 100, 19, None)])
 def test_conv2d(dt, k, s, cin, cout, H, act):
     torch.manual_seed(k * 100 + cin)
