@@ -57,6 +57,14 @@ template <typename T>
 __device__ __forceinline__ void store16(T* p, const Vec16<T>& r) {
   *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(&r.v);
 }
+// non-temporal (streaming) 16-byte store: the halo convs' outputs (A/B on the L b64 3x3
+// shapes: -2..-4 %; on the 1x1 / decoder GEMMs, whose outputs the next kernel re-reads from
+// L2, it cost up to +13 %, so only conv_halo uses it)
+template <typename T>
+__device__ __forceinline__ void store16_nt(T* p, const Vec16<T>& r) {
+  typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(*reinterpret_cast<const u32x4_nt*>(&r.v), reinterpret_cast<u32x4_nt*>(p));
+}
 
 // ---------------------------------------------------------------- activations
 // sigmoid / SiLU through v_exp_f32 + v_rcp_f32 (1 ulp): a plain `/` compiles to the IEEE

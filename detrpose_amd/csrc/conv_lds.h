@@ -78,7 +78,8 @@ __device__ __forceinline__ bool vec_aligned(const dp_conv_desc& d) {
 
 // One output pixel's NPL = 4*TN channels of lane group g (lane_chan map over the wave's
 // channel base nbw) from the accumulators of one MFMA row-fragment: bias/act/LAB in f32,
-// residual add, 16-byte stores (scalar tail when the chunk is not whole or not aligned).
+// residual add, 16-byte non-temporal stores (scalar tail when the chunk is not whole or not
+// aligned).
 template <int ACT, typename TO, int TN>
 __device__ __forceinline__ void epi_pixel(const dp_conv_desc& d, const f32x4 (&acc)[TN], const float (&bias)[4 * TN],
                                           int b, int oy, int ox, int nbw, int g, bool full) {
@@ -118,7 +119,7 @@ __device__ __forceinline__ void epi_pixel(const dp_conv_desc& d, const f32x4 (&a
         for (int t = 0; t < VO; ++t) ch[c].set(t, v[c * VO + t]);
     }
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) store16(out + oo + c * 4 * VO, ch[c]);
+    for (int c = 0; c < CPL; ++c) store16_nt(out + oo + c * 4 * VO, ch[c]);
     if (up) {
       const int64_t ub = (int64_t)b * d.up_bstride + nb;
 #pragma unroll
@@ -127,7 +128,7 @@ __device__ __forceinline__ void epi_pixel(const dp_conv_desc& d, const f32x4 (&a
         for (int dx = 0; dx < 2; ++dx) {
           TO* upp = up + ub + ((int64_t)(2 * oy + dy) * (2 * d.out_w) + 2 * ox + dx) * d.up_pstride;
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) store16(upp + c * 4 * VO, ch[c]);
+          for (int c = 0; c < CPL; ++c) store16_nt(upp + c * 4 * VO, ch[c]);
         }
     }
   } else {
