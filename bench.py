@@ -69,6 +69,9 @@ def parse(argv=None):
     ap.add_argument("--latency-runs", type=int, default=1000)
     ap.add_argument("--latency-warmup", type=int, default=400)
     ap.add_argument("--profile-ops", type=str, default="", help="write per-op times (JSON) to this path")
+    ap.add_argument("--shared-gpu-rehearsal", action="store_true",
+                    help="N>1 on a one-GPU box: every rank on cuda:0, gloo collectives with host staging "
+                         "(checks the N-rank path on real kernels; not a scaling number)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="test hook: gloo on CPU with a stub step (checks launch, world size and gather order)")
     return ap.parse_args(argv)
@@ -234,7 +237,7 @@ def main():
     if a.cpu_dry_run:
         return cpu_dry_run(a)
     from detrpose_amd import dist as dp
-    rank, world, dev = dp.init("nccl")
+    rank, world, dev = dp.init("nccl", shared_gpu=a.shared_gpu_rehearsal)
     if world != a.gpus:
         raise SystemExit(f"bench: torch.distributed world size {world} != --gpus {a.gpus}")
     dist = dp.dist if world > 1 else None
@@ -355,6 +358,13 @@ def main():
             "kernel_ms_per_step": {k: round(v, 3) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])},
             "msda_algorithmic_gbs": round(msda_gbs, 1) if msda_gbs else None,
         }
+        if dist is not None:
+            # rank 0's slice of the all-gathered buffer is its own output (rank order kept)
+            n0 = plan.out_flat.numel()
+            out["gather_rank0_matches"] = bool(torch.equal(gathered[:n0], plan.out_flat))
+        if a.shared_gpu_rehearsal:
+            out["rehearsal"] = (f"{world} ranks sharing one GPU, gloo collectives with host staging: checks the "
+                                "N-rank launch/barrier/gather path on real kernels; not a scaling number")
         if world == 1 and not a.no_latency:
             out["latency_bs1"] = latency_bs1(model, pp, dev, a.latency_runs, a.latency_warmup)
         if world == 1 and not a.no_secondary:

@@ -24,11 +24,19 @@ def env_ranks() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str = "nccl") -> tuple[int, int, torch.device]:
+def init(backend: str = "nccl", shared_gpu: bool = False) -> tuple[int, int, torch.device]:
     """Initialise the process group when launched with WORLD_SIZE > 1 (backend 'nccl' is
-    RCCL on ROCm; 'gloo' for CPU tests). Returns (rank, world, device)."""
+    RCCL on ROCm; 'gloo' for CPU tests). Returns (rank, world, device).
+    shared_gpu: rehearsal of the N-rank path on a one-GPU box -- every rank computes on
+    cuda:0 and the collectives run on gloo with host staging (RCCL refuses two ranks on one
+    GPU); it checks the launcher, plan/graph per rank, barriers and the gather order on real
+    kernels, and is never a scaling measurement."""
     rank, world, local = env_ranks()
-    if backend == "nccl":
+    if shared_gpu:
+        backend = "gloo"
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+    elif backend == "nccl":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
@@ -37,6 +45,10 @@ def init(backend: str = "nccl") -> tuple[int, int, torch.device]:
         kw = {"device_id": dev} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
     return rank, world, dev
+
+
+def _host_staged() -> bool:
+    return dist.is_initialized() and dist.get_backend() == "gloo"
 
 
 def shard(global_batch: int, rank: int, world: int) -> tuple[int, int]:
@@ -56,6 +68,13 @@ def gather_outputs(out_flat: torch.Tensor, world: int, out: torch.Tensor | None 
         return out_flat
     if out is None:
         out = torch.empty(world * out_flat.numel(), dtype=out_flat.dtype, device=out_flat.device)
+    if out_flat.is_cuda and _host_staged():
+        # gloo has no device buffers: gather host copies, then one upload (shared-GPU rehearsal)
+        host = out_flat.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host)
+        out.copy_(torch.cat(parts))
+        return out
     dist.all_gather_into_tensor(out, out_flat)
     return out
 
@@ -82,6 +101,6 @@ def max_over_ranks(value: float, world: int, device: torch.device) -> float:
     """Slowest rank's value (the bench's whole-job time)."""
     if world == 1:
         return float(value)
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device="cpu" if _host_staged() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

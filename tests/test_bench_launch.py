@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -38,3 +40,18 @@ def test_world_size_must_match_gpus():
              env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "!= --gpus 2" in (r.stderr + r.stdout)
+
+
+@pytest.mark.gpu
+def test_gpus2_shared_gpu_rehearsal_runs_real_kernels():
+    """The N-rank bench path on a one-GPU box: `--gpus 2` spawns two ranks that each plan,
+    capture and replay the real HIP forward on cuda:0, time between barriers, take the max
+    over ranks and all-gather out_flat (gloo, host-staged: RCCL refuses two ranks on one GPU).
+    Rank 0's slice of the gathered buffer must be its own output."""
+    r = _run(["--gpus", "2", "--shared-gpu-rehearsal", "--size", "n", "--batch", "4", "--steps", "3", "--warmup", "1",
+              "--no-cpu-baseline", "--no-latency", "--no-secondary"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json_line(r.stdout)
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 8
+    assert out["outputs_finite"] and out["gather_rank0_matches"]
+    assert "rehearsal" in out and out["value"] > 0
