@@ -26,6 +26,10 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--libs", default="")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--refs", default="random", choices=["random", "clustered", "sorted"],
+                    help="reference points: uniform per token; 60 person centres per image with their 18 "
+                         "tokens within +-0.05 (the decoder's layout); or clustered with the queries "
+                         "ordered by centre y (a spatial token order)")
     a = ap.parse_args()
     from detrpose_amd import _lib
     geo = {"n": (128, [(80, 80), (40, 40)], 6, 8), "l": (256, [(80, 80), (40, 40), (20, 20)], 4, 8),
@@ -42,7 +46,14 @@ def main():
     oa[:, :nH * L * P * 2] = torch.randn(rows, nH * L * P * 2, device="cuda", generator=g) * 2
     oa[:, nH * L * P * 2:] = torch.randn(rows, nH * L * P, device="cuda", generator=g)
     oa = oa.to(torch.bfloat16)
-    ref = torch.rand(rows, 2, device="cuda", generator=g) * 0.9 + 0.05
+    if a.refs == "random":
+        ref = torch.rand(rows, 2, device="cuda", generator=g) * 0.9 + 0.05
+    else:
+        ctr = torch.rand(B, 60, 1, 2, device="cuda", generator=g) * 0.8 + 0.1
+        if a.refs == "sorted":
+            order = ctr[:, :, 0, 1].argsort(dim=1)
+            ctr = torch.gather(ctr, 1, order[:, :, None, None].expand_as(ctr))
+        ref = (ctr + (torch.rand(B, 60, 18, 2, device="cuda", generator=g) - 0.5) * 0.1).reshape(rows, 2).contiguous()
     out = torch.empty(rows, Cc, device="cuda", dtype=torch.bfloat16)
     hw = (C.c_int32 * (2 * L))(*[v for s in shapes for v in s])
     libs = []
