@@ -17,11 +17,13 @@ ranks as a child process (before anything touches the GPU) and exits with its co
 run whose world size differs from --gpus fails.
 
 Also reported (rank 0):
-  roofline      the dominant kernel family (implicit-GEMM conv/linear, dp_conv2d):
-                algorithmic bytes (or FLOPs) of its launches / their HIP-event time;
-                `traffic` = measured HBM bytes of those launches from the committed
-                rocprofv3 PMC passes, quoted only when they were taken on this exact
-                source (detrpose_amd.build.source_hash);
+  roofline      the dominant kernel: the kernel instantiation with the most device time per
+                step (dp_conv2d launches are named by the dispatcher, dp_conv2d_describe),
+                bound by its own launches' algorithmic bytes vs FLOPs; achieved = their
+                FLOPs (or bytes) / their HIP-event time. `traffic` = measured HBM bytes of
+                those launches from the committed rocprofv3 PMC passes, quoted only when
+                they were taken on this exact source (detrpose_amd.build.source_hash).
+                Beside it the dp_conv2d family and the per-launch bound over every launch;
   latency_bs1   the reference's latency protocol (torch_benchmark.py:29-51): batch 1,
                 400 warm-up and 1000 timed Model(images, sizes) calls (hipGraph replay,
                 synchronised each), mean of the fastest 100 and the median;
@@ -102,8 +104,8 @@ def maybe_spawn(a) -> int | None:
 # ----------------------------------------------------------------------------- legs
 
 
-def pmc_traffic(a, launches):
-    """Measured HBM bytes per step of the conv family from the committed rocprofv3 PMC
+def pmc_traffic(a, kernel, launches):
+    """Measured HBM bytes per step of one kernel instantiation from the committed rocprofv3 PMC
     passes (scripts/pmc_traffic.py), only if they were taken on this exact source and
     workload; otherwise (None, reason)."""
     from detrpose_amd.build import source_hash
@@ -115,10 +117,10 @@ def pmc_traffic(a, launches):
         return None, f"PMC profile is for source {d.get('source_hash')}, this is {source_hash()}: not quoted"
     if tuple(d.get("workload", ())) != (a.size, a.batch, a.dtype):
         return None, "PMC profile is for another workload"
-    fam = d["families"].get("conv")
-    if not fam or round(fam["launches"]) != launches:
-        return None, "PMC launch count differs"
-    return round(fam["total_bytes"]), f"rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE ({PMC_FILE}, source {d['source_hash']})"
+    k = d.get("kernels", {}).get(kernel)
+    if not k or round(k["launches"]) != launches:
+        return None, "PMC profile has no entry with this launch count for the kernel"
+    return round(k["total_bytes"]), f"rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE ({PMC_FILE}, source {d['source_hash']})"
 
 
 def cpu_baseline(size, cap_seconds):
@@ -154,6 +156,83 @@ def cpu_baseline(size, cap_seconds):
                       f"threads), batch 1 and 8, 2 warm-up + " + " / ".join(f"{v[1]} timed at b{b}"
                                                                                 for b, v in res.items())
                       + f"; value = best batch (b{best})"}
+
+
+def _bound(nbytes, flops, peak):
+    """(bound kind, lower-bound ms) of algorithmic bytes / FLOPs on MI355X."""
+    t_hbm = nbytes / (PEAK_HBM_GBS * 1e9)
+    t_mfma = flops / (peak * 1e12)
+    return ("hbm" if t_hbm >= t_mfma else "mfma"), max(t_hbm, t_mfma) * 1e3
+
+
+def roofline_report(a, plan, op_ms, op_fn, peak):
+    """Roofline of the dominant kernel: the kernel instantiation (Plan.kernel_of: rocprofv3's
+    canonical name) with the most device time per step, bound by its own launches'
+    algorithmic bytes vs FLOPs. Beside it: the dp_conv2d family (rounds 1-3's line), and the
+    per-launch bound max(bytes / HBM peak, FLOPs / MFMA peak) summed over EVERY launch of the
+    step (each op records its algorithmic bytes and FLOPs, Plan.cost)."""
+    kern = {n: plan.kernel_of(n) for n in op_ms}
+    groups = {}
+    for n, ms in op_ms.items():
+        g = groups.setdefault(kern[n], {"ms": 0.0, "bytes": 0.0, "flops": 0.0, "launches": 0, "ops": []})
+        g["ms"] += ms
+        g["bytes"] += plan.op_bytes[n]
+        g["flops"] += plan.op_flops[n]
+        g["launches"] += 1
+        g["ops"].append(n)
+    dom = max(groups, key=lambda k: groups[k]["ms"])
+    g = groups[dom]
+    kind, lb = _bound(g["bytes"], g["flops"], peak)
+    gbs = g["bytes"] / (g["ms"] * 1e-3) / 1e9
+    tfs = g["flops"] / (g["ms"] * 1e-3) / 1e12
+    traffic, traffic_note = pmc_traffic(a, dom, g["launches"])
+    total_ms = sum(op_ms.values())
+    per_op = {n: _bound(plan.op_bytes[n], plan.op_flops[n], peak)[1] for n in op_ms}
+    conv = [n for n in op_ms if op_fn[n] == "dp_conv2d"]
+    c_ms = sum(op_ms[n] for n in conv)
+    c_b = sum(plan.op_bytes[n] for n in conv)
+    c_f = sum(plan.op_flops[n] for n in conv)
+    c_kind, _ = _bound(c_b, c_f, peak)
+    c_lb = sum(per_op[n] for n in conv)
+    top = sorted(groups.items(), key=lambda kv: -kv[1]["ms"])[:8]
+    return {
+        "bound": kind,
+        "kernel": dom,
+        "achieved": round(tfs if kind == "mfma" else gbs, 2),
+        "peak": peak if kind == "mfma" else PEAK_HBM_GBS,
+        "unit": "TFLOP/s" if kind == "mfma" else "GB/s",
+        "frac": round(tfs / peak if kind == "mfma" else gbs / PEAK_HBM_GBS, 4),
+        "traffic": traffic,
+        "traffic_note": traffic_note,
+        "launches_per_step": g["launches"],
+        "ms_per_step": round(g["ms"], 4),
+        "avg_launch_us": round(1e3 * g["ms"] / g["launches"], 2),
+        "flops_per_step": g["flops"],
+        "algorithmic_bytes_per_step": round(g["bytes"]),
+        "achieved_tflops": round(tfs, 2),
+        "achieved_gbs": round(gbs, 1),
+        "bound_ms": round(lb, 4),
+        "how": "achieved = the kernel's algorithmic FLOPs (or bytes) over its launches in one step / their summed "
+               "HIP-event time (Plan.profile, median of 3 passes on the launch stream); the same FLOPs x profiled "
+               "steps / rocprofv3 TotalDurationNs reproduces it",
+        "family": {"kernel": "dp_conv2d family (conv_stream/conv_halo/stem-direct: every dense conv/linear launch)",
+                   "bound": c_kind, "ms_per_step": round(c_ms, 3), "launches_per_step": len(conv),
+                   "algorithmic_bytes": round(c_b), "achieved_gbs": round(c_b / (c_ms * 1e-3) / 1e9, 1),
+                   "achieved_tflops": round(c_f / (c_ms * 1e-3) / 1e12, 2),
+                   "hbm_frac": round(c_b / (c_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                   "mfma_frac": round(c_f / (c_ms * 1e-3) / 1e12 / peak, 4),
+                   "per_launch_bound_ms": round(c_lb, 3), "bound_over_actual": round(c_lb / c_ms, 4)},
+        "all_launches": {"ms_per_step": round(total_ms, 3), "launches": len(op_ms),
+                         "covered_by_per_op_bounds": round(sum(op_ms[n] for n in op_ms if n in plan.op_bytes)
+                                                           / total_ms, 4),
+                         "per_launch_bound_ms": round(sum(per_op.values()), 3),
+                         "bound_over_actual": round(sum(per_op.values()) / total_ms, 4)},
+        "top_kernels": [{"kernel": k, "ms_per_step": round(v["ms"], 3), "launches": v["launches"],
+                         "bound": _bound(v["bytes"], v["flops"], peak)[0],
+                         "bound_over_actual": round(_bound(v["bytes"], v["flops"], peak)[1] / v["ms"], 4)}
+                        for k, v in top],
+    }
+
 
 
 def latency_bs1(model, pp, dev, runs, warmup):
@@ -258,7 +337,7 @@ def main():
 
     def step():
         if a.no_graph:
-            plan.run()
+            plan.run(post=True)
         else:
             g.replay()
         if dist is not None:
@@ -295,45 +374,19 @@ def main():
     if rank == 0:
         # per-op HIP-event pass over the same plan (outside the timed region)
         op_ms = plan.profile(reps=3)
-        op_fn = {nm: f.__name__ for nm, f, _ in plan.ops}
-        conv_names = [n for n in plan.conv_bytes if n in op_ms and op_fn[n] == "dp_conv2d"]
-        conv_ms = sum(op_ms[n] for n in conv_names)
-        conv_flops = sum(plan.op_flops[n] for n in conv_names)
-        conv_alg_bytes = sum(plan.conv_bytes[n] for n in conv_names)
-        traffic, traffic_note = pmc_traffic(a, len(conv_names))
-        total_ms = sum(op_ms.values())
-        achieved = conv_flops / (conv_ms * 1e-3) / 1e12
+        op_fn = {nm: f.__name__ for nm, f, _ in plan.ops + plan.post_ops}
         peak = PEAK_BF16_TFLOPS if a.dtype == "bf16" else PEAK_F32_TFLOPS
+        roofline = roofline_report(a, plan, op_ms, op_fn, peak)
         fam = {}
         for n, ms in op_ms.items():
             fam[op_fn[n]] = fam.get(op_fn[n], 0.0) + ms
-        msda = [n for n in plan.op_bytes if n in op_ms]
+        msda = [n for n in op_ms if n.endswith(".msda")]
         msda_gbs = sum(plan.op_bytes[n] for n in msda) / (sum(op_ms[n] for n in msda) * 1e-3) / 1e9 if msda else None
         if a.profile_ops:
             with open(a.profile_ops, "w") as f:
                 json.dump({"op_ms": op_ms, "op_flops": plan.op_flops, "op_bytes": plan.op_bytes,
-                           "conv_bytes": plan.conv_bytes}, f, indent=1)
+                           "op_kernel": {n: plan.kernel_of(n) for n in op_ms}}, f, indent=1)
         gflop = GFLOP_PER_IMAGE[a.size]
-        # the family's lower bound is the larger of its HBM time and its MFMA time
-        gbs = conv_alg_bytes / (conv_ms * 1e-3) / 1e9
-        hbm_bound = conv_alg_bytes / (PEAK_HBM_GBS * 1e9) >= conv_flops / (peak * 1e12)
-        # per-launch bound: sum over launches of max(bytes / HBM peak, flops / MFMA peak)
-        lb_ms = sum(max(plan.conv_bytes[n] / (PEAK_HBM_GBS * 1e9), plan.op_flops[n] / (peak * 1e12))
-                    for n in conv_names) * 1e3
-        roofline = {"bound": "hbm" if hbm_bound else "mfma",
-                    "kernel": "dp_conv2d family (conv_stream/conv_halo kernels: all dense conv/linear launches "
-                              "of one step)",
-                    "achieved": round(gbs if hbm_bound else achieved, 2),
-                    "peak": PEAK_HBM_GBS if hbm_bound else peak,
-                    "unit": "GB/s" if hbm_bound else "TFLOP/s",
-                    "frac": round(gbs / PEAK_HBM_GBS if hbm_bound else achieved / peak, 4),
-                    "traffic": traffic,
-                    "traffic_note": traffic_note,
-                    "algorithmic_bytes": round(conv_alg_bytes),
-                    "achieved_tflops": round(achieved, 2), "mfma_frac": round(achieved / peak, 4),
-                    "per_launch_bound_ms": round(lb_ms, 3), "bound_over_actual": round(lb_ms / conv_ms, 4),
-                    "launches_per_step": len(conv_names), "ms_per_step": round(conv_ms, 3),
-                    "time_share": round(conv_ms / total_ms, 3)}
         out = {
             "metric": METRIC,
             "value": round(value, 2),

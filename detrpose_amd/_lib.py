@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DETRPOSE_HIP_LIB", os.path.join(_HERE, "lib", "libdetrpose_hip.so"))
 
 DP_F32, DP_BF16 = 0, 1
+DP_MSDA_OFFATTN_F32 = 0x100
 ACT = {None: 0, "none": 0, "relu": 1, "silu": 2, "gelu": 3}
 
 i32, i64, f32, vp = C.c_int32, C.c_int64, C.c_float, C.c_void_p
@@ -65,7 +66,9 @@ def contiguous_rows(ld: int, base: int = 0) -> RowMap:
 _SIGS = {
     "dp_last_error": (C.c_char_p, []),
     "dp_version": (i32, []),
+    "dp_source_hash": (C.c_char_p, []),
     "dp_conv2d": (i32, [C.POINTER(ConvDesc), vp]),
+    "dp_conv2d_describe": (i32, [C.POINTER(ConvDesc), C.c_char_p, i32]),
     "dp_dwconv2d": (i32, [C.POINTER(ConvDesc), vp]),
     "dp_stem_conv": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, f32, f32, vp, i64, i32, i32, vp]),
     "dp_maxpool2x2_pad_rb": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, vp]),
@@ -131,8 +134,26 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    verify_source(lib)
     _lib = lib
     return lib
+
+
+def verify_source(lib, expected: str | None = None):
+    """Refuse a library built from other sources than the ones shipped beside it (the .so is
+    git-ignored and travels prebuilt; a stale one would otherwise be tested and benched
+    silently). DETRPOSE_ALLOW_STALE_LIB=1 skips the check (A/B variant libraries only)."""
+    if os.environ.get("DETRPOSE_ALLOW_STALE_LIB"):
+        return
+    from .build import CSRC, lib_source_hash
+    if expected is None:
+        if not os.path.isdir(CSRC):
+            return
+        expected = lib_source_hash()
+    got = lib.dp_source_hash().decode()
+    if got != expected:
+        raise HipError(f"{LIB_PATH} was built from sources {got}, the shipped sources are {expected}: "
+                       f"rebuild it with `python -m detrpose_amd.build`")
 
 
 def check(rc: int, what: str = ""):

@@ -16,6 +16,13 @@ Scope: the losses of the shipped configs, `['vfl', 'keypoints']` with weight_dic
 {loss_vfl, loss_keypoints, loss_oks} (configs/detrpose/include/detrpose_hgnetv2.py). The
 'labels', 'mal', 'local' and 'matching' losses and the denoising (dn_*) outputs raise
 NotImplementedError. There is no CPU path.
+
+Two deliberate departures from matcher.py: (1) the reference drops the keypoint costs of a head
+whose keypoints sum to <= 0 (matcher.py:70-93) and matches on the class cost alone; keypoints
+come out of a sigmoid or of the refinement around sigmoid anchors, so that branch never runs
+and the keypoint costs are always added here. (2) NaN / inf costs make scipy raise; here the
+image's queries get match -2 and dp_pose_loss returns a NaN loss_vfl for the head, so a
+diverged step shows in the loss instead of silently training on a partial matching.
 """
 from __future__ import annotations
 

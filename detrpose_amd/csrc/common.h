@@ -17,6 +17,20 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 void dp_set_error(const char* fmt, ...);
 int dp_check_launch(const char* what);
 
+// dp_conv2d_describe: while a describe buffer is set (this thread), the conv launch sites
+// write the kernel instantiation they would launch and return 0 instead of launching
+char* dp_describe_buf(int* len);
+void dp_describe_set(char* buf, int len);
+#define DP_DESCRIBE(...)                      \
+  do {                                        \
+    int dp_dlen_ = 0;                         \
+    if (char* dp_dbuf_ = dp_describe_buf(&dp_dlen_)) { \
+      snprintf(dp_dbuf_, dp_dlen_, __VA_ARGS__); \
+      return 0;                               \
+    }                                         \
+  } while (0)
+#define DP_TF(b) ((b) ? "true" : "false")
+
 #define DP_REQUIRE(cond, ...)                 \
   do {                                        \
     if (!(cond)) {                            \

@@ -220,6 +220,8 @@ int launch(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   const int M = d.batch * d.out_h * d.out_w;
   const int mt = (M + BM - 1) / BM, nt = (d.cout + BN - 1) / BN;
   const bool k1 = d.kh == 1 && d.kw == 1 && d.pad_t == 0 && d.pad_l == 0;
+  DP_DESCRIBE("conv_gemm_kernel<%s, %s, %d, %d, %d, %d, %d, %s>", sizeof(T) == 2 ? "bf16" : "float",
+              sizeof(TO) == 2 ? "bf16" : "float", BM, BN, BK, WGM, DP_CONV_PD, DP_TF(sizeof(TO) != sizeof(T) || k1));
   dim3 grid(mt * nt), block(256);
   constexpr int PD = DP_CONV_PD;
   if constexpr (sizeof(TO) != sizeof(T)) {
@@ -272,7 +274,20 @@ int dispatch(const dp_conv_desc& d, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int dp_conv2d(const dp_conv_desc* dp, void* stream) {
+static int conv2d_impl(const dp_conv_desc* dp, void* stream);
+
+extern "C" int dp_conv2d(const dp_conv_desc* dp, void* stream) { return conv2d_impl(dp, stream); }
+
+extern "C" int dp_conv2d_describe(const dp_conv_desc* dp, char* buf, int32_t buflen) {
+  DP_REQUIRE(buf != nullptr && buflen > 0, "dp_conv2d_describe: no buffer");
+  buf[0] = 0;
+  dp_describe_set(buf, buflen);
+  const int r = conv2d_impl(dp, nullptr);
+  dp_describe_set(nullptr, 0);
+  return r;
+}
+
+static int conv2d_impl(const dp_conv_desc* dp, void* stream) {
   DP_REQUIRE(dp != nullptr, "dp_conv2d: null descriptor");
   const dp_conv_desc& d = *dp;
   const int VEC = d.dtype == DP_BF16 ? 8 : 4;

@@ -189,7 +189,10 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   // next tile's wait may leave them in flight, since VMEM ops retire in issue order and the
   // patch / weight DMAs it waits for were issued before them
   constexpr int NSTORE = NAT ? TM * TN : TM * (NPL / 8);
-  const bool plain_full = !d.res && !d.up && (NAT || (vec_ok && d.cout == BN));
+  // the counted wait below assumes every wave issued exactly NSTORE stores in the previous
+  // tile's epilogue: only tiles whose every output channel exists (cout == BN) qualify, NAT
+  // tiles included (their epilogue skips the stores of channels >= cout)
+  const bool plain_full = !d.res && !d.up && d.cout == BN && (NAT || vec_ok);
   bool prev_full = false;
   int u = 0;
   for (int tile = L; tile < ntiles; tile += G, ++u) {
@@ -389,6 +392,8 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
 
 template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false, int NKC = 0>
 int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloPool pool = {}) {
+  DP_DESCRIBE("conv_halo_kernel<%d, %d, %d, %d, %d, %d, %s, %s, %d, %s, %d>", TH, NW, KH, KW, S, BN, DP_TF(RESW),
+              DP_TF(DBUF), ACT, DP_TF(POOL), NKC);
   auto kern = conv_halo_kernel<TH, NW, KH, KW, S, BN, RESW, DBUF, ACT, POOL, NKC>;
   static const int occ = [&] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,

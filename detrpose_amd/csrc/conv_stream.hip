@@ -435,6 +435,8 @@ constexpr int ring_a() {
 template <int BM, int BN, int WGM, int NW, bool K1, int ACT, typename TO, int EPI>
 int launch_one(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
   constexpr int SA = ring_a<BM, BN, NW>();
+  DP_DESCRIBE("conv_stream_kernel<%d, %d, %d, %d, %d, %s, %d, %s, %d>", BM, BN, WGM, NW, SA, DP_TF(K1), ACT,
+              sizeof(TO) == 2 ? "bf16" : "float", EPI);
   auto kern = conv_stream_kernel<BM, BN, WGM, NW, SA, K1, ACT, TO, EPI>;
   static const int occ = [&] {
     const int o = occupancy(kern, NW * 64);

@@ -75,6 +75,8 @@ struct LsapSmem {
   unsigned char* SC;
 };
 
+constexpr int DP_MATCH_INFEASIBLE = -2;
+
 __global__ __launch_bounds__(64) void hungarian_kernel(
     const float* __restrict__ logits, int64_t lg_h, int64_t lg_b, int lg_q, int ncls,
     const float* __restrict__ kps, int64_t kp_h, int64_t kp_b, int kp_q, int nkp,
@@ -130,6 +132,7 @@ __global__ __launch_bounds__(64) void hungarian_kernel(
   auto cost = [&](int i, int j) -> double { return (double)(tr ? s.cost[j * nt + i] : s.cost[i * nt + j]); };
 
   // ---- shortest augmenting path, one row at a time (oracle/lsap_cpu.py)
+  bool feasible = true;
   for (int cur = 0; cur < nr; ++cur) {
     for (int j = lane; j < nc; j += 64) {
       s.spc[j] = INFINITY;
@@ -191,7 +194,10 @@ __global__ __launch_bounds__(64) void hungarian_kernel(
       else i = r4c;
       __syncthreads();
     }
-    if (!ok) break;
+    if (!ok) {
+      feasible = false;
+      break;
+    }
     // dual update (u of the scanned rows, v of the scanned columns)
     for (int ii = lane; ii < nr; ii += 64)
       if (ii == cur) s.u[ii] += min_val;
@@ -211,6 +217,13 @@ __global__ __launch_bounds__(64) void hungarian_kernel(
       }
     }
     __syncthreads();
+  }
+  if (!feasible) {
+    // NaN / inf costs: scipy's linear_sum_assignment raises; here every query of the image
+    // gets DP_MATCH_INFEASIBLE and dp_pose_loss turns that head's losses into NaN
+    __syncthreads();
+    for (int q = lane; q < Q; q += 64) mt[q] = DP_MATCH_INFEASIBLE;
+    return;
   }
   // match[q] = target of query q
   for (int r = lane; r < nr; r += 64) {
@@ -315,6 +328,7 @@ __global__ __launch_bounds__(256) void pose_loss_kernel(
     const int t = H.match[e];
     int label = -1;
     float ts = 0.f;
+    if (t == DP_MATCH_INFEASIBLE) s_vfl = NAN;   // the matching failed: report it in the loss
     if (t >= 0) {
       const int tg = tgt_off[b] + t;
       label = tgt_label[tg];

@@ -23,5 +23,16 @@ int dp_check_launch(const char* what) {
   return 0;
 }
 
+static thread_local char* g_describe = nullptr;
+static thread_local int g_describe_len = 0;
+char* dp_describe_buf(int* len) {
+  *len = g_describe_len;
+  return g_describe;
+}
+void dp_describe_set(char* buf, int len) {
+  g_describe = buf;
+  g_describe_len = len;
+}
+
 extern "C" const char* dp_last_error(void) { return g_err; }
 extern "C" int dp_version(void) { return 1; }

@@ -24,9 +24,9 @@ struct Levels {
   int h[MAXL], w[MAXL], start[MAXL];
 };
 
-template <typename T>
+template <typename T, typename OA>
 __global__ __launch_bounds__(256) void msda_kernel(const T* __restrict__ value, int S, Levels lv, int L,
-                                                   const T* __restrict__ offattn, const float* __restrict__ ref,
+                                                   const OA* __restrict__ offattn, const float* __restrict__ ref,
                                                    T* __restrict__ out, int ld_out, int lq, int rows, int nhead, int dh,
                                                    int P, int TB) {
   constexpr int VEC = Vec16<T>::N;
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void msda_kernel(const T* __restrict__ value, 
     const int tl = th / nhead, h = th - tl * nhead;
     const int r = r0 + tl;
     if (r >= rows) continue;
-    const T* oa = offattn + (int64_t)r * ncol;
+    const OA* oa = offattn + (int64_t)r * ncol;
     const float rx = ref[2 * r], ry = ref[2 * r + 1];
     float lg[MAXLP];
     float mx = -INFINITY;
@@ -127,9 +127,9 @@ __global__ __launch_bounds__(256) void msda_kernel(const T* __restrict__ value, 
 //  * XCD-aware order: logical block = (blockIdx % 8) * (G / 8) + blockIdx / 8 gives each
 //    of the 8 XCDs a contiguous token range, i.e. whole images: an image's 4.3 MB value
 //    slab (L) is pulled into ONE XCD's L2 instead of all eight.
-template <int NH, int CPT, int L, int P>
+template <int NH, int CPT, int L, int P, typename OA>
 __global__ __launch_bounds__(256) void msda_wave_kernel(const bf16_t* __restrict__ value, int S, Levels lv,
-                                                        const bf16_t* __restrict__ offattn,
+                                                        const OA* __restrict__ offattn,
                                                         const float* __restrict__ ref, bf16_t* __restrict__ out,
                                                         int ld_out, int lq, int rows, int nblk) {
   constexpr int LP = L * P;
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void msda_wave_kernel(const bf16_t* __restrict
   char* ent = lds[wave] + (t < TPW ? (t * NH + h) * ESTR : 0);
 
   // ---- setup: lane c takes points j = c + CPT*k
-  const bf16_t* oa = offattn + (int64_t)rr * (NH * LP * 3);
+  const OA* oa = offattn + (int64_t)rr * (NH * LP * 3);
   float lg[NPP];
   float mx = -INFINITY;
 #pragma unroll
@@ -230,21 +230,22 @@ __global__ __launch_bounds__(256) void msda_wave_kernel(const bf16_t* __restrict
   *reinterpret_cast<bf16x8*>(out + (int64_t)r * ld_out + h * (CPT * 8) + c * 8) = o;
 }
 
-template <int NH, int CPT, int L, int P>
-int launch_wave(const bf16_t* value, int S, const Levels& lv, const bf16_t* offattn, const float* ref, bf16_t* out,
+template <int NH, int CPT, int L, int P, typename OA>
+int launch_wave(const bf16_t* value, int S, const Levels& lv, const OA* offattn, const float* ref, bf16_t* out,
                 int ld_out, int lq, int rows, hipStream_t s) {
   constexpr int TPW = 64 / (NH * CPT);
   const int nblk = (rows + 4 * TPW - 1) / (4 * TPW);
   const int grid = (nblk + 7) / 8 * 8;
-  hipLaunchKernelGGL((msda_wave_kernel<NH, CPT, L, P>), dim3(grid), dim3(256), 0, s, value, S, lv, offattn, ref, out,
-                     ld_out, lq, rows, nblk);
+  hipLaunchKernelGGL((msda_wave_kernel<NH, CPT, L, P, OA>), dim3(grid), dim3(256), 0, s, value, S, lv, offattn, ref,
+                     out, ld_out, lq, rows, nblk);
   return dp_check_launch("dp_msda(wave)");
 }
 
 // the (nhead, dh, L, P) shapes of the DETRPose configs (N: 8x16, 2 levels x 6 points;
 // L: 8x32, 3x4; X: 8x48, 3x4); -1 = no instantiation (generic kernel)
+template <typename OA>
 int dispatch_wave(const bf16_t* value, int S, const Levels& lv, int L, int P, int nhead, int dh,
-                  const bf16_t* offattn, const float* ref, bf16_t* out, int ld_out, int lq, int rows, hipStream_t s) {
+                  const OA* offattn, const float* ref, bf16_t* out, int ld_out, int lq, int rows, hipStream_t s) {
   if (nhead != 8) return -1;
   if (dh == 32 && L == 3 && P == 4) return launch_wave<8, 4, 3, 4>(value, S, lv, offattn, ref, out, ld_out, lq, rows, s);
   if (dh == 16 && L == 2 && P == 6) return launch_wave<8, 2, 2, 6>(value, S, lv, offattn, ref, out, ld_out, lq, rows, s);
@@ -258,6 +259,11 @@ int dispatch_wave(const bf16_t* value, int S, const Levels& lv, int L, int P, in
 extern "C" int dp_msda(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
                        const void* offattn, const float* ref, void* out, int32_t ld_out, int32_t lq, int32_t nhead,
                        int32_t dh, int32_t npoints, int32_t dtype, void* stream) {
+  // DP_MSDA_OFFATTN_F32 in dtype: offattn is f32 whatever the value dtype (the training step's
+  // offsets Linear output, which the backward differentiates at)
+  const bool oa32 = (dtype & DP_MSDA_OFFATTN_F32) != 0;
+  dtype &= ~DP_MSDA_OFFATTN_F32;
+  DP_REQUIRE(dtype == DP_BF16 || dtype == DP_F32, "dp_msda: bad dtype %d", dtype);
   const int VEC = dtype == DP_BF16 ? 8 : 4;
   DP_REQUIRE(value && offattn && ref && out && lvl_hw, "dp_msda: null pointer");
   DP_REQUIRE(nlevels >= 1 && nlevels <= MAXL, "dp_msda: nlevels=%d (max %d)", nlevels, MAXL);
@@ -276,8 +282,10 @@ extern "C" int dp_msda(const void* value, int32_t batch, int32_t S, const int32_
   static const bool generic = getenv("DETRPOSE_MSDA_GENERIC") != nullptr;
   if (dtype == DP_BF16 && !generic && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(value) & 15) == 0) {
-    const int rc = dispatch_wave((const bf16_t*)value, S, lv, nlevels, npoints, nhead, dh, (const bf16_t*)offattn, ref,
-                                 (bf16_t*)out, ld_out, lq, rows, as_stream(stream));
+    const int rc = oa32 ? dispatch_wave((const bf16_t*)value, S, lv, nlevels, npoints, nhead, dh,
+                                        (const float*)offattn, ref, (bf16_t*)out, ld_out, lq, rows, as_stream(stream))
+                        : dispatch_wave((const bf16_t*)value, S, lv, nlevels, npoints, nhead, dh,
+                                        (const bf16_t*)offattn, ref, (bf16_t*)out, ld_out, lq, rows, as_stream(stream));
     if (rc != -1) return rc;
   }
   const int cpt = dh / VEC;
@@ -285,11 +293,14 @@ extern "C" int dp_msda(const void* value, int32_t batch, int32_t S, const int32_
   if (TB < 1) TB = 1;
   const size_t lds = (size_t)TB * nhead * nlevels * npoints * 4 * 8;
   dim3 grid((unsigned)((rows + TB - 1) / TB)), block(256);
-  if (dtype == DP_BF16)
-    hipLaunchKernelGGL(msda_kernel<bf16_t>, grid, block, lds, as_stream(stream), (const bf16_t*)value, S, lv, nlevels,
-                       (const bf16_t*)offattn, ref, (bf16_t*)out, ld_out, lq, rows, nhead, dh, npoints, TB);
+  if (dtype == DP_BF16 && oa32)
+    hipLaunchKernelGGL((msda_kernel<bf16_t, float>), grid, block, lds, as_stream(stream), (const bf16_t*)value, S, lv,
+                       nlevels, (const float*)offattn, ref, (bf16_t*)out, ld_out, lq, rows, nhead, dh, npoints, TB);
+  else if (dtype == DP_BF16)
+    hipLaunchKernelGGL((msda_kernel<bf16_t, bf16_t>), grid, block, lds, as_stream(stream), (const bf16_t*)value, S, lv,
+                       nlevels, (const bf16_t*)offattn, ref, (bf16_t*)out, ld_out, lq, rows, nhead, dh, npoints, TB);
   else
-    hipLaunchKernelGGL(msda_kernel<float>, grid, block, lds, as_stream(stream), (const float*)value, S, lv, nlevels,
-                       (const float*)offattn, ref, (float*)out, ld_out, lq, rows, nhead, dh, npoints, TB);
+    hipLaunchKernelGGL((msda_kernel<float, float>), grid, block, lds, as_stream(stream), (const float*)value, S, lv,
+                       nlevels, (const float*)offattn, ref, (float*)out, ld_out, lq, rows, nhead, dh, npoints, TB);
   return dp_check_launch("dp_msda");
 }

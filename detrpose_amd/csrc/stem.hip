@@ -252,6 +252,8 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(const bf16_t* __restri
 
 template <int KS, int CIN, int COUT, bool POOL>
 int launch_direct(const dp_conv_desc& d, hipStream_t s, bf16_t* pool, int64_t pbs, int pps) {
+  DP_DESCRIBE("conv_direct_kernel<%d, %d, %d, %s, %d>", KS, CIN, COUT, DP_TF(POOL),
+              d.act == DP_ACT_RELU ? DP_ACT_RELU : DP_ACT_NONE);
   const int gx = (d.in_w + 15) / 16;
   const int64_t ngroups = (int64_t)d.batch * d.in_h * gx;
   int blocks = (int)((ngroups + 4 * 4 - 1) / (4 * 4));   // 4 waves x G = 4 groups per block pass

@@ -182,9 +182,12 @@ class Plan:
         self.arena = []          # every device buffer the launches point into
         self.bufs = {}           # named FMaps / tensors for inspection
         self.op_out = {}         # op name -> output FMap (debug / tests)
-        self.op_flops = {}       # op name -> algorithmic FLOPs (conv / linear launches)
-        self.op_bytes = {}       # op name -> algorithmic HBM bytes (MSDA)
-        self.conv_bytes = {}     # op name -> algorithmic HBM bytes of a dense conv/linear launch
+        # per-launch roofline accounting (bench.py): every op records its algorithmic HBM bytes
+        # (compulsory reads + writes) and FLOPs; dp_conv2d launches also the kernel
+        # instantiation the dispatcher picks (dp_conv2d_describe)
+        self.op_flops = {}       # op name -> algorithmic FLOPs
+        self.op_bytes = {}       # op name -> algorithmic HBM bytes
+        self.op_kernel = {}      # op name -> kernel instantiation (rocprofv3's demangled name)
         self.out_flat = None
         self.input = None
         self.outputs = {}
@@ -197,6 +200,20 @@ class Plan:
     # -- recording
     def _op(self, name, fn, *args):
         self.ops.append((name, fn, args))
+
+    def cost(self, name, nbytes, flops=0.0):
+        self.op_bytes[name] = float(nbytes)
+        self.op_flops[name] = float(flops)
+
+    def kernel_of(self, name) -> str:
+        """The kernel a launch runs: the dispatcher's choice for dp_conv2d, else the entry point."""
+        k = self.op_kernel.get(name)
+        if k:
+            return k
+        for n, fn, _ in self.ops + self.post_ops:
+            if n == name:
+                return fn.__name__
+        raise KeyError(name)
 
     def run(self, stream=None, debug=None, post=False):
         """Replay the forward launches; with post=True also the appended PostProcess (the
@@ -211,12 +228,14 @@ class Plan:
                 debug(name, self.op_out.get(name))
 
     def profile(self, reps=3):
-        """Per-op device time (ms, median of `reps` passes) with HIP events around each launch."""
+        """Per-op device time (ms, median of `reps` passes) with HIP events around each launch
+        (the forward and, when appended, PostProcess: the launches one graph replay runs)."""
         s = torch.cuda.current_stream(self.engine.device)
-        times = {name: [] for name, _, _ in self.ops}
+        ops = self.ops + self.post_ops
+        times = {name: [] for name, _, _ in ops}
         for _ in range(reps):
             evs = []
-            for name, fn, args in self.ops:
+            for name, fn, args in ops:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(s)
@@ -248,6 +267,7 @@ class Plan:
         self.post_ops = [("postprocess", eng.lib.dp_postprocess, (logits.data_ptr(), kps.data_ptr(), ts.data_ptr(), B,
                                                                   Q, NC, K, num_select, sc.data_ptr(), lb.data_ptr(),
                                                                   ok.data_ptr()))]
+        self.cost("postprocess", 4 * B * Q * (NC + 2 * K) + B * num_select * (4 + 8 + 8 * K), 0)
         self.post = {"scores": sc, "labels": lb, "keypoints": ok, "target_sizes": ts, "num_select": num_select}
         self._graph = None
         return self.post
@@ -518,17 +538,22 @@ class Engine:
             d.in_seg_ch, d.in_seg_stride = seg
         plan.keep.append(d)
         plan.op_out[name] = out
+        e = self.tdtype.itemsize
+        rows = x.B * out.H * out.W
         if not pc.depthwise:
-            plan.op_flops[name] = 2.0 * x.B * out.H * out.W * out.C * pc.kh * pc.kw * x.C
             # compulsory traffic: input read once, weights once, output (+residual, +x2 copy)
-            e = self.tdtype.itemsize
             eo = 4 if out_f32 else e
-            rows = x.B * out.H * out.W
-            plan.conv_bytes[name] = (e * x.B * x.H * x.W * x.C + e * pc.cout * pc.kh * pc.kw * pc.cin
-                                     + eo * rows * out.C * (1 + (res is not None) + 4 * (up is not None))
-                                     + (e * rows * pool.C if pool is not None else 0))
+            plan.cost(name, e * x.B * x.H * x.W * x.C + e * pc.cout * pc.kh * pc.kw * pc.cin
+                      + eo * rows * out.C * (1 + (res is not None) + 4 * (up is not None))
+                      + (e * rows * pool.C if pool is not None else 0),
+                      2.0 * rows * out.C * pc.kh * pc.kw * x.C)
+            if pool is None:
+                buf = C.create_string_buffer(256)
+                if self.lib.dp_conv2d_describe(C.byref(d), buf, 256) == 0:
+                    plan.op_kernel[name] = buf.value.decode()
         else:
-            plan.op_flops[name] = 2.0 * x.B * out.H * out.W * out.C * pc.kh * pc.kw
+            plan.cost(name, e * x.B * x.H * x.W * x.C + e * rows * out.C + 4 * pc.kh * pc.kw * out.C,
+                      2.0 * rows * out.C * pc.kh * pc.kw)
         if pool is not None:
             # conv + MaxPool2d(2, 1) of the same padded input in one pass (dp_conv2d_pool)
             assert not pc.depthwise and pool.C == x.C and (pool.B, pool.H, pool.W) == (x.B, x.H, x.W)
@@ -671,8 +696,8 @@ class Engine:
         plan.op_out["stem"] = out
         h1, w1_ = (H + 1) // 2, (W + 1) // 2
         m1, m3 = B * h1 * w1_, B * out.H * out.W
-        plan.op_flops["stem"] = 2.0 * (m1 * 32 * 27 + m1 * 16 * 128 + m1 * 32 * 64 + m3 * 32 * 576 + m3 * out.C * 32)
-        plan.conv_bytes["stem"] = 4.0 * B * 3 * H * W + 2.0 * m3 * out.C
+        plan.cost("stem", 4.0 * B * 3 * H * W + 2.0 * m3 * out.C,
+                  2.0 * (m1 * 32 * 27 + m1 * 16 * 128 + m1 * 32 * 64 + m3 * 32 * 576 + m3 * out.C * 32))
 
     def _plan_stem(self, plan, img, B, H, W, h1, w1):
         """StemBlock.forward (hgnetv2.py:204-220) as five launches; returns stem3's map."""
@@ -683,6 +708,7 @@ class Engine:
         plan._op("stem1", self.lib.dp_stem_conv, img.data_ptr(), B, H, W, wst.data_ptr(), bst.data_ptr(), mid,
                  1 if lab else 0, C.c_float(lab[0] if lab else 1.0), C.c_float(lab[1] if lab else 0.0), s1.ptr, s1.bs,
                  s1.ps, self.code)
+        plan.cost("stem1", 4.0 * B * 3 * H * W + self.tdtype.itemsize * B * h1 * w1 * mid, 2.0 * B * h1 * w1 * mid * 27)
         s2a = self._fmap(B, h1, w1, P["stem2a"].cout)
         cat = self._fmap(B, h1, w1, 2 * mid)
         if self.code == _lib.DP_BF16 and mid % 8 == 0 and mid <= 64 and P["stem2a"].cout <= 32:
@@ -692,6 +718,7 @@ class Engine:
             self._conv(plan, "stem2a", s1, P["stem2a"], s2a)   # F.pad(0,1,0,1) == zero read past the edge
             plan._op("stem_pool", self.lib.dp_maxpool2x2_pad_rb, s1.ptr, s1.bs, s1.ps, B, h1, w1, mid, cat.ptr,
                      cat.bs, cat.ps, self.code)
+            plan.cost("stem_pool", 2.0 * self.tdtype.itemsize * B * h1 * w1 * mid, 3.0 * B * h1 * w1 * mid)
         self._conv(plan, "stem2b", s2a, P["stem2b"], cat.ch(mid, mid))
         h2, w2 = (h1 + 1) // 2, (w1 + 1) // 2
         s3 = self._fmap(B, h2, w2, mid)
@@ -779,6 +806,8 @@ class Engine:
         pos = A["pos"]
         plan._op(name + ".pos", self.lib.dp_add_rows, qin.ptr, contiguous_rows(Cc), tok.ptr, contiguous_rows(Cc),
                  pos.data_ptr(), rowmap(0, n, 0, Cc), rows, Cc, self.code)
+        es = self.tdtype.itemsize
+        plan.cost(name + ".pos", es * (2 * rows + n) * Cc, rows * Cc)
         qkv = self._empty(rows * 3 * Cc, dtype=self.tdtype)
         qkv_f = FMap(qkv, 0, 1, 1, rows, 3 * Cc, 3 * Cc, rows * 3 * Cc)
         self._conv(plan, name + ".qk", qin, A["qk"], qkv_f.ch(0, 2 * Cc))
@@ -787,11 +816,13 @@ class Engine:
         e = qkv.element_size()
         plan._op(name + ".attn", self.lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
                  qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B, 1, n, 0, 1, n, nh, Cc // nh, self.code)
+        plan.cost(name + ".attn", es * rows * 4 * Cc, 4.0 * B * n * n * Cc)
         ao = self._fmap(1, 1, rows, Cc)
         self._conv(plan, name + ".out", att, A["out"], ao)
         s1 = self._fmap(1, 1, rows, Cc)
         self._ln(plan, name + ".n1", s1.ptr, contiguous_rows(Cc), tok.ptr, contiguous_rows(Cc), ao.ptr,
                  contiguous_rows(Cc), A["n1"], rows, Cc)
+        plan.cost(name + ".n1", es * rows * Cc * 3, 8.0 * rows * Cc)
         f1 = self._fmap(1, 1, rows, A["l1"].cout)
         self._conv(plan, name + ".l1", s1, A["l1"], f1)
         f2 = self._fmap(1, 1, rows, Cc)
@@ -799,6 +830,7 @@ class Engine:
         out = self._fmap(B, H, W, Cc)
         self._ln(plan, name + ".n2", out.ptr, contiguous_rows(Cc), s1.ptr, contiguous_rows(Cc), f2.ptr,
                  contiguous_rows(Cc), A["n2"], rows, Cc)
+        plan.cost(name + ".n2", es * rows * Cc * 3, 8.0 * rows * Cc)
         return out
 
     def _plan_transformer(self, plan, memory, shapes):
@@ -826,7 +858,9 @@ class Engine:
                      eof.data_ptr(), P["enc_output"].b.data_ptr(), g_.data_ptr(), b_.data_ptr(), C.c_float(1e-5),
                      P["mask"].data_ptr(), S, P["masked_row"].data_ptr(), wc.data_ptr(), bc.data_ptr(), wc.shape[0],
                      score.data_ptr())
-            plan.op_flops["ts.enc_out_ln"] = 2.0 * rows_m * Cc * Cc
+            ncl = wc.shape[0]
+            plan.cost("ts.enc_out_ln", 2 * 2 * rows_m * Cc + 2 * Cc * Cc + 4 * rows_m,
+                      2.0 * rows_m * Cc * Cc + 2.0 * rows_m * Cc * ncl + 8.0 * rows_m * Cc)
             eo = None
         else:
             eo = self._fmap(1, 1, rows_m, Cc)
@@ -839,16 +873,22 @@ class Engine:
             plan._op("ts.enc_norm", lib.dp_layernorm_classmax, om.ptr, eo.ptr, g_.data_ptr(), b_.data_ptr(),
                      C.c_float(1e-5), rows_m, Cc, P["mask"].data_ptr(), S, P["masked_row"].data_ptr(), wc.data_ptr(),
                      bc.data_ptr(), wc.shape[0], score.data_ptr(), self.code)
+            plan.cost("ts.enc_norm", self.tdtype.itemsize * 2 * rows_m * Cc + 4 * rows_m,
+                      2.0 * rows_m * Cc * wc.shape[0] + 8.0 * rows_m * Cc)
         else:
             self._ln(plan, "ts.enc_norm", om.ptr, contiguous_rows(Cc), eo.ptr, contiguous_rows(Cc), None, None,
                      P["enc_norm"], rows_m, Cc, mask=(P["mask"], S, P["masked_row"]))
             plan._op("ts.class_max", lib.dp_class_max, om.ptr, rows_m, Cc, wc.data_ptr(), bc.data_ptr(), wc.shape[0],
                      score.data_ptr(), self.code)
+            plan.cost("ts.enc_norm", self.tdtype.itemsize * 2 * rows_m * Cc, 8.0 * rows_m * Cc)
+            plan.cost("ts.class_max", self.tdtype.itemsize * rows_m * Cc + 4 * rows_m, 2.0 * rows_m * Cc * wc.shape[0])
         topv = self._empty(B, nq, dtype=torch.float32)
         topi = self._empty(B, nq, dtype=torch.int64)
         plan._op("ts.topk", lib.dp_topk, score.data_ptr(), B, S, S, nq, topv.data_ptr(), topi.data_ptr())
+        plan.cost("ts.topk", 4 * B * S + 12 * B * nq, 0)
         tm = self._fmap(1, 1, B * nq, Cc)
         plan._op("ts.gather", lib.dp_gather_rows, om.ptr, S * Cc, topi.data_ptr(), B, nq, Cc, tm.ptr, self.code)
+        plan.cost("ts.gather", 2 * dt.itemsize * B * nq * Cc + 8 * B * nq, 0)
         x = tm
         for i, pc in enumerate(P["enc_pose"]):
             y = self._fmap(1, 1, B * nq, pc.cout)
@@ -861,6 +901,7 @@ class Engine:
         ref = self._empty(B, nq, T, 2, dtype=torch.float32)
         plan._op("ts.refpoints", lib.dp_refpoint_init, delta.data_ptr(), P["anchors"].data_ptr(), topi.data_ptr(), B,
                  nq, K, ref.data_ptr())
+        plan.cost("ts.refpoints", 4 * B * nq * (2 * K + 2 + 2 * T) + 8 * B * nq, 8.0 * B * nq * K)
         plan.bufs.update(topk_idx=topi, topk_val=topv, enc_output_norm=om, score=score)
         aux = plan.aux
         if aux:
@@ -870,8 +911,10 @@ class Engine:
             interm_logits = self._empty(B, nq, ecs.n, dtype=torch.float32)
             plan._op("aux.interm_cls", lib.dp_linear_small, tm.ptr, contiguous_rows(Cc), self.code, B * nq, ecs.k,
                      ecs.wt.data_ptr(), ecs.b.data_ptr(), ecs.n, ecs.n, 0, None, interm_logits.data_ptr())
+            plan.cost("aux.interm_cls", dt.itemsize * B * nq * Cc + 4 * B * nq * ecs.n, 2.0 * B * nq * Cc * ecs.n)
             interm_ref = self._empty(B, nq, T, 2, dtype=torch.float32)
             plan._op("aux.interm_ref", lib.dp_broadcast, ref.data_ptr(), ref.numel() * 4, interm_ref.data_ptr(), 1)
+            plan.cost("aux.interm_ref", 8 * ref.numel(), 0)
         # ---- decoder (transformer.py:558-925)
         rows = B * nq * T               # all tokens
         krows = B * nq * K              # keypoint tokens
@@ -879,6 +922,7 @@ class Engine:
         tgtB = self._empty(rows * Cc, dtype=dt)
         tmpl = P["tgt_tmpl"]
         plan._op("dec.tgt", lib.dp_broadcast, tmpl.data_ptr(), tmpl.numel() * tmpl.element_size(), tgtA.data_ptr(), B)
+        plan.cost("dec.tgt", tmpl.numel() * tmpl.element_size() * (1 + B), 0)
         kp_map = rowmap(Cc, K, T * Cc, Cc)       # keypoint token rows of a [rows][C] tensor
         # bf16: the row-block fused decoder kernels (csrc/decoder.hip); fp32 parity mode keeps
         # one launch per reference op
@@ -940,17 +984,23 @@ class Engine:
             score2 = self._empty(B * nq, cls.n, dtype=torch.float32)
             plan._op(n + ".cls", lib.dp_linear_small, x_rows, rowmap(0, 1, T * Cc, 0), self.code, B * nq,
                      cls.k, cls.wt.data_ptr(), cls.b.data_ptr(), cls.n, cls.n, 0, None, score2.data_ptr())
+            plan.cost(n + ".cls", e * B * nq * Cc + 4 * B * nq * cls.n, 2.0 * B * nq * Cc * cls.n)
             lv0 = plan.bufs["encoder"][0]
             st = self._empty(B * nq, K * 5, dtype=torch.float32)
             plan._op(n + ".lqe_stats", lib.dp_lqe_stats, lv0.ptr, lv0.bs, lv0.H, lv0.W, Cc, kps_l.data_ptr(), B, nq,
                      K, st.data_ptr(), self.code)
+            # 4 bilinear corners of C channels per keypoint (gathered), kps in, stats out
+            plan.cost(n + ".lqe_stats", 4 * e * B * nq * K * Cc + 4 * B * nq * K * 7, 8.0 * B * nq * K * Cc)
             hid = self._empty(B * nq, lqe[0].n, dtype=torch.float32)
             plan._op(n + ".lqe0", lib.dp_linear_small, st.data_ptr(), contiguous_rows(K * 5), DP_F32, B * nq,
                      lqe[0].k, lqe[0].wt.data_ptr(), lqe[0].b.data_ptr(), lqe[0].n, lqe[0].n, lqe[0].act, None,
                      hid.data_ptr())
+            plan.cost(n + ".lqe0", 4 * B * nq * (K * 5 + lqe[0].n) + 4 * lqe[0].k * lqe[0].n,
+                      2.0 * B * nq * lqe[0].k * lqe[0].n)
             plan._op(n + ".lqe1", lib.dp_linear_small, hid.data_ptr(), contiguous_rows(lqe[0].n), DP_F32, B * nq,
                      lqe[1].k, lqe[1].wt.data_ptr(), lqe[1].b.data_ptr(), lqe[1].n, cls.n, 0,
                      score2.data_ptr(), logits_l.data_ptr())
+            plan.cost(n + ".lqe1", 4 * B * nq * (lqe[0].n + 2 * cls.n), 2.0 * B * nq * lqe[1].k * cls.n)
         eps = C.c_float(1e-5)
 
         def lin(pc, frag, k):
@@ -970,16 +1020,21 @@ class Engine:
                 phf = P["pos_head_frag"]
                 plan._op(n + ".pos", lib.dp_query_pos, ref.data_ptr(), krows, K, P["dim_t"].data_ptr(),
                          *lin(ph[0], phf[0], Cc), *lin(ph[1], phf[1], Cc), pos.ptr, src.data_ptr(), kp_map, Cc)
+                # refs in; pos out; keypoint rows of the layer input read + written; two C x C weights
+                plan.cost(n + ".pos", 8 * B * nq * T + 3 * e * krows * Cc + 2 * e * Cc * Cc,
+                          4.0 * krows * Cc * Cc + 4.0 * krows * Cc)
             else:
                 # query pos from the current reference points (transformer.py:588-592)
                 plan._op(n + ".sine", lib.dp_sine_embed, ref.data_ptr(), B * nq, K, Cc, P["dim_t"].data_ptr(),
                          se.ptr, self.code)
+                plan.cost(n + ".sine", 8 * B * nq * T + e * krows * Cc, 4.0 * krows * Cc)
                 self._conv(plan, n + ".pos0", se, P["pos_head"][0], h1)
                 self._conv(plan, n + ".pos1", h1, P["pos_head"][1], pos)
                 # in-place with_pos_embed on the layer input (transformer.py:369): also turns the previous
                 # layer's output_pose into output_pose_detach + pos (aliasing kept on purpose)
                 plan._op(n + ".addpos", lib.dp_add_rows, src.data_ptr(), kp_map, src.data_ptr(), kp_map, pos.ptr,
                          contiguous_rows(Cc), krows, Cc, self.code)
+                plan.cost(n + ".addpos", 3 * e * krows * Cc, krows * Cc)
             if mha:
                 # within-instance MHA + out_proj + residual + LN (transformer.py:403-406), then the
                 # across-instance one over the nq queries of a token slot (transformer.py:409-422)
@@ -993,65 +1048,82 @@ class Engine:
                          nq * T, 1, T, nq, *lin(L["across_qkv"], fr["across_qkv"], Cc),
                          *lin(L["across_out"], fr["across_out"], Cc), an[0].data_ptr(), an[1].data_ptr(), eps, Cc, nh,
                          pos.ptr, cr(Cc), T, 1, oa.ptr, oa.ps, *lin(L["offattn"], fr["offattn"], Cc), oa.C)
-                mha_flops = 2.0 * rows * Cc * 4 * Cc
-                plan.op_flops[n + ".w_mha"] = plan.op_flops[n + ".a_mha"] = mha_flops
+                # projections (q, k, v, out) + QK^T and PV over each token's sequence, + the fused
+                # offsets/logits Linear in the across launch; rows in / out, pos rows, weights
+                proj = 2.0 * rows * Cc * 4 * Cc
+                plan.cost(n + ".w_mha", 2 * e * rows * Cc + 2 * 4 * Cc * Cc, proj + 4.0 * rows * T * Cc)
+                plan.cost(n + ".a_mha", 2 * e * rows * Cc + e * krows * Cc + e * rows * oa.C + 2 * Cc * (4 * Cc + oa.C),
+                          proj + 4.0 * rows * nq * Cc + 2.0 * rows * Cc * oa.C)
             else:
                 # within-instance MHA over the T tokens of a query (transformer.py:403-406)
                 self._conv(plan, n + ".w_qkv", src_f, L["within_qkv"], qkv_f)
                 plan._op(n + ".w_attn", lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
                          qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B * nq, 1, T, 0, 1, T, nh, Cc // nh, self.code)
+                plan.cost(n + ".w_attn", 4 * e * rows * Cc, 4.0 * rows * T * Cc)
                 if fused:
                     wn, fr = L["within_norm"], L["frag"]
                     plan._op(n + ".w_out_ln", lib.dp_linear_layernorm, dst.data_ptr(), cr(Cc), att.ptr, cr(Cc), Cc,
                              *lin(L["within_out"], fr["within_out"], Cc), src.data_ptr(), cr(Cc), wn[0].data_ptr(),
                              wn[1].data_ptr(), eps, rows, Cc, None, rowmap(group=1), 1, 0)
+                    plan.cost(n + ".w_out_ln", 3 * e * rows * Cc + e * Cc * Cc, 2.0 * rows * Cc * Cc + 8.0 * rows * Cc)
                 else:
                     self._conv(plan, n + ".w_out", att, L["within_out"], ao)
                     self._ln(plan, n + ".w_norm", dst.data_ptr(), contiguous_rows(Cc), src.data_ptr(), contiguous_rows(Cc),
                              ao.ptr, contiguous_rows(Cc), L["within_norm"], rows, Cc)
+                    plan.cost(n + ".w_norm", 3 * e * rows * Cc, 8.0 * rows * Cc)
                 # across-instance MHA over the nq queries of a token slot (transformer.py:409-419)
                 self._conv(plan, n + ".a_qkv", dst_f, L["across_qkv"], qkv_f)
                 plan._op(n + ".a_attn", lib.dp_attention, qkv.data_ptr(), 3 * Cc, qkv.data_ptr() + Cc * e,
                          qkv.data_ptr() + 2 * Cc * e, 3 * Cc, att.ptr, Cc, B, T, nq * T, 1, T, nq, nh, Cc // nh,
                          self.code)
+                plan.cost(n + ".a_attn", 4 * e * rows * Cc, 4.0 * rows * nq * Cc)
                 # out_proj + LN + second in-place pos add -> x1 = gx[:, :C]   (transformer.py:419-422)
                 if fused:
                     an, fr = L["across_norm"], L["frag"]
                     plan._op(n + ".a_out_ln", lib.dp_linear_layernorm, gx.data_ptr(), cr(2 * Cc), att.ptr, cr(Cc), Cc,
                              *lin(L["across_out"], fr["across_out"], Cc), dst.data_ptr(), cr(Cc), an[0].data_ptr(),
                              an[1].data_ptr(), eps, rows, Cc, pos.ptr, cr(Cc), T, 1)
+                    plan.cost(n + ".a_out_ln", 3 * e * rows * Cc + e * krows * Cc + e * Cc * Cc,
+                              2.0 * rows * Cc * Cc + 8.0 * rows * Cc)
                 else:
                     self._conv(plan, n + ".a_out", att, L["across_out"], ao)
                     self._ln(plan, n + ".a_norm", gx.data_ptr(), contiguous_rows(2 * Cc), dst.data_ptr(),
                              contiguous_rows(Cc), ao.ptr, contiguous_rows(Cc), L["across_norm"], rows, Cc,
                              post=(pos.ptr, contiguous_rows(Cc)), post_group=T, post_skip=1)
+                    plan.cost(n + ".a_norm", 3 * e * rows * Cc + e * krows * Cc, 8.0 * rows * Cc)
             # MSDA (ms_deform_attn.py:384-444) -> gx[:, C:]
             if not mha:
                 self._conv(plan, n + ".offattn", gx_f.ch(0, Cc), L["offattn"], oa)
             plan._op(n + ".msda", lib.dp_msda, memory.data_ptr(), B, S, lvl_hw, len(shapes), oa.ptr, ref.data_ptr(),
                      gx.data_ptr() + Cc * e, 2 * Cc, nq * T, nh, Cc // nh, npnt, self.code)
-            # SURVEY.md §8d algorithmic bytes: value once + offsets/logits + ref + output
-            plan.op_bytes[n + ".msda"] = e * (B * S * Cc + rows * oa.C + rows * Cc) + 4 * rows * 2
+            # SURVEY.md §8d algorithmic bytes: value once + offsets/logits + ref + output;
+            # FLOPs: 4 corners x (bilinear weight FMA) per channel per sampling point + softmax
+            plan.cost(n + ".msda", e * (B * S * Cc + rows * oa.C + rows * Cc) + 4 * rows * 2,
+                      10.0 * rows * nh * nl_ * npnt * (Cc // nh))
             # Gate (transformer.py:222-235), FFN (transformer.py:380-385)
             if fused:
                 gn, n2, fr = L["gate_norm"], L["norm2"], L["frag"]
                 plan._op(n + ".gate_ln", lib.dp_gate_linear_layernorm, dst.data_ptr(), cr(Cc), gx.data_ptr(),
                          cr(2 * Cc), *lin(L["gate"], fr["gate"], 2 * Cc), gn[0].data_ptr(), gn[1].data_ptr(), eps,
                          rows, Cc)
+                plan.cost(n + ".gate_ln", 3 * e * rows * Cc + e * 4 * Cc * Cc, 2.0 * rows * 4 * Cc * Cc + 12.0 * rows * Cc)
                 fd = tr.dim_feedforward
                 plan._op(n + ".ffn_ln", lib.dp_ffn_layernorm, dst.data_ptr(), cr(Cc), dst.data_ptr(), cr(Cc),
                          *lin(L["ffn1"], fr["ffn1"], Cc), fd, *lin(L["ffn2"], fr["ffn2"], fd), n2[0].data_ptr(),
                          n2[1].data_ptr(), eps, rows, Cc)
+                plan.cost(n + ".ffn_ln", 2 * e * rows * Cc + e * 2 * Cc * fd, 4.0 * rows * Cc * fd + 8.0 * rows * Cc)
                 last_op = n + ".ffn_ln"
             else:
                 self._conv(plan, n + ".gate", gx_f, L["gate"], gt)
                 plan._op(n + ".gate_ln", lib.dp_gate_layernorm, dst.data_ptr(), Cc, gt.ptr, gx.data_ptr(),
                          L["gate_norm"][0].data_ptr(), L["gate_norm"][1].data_ptr(), C.c_float(1e-5), rows, Cc,
                          self.code)
+                plan.cost(n + ".gate_ln", 5 * e * rows * Cc, 12.0 * rows * Cc)
                 self._conv(plan, n + ".ffn1", dst_f, L["ffn1"], f1)
                 self._conv(plan, n + ".ffn2", f1, L["ffn2"], f2)
                 self._ln(plan, n + ".norm2", dst.data_ptr(), contiguous_rows(Cc), dst.data_ptr(), contiguous_rows(Cc),
                          f2.ptr, contiguous_rows(Cc), L["norm2"], rows, Cc)
+                plan.cost(n + ".norm2", 3 * e * rows * Cc, 8.0 * rows * Cc)
                 last_op = n + ".norm2"
             plan.bufs["layers"].append(dst)
             # ---- heads (transformer.py:701-728)
@@ -1063,12 +1135,14 @@ class Engine:
                 self._conv(plan, n + ".pre2", ph2, pp[2], FMap(pre, 0, 1, 1, krows, 2, 2, pre.numel()), out_f32=True)
                 plan._op(n + ".pre_pose", lib.dp_pre_pose, pre.data_ptr(), ref.data_ptr(), B * nq, K,
                          ref_init.data_ptr())
+                plan.cost(n + ".pre_pose", 4 * krows * 2 * 2 + 8 * B * nq * T, 10.0 * krows * 2)
                 if aux:
                     # pre_scores = class_head[0](output_instance) (transformer.py:708)
                     c0 = P["layers"][0]["cls"]
                     plan._op(n + ".pre_cls", lib.dp_linear_small, dst.data_ptr(), rowmap(0, 1, T * Cc, 0), self.code,
                              B * nq, c0.k, c0.wt.data_ptr(), c0.b.data_ptr(), c0.n, c0.n, 0, None,
                              pre_logits.data_ptr())
+                    plan.cost(n + ".pre_cls", e * B * nq * Cc + 4 * B * nq * c0.n, 2.0 * B * nq * Cc * c0.n)
             ph = L["pose"]
             cur, prev = corners[l % ncorn], corners[(l - 1) % ncorn]
             if fused:
@@ -1078,6 +1152,8 @@ class Engine:
                 pw = [v for i in range(3) for v in lin(ph[i], L["frag"]["pose"][i], Cc)]
                 plan._op(n + ".pose", lib.dp_pose_mlp, dst.data_ptr(), kp_map, src.data_ptr() if l > 0 else None,
                          kp_map, krows, *pw, nb, prev.data_ptr() if l > 0 else None, cur.data_ptr(), Cc)
+                plan.cost(n + ".pose", e * krows * Cc * (1 + (l > 0)) + 4 * krows * nb * (1 + (l > 0))
+                          + e * Cc * (2 * Cc + nb), 2.0 * krows * Cc * (2 * Cc + nb))
                 plan.bufs["layer_ops"].append((last_op, n + ".pose"))
             else:
                 if l == 0:
@@ -1087,6 +1163,7 @@ class Engine:
                     # output_pose + this layer's pos (in-place aliasing, transformer.py:369/716/922)
                     plan._op(n + ".pin", lib.dp_add_rows, pin.ptr, contiguous_rows(Cc), dst.data_ptr(), kp_map,
                              src.data_ptr(), kp_map, krows, Cc, self.code)
+                    plan.cost(n + ".pin", 3 * e * krows * Cc, krows * Cc)
                     x_in = pin
                 self._conv(plan, n + ".pose0", x_in, ph[0], ph1)
                 self._conv(plan, n + ".pose1", ph1, ph[1], ph2)
@@ -1096,6 +1173,7 @@ class Engine:
                 plan.bufs["layer_ops"].append((last_op, n + ".pose2"))
             plan._op(n + ".refine", lib.dp_pose_refine, cur.data_ptr(), P["project"].data_ptr(), tr.reg_max,
                      ref_init.data_ptr(), C.c_float(P["reg_scale"]), B * nq, K, layer_kps[l].data_ptr(), ref.data_ptr())
+            plan.cost(n + ".refine", 4 * krows * (nb + 2 + 2) + 8 * B * nq * T, 5.0 * krows * nb)
             if l == nlayers - 1 or aux:
                 class_lqe(n, L, dst.data_ptr(), layer_kps[l], layer_logits[l])
             if l == nlayers - 1:

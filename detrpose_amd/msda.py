@@ -109,15 +109,18 @@ class MSDeformAttnFunction(torch.autograd.Function):
             raise ValueError("msda: spatial shapes do not match value")
         lq = rows // N
         value = value.contiguous()
-        # the forward reads offattn in value's dtype: the backward differentiates at those values
-        oa = offattn.detach().to(value.dtype).contiguous()
+        # offsets / logits stay f32 whatever value's dtype (DP_MSDA_OFFATTN_F32): bf16 would round
+        # offsets of tens of pixels by up to ~0.1 px, and the backward differentiates at the
+        # f32 values, as the reference's f32 Linear outputs
+        oa = offattn.detach().float().contiguous()
         ref = ref.detach().float().contiguous()
         out = torch.empty(N, lq, Cc, device=value.device, dtype=value.dtype)
         hw, nl = _shapes_arg(shapes)
         lib = _lib.load()
         s = torch.cuda.current_stream(value.device).cuda_stream
         _lib.check(lib.dp_msda(value.data_ptr(), N, S, hw, nl, oa.data_ptr(), ref.data_ptr(), out.data_ptr(), Cc, lq,
-                               n_heads, Cc // n_heads, n_points, _DT[value.dtype], C.c_void_p(s)), "dp_msda")
+                               n_heads, Cc // n_heads, n_points, _DT[value.dtype] | _lib.DP_MSDA_OFFATTN_F32,
+                               C.c_void_p(s)), "dp_msda")
         ctx.save_for_backward(value, oa, ref)
         ctx.shapes = [tuple(int(v) for v in hw_) for hw_ in shapes]
         ctx.n_heads, ctx.n_points = n_heads, n_points
@@ -132,7 +135,7 @@ class MSDeformAttnFunction(torch.autograd.Function):
         gv = torch.empty(N, S, Cc, device=value.device, dtype=torch.float32)
         goa = torch.empty(oa.shape, device=value.device, dtype=torch.float32)
         gref = torch.empty(rows, 2, device=value.device, dtype=torch.float32) if ctx.needs_input_grad[3] else None
-        oa32 = oa.float()
+        oa32 = oa
         hw, nl = _shapes_arg(ctx.shapes)
         lib = _lib.load()
         s = torch.cuda.current_stream(value.device).cuda_stream

@@ -63,6 +63,15 @@ typedef struct dp_rowmap {
 
 const char* dp_last_error(void);
 int dp_version(void);
+/* Content hash of the sources this library was built from (detrpose_amd/build.py bakes it in;
+ * the Python loader refuses a library whose hash differs from the shipped sources). */
+const char* dp_source_hash(void);
+
+/* The kernel instantiation dp_conv2d would launch for *d, written to buf (no launch, no
+ * device access), in the demangled form rocprofv3 prints, e.g.
+ * "conv_halo_kernel<8, 4, 3, 3, 1, 128, false, false, 2, false, 0>". For per-kernel roofline
+ * accounting (bench.py). Returns 0, or DP_EINVAL for a descriptor dp_conv2d would refuse. */
+int dp_conv2d_describe(const dp_conv_desc* d, char* buf, int32_t buflen);
 
 /* nn.Conv2d (+ folded BatchNorm / FrozenBatchNorm2d) + act (+ LAB) (+ residual),
  * dense groups=1. Replaces ConvBNAct (hgnetv2.py:82-134), ConvNormLayer(_fuse)
@@ -159,6 +168,7 @@ int dp_attention(const void* q, int32_t ld_q, const void* k, const void* v, int3
  *  value:  [batch][S][nhead*dh] dtype; level l occupies rows [lvl_start[l], +h*w)
  *  offattn:[batch*lq][nhead*L*P*3] dtype: offsets (h,l,p,xy) then logits (h,l,p)
  *  ref:    [batch*lq][2] f32 (x, y) in [0,1];  out: [batch*lq] rows of ld_out, dtype */
+enum { DP_MSDA_OFFATTN_F32 = 0x100 };  /* or'ed into dp_msda's dtype: offattn is f32 (training op) */
 int dp_msda(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */,
             int32_t nlevels, const void* offattn, const float* ref, void* out, int32_t ld_out,
             int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, int32_t dtype, void* stream);
@@ -347,7 +357,11 @@ int dp_pose_mlp(const void* x, dp_rowmap xm, const void* x2, dp_rowmap x2m, int3
  * logits (H, B, Q, ncls) and keypoints (H, B, Q, 2K) f32 at the given element strides;
  * cost = cost_class * focal + cost_kp * L1 + cost_oks * (1 - OKS) per image, solved by
  * scipy's shortest augmenting path (linear_sum_assignment, matcher.py:97) in f64 on the
- * GPU. match (H, B, Q) int32 = the image-local target index of query q, or -1.
+ * GPU. match (H, B, Q) int32 = the image-local target index of query q, or -1; -2 for every
+ * query of an image whose cost block is infeasible (NaN / inf costs, where scipy raises):
+ * dp_pose_loss then returns a NaN loss_vfl for that head. The reference drops the keypoint
+ * costs when a head's keypoints sum to <= 0 (matcher.py:70); sigmoid / refined keypoints
+ * never do, so that branch is not built (the keypoint costs are always added).
  * max_t = the most targets of any image (LDS sizing). cost_out (H, B, Q, max_t) or NULL. */
 int dp_hungarian_match(const float* logits, int64_t lg_h, int64_t lg_b, int32_t lg_q, int32_t ncls,
                        const float* kps, int64_t kp_h, int64_t kp_b, int32_t kp_q, int32_t nkp,

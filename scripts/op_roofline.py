@@ -27,11 +27,11 @@ def main():
     fn = {n: f.__name__ for n, f, _ in p.ops}
     om = json.load(open(a.json))["op_ms"]
     rows = []
-    for n in p.conv_bytes:
+    for n in p.op_bytes:
         if fn[n] != "dp_conv2d" or n not in om:
             continue
-        lb = max(p.conv_bytes[n] / 8e12, p.op_flops[n] / 2.5e15) * 1e3
-        rows.append((om[n] - lb, n, om[n], lb, p.conv_bytes[n] / 1e9, p.op_flops[n] / 1e12))
+        lb = max(p.op_bytes[n] / 8e12, p.op_flops[n] / 2.5e15) * 1e3
+        rows.append((om[n] - lb, n, om[n], lb, p.op_bytes[n] / 1e9, p.op_flops[n] / 1e12))
     rows.sort(reverse=True)
     print(f"conv family: measured {sum(r[2] for r in rows):.3f} ms, roofline {sum(r[3] for r in rows):.3f} ms")
     print(f"{'op':28s} {'ms':>7s} {'lb ms':>7s} {'GB':>6s} {'TF':>6s} {'TB/s':>6s} {'TF/s':>6s}")

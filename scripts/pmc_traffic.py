@@ -34,13 +34,13 @@ def family(name):
     return "other"
 
 
-def agg(path, counter):
+def agg(path, counter, key=family):
     tot = collections.defaultdict(float)
     calls = collections.Counter()
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        f = family(r["Kernel_Name"])
+        f = key(r["Kernel_Name"])
         tot[f] += float(r["Counter_Value"]) * 1024.0
         calls[f] += 1
     return tot, calls
@@ -58,6 +58,14 @@ def main():
         out["families"][f] = {"read_bytes_corrected": rd, "write_bytes": wr, "total_bytes": rd + wr,
                               "launches": calls[f] / nfwd}
         print(f"{f:22s} read {rd / 1e9:7.3f} GB  write {wr / 1e9:7.3f} GB  per forward ({calls[f] / nfwd:.0f} launches)")
+    # per kernel instantiation (canonical rocprofv3 name, detrpose_amd.profiling): bench.py quotes
+    # the dominant kernel's measured traffic from here
+    from detrpose_amd.profiling import canonical_kernel_name
+    kf, kc = agg(sys.argv[1], "FETCH_SIZE", canonical_kernel_name)
+    kw, _ = agg(sys.argv[2], "WRITE_SIZE", canonical_kernel_name)
+    out["kernels"] = {k: {"read_bytes_corrected": 2.0 * kf[k] / nfwd, "write_bytes": kw.get(k, 0.0) / nfwd,
+                          "total_bytes": (2.0 * kf[k] + kw.get(k, 0.0)) / nfwd, "launches": kc[k] / nfwd}
+                      for k in sorted(kf, key=lambda k: -kf[k])}
     if len(sys.argv) > 3:
         with open(sys.argv[3], "w") as fh:
             json.dump(out, fh, indent=1)

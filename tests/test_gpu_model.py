@@ -70,6 +70,7 @@ def test_fp32_matches_reference(golden_dir, size, batch):
 # 0.041 / 0.014 / 0.027, mean 4-7e-3. Bounds: ~1.5x the worst max, ~2x the worst mean.
 BF16_TOL_KP, BF16_TOL_KP_MEAN = 2e-2, 3.5e-3
 BF16_TOL_LOGIT, BF16_TOL_LOGIT_MEAN = 5e-2, 1.6e-2
+BF16_TOPK_OVERLAP = 0.65
 
 
 def _oracle(size, model):
@@ -95,12 +96,18 @@ def test_bf16_forced_selection_matches_oracle(golden_dir, size, batch):
     assert torch.isfinite(kp).all() and torch.isfinite(lg).all()
     dk = (kp - ref["pred_keypoints"]).abs()
     dl = (lg - ref["pred_logits"]).abs()
+    # the bf16 selection against the reference's own (golden fp32) top-k, image by image
+    ov = [len(set(idx[b].tolist()) & set(g["topk_idx"][b].tolist())) for b in range(batch)]
     msg = (f"{size} bf16 vs fp32 oracle (forced selection): max|dkp| {dk.max():.3g} (mean {dk.mean():.3g}), "
-           f"max|dlogit| {dl.max():.3g} (mean {dl.mean():.3g}), topk overlap with fp32 "
-           f"{len(set(idx.reshape(-1).tolist()) & set(g['topk_idx'].reshape(-1).tolist()))}/{idx.numel()}")
+           f"max|dlogit| {dl.max():.3g} (mean {dl.mean():.3g}), topk overlap with the reference {ov} of "
+           f"{idx.shape[1]} per image")
     print(msg)
     assert dk.max() <= BF16_TOL_KP and dl.max() <= BF16_TOL_LOGIT, msg
     assert dk.mean() <= BF16_TOL_KP_MEAN and dl.mean() <= BF16_TOL_LOGIT_MEAN, msg
+    # measured (r3k): N 83/120, L 58/60, X 58/60. A floor, so a regression in the fused
+    # two-stage head (which queries it selects) fails here even though the forced-selection
+    # oracle follows whatever the kernel picked
+    assert sum(ov) >= BF16_TOPK_OVERLAP * idx.numel() and min(ov) >= 0.5 * idx.shape[1], msg
 
 
 def test_bf16_b64_headline_batch_is_batch_invariant(golden_dir):

@@ -33,6 +33,40 @@ def test_library_exports_header_symbols():
     assert lib.dp_version() >= 1
 
 
+def test_library_source_hash_guard():
+    """The .so carries the hash of the sources it was built from; the loader refuses a
+    library whose hash differs from the sources shipped beside it (a stale prebuilt .so)."""
+    from detrpose_amd.build import lib_source_hash
+    lib = _lib.load()
+    assert lib.dp_source_hash().decode() == lib_source_hash()
+    _lib.verify_source(lib)   # matching hash: accepted
+    with pytest.raises(_lib.HipError, match="rebuild"):
+        _lib.verify_source(lib, expected="0000000000000000")
+
+
+def test_plan_costs_and_kernel_names():
+    """Every launch of a plan records its algorithmic bytes and FLOPs (bench.py's per-launch
+    bounds) and every dp_conv2d launch the kernel instantiation the dispatcher picks."""
+    from detrpose_amd.profiling import canonical_kernel_name
+    model, _ = build_model("l")
+    load_synthetic(model, 0)
+    plan = Engine(model, "bf16", device="cpu").plan(4)
+    plan.add_postprocess()
+    for name, fn, _ in plan.ops + plan.post_ops:
+        assert name in plan.op_bytes and name in plan.op_flops, name
+        assert plan.op_bytes[name] > 0, name
+        if fn.__name__ == "dp_conv2d":
+            k = plan.kernel_of(name)
+            assert k.startswith(("conv_halo_kernel<", "conv_stream_kernel<", "conv_direct_kernel<")), (name, k)
+    assert "conv_halo_kernel<8, 4, 3, 3, 1, 128, false, false, 2, false, 0>" in plan.op_kernel.values()
+    # rocprofv3's mangled and demangled spellings reduce to the describe form
+    assert canonical_kernel_name("_ZN12_GLOBAL__N_118conv_stream_kernelILi256ELi256ELi2ELi8ELi2ELb1ELi2EDF16bLi0EEEv"
+                                 "12dp_conv_desciiii") == "conv_stream_kernel<256, 256, 2, 8, 2, true, 2, bf16, 0>"
+    assert canonical_kernel_name('"void (anonymous namespace)::conv_halo_kernel<8, 4, 3, 3, 1, 128, false, false, 2, '
+                                 'false, 0>(dp_conv_desc, int, int, int, int, (anonymous namespace)::HaloPool)"') == \
+        "conv_halo_kernel<8, 4, 3, 3, 1, 128, false, false, 2, false, 0>"
+
+
 def test_conv_desc_layout_matches_header():
     # the ctypes mirror must have the header's field order (checked by name list)
     txt = open(os.path.join(REPO, "include", "detrpose_hip.h")).read()
