@@ -28,7 +28,9 @@ def family(name):
                 "msda_kernel", "msda_wave_kernel", "add_rows_kernel", "stem_conv_kernel", "stem1_mfma_kernel",
                 "maxpool_kernel", "class_max_kernel",
                 "topk_kernel", "gate_ln_kernel", "sine_embed_kernel", "lqe_kernel", "pose_refine_kernel",
-                "linear_ln_kernel", "ffn_ln_kernel", "query_pos_kernel", "pose_mlp_kernel", "ln_classmax_kernel"):
+                "linear_ln_kernel", "ffn_ln_kernel", "query_pos_kernel", "pose_mlp_kernel", "ln_classmax_kernel",
+                "mha_ln_kernel", "linear_ln_cls_kernel", "attn_long_kernel", "stem_fused_kernel", "dwconv_tile_kernel",
+                "linear_small_kernel", "gate_ln_kernel"):
         if key in name:
             return key
     return "other"

@@ -225,13 +225,153 @@ def golden_train_forward(ref, size, batch, wseed=0):
     return st
 
 
+def dn_targets(B, K, sizes, seed):
+    """Synthetic COCO-style targets: labels, xyxy boxes, (x, y) keypoints + visibility (0/1),
+    area, all normalised."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for b, n in enumerate(sizes):
+        c = torch.rand(n, 2, generator=g) * 0.6 + 0.2
+        wh = torch.rand(n, 2, generator=g) * 0.3 + 0.05
+        boxes = torch.cat([c - wh / 2, c + wh / 2], 1)
+        xy = (c[:, None] + (torch.rand(n, K, 2, generator=g) - 0.5) * wh[:, None]).clamp(0, 1)
+        vis = (torch.rand(n, K, generator=g) > 0.25).float()
+        out.append({"labels": (torch.arange(n) + b) % 2, "boxes": boxes,
+                    "keypoints": torch.cat([xy.flatten(1), vis], 1), "area": wh.prod(1) * 0.53})
+    return out
+
+
+def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5):
+    """The reference's full training step with OKS-denoising queries (transformer.py:1265-1385,
+    dn_component.py:39-183) on CPU: training-mode forward WITH targets, the Criterion with its
+    dn_* losses (criterion.py:385-435), loss.backward(). BatchNorm layers in eval mode (frozen
+    BN) and the encoder outputs detached (a forward hook returns them detached), so the
+    gradients are those of the transformer's parameters (BASELINE config 5's decoder half).
+
+    Deliberate changes to the reference's run, none of which touches its arithmetic:
+      - torch.Tensor.cuda is the identity while it runs (prepare_for_cdn and the criterion's
+        DN indices call .cuda(): dn_component.py:115-116, 141-142, criterion.py:393-395);
+      - prepare_for_cdn is wrapped to record the DN inputs it draws (noised labels, noised
+        keypoints, attention mask, dn_meta), so the build can be fed the same ones;
+      - torch.argsort is the stable sort inside the criterion (see the module docstring);
+      - each class_embed[l] gets a copy of its input (a forward pre-hook returning x.clone()).
+        Its input output[:, :, 0] is a view of the decoder output that the next layer's
+        in-place with_pos_embed (transformer.py:369) bumps the version of, so in fp32 autograd
+        refuses the backward ("modified by an inplace operation"); the values of token 0
+        are never modified, so the copy changes no value or gradient. It is what the
+        reference's AMP training run does anyway (autocast's casts are copies).
+    Stored: targets, DN inputs, every loss, the outputs of every head, and for every
+    transformer parameter its gradient (full, f32)."""
+    from detrpose_amd.synthetic import load_synthetic, synthetic_images
+    import src.models.detrpose.transformer as tmod
+    Criterion, HungarianMatcher = _import_criterion()
+    torch.manual_seed(0)
+    model, _ = make_golden.build_reference(ref, size)
+    load_synthetic(model, seed=wseed)
+    model.train()
+    for m in model.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.eval()
+    K = model.transformer.num_body_points
+    images = synthetic_images(batch, seed=1)
+    targets = dn_targets(batch, K, sizes, tseed)
+    hk = model.encoder.register_forward_hook(lambda mod, a, out: [o.detach() for o in out])
+    hcls = [m.register_forward_pre_hook(lambda mod, a: (a[0].clone(),) + tuple(a[1:]))
+            for m in model.transformer.class_embed]
+    cap = {}
+    orig_cdn = tmod.prepare_for_cdn
+
+    def cdn_spy(*a, **kw):
+        r = orig_cdn(*a, **kw)
+        cap["cdn"] = r
+        return r
+
+    orig_cuda = torch.Tensor.cuda
+    orig_argsort = torch.argsort
+    matcher = HungarianMatcher(cost_class=2.0, cost_keypoints=10.0, cost_oks=4.0, focal_alpha=0.25,
+                               num_body_points=K)
+    crit = Criterion(num_classes=2, matcher=matcher, weight_dict={"loss_vfl": 2.0, "loss_keypoints": 10.0,
+                                                                 "loss_oks": 4.0},
+                     losses=["vfl", "keypoints"], num_body_points=K, focal_alpha=0.25)
+    tmod.prepare_for_cdn = cdn_spy
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        torch.manual_seed(dn_seed)
+        out = model(images, targets)
+        torch.argsort = lambda x, dim=-1, descending=False, **kw: torch.sort(x, dim=dim, descending=descending,
+                                                                             stable=True)[1]
+        losses = crit(out, targets)
+        torch.argsort = orig_argsort
+        total = sum(losses.values())
+        total.backward()
+    finally:
+        tmod.prepare_for_cdn = orig_cdn
+        torch.Tensor.cuda = orig_cuda
+        torch.argsort = orig_argsort
+        hk.remove()
+        for h in hcls:
+            h.remove()
+    label, pose, mask, meta = cap["cdn"]
+    st = {"meta": np.array([batch, wseed, 1, tseed, dn_seed], np.int64), "sizes": np.array(sizes, np.int64)}
+    T = sum(sizes)
+    st["tgt_labels"] = torch.cat([t["labels"] for t in targets]).numpy()
+    st["tgt_boxes"] = torch.cat([t["boxes"] for t in targets]).numpy()
+    st["tgt_kps"] = torch.cat([t["keypoints"] for t in targets]).numpy()
+    st["tgt_area"] = torch.cat([t["area"] for t in targets]).numpy()
+    # DN inputs as drawn: the label embedding rows come from label_enc, so store which
+    # label each DN slot embeds (-1: padding) by matching the rows back to label_enc
+    le = model.transformer.label_enc.weight.detach()
+    lab = label[:, :, 0].detach()   # (B, pad, C)
+    d = ((lab[:, :, None, :] - le[None, None]) ** 2).sum(-1)
+    slot = d.argmin(-1)
+    pad_zero = lab.abs().sum(-1) == 0
+    st["dn_label"] = torch.where(pad_zero, torch.full_like(slot, -1), slot).numpy()
+    assert float(d.min(-1)[0][~pad_zero].max()) == 0.0
+    st["dn_pose_unsig"] = pose.detach().numpy()
+    st["dn_attn_mask"] = mask.numpy()
+    st["dn_pad_size"] = np.array(meta["pad_size"])
+    st["dn_num_group"] = np.array(meta["num_dn_group"])
+    keys = sorted(losses)
+    st["loss_keys"] = np.array(keys)
+    st["loss_vals"] = np.array([float(losses[k]) for k in keys], np.float64)
+
+    def head(name, o):
+        st[name + ".pred_logits"] = o["pred_logits"].detach().numpy()
+        st[name + ".pred_keypoints"] = o["pred_keypoints"].detach().numpy()
+
+    head("out", out)
+    for i, o in enumerate(out["aux_outputs"]):
+        head(f"aux{i}", o)
+    head("pre", out["aux_pre_outputs"])
+    head("interm", out["aux_interm_outputs"][0])
+    for i, o in enumerate(out["dn_aux_outputs"]):
+        head(f"dn{i}", o)
+    head("dn_pre", out["dn_aux_pre_outputs"])
+    ng = 0
+    for n, p in model.transformer.named_parameters():
+        if p.grad is not None:
+            st["grad." + n] = p.grad.numpy()
+            ng += 1
+    print(f"  [{size}] DN train step b{batch} targets {sizes}: pad {meta['pad_size']} groups {meta['num_dn_group']}, "
+          f"{len(keys)} losses, total {float(total):.6f}, {ng} parameter gradients")
+    return st
+
+
 def main():
     torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
     Criterion, HungarianMatcher = _import_criterion()
     ref = make_golden._import_reference()
+    if os.environ.get("ONLY_DN"):
+        st = golden_train_dn(ref, "n", 2, [3, 1])
+        np.savez_compressed(os.path.join(HERE, "train_dn_n_b2.npz"), **st)
+        print("wrote train_dn_n_b2.npz")
+        return
     st = golden_train_forward(ref, "n", 2)
     np.savez_compressed(os.path.join(HERE, "train_forward_n_b2.npz"), **st)
     print("wrote train_forward_n_b2.npz")
+    st = golden_train_dn(ref, "n", 2, [3, 1])
+    np.savez_compressed(os.path.join(HERE, "train_dn_n_b2.npz"), **st)
+    print("wrote train_dn_n_b2.npz")
     for name, (B, Q, ncls, K, n_aux, sizes, seed) in CASES.items():
         st = make_case(Criterion, HungarianMatcher, B, Q, ncls, K, n_aux, sizes, seed)
         np.savez_compressed(os.path.join(HERE, f"criterion_{name}.npz"), **st)

@@ -1,0 +1,93 @@
+"""The training oracle (oracle/train_cpu.py: training-mode transformer with OKS-denoising
+queries + the criterion's dn_* losses, differentiated by torch autograd) against the
+reference's own training step (tests/golden/train_dn_n_b2.npz, made by
+tests/golden/make_train_golden.py): every head output, every loss and the gradient of
+every transformer parameter. CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from detrpose_amd import build_model
+from detrpose_amd.configs import get_config
+from detrpose_amd.synthetic import load_synthetic, synthetic_images
+
+
+def dn_inputs(g):
+    return {"label": g["dn_label"], "pose_unsig": g["dn_pose_unsig"], "attn_mask": g["dn_attn_mask"],
+            "num_group": int(g["dn_num_group"])}
+
+
+def targets_of(g):
+    sizes = [int(v) for v in g["sizes"]]
+    return sizes, torch.as_tensor(g["tgt_labels"]), torch.as_tensor(g["tgt_kps"]), torch.as_tensor(g["tgt_area"])
+
+
+def oracle_train_step(size, g, sd=None):
+    """Encoder outputs of the golden images (oracle eval forward, frozen BN), then the
+    oracle's training transformer + criterion with the golden DN draws; returns
+    (res, losses, grads) with grads keyed like the golden (parameter names under transformer.)."""
+    from oracle.detrpose_cpu import backbone, encoder
+    from oracle.train_cpu import losses, train_transformer
+    cfg = get_config(size)
+    model, _ = build_model(size)
+    params = {k for k, v in model.named_parameters() if v.requires_grad}
+    if sd is None:
+        load_synthetic(model, seed=int(g["meta"][1]))
+        sd = {k: v.detach().float() for k, v in model.state_dict().items()}
+    B = int(g["meta"][0])
+    images = synthetic_images(B, seed=int(g["meta"][2]))
+    with torch.no_grad():
+        bc, ec = cfg["backbone"], cfg["encoder"]
+        feats = encoder(backbone(images, sd, bc["name"], bc["return_idx"], bc["use_lab"]), sd, ec)
+    P = {k: (v.clone().requires_grad_(True) if k.startswith("transformer.") and k in params else v)
+         for k, v in sd.items()}
+    res = train_transformer(feats, P, cfg["transformer"], dn=dn_inputs(g))
+    sizes, lab, kps, area = targets_of(g)
+    ld, _, _ = losses(res, sizes, lab, kps, area, cfg["transformer"]["num_body_points"],
+                      cfg["transformer"]["num_classes"])
+    sum(ld.values()).backward()
+    grads = {"grad." + k[len("transformer."):]: v.grad for k, v in P.items()
+             if isinstance(v, torch.Tensor) and v.requires_grad and v.grad is not None}
+    return res, ld, grads, feats
+
+
+@pytest.fixture(scope="module")
+def dn_case(golden_dir):
+    g = np.load(os.path.join(golden_dir, "train_dn_n_b2.npz"))
+    return g, oracle_train_step("n", g)
+
+
+def test_oracle_dn_heads_match_reference(dn_case):
+    g, (res, _, _, _) = dn_case
+    heads = {"out": res["final"], "pre": res["pre"], "interm": res["interm"], "dn_pre": res["dn_pre"]}
+    heads.update({f"aux{i}": h for i, h in enumerate(res["aux"])})
+    heads.update({f"dn{i}": h for i, h in enumerate(res["dn"])})
+    for name, h in heads.items():
+        for k in ("pred_logits", "pred_keypoints"):
+            np.testing.assert_allclose(h[k].detach().numpy(), g[f"{name}.{k}"], atol=2e-4, rtol=1e-4,
+                                       err_msg=f"{name}.{k}")
+
+
+def test_oracle_dn_losses_match_reference(dn_case):
+    g, (_, ld, _, _) = dn_case
+    assert list(ld) == [str(k) for k in g["loss_keys"]]
+    np.testing.assert_allclose([float(v) for v in ld.values()], g["loss_vals"], rtol=1e-5, atol=1e-6)
+
+
+def test_oracle_dn_gradients_match_reference(dn_case):
+    """Every transformer parameter gradient within 1e-4 of its own scale (max |g|)."""
+    g, (_, _, grads, _) = dn_case
+    names = [k for k in g.files if k.startswith("grad.")]
+    assert sorted(names) == sorted(grads), set(names) ^ set(grads)
+    worst = []
+    for k in names:
+        ref = g[k]
+        got = grads[k].numpy()
+        scale = max(float(np.abs(ref).max()), 1e-12)
+        err = float(np.abs(got - ref).max()) / scale
+        worst.append((err, k))
+        assert err <= 1e-4, (k, err)
+    worst.sort(reverse=True)
+    print("worst relative gradient errors:", worst[:5])
