@@ -55,6 +55,18 @@ class LossHead(C.Structure):
                 ("match", vp)]
 
 
+class GemmDesc(C.Structure):
+    """Mirror of dp_gemm_desc."""
+    _fields_ = [("a", vp), ("a_bs", i64), ("a_rs", i64), ("a_ks", i64),
+                ("b", vp), ("b_bs", i64), ("b_ks", i64), ("b_ns", i64),
+                ("c", vp), ("c_bs", i64), ("c_rs", i64),
+                ("batch", i32), ("m", i32), ("n", i32), ("k", i32),
+                ("in_dtype", i32), ("out_dtype", i32),
+                ("bias", vp), ("alpha", f32), ("beta", f32), ("act", i32),
+                ("gate", vp), ("gate_bs", i64), ("gate_rs", i64), ("gate_dtype", i32),
+                ("split_k", i32)]
+
+
 def rowmap(base=0, group=1, stride_g=0, stride_r=0) -> RowMap:
     return RowMap(int(base), int(group), int(stride_g), int(stride_r))
 
@@ -84,7 +96,7 @@ _SIGS = {
     "dp_resize_pad": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, f32, vp]),
     "dp_msda_core_fwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "dp_msda_core_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, i32, vp]),
-    "dp_msda_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, i32, vp]),
+    "dp_msda_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp]),
     "dp_topk": (i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
     "dp_class_max": (i32, [vp, i32, i32, vp, vp, i32, vp, i32, vp]),
     "dp_gather_rows": (i32, [vp, i64, vp, i32, i32, i32, vp, i32, vp]),
@@ -110,6 +122,25 @@ _SIGS = {
     "dp_match_union": (i32, [vp, i32, i32, i32, vp, vp, vp]),
     "dp_pose_loss": (i32, [C.POINTER(LossHead), i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp,
                            f32, f32, f32, f32, vp, vp, vp, vp, vp]),
+    # training step (include/detrpose_hip.h, "Training step")
+    "dp_gemm": (i32, [C.POINTER(GemmDesc), vp]),
+    "dp_ln_fwd": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp, i32, i32, i32, vp]),
+    "dp_ln_bwd": (i32, [vp, vp, i32, vp, vp, vp, i32, i32, vp, vp, i32, i32, vp]),
+    "dp_colsum": (i32, [vp, i64, i32, i32, vp, i32, i32, vp]),
+    "dp_attn_fwd": (i32, [vp, i32, vp, vp, i32, vp, i32, vp, vp, i32, i32, i64, i64, i64, i32, i32, i32, i32, vp]),
+    "dp_attn_bwd": (i32, [vp, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, i64, i64, i64, i32, i32,
+                          i32, i32, vp]),
+    "dp_gate_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
+    "dp_gate_bwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, vp]),
+    "dp_query_build": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp]),
+    "dp_query_build_bwd": (i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, i32, vp]),
+    "dp_pose_refine_bwd": (i32, [vp, vp, i32, f32, vp, i32, i32, vp, i32, vp]),
+    "dp_sigmoid_bwd": (i32, [vp, vp, vp, i32, i32, i64, i64, i64, vp]),
+    "dp_lqe_stats_bwd": (i32, [vp, i64, i32, i32, i32, vp, vp, i32, i32, i32, vp, i32, vp]),
+    "dp_scatter_rows": (i32, [vp, i32, vp, i32, i32, i32, vp, i64, i32, i32, i32, vp]),
+    "dp_gather_rows_masked": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, vp, i32, vp]),
+    "dp_convert_rows": (i32, [vp, i32, i64, vp, i32, i64, i32, i32, f32, i32, vp]),
+    "dp_zero": (i32, [vp, i64, vp]),
 }
 
 EXPORTED = tuple(k for k in _SIGS)

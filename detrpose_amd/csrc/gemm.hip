@@ -1,0 +1,318 @@
+// General strided (batched) GEMM on MFMA for the training step: every nn.Linear forward,
+// its input gradient (dgrad) and its weight gradient (wgrad) is one dp_gemm call with the
+// right strides, so no operand is ever transposed in memory.
+//
+//   C(b, m, n) = epilogue( alpha * sum_k A(b, m, k) * B(b, k, n) )
+//   A(b, m, k) = a[b*a_bs + m*a_rs + k*a_ks],  B(b, k, n) = b[b*b_bs + k*b_ks + n*b_ns],
+//   C(b, m, n) = c[b*c_bs + m*c_rs + n].
+//   Linear y = x W^T:  A = x (a_rs = ld, a_ks = 1), B(k, n) = W[n][k] (b_ks = 1, b_ns = K)
+//   dgrad dx = dy W:   A = dy,                       B(k, n) = W[k][n] (b_ks = K, b_ns = 1)
+//   wgrad dW = dy^T x: A(m, k) = dy[k][m] (a_rs = 1, a_ks = ld), B(k, n) = x[k][n]
+//
+// Tile: 64x64 outputs per 256-thread block (4 waves, 32x32 each = 2x2 MFMA 16x16 tiles), K step
+// of 128 bytes per row (64 bf16 / 32 f32). A and B tiles are staged in LDS k-contiguous
+// ([row][k], 16-byte padded rows) whatever their global layout: a k-contiguous operand loads
+// 16-byte row chunks, an m/n-contiguous one loads 16-byte column chunks and scatters them,
+// anything else loads elements. The next K step's global loads are issued into registers
+// before the MFMAs of the current one (register double buffer, one LDS buffer per operand).
+// bf16 inputs: mfma_f32_16x16x32_bf16; f32 inputs: mfma_f32_16x16x4f32 (exact f32 products).
+// Split-K (when the M x N grid cannot fill the chip, e.g. wgrad over 10^5 rows): each block
+// adds alpha * its partial product into f32 C with atomics (C pre-initialised by the caller).
+#include "common.h"
+
+namespace {
+
+constexpr int TM = 64, TN = 64;
+
+template <typename TI>
+struct GemmTraits;
+template <>
+struct GemmTraits<bf16_t> {
+  static constexpr int BK = 64, VEC = 8, PITCH = 72;   // 144-byte LDS rows
+};
+template <>
+struct GemmTraits<float> {
+  static constexpr int BK = 32, VEC = 4, PITCH = 36;   // 144-byte LDS rows
+};
+
+struct Operand {
+  const void* p;
+  int64_t bs, rs, ks;   // batch, row (m or n), k strides (elements)
+  int rows;             // M or N
+};
+
+// global -> registers for one 64 x BK tile of an operand (row r, k), zero outside.
+// mode 0: k contiguous (ks == 1): 2 x 16-byte chunks per thread of (row, k-chunk)
+// mode 1: rows contiguous (rs == 1): 2 x 16-byte chunks per thread of (k, row-chunk)
+// mode 2: generic: per-element loads
+template <typename TI>
+struct TileRegs {
+  static constexpr int BK = GemmTraits<TI>::BK, VEC = GemmTraits<TI>::VEC;
+  static constexpr int NE = TM * BK / 256;   // elements per thread (16 bf16 / 8 f32)
+  TI v[NE];
+};
+
+template <typename TI>
+__device__ __forceinline__ void load_tile(TileRegs<TI>& t, const Operand& op, int mode, int64_t base, int r0, int k0,
+                                          int K) {
+  constexpr int BK = GemmTraits<TI>::BK, VEC = GemmTraits<TI>::VEC;
+  const TI* p = reinterpret_cast<const TI*>(op.p) + base;
+  const int tid = threadIdx.x;
+  if (mode == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / (BK / VEC), kc = (c % (BK / VEC)) * VEC;
+      const int gr = r0 + r, gk = k0 + kc;
+      if (gr < op.rows && gk + VEC <= K) {
+        *reinterpret_cast<uint4*>(&t.v[i * VEC]) = *reinterpret_cast<const uint4*>(p + (int64_t)gr * op.rs + gk);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e)
+          t.v[i * VEC + e] = (gr < op.rows && gk + e < K) ? p[(int64_t)gr * op.rs + gk + e] : (TI)0.f;
+      }
+    }
+  } else if (mode == 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int kk = c / (TM / VEC), rc = (c % (TM / VEC)) * VEC;
+      const int gr = r0 + rc, gk = k0 + kk;
+      if (gk < K && gr + VEC <= op.rows) {
+        *reinterpret_cast<uint4*>(&t.v[i * VEC]) = *reinterpret_cast<const uint4*>(p + (int64_t)gk * op.ks + gr);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e)
+          t.v[i * VEC + e] = (gk < K && gr + e < op.rows) ? p[(int64_t)gk * op.ks + gr + e] : (TI)0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < TileRegs<TI>::NE; ++e) {
+      const int idx = tid + 256 * e;
+      const int r = idx / BK, kk = idx % BK;
+      const int gr = r0 + r, gk = k0 + kk;
+      t.v[e] = (gr < op.rows && gk < K) ? p[(int64_t)gr * op.rs + (int64_t)gk * op.ks] : (TI)0.f;
+    }
+  }
+}
+
+template <typename TI>
+__device__ __forceinline__ void store_tile(const TileRegs<TI>& t, TI* lds, int mode) {
+  constexpr int BK = GemmTraits<TI>::BK, VEC = GemmTraits<TI>::VEC, PITCH = GemmTraits<TI>::PITCH;
+  const int tid = threadIdx.x;
+  if (mode == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / (BK / VEC), kc = (c % (BK / VEC)) * VEC;
+      *reinterpret_cast<uint4*>(lds + r * PITCH + kc) = *reinterpret_cast<const uint4*>(&t.v[i * VEC]);
+    }
+  } else if (mode == 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int kk = c / (TM / VEC), rc = (c % (TM / VEC)) * VEC;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) lds[(rc + e) * PITCH + kk] = t.v[i * VEC + e];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < TileRegs<TI>::NE; ++e) {
+      const int idx = tid + 256 * e;
+      lds[(idx / BK) * PITCH + idx % BK] = t.v[e];
+    }
+  }
+}
+
+struct GemmArgs {
+  Operand A, B;
+  float* cf;
+  bf16_t* cb;
+  int64_t c_bs, c_rs;
+  int M, N, K, batch, splits, kchunk;
+  const float* bias;
+  float alpha, beta;
+  int act;
+  const void* gate;
+  int64_t g_bs, g_rs;
+  int gate_bf16;
+  int modeA, modeB;
+  int tiles_n;
+};
+
+template <typename TI>
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs g) {
+  constexpr int BK = GemmTraits<TI>::BK, PITCH = GemmTraits<TI>::PITCH;
+  __shared__ __attribute__((aligned(16))) TI As[TM * PITCH];
+  __shared__ __attribute__((aligned(16))) TI Bs[TN * PITCH];
+  const int tile = blockIdx.x;
+  const int tm = tile / g.tiles_n, tn = tile - tm * g.tiles_n;
+  const int zb = blockIdx.y;
+  const int bidx = zb / g.splits, split = zb - bidx * g.splits;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int kb = split * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  const int64_t abase = (int64_t)bidx * g.A.bs, bbase = (int64_t)bidx * g.B.bs;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  TileRegs<TI> ra, rb;
+  // k is measured from kb inside the chunk (the operand base absorbs kb)
+  Operand A = g.A, B = g.B;
+  const int64_t aoff = abase + (int64_t)kb * A.ks, boff = bbase + (int64_t)kb * B.ks;
+  const int KC = ke - kb;
+  if (KC > 0) {
+    load_tile<TI>(ra, A, g.modeA, aoff, m0, 0, KC);
+    load_tile<TI>(rb, B, g.modeB, boff, n0, 0, KC);
+  }
+  for (int k0 = 0; k0 < KC; k0 += BK) {
+    __syncthreads();
+    store_tile<TI>(ra, As, g.modeA);
+    store_tile<TI>(rb, Bs, g.modeB);
+    __syncthreads();
+    if (k0 + BK < KC) {
+      load_tile<TI>(ra, A, g.modeA, aoff, m0, k0 + BK, KC);
+      load_tile<TI>(rb, B, g.modeB, boff, n0, k0 + BK, KC);
+    }
+    if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        const int ko = ks * 32 + (lane >> 4) * 8;
+        bf16x8 af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(As + (wm + 16 * i + (lane & 15)) * PITCH + ko);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn + 16 * j + (lane & 15)) * PITCH + ko);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK / 4; ++ks) {
+        const int ko = ks * 4 + (lane >> 4);
+        float af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = As[(wm + 16 * i + (lane & 15)) * PITCH + ko];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfr[j] = Bs[(wn + 16 * j + (lane & 15)) * PITCH + ko];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue: lane holds C[row = 4 (lane >> 4) + r][col = lane & 15] of each 16x16 tile
+  const int64_t cb = (int64_t)bidx * g.c_bs;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + 16 * j + (lane & 15);
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+        if (m >= g.M) continue;
+        const int64_t o = cb + (int64_t)m * g.c_rs + n;
+        float v = g.alpha * acc[i][j][r];
+        if (g.splits > 1) {
+          unsafeAtomicAdd(g.cf + o, v);
+          continue;
+        }
+        if (g.bias) v += g.bias[n];
+        if (g.beta != 0.f) v += g.beta * (g.cf ? g.cf[o] : (float)g.cb[o]);
+        if (g.act == DP_ACT_RELU) v = fmaxf(v, 0.f);
+        if (g.gate) {
+          const int64_t go = (int64_t)bidx * g.g_bs + (int64_t)m * g.g_rs + n;
+          const float gv = g.gate_bf16 ? (float)reinterpret_cast<const bf16_t*>(g.gate)[go]
+                                       : reinterpret_cast<const float*>(g.gate)[go];
+          if (!(gv > 0.f)) v = 0.f;
+        }
+        if (g.cf) g.cf[o] = v;
+        else g.cb[o] = (bf16_t)v;
+      }
+    }
+}
+
+int operand_mode(const Operand& op, int vec, int64_t align_bytes_ok) {
+  if (op.ks == 1 && op.rs % vec == 0 && align_bytes_ok) return 0;
+  if (op.rs == 1 && op.ks % vec == 0 && align_bytes_ok) return 1;
+  return 2;
+}
+
+}  // namespace
+
+extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
+  DP_REQUIRE(dp != nullptr, "dp_gemm: null descriptor");
+  const dp_gemm_desc& d = *dp;
+  DP_REQUIRE(d.a && d.b && d.c, "dp_gemm: null operand");
+  DP_REQUIRE(d.m > 0 && d.n > 0 && d.k > 0 && d.batch > 0, "dp_gemm: bad sizes m=%d n=%d k=%d batch=%d", d.m, d.n,
+             d.k, d.batch);
+  DP_REQUIRE(d.in_dtype == DP_BF16 || d.in_dtype == DP_F32, "dp_gemm: bad input dtype %d", d.in_dtype);
+  DP_REQUIRE(d.out_dtype == DP_BF16 || d.out_dtype == DP_F32, "dp_gemm: bad output dtype %d", d.out_dtype);
+  DP_REQUIRE(d.act == DP_ACT_NONE || d.act == DP_ACT_RELU, "dp_gemm: act %d (none / relu)", d.act);
+  DP_REQUIRE(d.split_k >= 0, "dp_gemm: split_k %d", d.split_k);
+  const int es = d.in_dtype == DP_BF16 ? 2 : 4;
+  const int vec = 16 / es;
+  const int BK = d.in_dtype == DP_BF16 ? 64 : 32;
+  GemmArgs g{};
+  g.A = Operand{d.a, d.a_bs, d.a_rs, d.a_ks, d.m};
+  g.B = Operand{d.b, d.b_bs, d.b_ns, d.b_ks, d.n};
+  const bool aal = (reinterpret_cast<uintptr_t>(d.a) & 15) == 0 && d.a_bs % vec == 0;
+  const bool bal = (reinterpret_cast<uintptr_t>(d.b) & 15) == 0 && d.b_bs % vec == 0;
+  g.modeA = operand_mode(g.A, vec, aal);
+  g.modeB = operand_mode(g.B, vec, bal);
+  g.cf = d.out_dtype == DP_F32 ? reinterpret_cast<float*>(d.c) : nullptr;
+  g.cb = d.out_dtype == DP_BF16 ? reinterpret_cast<bf16_t*>(d.c) : nullptr;
+  g.c_bs = d.c_bs;
+  g.c_rs = d.c_rs;
+  g.M = d.m, g.N = d.n, g.K = d.k, g.batch = d.batch;
+  g.bias = d.bias;
+  g.alpha = d.alpha;
+  g.beta = d.beta;
+  g.act = d.act;
+  g.gate = d.gate;
+  g.g_bs = d.gate_bs;
+  g.g_rs = d.gate_rs;
+  g.gate_bf16 = d.gate_dtype == DP_BF16;
+  const int tm = (d.m + TM - 1) / TM, tn = (d.n + TN - 1) / TN;
+  g.tiles_n = tn;
+  // split-K when the output grid cannot fill the chip and K is long (f32 C, plain epilogue)
+  int splits = 1;
+  const int ksteps = (d.k + BK - 1) / BK;
+  const int64_t tiles = (int64_t)tm * tn * d.batch;
+  if (d.split_k > 0) {
+    splits = d.split_k;
+  } else if (tiles < 512 && ksteps >= 8 && d.out_dtype == DP_F32 && !d.bias && d.act == DP_ACT_NONE && !d.gate &&
+             d.beta == 1.f) {
+    splits = (int)((512 + tiles - 1) / tiles);
+    if (splits > ksteps / 4) splits = ksteps / 4;
+    if (splits < 1) splits = 1;
+  }
+  if (splits > ksteps) splits = ksteps;
+  DP_REQUIRE(splits == 1 || (d.out_dtype == DP_F32 && !d.bias && d.act == DP_ACT_NONE && !d.gate && d.beta == 1.f),
+             "dp_gemm: split-K accumulates into f32 C (beta 1, no bias / act / gate)");
+  g.splits = splits;
+  g.kchunk = ((ksteps + splits - 1) / splits) * BK;
+  DP_REQUIRE(tiles * 1 < (1ll << 31) && (int64_t)d.batch * splits < 65536, "dp_gemm: grid too large");
+  dim3 grid((unsigned)(tm * tn), (unsigned)(d.batch * splits)), block(256);
+  hipStream_t s = as_stream(stream);
+  if (d.in_dtype == DP_BF16)
+    hipLaunchKernelGGL(gemm_kernel<bf16_t>, grid, block, 0, s, g);
+  else
+    hipLaunchKernelGGL(gemm_kernel<float>, grid, block, 0, s, g);
+  return dp_check_launch("dp_gemm");
+}

@@ -137,9 +137,9 @@ template <typename T>
 __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(const T* __restrict__ value, int S, TLevels lv, int L,
                                                              int P, const float* __restrict__ oa,
                                                              const float* __restrict__ ref, const T* __restrict__ gout,
-                                                             float* __restrict__ gvalue, float* __restrict__ goa,
-                                                             float* __restrict__ gref, int lq, int pairs, int nh,
-                                                             int dh) {
+                                                             int ldg, float* __restrict__ gvalue,
+                                                             float* __restrict__ goa, float* __restrict__ gref, int lq,
+                                                             int pairs, int nh, int dh) {
   constexpr int VEC = Vec16<T>::N;
   const int cpt = dh / VEC;
   const int ppw = 64 / cpt;
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(const T* __restrict
   float* grow = goa + (int64_t)r * ncol;
   const float* lg = orow + nh * LP * 2 + h * LP;
   float go[VEC];
-  load_vec(gout + (int64_t)r * C + ch, go);
+  load_vec(gout + (int64_t)r * ldg + ch, go);
   float mx = -INFINITY;
   for (int j = 0; j < LP; ++j) mx = fmaxf(mx, lg[j]);
   float den = 0.f;
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(const T* __restrict
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (row[k] < 0) continue;
+      if (row[k] < 0 || !gvalue) continue;
       float* gp = gvalue + ((int64_t)b * S + row[k]) * C + ch;
       const float sc = a * wk[k];
 #pragma unroll
@@ -307,30 +307,31 @@ extern "C" int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, con
 }
 
 extern "C" int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
-                           const float* offattn, const float* ref, const void* grad_out, int32_t lq, int32_t nhead,
-                           int32_t dh, int32_t npoints, float* grad_value, float* grad_offattn, float* grad_ref,
-                           int32_t dtype, void* stream) {
+                           const float* offattn, const float* ref, const void* grad_out, int32_t ld_grad_out,
+                           int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value,
+                           float* grad_offattn, float* grad_ref, int32_t dtype, void* stream) {
   TLevels lv;
   const int rc = check_core(value, batch, S, lvl_hw, nlevels, offattn, ref, lq, nhead, dh, npoints, dtype, &lv);
   if (rc) return rc;
-  DP_REQUIRE(grad_out && grad_value && grad_offattn, "dp_msda_bwd: null gradient pointer");
-  DP_REQUIRE((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0, "dp_msda_bwd: grad_out must be 16-byte aligned");
+  DP_REQUIRE(grad_out && grad_offattn, "dp_msda_bwd: null gradient pointer");
+  const int VEC = dtype == DP_BF16 ? 8 : 4;
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_grad_out % VEC == 0 && ld_grad_out >= nhead * dh,
+             "dp_msda_bwd: grad_out must be 16-byte aligned per row (ld %d)", ld_grad_out);
   hipStream_t s = as_stream(stream);
   // grad_value (and grad_ref) are accumulated by atomics: clear them on the stream first
-  if (hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess ||
+  if ((grad_value && hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess) ||
       (grad_ref && hipMemsetAsync(grad_ref, 0, (size_t)batch * lq * 2 * sizeof(float), s) != hipSuccess))
     return dp_check_launch("dp_msda_bwd(memset)");
-  const int VEC = dtype == DP_BF16 ? 8 : 4;
   const int ppw = 64 / (dh / VEC);
   const int pairs = batch * lq * nhead;
   const int grid = ((pairs + ppw - 1) / ppw + 3) / 4;
   if (dtype == DP_BF16)
     hipLaunchKernelGGL(msda_fused_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)value, S, lv,
-                       nlevels, npoints, offattn, ref, (const bf16_t*)grad_out, grad_value, grad_offattn, grad_ref, lq,
+                       nlevels, npoints, offattn, ref, (const bf16_t*)grad_out, ld_grad_out, grad_value, grad_offattn, grad_ref, lq,
                        pairs, nhead, dh);
   else
     hipLaunchKernelGGL(msda_fused_bwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)value, S, lv, nlevels,
-                       npoints, offattn, ref, (const float*)grad_out, grad_value, grad_offattn, grad_ref, lq, pairs,
+                       npoints, offattn, ref, (const float*)grad_out, ld_grad_out, grad_value, grad_offattn, grad_ref, lq, pairs,
                        nhead, dh);
   return dp_check_launch("dp_msda_bwd");
 }

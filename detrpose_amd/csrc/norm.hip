@@ -59,9 +59,11 @@ __global__ __launch_bounds__(256) void add_rows_kernel(T* out, dp_rowmap om, con
   const int i = (int)(gid - r * nch) * VEC;
   float x[VEC], y[VEC];
   vload<T, VEC>(a + rowmap_off(am, r) + i, x);
-  vload<T, VEC>(b + rowmap_off(bm, r) + i, y);
+  if (b) {   // b == NULL: a row copy through the maps
+    vload<T, VEC>(b + rowmap_off(bm, r) + i, y);
 #pragma unroll
-  for (int t = 0; t < VEC; ++t) x[t] += y[t];
+    for (int t = 0; t < VEC; ++t) x[t] += y[t];
+  }
   vstore<T, VEC>(out + rowmap_off(om, r) + i, x);
 }
 

@@ -1,0 +1,835 @@
+// Row ops of the training step: forward versions that save what the
+// backward needs, and the backward kernels, for the transformer's training forward with
+// OKS-denoising queries. The Linear layers are dp_gemm (gemm.hip); the MSDA module is
+// dp_msda / dp_msda_bwd (msda.hip, msda_train.hip). Reference lines on each entry point in
+// include/detrpose_hip.h. f32 math everywhere; activations / activation gradients of dtype.
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ T* tp(void* p) {
+  return reinterpret_cast<T*>(p);
+}
+template <typename T>
+__device__ __forceinline__ const T* tp(const void* p) {
+  return reinterpret_cast<const T*>(p);
+}
+
+constexpr int LN_E = 8;   // c <= 512: up to 8 elements per lane
+
+// ---------------------------------------------------------------- LayerNorm
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(T* __restrict__ y, int ld_y, const T* __restrict__ x,
+                                                     const T* __restrict__ res, T* __restrict__ s,
+                                                     float* __restrict__ stats, const float* __restrict__ g,
+                                                     const float* __restrict__ bt, float eps, int rows, int c,
+                                                     const T* __restrict__ post, int pgroup, int pskip) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  float v[LN_E];
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < LN_E; ++t) {
+    const int j = lane + 64 * t;
+    v[t] = 0.f;
+    if (j < c) {
+      v[t] = to_f32(x[(int64_t)r * c + j]) + (res ? to_f32(res[(int64_t)r * c + j]) : 0.f);
+      if (s) s[(int64_t)r * c + j] = from_f32<T>(v[t]);
+      sum += v[t];
+    }
+  }
+  const float mean = wave_sum(sum) / c;
+  float q = 0.f;
+#pragma unroll
+  for (int t = 0; t < LN_E; ++t)
+    if (lane + 64 * t < c) q += (v[t] - mean) * (v[t] - mean);
+  const float rstd = rsqrtf(wave_sum(q) / c + eps);
+  if (lane == 0) {
+    stats[2 * (int64_t)r] = mean;
+    stats[2 * (int64_t)r + 1] = rstd;
+  }
+  int64_t prow = -1;
+  if (post) {
+    const int gi = r % pgroup;
+    if (gi >= pskip) prow = (int64_t)(r / pgroup) * (pgroup - pskip) + gi - pskip;
+  }
+#pragma unroll
+  for (int t = 0; t < LN_E; ++t) {
+    const int j = lane + 64 * t;
+    if (j < c) {
+      float o = (v[t] - mean) * rstd * g[j] + bt[j];
+      if (prow >= 0) o += to_f32(post[prow * c + j]);
+      y[(int64_t)r * ld_y + j] = from_f32<T>(o);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(T* __restrict__ dx, const T* __restrict__ dy, int ld_dy,
+                                                     const T* __restrict__ s, const float* __restrict__ stats,
+                                                     const float* __restrict__ g, int rows, int c,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta, int acc) {
+  __shared__ float red[2][4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pg[LN_E], pb[LN_E];
+#pragma unroll
+  for (int t = 0; t < LN_E; ++t) pg[t] = pb[t] = 0.f;
+  for (int r = blockIdx.x * 4 + wave; r < rows; r += gridDim.x * 4) {
+    const float mean = stats[2 * (int64_t)r], rstd = stats[2 * (int64_t)r + 1];
+    float xh[LN_E], gy[LN_E], d[LN_E];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < LN_E; ++t) {
+      const int j = lane + 64 * t;
+      xh[t] = gy[t] = d[t] = 0.f;
+      if (j < c) {
+        d[t] = to_f32(dy[(int64_t)r * ld_dy + j]);
+        xh[t] = (to_f32(s[(int64_t)r * c + j]) - mean) * rstd;
+        gy[t] = d[t] * g[j];
+        s1 += gy[t];
+        s2 += gy[t] * xh[t];
+        pg[t] += d[t] * xh[t];
+        pb[t] += d[t];
+      }
+    }
+    s1 = wave_sum(s1) / c;
+    s2 = wave_sum(s2) / c;
+#pragma unroll
+    for (int t = 0; t < LN_E; ++t) {
+      const int j = lane + 64 * t;
+      if (j < c) {
+        float o = rstd * (gy[t] - s1 - xh[t] * s2);
+        T* p = dx + (int64_t)r * c + j;
+        if (acc) o += to_f32(*p);
+        *p = from_f32<T>(o);
+      }
+    }
+  }
+  if (!dgamma) return;
+#pragma unroll
+  for (int t = 0; t < LN_E; ++t) {
+    const int j = lane + 64 * t;
+    if (j < c) {
+      red[0][wave][j] = pg[t];
+      red[1][wave][j] = pb[t];
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < c; j += 256) {
+    unsafeAtomicAdd(dgamma + j, red[0][0][j] + red[0][1][j] + red[0][2][j] + red[0][3][j]);
+    unsafeAtomicAdd(dbeta + j, red[1][0][j] + red[1][1][j] + red[1][2][j] + red[1][3][j]);
+  }
+}
+
+// ---------------------------------------------------------------- column sums (bias grads)
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, int64_t ld, int rows, int n,
+                                                     float* __restrict__ out, int rows_per) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r) acc += to_f32(x[(int64_t)r * ld + j]);
+  unsafeAtomicAdd(out + j, acc);
+}
+
+// ---------------------------------------------------------------- attention core
+// One wave per (sequence, head). K and V of the sequence's head in LDS (f32); lane i owns
+// query rows i, i + 64, ... P is saved as [key j][query i] so the writes are coalesced.
+constexpr int ATT_DH = 64;
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_fwd_kernel(const T* __restrict__ q, int ldq, const T* __restrict__ k,
+                                                      const T* __restrict__ v, int ldkv, T* __restrict__ out, int ldo,
+                                                      float* __restrict__ psave, const uint8_t* __restrict__ mask,
+                                                      int n_inner, int64_t so, int64_t si, int64_t st, int L,
+                                                      int nhead, int dh, float scale) {
+  extern __shared__ float sm[];
+  float* Ks = sm;
+  float* Vs = sm + L * dh;
+  const int lane = threadIdx.x;
+  const int h = blockIdx.x % nhead;
+  const int seq = blockIdx.x / nhead;
+  const int o = seq / n_inner, ii = seq - o * n_inner;
+  const int64_t row0 = o * so + ii * si;
+  for (int e = lane; e < L * dh; e += 64) {
+    const int t = e / dh, dd = e - t * dh;
+    const int64_t rr = row0 + t * st;
+    Ks[e] = to_f32(k[rr * ldkv + h * dh + dd]);
+    Vs[e] = to_f32(v[rr * ldkv + h * dh + dd]);
+  }
+  __syncthreads();
+  float* P = psave + (int64_t)blockIdx.x * L * L;
+  for (int i = lane; i < L; i += 64) {
+    const int64_t ri = row0 + i * st;
+    float qi[ATT_DH];
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd) qi[dd] = dd < dh ? to_f32(q[ri * ldq + h * dh + dd]) * scale : 0.f;
+    float m = -INFINITY, l = 0.f;
+    for (int j = 0; j < L; ++j) {
+      if (mask && mask[i * L + j]) continue;
+      float sc = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < ATT_DH; ++dd)
+        if (dd < dh) sc = fmaf(qi[dd], Ks[j * dh + dd], sc);
+      const float mn = fmaxf(m, sc);
+      l = l * __expf(m - mn) + __expf(sc - mn);
+      m = mn;
+    }
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    float acc[ATT_DH];
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
+    for (int j = 0; j < L; ++j) {
+      float p = 0.f;
+      if (!(mask && mask[i * L + j])) {
+        float sc = 0.f;
+#pragma unroll
+        for (int dd = 0; dd < ATT_DH; ++dd)
+          if (dd < dh) sc = fmaf(qi[dd], Ks[j * dh + dd], sc);
+        p = __expf(sc - m) * inv;
+      }
+      P[(int64_t)j * L + i] = p;
+#pragma unroll
+      for (int dd = 0; dd < ATT_DH; ++dd)
+        if (dd < dh) acc[dd] = fmaf(p, Vs[j * dh + dd], acc[dd]);
+    }
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd)
+      if (dd < dh) out[ri * ldo + h * dh + dd] = from_f32<T>(acc[dd]);
+  }
+}
+
+// Backward: dV_j = sum_i P_ij dO_i; dS_ij = P_ij (dO_i . V_j - sum_j' P_ij' dO_i . V_j');
+// dQ_i = scale sum_j dS_ij K_j; dK_j = scale sum_i dS_ij Q_i (q read unscaled). dS overwrites P.
+template <typename T>
+__global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, int ldq, const T* __restrict__ k,
+                                                      const T* __restrict__ v, int ldkv, float* __restrict__ psave,
+                                                      const T* __restrict__ dout, int ldo, T* __restrict__ dq, int lddq,
+                                                      T* __restrict__ dk, T* __restrict__ dv, int lddkv, int n_inner,
+                                                      int64_t so, int64_t si, int64_t st, int L, int nhead, int dh,
+                                                      float scale) {
+  extern __shared__ float sm[];
+  float* Qs = sm;
+  float* Ks = sm + L * dh;
+  float* Vs = sm + 2 * L * dh;
+  float* Ds = sm + 3 * L * dh;   // dO
+  const int lane = threadIdx.x;
+  const int h = blockIdx.x % nhead;
+  const int seq = blockIdx.x / nhead;
+  const int o = seq / n_inner, ii = seq - o * n_inner;
+  const int64_t row0 = o * so + ii * si;
+  for (int e = lane; e < L * dh; e += 64) {
+    const int t = e / dh, dd = e - t * dh;
+    const int64_t rr = row0 + t * st;
+    Qs[e] = to_f32(q[rr * ldq + h * dh + dd]);
+    Ks[e] = to_f32(k[rr * ldkv + h * dh + dd]);
+    Vs[e] = to_f32(v[rr * ldkv + h * dh + dd]);
+    Ds[e] = to_f32(dout[rr * ldo + h * dh + dd]);
+  }
+  __syncthreads();
+  float* P = psave + (int64_t)blockIdx.x * L * L;
+  // dV (lane = key j), before P is overwritten
+  for (int j = lane; j < L; j += 64) {
+    float acc[ATT_DH];
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
+    for (int i = 0; i < L; ++i) {
+      const float p = P[(int64_t)j * L + i];
+#pragma unroll
+      for (int dd = 0; dd < ATT_DH; ++dd)
+        if (dd < dh) acc[dd] = fmaf(p, Ds[i * dh + dd], acc[dd]);
+    }
+    const int64_t rj = row0 + j * st;
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd)
+      if (dd < dh) dv[rj * lddkv + h * dh + dd] = from_f32<T>(acc[dd]);
+  }
+  __syncthreads();   // every lane's P reads of this block are done before dS overwrites it
+  // dS and dQ (lane = query i)
+  for (int i = lane; i < L; i += 64) {
+    float di = 0.f;
+    for (int j = 0; j < L; ++j) {
+      const float p = P[(int64_t)j * L + i];
+      float dp = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < ATT_DH; ++dd)
+        if (dd < dh) dp = fmaf(Ds[i * dh + dd], Vs[j * dh + dd], dp);
+      di = fmaf(p, dp, di);
+    }
+    float acc[ATT_DH];
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
+    for (int j = 0; j < L; ++j) {
+      const float p = P[(int64_t)j * L + i];
+      float dp = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < ATT_DH; ++dd)
+        if (dd < dh) dp = fmaf(Ds[i * dh + dd], Vs[j * dh + dd], dp);
+      const float ds = p * (dp - di);
+      P[(int64_t)j * L + i] = ds;
+#pragma unroll
+      for (int dd = 0; dd < ATT_DH; ++dd)
+        if (dd < dh) acc[dd] = fmaf(ds, Ks[j * dh + dd], acc[dd]);
+    }
+    const int64_t ri = row0 + i * st;
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd)
+      if (dd < dh) dq[ri * lddq + h * dh + dd] = from_f32<T>(acc[dd] * scale);
+  }
+  __threadfence_block();
+  __syncthreads();
+  // dK (lane = key j)
+  for (int j = lane; j < L; j += 64) {
+    float acc[ATT_DH];
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
+    for (int i = 0; i < L; ++i) {
+      const float ds = P[(int64_t)j * L + i];
+#pragma unroll
+      for (int dd = 0; dd < ATT_DH; ++dd)
+        if (dd < dh) acc[dd] = fmaf(ds, Qs[i * dh + dd], acc[dd]);
+    }
+    const int64_t rj = row0 + j * st;
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd)
+      if (dd < dh) dk[rj * lddkv + h * dh + dd] = from_f32<T>(acc[dd] * scale);
+  }
+}
+
+// ---------------------------------------------------------------- Gate
+template <typename T>
+__global__ void gate_fwd_kernel(const T* __restrict__ G, const T* __restrict__ xcat, T* __restrict__ gs,
+                                T* __restrict__ z, int rows, int c) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)rows * c) return;
+  const int64_t r = e / c;
+  const int j = (int)(e - r * c);
+  const int64_t b2 = r * 2 * c;
+  const float g1 = sigmoidf_(to_f32(G[b2 + j])), g2 = sigmoidf_(to_f32(G[b2 + c + j]));
+  gs[b2 + j] = from_f32<T>(g1);
+  gs[b2 + c + j] = from_f32<T>(g2);
+  z[e] = from_f32<T>(g1 * to_f32(xcat[b2 + j]) + g2 * to_f32(xcat[b2 + c + j]));
+}
+
+template <typename T>
+__global__ void gate_bwd_kernel(const T* __restrict__ dz, const T* __restrict__ gs, const T* __restrict__ xcat,
+                                T* __restrict__ dG, T* __restrict__ dx, int rows, int c) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)rows * c) return;
+  const int64_t r = e / c;
+  const int j = (int)(e - r * c);
+  const int64_t b2 = r * 2 * c;
+  const float d = to_f32(dz[e]);
+  const float g1 = to_f32(gs[b2 + j]), g2 = to_f32(gs[b2 + c + j]);
+  const float x1 = to_f32(xcat[b2 + j]), x2 = to_f32(xcat[b2 + c + j]);
+  dG[b2 + j] = from_f32<T>(d * x1 * g1 * (1.f - g1));
+  dG[b2 + c + j] = from_f32<T>(d * x2 * g2 * (1.f - g2));
+  dx[b2 + j] = from_f32<T>(d * g1);
+  dx[b2 + c + j] = from_f32<T>(d * g2);
+}
+
+// ---------------------------------------------------------------- query construction
+template <typename T>
+__global__ void query_build_kernel(const float* __restrict__ te, const float* __restrict__ ke,
+                                   const float* __restrict__ ie, const float* __restrict__ le,
+                                   const float* __restrict__ pe, const int* __restrict__ lab, int pad, int nq, int nkp,
+                                   int c, int64_t total, T* __restrict__ tgt) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int T_ = nkp + 1, Qt = pad + nq;
+  const int ch = (int)(e % c);
+  int64_t r = e / c;
+  const int t = (int)(r % T_);
+  r /= T_;
+  const int qq = (int)(r % Qt);
+  const int b = (int)(r / Qt);
+  float v;
+  if (qq < pad) {
+    const int l = lab[(int64_t)b * pad + qq];
+    v = l < 0 ? 0.f : (t == 0 ? le[(int64_t)l * c + ch] : pe[(int64_t)(t - 1) * c + ch]);
+  } else {
+    const int q = qq - pad;
+    v = t == 0 ? ie[ch] : te[(int64_t)q * c + ch] + ke[(int64_t)(t - 1) * c + ch];
+  }
+  tgt[e] = from_f32<T>(v);
+}
+
+// task (blockIdx.y): 0 tgt_embed [nq][c], 1 keypoint_embedding [nkp][c], 2 instance [c],
+// 3 pose_enc [nkp][c], 4 label_enc (atomics: DN slots share labels)
+template <typename T>
+__global__ void query_build_bwd_kernel(const T* __restrict__ d, const int* __restrict__ lab, int B, int pad, int nq,
+                                       int nkp, int c, float* __restrict__ gte, float* __restrict__ gke,
+                                       float* __restrict__ gie, float* __restrict__ gle, float* __restrict__ gpe) {
+  const int T_ = nkp + 1, Qt = pad + nq;
+  const int task = blockIdx.y;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  auto at = [&](int b, int qq, int t, int ch) { return to_f32(d[(((int64_t)b * Qt + qq) * T_ + t) * c + ch]); };
+  if (task == 0) {
+    if (e >= nq * c) return;
+    const int q = e / c, ch = e % c;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b)
+      for (int t = 1; t < T_; ++t) s += at(b, pad + q, t, ch);
+    gte[e] += s;
+  } else if (task == 1) {
+    if (e >= nkp * c) return;
+    const int k = e / c, ch = e % c;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b)
+      for (int q = 0; q < nq; ++q) s += at(b, pad + q, k + 1, ch);
+    gke[e] += s;
+  } else if (task == 2) {
+    if (e >= c) return;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b)
+      for (int q = 0; q < nq; ++q) s += at(b, pad + q, 0, e);
+    gie[e] += s;
+  } else if (task == 3) {
+    if (e >= nkp * c || !gpe) return;
+    const int k = e / c, ch = e % c;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b)
+      for (int i = 0; i < pad; ++i)
+        if (lab[(int64_t)b * pad + i] >= 0) s += at(b, i, k + 1, ch);
+    gpe[e] += s;
+  } else {
+    if (e >= B * pad * c || !gle) return;
+    const int slot = e / c, ch = e % c;
+    const int b = slot / pad, i = slot % pad;
+    const int l = lab[slot];
+    if (l >= 0) unsafeAtomicAdd(gle + (int64_t)l * c + ch, at(b, i, 0, ch));
+  }
+}
+
+// ---------------------------------------------------------------- heads
+__global__ void pose_refine_bwd_kernel(const float* __restrict__ corners, const float* __restrict__ proj, int nb,
+                                       float inv_s, const float* __restrict__ dk, int n, float* __restrict__ dc,
+                                       int acc) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;   // (row, kp, coordinate)
+  if (e >= n) return;
+  const float* cr = corners + (int64_t)e * nb;
+  float mx = -INFINITY;
+  for (int i = 0; i < nb; ++i) mx = fmaxf(mx, cr[i]);
+  float den = 0.f, num = 0.f;
+  for (int i = 0; i < nb; ++i) {
+    const float p = __expf(cr[i] - mx);
+    den += p;
+    num += p * proj[i];
+  }
+  const float mean_w = num / den;
+  const float g = dk[e] * inv_s;
+  float* o = dc + (int64_t)e * nb;
+  for (int i = 0; i < nb; ++i) {
+    const float p = __expf(cr[i] - mx) / den;
+    const float v = g * p * (proj[i] - mean_w);
+    o[i] = acc ? o[i] + v : v;
+  }
+}
+
+__global__ void sigmoid_bwd_kernel(const float* __restrict__ y, const float* __restrict__ dy, float* __restrict__ dx,
+                                   int rows, int n, int64_t ldy, int64_t lddy, int64_t lddx) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)rows * n) return;
+  const int64_t r = e / n;
+  const int j = (int)(e - r * n);
+  const float s = y[r * ldy + j];
+  dx[r * lddx + j] = dy[r * lddy + j] * s * (1.f - s);
+}
+
+// one wave per keypoint: the forward's sample + top-4 (lqe_kernel in heads.hip: channels
+// lane*E .. lane*E + E - 1, ties to the lowest lane / element) recomputed, then
+// d stat / d(x, y) through the bilinear weights (feat detached).
+template <typename T, int E>
+__global__ __launch_bounds__(256) void lqe_bwd_kernel(const T* __restrict__ feat, int64_t fbs, int h, int w, int c,
+                                                      const float* __restrict__ kps, const float* __restrict__ dst,
+                                                      int nq, int nkp, int total, float* __restrict__ dkps) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= total) return;
+  const int b = (unsigned)g / (unsigned)(nq * nkp);
+  const float x = kps[2 * (int64_t)g] * w - 0.5f, y = kps[2 * (int64_t)g + 1] * h - 0.5f;
+  const float fx = floorf(x), fy = floorf(y);
+  const int x0 = (int)fx, y0 = (int)fy;
+  const float ax = x - fx, ay = y - fy;
+  const float wt[4] = {(1.f - ax) * (1.f - ay), ax * (1.f - ay), (1.f - ax) * ay, ax * ay};
+  // d wt / d ax, d wt / d ay
+  const float wx[4] = {-(1.f - ay), (1.f - ay), -ay, ay};
+  const float wy[4] = {-(1.f - ax), -ax, (1.f - ax), ax};
+  float v[E], gx[E], gy[E];
+#pragma unroll
+  for (int t = 0; t < E; ++t) v[t] = gx[t] = gy[t] = 0.f;
+  const T* fb = feat + (int64_t)b * fbs + lane * E;
+#pragma unroll
+  for (int cn = 0; cn < 4; ++cn) {
+    const int xi = x0 + (cn & 1), yi = y0 + (cn >> 1);
+    if (xi < 0 || xi >= w || yi < 0 || yi >= h) continue;
+    const T* p = fb + ((int64_t)yi * w + xi) * c;
+#pragma unroll
+    for (int t = 0; t < E; ++t) {
+      const float f = to_f32(p[t]);
+      v[t] = fmaf(wt[cn], f, v[t]);
+      gx[t] = fmaf(wx[cn], f, gx[t]);
+      gy[t] = fmaf(wy[cn], f, gy[t]);
+    }
+  }
+  const float* ds = dst + (int64_t)g * 5;
+  const float dmean = ds[4] * 0.25f;
+  float ax_acc = 0.f, ay_acc = 0.f;
+  unsigned used = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    float lm = -INFINITY;
+    int li = -1;
+#pragma unroll
+    for (int t = 0; t < E; ++t)
+      if (!(used & (1u << t)) && v[t] > lm) {
+        lm = v[t];
+        li = t;
+      }
+    const float wm = wave_max(lm);
+    const unsigned long long ball = __ballot(lm == wm && li >= 0);
+    const int winner = __ffsll((long long)ball) - 1;
+    if (lane == winner) {
+      used |= 1u << li;
+      const float coef = ds[s] + dmean;
+#pragma unroll
+      for (int t = 0; t < E; ++t)
+        if (t == li) {
+          ax_acc += coef * gx[t];
+          ay_acc += coef * gy[t];
+        }
+    }
+  }
+  ax_acc = wave_sum(ax_acc);
+  ay_acc = wave_sum(ay_acc);
+  if (lane == 0) {
+    dkps[2 * (int64_t)g] += ax_acc * w;
+    dkps[2 * (int64_t)g + 1] += ay_acc * h;
+  }
+}
+
+// ---------------------------------------------------------------- row moves
+template <typename T>
+__global__ void scatter_rows_kernel(const T* __restrict__ src, int lds, const int64_t* __restrict__ idx, int k, int c,
+                                    T* __restrict__ dst, int64_t dbs, int ldd, int acc, int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int ch = (int)(e % c);
+  const int64_t rj = e / c;   // b * k + j
+  const int b = (int)(rj / k);
+  const int64_t dr = idx[rj];
+  T* p = dst + (int64_t)b * dbs + dr * ldd + ch;
+  float v = to_f32(src[rj * lds + ch]);
+  if (acc) v += to_f32(*p);
+  *p = from_f32<T>(v);
+}
+
+template <typename T>
+__global__ void gather_masked_kernel(const T* __restrict__ src, int64_t sbs, const int64_t* __restrict__ idx,
+                                     const uint8_t* __restrict__ mask, int period, int k, int c, T* __restrict__ dst,
+                                     int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int ch = (int)(e % c);
+  const int64_t rj = e / c;
+  const int b = (int)(rj / k);
+  const int64_t sr = idx[rj];
+  const bool m = mask && mask[sr % period];
+  dst[e] = m ? from_f32<T>(0.f) : src[(int64_t)b * sbs + sr * c + ch];
+}
+
+template <typename TS, typename TD>
+__global__ void convert_kernel(const TS* __restrict__ src, int64_t lds, TD* __restrict__ dst, int64_t ldd, int rows,
+                               int n, float scale, int acc) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)rows * n) return;
+  const int64_t r = e / n;
+  const int j = (int)(e - r * n);
+  float v = to_f32(src[r * lds + j]) * scale;
+  TD* p = dst + r * ldd + j;
+  if (acc) v += to_f32(*p);
+  *p = from_f32<TD>(v);
+}
+
+inline unsigned nblk(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+// dynamic LDS above 64 KB needs the per-kernel attribute (once per instantiation)
+template <typename K>
+void allow_lds(K kern) {
+  static bool done = [&] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    return true;
+  }();
+  (void)done;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" int dp_ln_fwd(void* y, int32_t ld_y, const void* x, const void* res, void* s, float* stats,
+                         const float* gamma, const float* beta, float eps, int32_t rows, int32_t c, const void* post,
+                         int32_t post_group, int32_t post_skip, int32_t dtype, void* stream) {
+  DP_REQUIRE(y && x && stats && gamma && beta, "dp_ln_fwd: null pointer");
+  DP_REQUIRE(c > 0 && c <= 64 * LN_E && rows > 0 && ld_y >= c, "dp_ln_fwd: c=%d rows=%d ld_y=%d", c, rows, ld_y);
+  DP_REQUIRE(!post || (post_group > post_skip && post_skip >= 0), "dp_ln_fwd: bad post map");
+  hipStream_t st = as_stream(stream);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(nblk(rows, 4)), dim3(256), 0, st, (bf16_t*)y, ld_y,
+                       (const bf16_t*)x, (const bf16_t*)res, (bf16_t*)s, stats, gamma, beta, eps, rows, c,
+                       (const bf16_t*)post, post_group, post_skip);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(nblk(rows, 4)), dim3(256), 0, st, (float*)y, ld_y, (const float*)x,
+                       (const float*)res, (float*)s, stats, gamma, beta, eps, rows, c, (const float*)post, post_group,
+                       post_skip);
+  return dp_check_launch("dp_ln_fwd");
+}
+
+extern "C" int dp_ln_bwd(void* dx, const void* dy, int32_t ld_dy, const void* s, const float* stats,
+                         const float* gamma, int32_t rows, int32_t c, float* dgamma, float* dbeta, int32_t accumulate,
+                         int32_t dtype, void* stream) {
+  DP_REQUIRE(dx && dy && s && stats && gamma, "dp_ln_bwd: null pointer");
+  DP_REQUIRE(c > 0 && c <= 64 * LN_E && rows > 0 && ld_dy >= c, "dp_ln_bwd: c=%d rows=%d", c, rows);
+  DP_REQUIRE((dgamma == nullptr) == (dbeta == nullptr), "dp_ln_bwd: dgamma / dbeta both or neither");
+  int grid = (rows + 3) / 4;
+  if (grid > 2048) grid = 2048;
+  hipStream_t st = as_stream(stream);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, (bf16_t*)dx, (const bf16_t*)dy, ld_dy,
+                       (const bf16_t*)s, stats, gamma, rows, c, dgamma, dbeta, accumulate);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, (float*)dx, (const float*)dy, ld_dy,
+                       (const float*)s, stats, gamma, rows, c, dgamma, dbeta, accumulate);
+  return dp_check_launch("dp_ln_bwd");
+}
+
+extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, float* out, int32_t accumulate,
+                         int32_t dtype, void* stream) {
+  DP_REQUIRE(x && out && rows > 0 && n > 0 && ld >= n, "dp_colsum: bad arguments");
+  hipStream_t st = as_stream(stream);
+  if (!accumulate && hipMemsetAsync(out, 0, (size_t)n * 4, st) != hipSuccess) return dp_check_launch("dp_colsum");
+  const int chunks = rows < 256 ? 1 : (rows + 255) / 256 > 512 ? 512 : (rows + 255) / 256;
+  const int per = (rows + chunks - 1) / chunks;
+  dim3 grid(nblk(n, 256), (unsigned)chunks);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, ld, rows, n, out, per);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)x, ld, rows, n, out, per);
+  return dp_check_launch("dp_colsum");
+}
+
+extern "C" int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out,
+                           int32_t ld_o, float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner,
+                           int64_t so, int64_t si, int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype,
+                           void* stream) {
+  DP_REQUIRE(q && k && v && out && p_save, "dp_attn_fwd: null pointer");
+  DP_REQUIRE(seqlen > 0 && seqlen <= 256 && dh > 0 && dh <= ATT_DH && seqlen * dh <= 8192,
+             "dp_attn_fwd: seqlen %d x dh %d (<= 256, <= 64, product <= 8192)", seqlen, dh);
+  DP_REQUIRE((int64_t)n_outer * n_inner * nhead < (1ll << 31), "dp_attn_fwd: too many sequences");
+  const size_t lds = (size_t)2 * seqlen * dh * 4;
+  const float scale = 1.f / sqrtf((float)dh);
+  dim3 grid((unsigned)(n_outer * n_inner * nhead));
+  hipStream_t s = as_stream(stream);
+  if (lds > 64 * 1024) dtype == DP_BF16 ? allow_lds(attn_fwd_kernel<bf16_t>) : allow_lds(attn_fwd_kernel<float>);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, dim3(64), lds, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
+                       (const bf16_t*)v, ld_kv, (bf16_t*)out, ld_o, p_save, mask, n_inner, so, si, st, seqlen, nhead,
+                       dh, scale);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(64), lds, s, (const float*)q, ld_q, (const float*)k,
+                       (const float*)v, ld_kv, (float*)out, ld_o, p_save, mask, n_inner, so, si, st, seqlen, nhead, dh,
+                       scale);
+  return dp_check_launch("dp_attn_fwd");
+}
+
+extern "C" int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv,
+                           const float* p_save, const void* dout, int32_t ld_o, void* dq, int32_t ld_dq, void* dk,
+                           void* dv, int32_t ld_dkv, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
+                           int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype, void* stream) {
+  DP_REQUIRE(q && k && v && p_save && dout && dq && dk && dv, "dp_attn_bwd: null pointer");
+  DP_REQUIRE(seqlen > 0 && seqlen <= 256 && dh > 0 && dh <= ATT_DH && seqlen * dh <= 8192,
+             "dp_attn_bwd: seqlen %d x dh %d (<= 256, <= 64, product <= 8192)", seqlen, dh);
+  const size_t lds = (size_t)4 * seqlen * dh * 4;
+  const float scale = 1.f / sqrtf((float)dh);
+  dim3 grid((unsigned)(n_outer * n_inner * nhead));
+  hipStream_t s = as_stream(stream);
+  float* P = const_cast<float*>(p_save);   // overwritten with dS (the forward's P is consumed)
+  if (lds > 64 * 1024) dtype == DP_BF16 ? allow_lds(attn_bwd_kernel<bf16_t>) : allow_lds(attn_bwd_kernel<float>);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(attn_bwd_kernel<bf16_t>, grid, dim3(64), lds, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
+                       (const bf16_t*)v, ld_kv, P, (const bf16_t*)dout, ld_o, (bf16_t*)dq, ld_dq, (bf16_t*)dk,
+                       (bf16_t*)dv, ld_dkv, n_inner, so, si, st, seqlen, nhead, dh, scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(64), lds, s, (const float*)q, ld_q, (const float*)k,
+                       (const float*)v, ld_kv, P, (const float*)dout, ld_o, (float*)dq, ld_dq, (float*)dk, (float*)dv,
+                       ld_dkv, n_inner, so, si, st, seqlen, nhead, dh, scale);
+  return dp_check_launch("dp_attn_bwd");
+}
+
+extern "C" int dp_gate_fwd(const void* G, const void* xcat, void* g, void* z, int32_t rows, int32_t c, int32_t dtype,
+                           void* stream) {
+  DP_REQUIRE(G && xcat && g && z && rows > 0 && c > 0, "dp_gate_fwd: bad arguments");
+  const int64_t n = (int64_t)rows * c;
+  hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(gate_fwd_kernel<bf16_t>, dim3(nblk(n, 256)), dim3(256), 0, s, (const bf16_t*)G,
+                       (const bf16_t*)xcat, (bf16_t*)g, (bf16_t*)z, rows, c);
+  else
+    hipLaunchKernelGGL(gate_fwd_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, s, (const float*)G, (const float*)xcat,
+                       (float*)g, (float*)z, rows, c);
+  return dp_check_launch("dp_gate_fwd");
+}
+
+extern "C" int dp_gate_bwd(const void* dz, const void* g, const void* xcat, void* dG, void* dxcat, int32_t rows,
+                           int32_t c, int32_t dtype, void* stream) {
+  DP_REQUIRE(dz && g && xcat && dG && dxcat && rows > 0 && c > 0, "dp_gate_bwd: bad arguments");
+  const int64_t n = (int64_t)rows * c;
+  hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, dim3(nblk(n, 256)), dim3(256), 0, s, (const bf16_t*)dz,
+                       (const bf16_t*)g, (const bf16_t*)xcat, (bf16_t*)dG, (bf16_t*)dxcat, rows, c);
+  else
+    hipLaunchKernelGGL(gate_bwd_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, s, (const float*)dz, (const float*)g,
+                       (const float*)xcat, (float*)dG, (float*)dxcat, rows, c);
+  return dp_check_launch("dp_gate_bwd");
+}
+
+extern "C" int dp_query_build(const float* tgt_embed, const float* kp_embed, const float* inst_embed,
+                              const float* label_enc, const float* pose_enc, const int32_t* dn_label, int32_t batch,
+                              int32_t pad, int32_t nq, int32_t nkp, int32_t c, void* tgt, int32_t dtype, void* stream) {
+  DP_REQUIRE(tgt_embed && kp_embed && inst_embed && tgt && batch > 0 && nq > 0 && nkp > 0 && c > 0,
+             "dp_query_build: bad arguments");
+  DP_REQUIRE(pad == 0 || (label_enc && pose_enc && dn_label), "dp_query_build: DN slots need label_enc / pose_enc");
+  const int64_t total = (int64_t)batch * (pad + nq) * (nkp + 1) * c;
+  hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(query_build_kernel<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, s, tgt_embed, kp_embed,
+                       inst_embed, label_enc, pose_enc, dn_label, pad, nq, nkp, c, total, (bf16_t*)tgt);
+  else
+    hipLaunchKernelGGL(query_build_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, tgt_embed, kp_embed,
+                       inst_embed, label_enc, pose_enc, dn_label, pad, nq, nkp, c, total, (float*)tgt);
+  return dp_check_launch("dp_query_build");
+}
+
+extern "C" int dp_query_build_bwd(const void* dtgt, const int32_t* dn_label, int32_t batch, int32_t pad, int32_t nq,
+                                  int32_t nkp, int32_t c, float* g_tgt_embed, float* g_kp_embed, float* g_inst_embed,
+                                  float* g_label_enc, int32_t n_label, float* g_pose_enc, int32_t dtype, void* stream) {
+  DP_REQUIRE(dtgt && g_tgt_embed && g_kp_embed && g_inst_embed, "dp_query_build_bwd: null pointer");
+  DP_REQUIRE(pad == 0 || dn_label, "dp_query_build_bwd: DN slots need dn_label");
+  (void)n_label;
+  int most = nq * c;
+  if (nkp * c > most) most = nkp * c;
+  if (batch * pad * c > most) most = batch * pad * c;
+  dim3 grid(nblk(most, 256), pad > 0 ? 5 : 3);
+  hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(query_build_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dtgt, dn_label, batch, pad,
+                       nq, nkp, c, g_tgt_embed, g_kp_embed, g_inst_embed, g_label_enc, g_pose_enc);
+  else
+    hipLaunchKernelGGL(query_build_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)dtgt, dn_label, batch, pad,
+                       nq, nkp, c, g_tgt_embed, g_kp_embed, g_inst_embed, g_label_enc, g_pose_enc);
+  return dp_check_launch("dp_query_build_bwd");
+}
+
+extern "C" int dp_pose_refine_bwd(const float* corners, const float* project, int32_t reg_max, float reg_scale,
+                                  const float* dkps, int32_t rows, int32_t nkp, float* dcorners, int32_t accumulate,
+                                  void* stream) {
+  DP_REQUIRE(corners && project && dkps && dcorners && rows > 0 && nkp > 0, "dp_pose_refine_bwd: bad arguments");
+  const int n = rows * nkp * 2;
+  hipLaunchKernelGGL(pose_refine_bwd_kernel, dim3(nblk(n, 256)), dim3(256), 0, as_stream(stream), corners, project,
+                     reg_max + 1, 1.f / fabsf(reg_scale), dkps, n, dcorners, accumulate);
+  return dp_check_launch("dp_pose_refine_bwd");
+}
+
+extern "C" int dp_sigmoid_bwd(const float* out, const float* dout, float* din, int32_t rows, int32_t n, int64_t ld_out,
+                              int64_t ld_dout, int64_t ld_din, void* stream) {
+  DP_REQUIRE(out && dout && din && rows > 0 && n > 0, "dp_sigmoid_bwd: bad arguments");
+  const int64_t tot = (int64_t)rows * n;
+  hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(nblk(tot, 256)), dim3(256), 0, as_stream(stream), out, dout, din, rows,
+                     n, ld_out, ld_dout, ld_din);
+  return dp_check_launch("dp_sigmoid_bwd");
+}
+
+extern "C" int dp_lqe_stats_bwd(const void* feat, int64_t feat_bstride, int32_t h, int32_t w, int32_t c,
+                                const float* kps, const float* dstats, int32_t batch, int32_t nq, int32_t nkp,
+                                float* dkps, int32_t dtype, void* stream) {
+  DP_REQUIRE(feat && kps && dstats && dkps, "dp_lqe_stats_bwd: null pointer");
+  DP_REQUIRE(c % 64 == 0 && c / 64 >= 1 && c / 64 <= 8, "dp_lqe_stats_bwd: c=%d (64..512, multiple of 64)", c);
+  const int total = batch * nq * nkp;
+  hipStream_t s = as_stream(stream);
+#define DP_LQEB(T_, E_)                                                                                         \
+  case E_:                                                                                                      \
+    hipLaunchKernelGGL((lqe_bwd_kernel<T_, E_>), dim3(nblk(total, 4)), dim3(256), 0, s, (const T_*)feat,        \
+                       feat_bstride, h, w, c, kps, dstats, nq, nkp, total, dkps);                               \
+    break;
+  if (dtype == DP_BF16) {
+    switch (c / 64) { DP_LQEB(bf16_t, 1) DP_LQEB(bf16_t, 2) DP_LQEB(bf16_t, 3) DP_LQEB(bf16_t, 4) DP_LQEB(bf16_t, 5)
+                      DP_LQEB(bf16_t, 6) DP_LQEB(bf16_t, 7) DP_LQEB(bf16_t, 8) }
+  } else {
+    switch (c / 64) { DP_LQEB(float, 1) DP_LQEB(float, 2) DP_LQEB(float, 3) DP_LQEB(float, 4) DP_LQEB(float, 5)
+                      DP_LQEB(float, 6) DP_LQEB(float, 7) DP_LQEB(float, 8) }
+  }
+#undef DP_LQEB
+  return dp_check_launch("dp_lqe_stats_bwd");
+}
+
+extern "C" int dp_scatter_rows(const void* src, int32_t ld_src, const int64_t* idx, int32_t batch, int32_t k,
+                               int32_t c, void* dst, int64_t dst_bstride, int32_t ld_dst, int32_t accumulate,
+                               int32_t dtype, void* stream) {
+  DP_REQUIRE(src && idx && dst && batch > 0 && k > 0 && c > 0, "dp_scatter_rows: bad arguments");
+  const int64_t total = (int64_t)batch * k * c;
+  hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(scatter_rows_kernel<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, s, (const bf16_t*)src, ld_src,
+                       idx, k, c, (bf16_t*)dst, dst_bstride, ld_dst, accumulate, total);
+  else
+    hipLaunchKernelGGL(scatter_rows_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, (const float*)src, ld_src,
+                       idx, k, c, (float*)dst, dst_bstride, ld_dst, accumulate, total);
+  return dp_check_launch("dp_scatter_rows");
+}
+
+extern "C" int dp_gather_rows_masked(const void* src, int64_t src_bstride, const int64_t* idx, const uint8_t* row_mask,
+                                     int32_t mask_period, int32_t batch, int32_t k, int32_t c, void* dst, int32_t dtype,
+                                     void* stream) {
+  DP_REQUIRE(src && idx && dst && batch > 0 && k > 0 && c > 0 && (!row_mask || mask_period > 0),
+             "dp_gather_rows_masked: bad arguments");
+  const int64_t total = (int64_t)batch * k * c;
+  hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16)
+    hipLaunchKernelGGL(gather_masked_kernel<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, s, (const bf16_t*)src,
+                       src_bstride, idx, row_mask, mask_period, k, c, (bf16_t*)dst, total);
+  else
+    hipLaunchKernelGGL(gather_masked_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, (const float*)src,
+                       src_bstride, idx, row_mask, mask_period, k, c, (float*)dst, total);
+  return dp_check_launch("dp_gather_rows_masked");
+}
+
+extern "C" int dp_convert_rows(const void* src, int32_t src_dtype, int64_t ld_src, void* dst, int32_t dst_dtype,
+                               int64_t ld_dst, int32_t rows, int32_t n, float scale, int32_t accumulate, void* stream) {
+  DP_REQUIRE(src && dst && rows > 0 && n > 0, "dp_convert_rows: bad arguments");
+  const int64_t tot = (int64_t)rows * n;
+  hipStream_t s = as_stream(stream);
+  dim3 grid(nblk(tot, 256)), block(256);
+  if (src_dtype == DP_BF16 && dst_dtype == DP_BF16)
+    hipLaunchKernelGGL((convert_kernel<bf16_t, bf16_t>), grid, block, 0, s, (const bf16_t*)src, ld_src, (bf16_t*)dst,
+                       ld_dst, rows, n, scale, accumulate);
+  else if (src_dtype == DP_BF16)
+    hipLaunchKernelGGL((convert_kernel<bf16_t, float>), grid, block, 0, s, (const bf16_t*)src, ld_src, (float*)dst,
+                       ld_dst, rows, n, scale, accumulate);
+  else if (dst_dtype == DP_BF16)
+    hipLaunchKernelGGL((convert_kernel<float, bf16_t>), grid, block, 0, s, (const float*)src, ld_src, (bf16_t*)dst,
+                       ld_dst, rows, n, scale, accumulate);
+  else
+    hipLaunchKernelGGL((convert_kernel<float, float>), grid, block, 0, s, (const float*)src, ld_src, (float*)dst,
+                       ld_dst, rows, n, scale, accumulate);
+  return dp_check_launch("dp_convert_rows");
+}
+
+extern "C" int dp_zero(void* p, int64_t bytes, void* stream) {
+  DP_REQUIRE(p && bytes >= 0, "dp_zero: bad arguments");
+  if (hipMemsetAsync(p, 0, (size_t)bytes, as_stream(stream)) != hipSuccess) return dp_check_launch("dp_zero");
+  return 0;
+}

@@ -1,0 +1,846 @@
+"""The transformer's training step on the HIP kernels: training-mode forward with OKS-denoising
+queries, the criterion (matching + losses + their gradients), and the backward through every
+transformer parameter — a fixed tape of C-ABI launches, like the inference Plan.
+
+Reference: Transformer.forward in training mode
+(src/models/detrpose/transformer.py:1219-1385), TransformerDecoder.forward training branch
+(558-603, 701-728, 903-916), DeformableTransformerDecoderLayer.forward (387-442), prepare_for_cdn
+(dn_component.py:39-183), Criterion.forward incl. the dn_* losses (criterion.py:285-435), then
+loss.backward() (src/solver/engine.py:55-60). The reference runs this through torch autograd;
+here every forward op that the backward needs saves its inputs / statistics into buffers of the
+step's arena, and the backward is written out op by op in reverse:
+
+  nn.Linear            dp_gemm forward / dgrad (dy W) / wgrad (dy^T x, split-K f32 atomics)
+                       + dp_colsum bias grads; ReLU backward is the dgrad GEMM's gate
+  nn.LayerNorm         dp_ln_fwd (saves the pre-norm sum and mean / rstd) / dp_ln_bwd
+  MultiheadAttention   in_proj / out_proj GEMMs + dp_attn_fwd (saves P) / dp_attn_bwd, with the
+                       DN attn_mask in the across attention
+  MSDeformAttn         dp_msda (f32 offsets) / dp_msda_bwd (offsets / logits gradients)
+  Gate                 dp_gate_fwd / dp_gate_bwd + its Linear
+  heads                pose / pre / class / LQE MLPs as GEMMs, dp_pose_refine(_bwd),
+                       dp_pre_pose + dp_sigmoid_bwd, dp_lqe_stats(_bwd)
+  query construction   dp_query_build(_bwd) (tgt_embed, keypoint / instance embeddings, DN
+                       label_enc / pose_enc rows)
+  two-stage            enc_output + LN + class + top-k forward over all rows; the backward
+                       recomputes enc_output + LN on the selected rows only (the only rows
+                       with a gradient)
+
+Scope: the transformer (the encoder memory is an input and is not differentiated: the encoder /
+backbone backward is the next step of BASELINE config 5). BatchNorm is not on this path.
+Parameter gradients accumulate into one f32 buffer (`TrainEngine.grads`, reference names).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import DP_BF16, DP_F32, GemmDesc, contiguous_rows, rowmap
+from .criterion import COCO_SIGMAS, CROWDPOSE_SIGMAS, pack_targets
+from .transformer import weighting_function
+
+DT = {"bf16": (torch.bfloat16, DP_BF16), "fp32": (torch.float32, DP_F32)}
+T_ = "transformer."
+
+
+def dn_match(sizes, pad_size, num_group):
+    """criterion.py:385-399: DN slot g*single_pad + t <-> target t of its image (positives)."""
+    single = pad_size // num_group
+    m = np.full((len(sizes), pad_size), -1, np.int32)
+    for b, n in enumerate(sizes):
+        for g in range(num_group):
+            m[b, g * single: g * single + n] = np.arange(n)
+    return m
+
+
+class Tape:
+    """Recorded launches with their descriptors kept alive."""
+
+    def __init__(self, lib, device):
+        self.lib = lib
+        self.device = device
+        self.ops = []
+        self.keep = []
+
+    def op(self, name, fn, *args):
+        self.ops.append((name, fn, args))
+
+    def run(self, stream=None, debug=None):
+        s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream)
+        for name, fn, args in self.ops:
+            rc = fn(*args, s)
+            if rc:
+                _lib.check(rc, name)
+            if debug is not None:
+                torch.cuda.synchronize()
+                debug(name)
+
+
+def _p(t, off=0):
+    return t.data_ptr() + off * t.element_size()
+
+
+class TrainEngine:
+    """Transformer training step for a DETRPose module (reference parameter names).
+
+    dtype 'fp32' (parity mode) or 'bf16' (bf16 activations and activation gradients, f32
+    accumulation, f32 LayerNorm statistics, f32 heads and parameter gradients)."""
+
+    def __init__(self, model, dtype="fp32", device="cuda"):
+        self.lib = _lib.load()
+        self.model = model
+        self.tr = tr = model.transformer
+        self.dtype_name = dtype
+        self.tdtype, self.code = DT[dtype]
+        self.device = torch.device(device)
+        self.C = tr.hidden_dim
+        self.nh = tr.nhead
+        self.nq = tr.num_queries
+        self.K = tr.num_body_points
+        self.T = self.K + 1
+        self.L = tr.num_decoder_layers
+        self.nlev = tr.num_feature_levels
+        self.npnt = tr.dec_n_points
+        self.F = tr.dim_feedforward
+        self.reg_max = tr.reg_max
+        self.nb = 2 * (tr.reg_max + 1)
+        self.ncls = tr.num_classes
+        # parameter gradients: one f32 arena, views under the reference names
+        self.pnames = [n for n, p in model.named_parameters() if n.startswith(T_) and p.requires_grad]
+        shapes = {n: tuple(p.shape) for n, p in model.named_parameters()}
+        total = sum(int(np.prod(shapes[n])) for n in self.pnames)
+        self.grad_flat = torch.zeros(total, dtype=torch.float32, device=self.device)
+        self.grads = {}
+        o = 0
+        for n in self.pnames:
+            k = int(np.prod(shapes[n]))
+            self.grads[n] = self.grad_flat[o:o + k].view(shapes[n])
+            o += k
+        self.load_weights()
+        self.plans = {}
+
+    # ------------------------------------------------------------------ weights
+    def load_weights(self):
+        """(Re)pack the module's current parameters: dtype copies for the GEMMs, f32 for
+        biases / norms / embeddings / the LQE MLP (f32 inputs)."""
+        sd = {k: v.detach() for k, v in self.model.state_dict().items()}
+        dev, dt = self.device, self.tdtype
+        self.sd32 = {k: v.to(dev, torch.float32).contiguous() for k, v in sd.items() if k.startswith(T_)}
+        self.w = {}
+        for k, v in self.sd32.items():
+            if k.endswith("weight") and v.dim() == 2:
+                self.w[k] = v.to(dt).contiguous()
+        C = self.C
+        for l in range(self.L):
+            ca = f"{T_}decoder.layers.{l}.cross_attn."
+            self.w[ca + "offattn.weight"] = torch.cat([self.sd32[ca + "sampling_offsets.weight"],
+                                                       self.sd32[ca + "attention_weights.weight"]], 0).to(dt).contiguous()
+            self.sd32[ca + "offattn.bias"] = torch.cat([self.sd32[ca + "sampling_offsets.bias"],
+                                                        self.sd32[ca + "attention_weights.bias"]], 0).contiguous()
+        g, b = self.sd32[T_ + "enc_output_norm.weight"].double(), self.sd32[T_ + "enc_output_norm.bias"].double()
+        bias = self.sd32[T_ + "enc_output.bias"].double()
+        mr = (bias - bias.mean()) / torch.sqrt(bias.var(unbiased=False) + 1e-5) * g + b
+        self.masked_row = mr.float().contiguous()
+        self.mask_u8 = self.sd32[T_ + "valid_mask"].reshape(-1).to(torch.uint8).contiguous() \
+            if T_ + "valid_mask" in self.sd32 else sd[T_ + "valid_mask"].reshape(-1).to(dev, torch.uint8).contiguous()
+        self.anchors = sd[T_ + "anchors"].reshape(-1, 2).to(dev, torch.float32).contiguous()
+        tr = self.tr
+        self.project = weighting_function(tr.reg_max, float(sd[T_ + "up"]), float(sd[T_ + "reg_scale"])).to(
+            dev, torch.float32).contiguous()
+        self.reg_scale = abs(float(sd[T_ + "reg_scale"]))
+        self.dim_t = sd[T_ + "decoder.dim_t"].to(dev, torch.float32).contiguous()
+        assert self.masked_row.shape[0] == C
+
+    # ------------------------------------------------------------------ launch helpers
+    def _gemm(self, tape, name, a, a_rs, a_ks, b, b_ks, b_ns, c, c_rs, m, n, k, in_code, out_code, bias=None,
+              alpha=1.0, beta=0.0, act=0, gate=None, gate_rs=0, gate_code=None, batch=1, a_bs=0, b_bs=0, c_bs=0,
+              gate_bs=0):
+        d = GemmDesc()
+        d.a, d.a_bs, d.a_rs, d.a_ks = a, a_bs, a_rs, a_ks
+        d.b, d.b_bs, d.b_ks, d.b_ns = b, b_bs, b_ks, b_ns
+        d.c, d.c_bs, d.c_rs = c, c_bs, c_rs
+        d.batch, d.m, d.n, d.k = batch, m, n, k
+        d.in_dtype, d.out_dtype = in_code, out_code
+        d.bias = bias
+        d.alpha, d.beta, d.act = alpha, beta, act
+        d.gate, d.gate_bs, d.gate_rs = gate, gate_bs, gate_rs
+        d.gate_dtype = self.code if gate_code is None else gate_code
+        d.split_k = 0
+        tape.keep.append(d)
+        tape.op(name, self.lib.dp_gemm, C.byref(d))
+        self.cur.cost(name, 2.0 * batch * m * n * k)
+
+    def lin(self, tape, name, x, ldx, rows, wkey, out, ldo, act=0, out_code=None, bias=True, beta=0.0, wt=None,
+            in_code=None):
+        """out = act(x W^T + b): nn.Linear forward."""
+        W = self.w[wkey] if wt is None else wt
+        N, K = W.shape
+        bk = wkey[:-len("weight")] + "bias"
+        b = self.sd32.get(bk) if bias else None
+        self._gemm(tape, name, x, ldx, 1, _p(W), 1, K, out, ldo, rows, N, K, self.code if in_code is None else in_code,
+                   self.code if out_code is None else out_code, bias=_p(b) if b is not None else None, beta=beta,
+                   act=act)
+
+    def dgrad(self, tape, name, dy, ldy, rows, wkey, dx, ldx, beta=0.0, gate=None, ld_gate=0, wt=None, in_code=None,
+              gate_code=None):
+        """dx (+)= (dy W) [* relu'(gate)]: nn.Linear input gradient."""
+        W = self.w[wkey] if wt is None else wt
+        N, K = W.shape
+        code = self.code if in_code is None else in_code
+        self._gemm(tape, name, dy, ldy, 1, _p(W), K, 1, dx, ldx, rows, K, N, code, code, beta=beta, gate=gate,
+                   gate_rs=ld_gate, gate_code=gate_code)
+
+    def wgrad(self, tape, name, dy, ldy, rows, wkey, x, ldx, gkey=None, in_code=None, dy32=None, ld32=None):
+        """dW += dy^T x and db += colsum(dy): nn.Linear parameter gradients."""
+        gkey = gkey or wkey
+        G = self.grads[gkey]
+        N, K = G.shape
+        code = self.code if in_code is None else in_code
+        self._gemm(tape, name + ".dW", dy, 1, ldy, x, ldx, 1, _p(G), K, N, K, rows, code, DP_F32, beta=1.0)
+        bk = gkey[:-len("weight")] + "bias"
+        if bk in self.grads:
+            src, ld, sc = (dy, ldy, code) if dy32 is None else (dy32, ld32, DP_F32)
+            tape.op(name + ".db", self.lib.dp_colsum, src, ld, rows, N, _p(self.grads[bk]), 1, sc)
+            self.cur.cost(name + ".db", 4.0 * rows * N)
+
+    # ------------------------------------------------------------------ plan
+    def plan(self, batch: int, pad: int, shapes) -> "TrainPlan":
+        key = (batch, pad, tuple(tuple(s) for s in shapes))
+        if key not in self.plans:
+            self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes])
+        return self.plans[key]
+
+
+class TrainPlan:
+    """Buffers and tapes for one (batch, DN pad size, feature shapes)."""
+
+    def __init__(self, eng: TrainEngine, B: int, P: int, shapes):
+        self.eng = eng
+        eng.cur = self
+        self.B, self.P, self.shapes = B, P, shapes
+        self.op_flops = {}
+        self.arena = []
+        lib = eng.lib
+        Cc, nh, nq, K, T, L, F = eng.C, eng.nh, eng.nq, eng.K, eng.T, eng.L, eng.F
+        dt, code = eng.tdtype, eng.code
+        e = dt.itemsize
+        Qt = P + nq
+        self.Qt = Qt
+        S = sum(h * w for h, w in shapes)
+        self.S = S
+        rows, krows, qrows = B * Qt * T, B * Qt * K, B * Qt
+        self.rows, self.krows, self.qrows = rows, krows, qrows
+        nb, ncol = eng.nb, nh * eng.nlev * eng.npnt * 3
+        sd = eng.sd32
+        dev = eng.device
+
+        def buf(*shape, dtype=None):
+            t = torch.empty(*shape, dtype=dtype or dt, device=dev)
+            self.arena.append(t)
+            return t
+
+        def f32(*shape):
+            return buf(*shape, dtype=torch.float32)
+
+        # ---------------- inputs
+        self.memory = buf(B, S, Cc)
+        self.dn_label = torch.full((B, max(P, 1)), -1, dtype=torch.int32, device=dev)
+        self.dn_ref = f32(B, max(P, 1), T, 2)
+        self.mask = torch.zeros(Qt, Qt, dtype=torch.uint8, device=dev)
+        self.lvl_hw = (C.c_int32 * (2 * len(shapes)))(*[v for hw in shapes for v in hw])
+        fw = Tape(lib, dev)
+        bw = Tape(lib, dev)
+        self.fw, self.bw = fw, bw
+        cr = contiguous_rows
+        kp_map = rowmap(Cc, K, T * Cc, Cc)   # keypoint token rows of a [rows][Cc] tensor
+
+        # ================= forward: two-stage selection (transformer.py:1219-1250)
+        mrows = B * S
+        eo = buf(mrows, Cc)
+        eng.lin(fw, "ts.enc_output", _p(self.memory), Cc, mrows, T_ + "enc_output.weight", _p(eo), Cc)
+        om = buf(mrows, Cc)
+        g_, b_ = sd[T_ + "enc_output_norm.weight"], sd[T_ + "enc_output_norm.bias"]
+        fw.op("ts.enc_norm", lib.dp_layernorm, _p(om), cr(Cc), _p(eo), cr(Cc), None, cr(Cc), _p(g_), _p(b_),
+              C.c_float(1e-5), mrows, Cc, None, rowmap(group=1), 1, 0, _p(eng.mask_u8), S, _p(eng.masked_row), code)
+        score = f32(mrows)
+        wc, bc = sd[T_ + "enc_out_class_embed.weight"], sd[T_ + "enc_out_class_embed.bias"]
+        fw.op("ts.class_max", lib.dp_class_max, _p(om), mrows, Cc, _p(wc), _p(bc), wc.shape[0], _p(score), code)
+        self.topv = f32(B, nq)
+        self.topi = torch.empty(B, nq, dtype=torch.int64, device=dev)
+        self.arena.append(self.topi)
+        fw.op("ts.topk", lib.dp_topk, _p(score), B, S, S, nq, _p(self.topv), _p(self.topi))
+        tm = buf(B * nq, Cc)
+        fw.op("ts.gather", lib.dp_gather_rows, _p(om), S * Cc, _p(self.topi), B, nq, Cc, _p(tm), code)
+        self.interm_logits = f32(B, nq, eng.ncls)
+        eng.lin(fw, "ts.interm_cls", _p(tm), Cc, B * nq, T_ + "enc_out_class_embed.weight", _p(self.interm_logits),
+                eng.ncls, out_code=DP_F32)
+        ep = [buf(B * nq, eng.w[f"{T_}enc_pose_embed.layers.{i}.weight"].shape[0]) for i in range(3)]
+        x, ldx = _p(tm), Cc
+        for i in range(3):
+            eng.lin(fw, f"ts.enc_pose{i}", x, ldx, B * nq, f"{T_}enc_pose_embed.layers.{i}.weight", _p(ep[i]),
+                    ep[i].shape[1], act=1)
+            x, ldx = _p(ep[i]), ep[i].shape[1]
+        delta = f32(B * nq, 2 * K)
+        eng.lin(fw, "ts.enc_pose3", x, ldx, B * nq, f"{T_}enc_pose_embed.layers.3.weight", _p(delta), 2 * K,
+                out_code=DP_F32)
+        self.ref0 = f32(B, nq, T, 2)
+        fw.op("ts.refpoints", lib.dp_refpoint_init, _p(delta), _p(eng.anchors), _p(self.topi), B, nq, K, _p(self.ref0))
+
+        # ================= queries (transformer.py:1253-1279, dn_component.py:132-153)
+        tgt0 = buf(B, Qt, T, Cc)
+        fw.op("q.build", lib.dp_query_build, _p(sd[T_ + "tgt_embed.weight"]), _p(sd[T_ + "keypoint_embedding.weight"]),
+              _p(sd[T_ + "instance_embedding.weight"]), _p(sd[T_ + "label_enc.weight"]),
+              _p(sd[T_ + "pose_enc.weight"]), _p(self.dn_label), B, P, nq, K, Cc, _p(tgt0), code)
+        refs = [f32(B, Qt, T, 2) for _ in range(L + 1)]
+        if P:
+            fw.op("q.dn_ref", lib.dp_convert_rows, _p(self.dn_ref), DP_F32, P * T * 2, _p(refs[0]), DP_F32,
+                  Qt * T * 2, B, P * T * 2, C.c_float(1.0), 0)
+        fw.op("q.ref", lib.dp_convert_rows, _p(self.ref0), DP_F32, nq * T * 2, _p(refs[0], P * T * 2), DP_F32,
+              Qt * T * 2, B, nq * T * 2, C.c_float(1.0), 0)
+        self.refs = refs
+
+        # ================= decoder layers (transformer.py:588-602, 387-442) + heads (701-728)
+        lv0 = shapes[0]
+        self.L_ = []
+        corners = [f32(krows, nb) for _ in range(L)]
+        kps = [f32(B, Qt, K, 2) for _ in range(L)]
+        logits = [f32(B, Qt, eng.ncls) for _ in range(L)]
+        self.pre_out = f32(B, Qt, K, 2)
+        self.pre_logits = f32(B, Qt, eng.ncls)
+        nhid = eng.sd32[f"{T_}lqe_embed.0.reg_conf.layers.0.weight"].shape[0]
+        prev_y = tgt0
+        for l in range(L):
+            n = f"dec{l}"
+            lp = f"{T_}decoder.layers.{l}."
+            S_ = {}
+            se = buf(krows, Cc)
+            fw.op(n + ".sine", lib.dp_sine_embed, _p(refs[l]), qrows, K, Cc, _p(eng.dim_t), _p(se), code)
+            ph = buf(krows, Cc)
+            pos = buf(krows, Cc)
+            hp = f"{T_}decoder.half_pose_ref_point_head.layers."
+            eng.lin(fw, n + ".pos0", _p(se), Cc, krows, hp + "0.weight", _p(ph), Cc, act=1)
+            eng.lin(fw, n + ".pos1", _p(ph), Cc, krows, hp + "1.weight", _p(pos), Cc)
+            x0 = buf(rows, Cc)
+            fw.op(n + ".x0", lib.dp_convert_rows, _p(prev_y), code, Cc, _p(x0), code, Cc, rows, Cc, C.c_float(1.0), 0)
+            fw.op(n + ".x0pos", lib.dp_add_rows, _p(x0), kp_map, _p(x0), kp_map, _p(pos), cr(Cc), krows, Cc, code)
+            # within-instance attention over the T tokens of a query
+            qkv_w = buf(rows, 3 * Cc)
+            eng.lin(fw, n + ".w_qkv", _p(x0), Cc, rows, lp + "within_attn.in_proj_weight", _p(qkv_w), 3 * Cc)
+            att_w = buf(rows, Cc)
+            P_w = f32(qrows * nh * T * T)
+            fw.op(n + ".w_attn", lib.dp_attn_fwd, _p(qkv_w), 3 * Cc, _p(qkv_w, Cc), _p(qkv_w, 2 * Cc), 3 * Cc, _p(att_w),
+                  Cc, _p(P_w), None, qrows, 1, T, 0, 1, T, nh, Cc // nh, code)
+            ao_w = buf(rows, Cc)
+            eng.lin(fw, n + ".w_out", _p(att_w), Cc, rows, lp + "within_attn.out_proj.weight", _p(ao_w), Cc)
+            x1, s_w, st_w = buf(rows, Cc), buf(rows, Cc), f32(rows, 2)
+            fw.op(n + ".w_norm", lib.dp_ln_fwd, _p(x1), Cc, _p(x0), _p(ao_w), _p(s_w), _p(st_w),
+                  _p(sd[lp + "within_norm.weight"]), _p(sd[lp + "within_norm.bias"]), C.c_float(1e-5), rows, Cc, None,
+                  1, 0, code)
+            # across-instance attention over the Qt queries of a token slot, DN attn_mask
+            qkv_a = buf(rows, 3 * Cc)
+            eng.lin(fw, n + ".a_qkv", _p(x1), Cc, rows, lp + "across_attn.in_proj_weight", _p(qkv_a), 3 * Cc)
+            att_a = buf(rows, Cc)
+            P_a = f32(B * T * nh * Qt * Qt)
+            fw.op(n + ".a_attn", lib.dp_attn_fwd, _p(qkv_a), 3 * Cc, _p(qkv_a, Cc), _p(qkv_a, 2 * Cc), 3 * Cc, _p(att_a),
+                  Cc, _p(P_a), _p(self.mask) if P else None, B, T, Qt * T, 1, T, Qt, nh, Cc // nh, code)
+            ao_a = buf(rows, Cc)
+            eng.lin(fw, n + ".a_out", _p(att_a), Cc, rows, lp + "across_attn.out_proj.weight", _p(ao_a), Cc)
+            xcat, s_a, st_a = buf(rows, 2 * Cc), buf(rows, Cc), f32(rows, 2)
+            # LN + the second in-place pos add (transformer.py:419-422) -> x3 = xcat[:, :Cc]
+            fw.op(n + ".a_norm", lib.dp_ln_fwd, _p(xcat), 2 * Cc, _p(x1), _p(ao_a), _p(s_a), _p(st_a),
+                  _p(sd[lp + "across_norm.weight"]), _p(sd[lp + "across_norm.bias"]), C.c_float(1e-5), rows, Cc,
+                  _p(pos), T, 1, code)
+            # MSDA (ms_deform_attn.py:384-444): offsets / logits in f32, output -> xcat[:, Cc:]
+            oa = f32(rows, ncol)
+            eng.lin(fw, n + ".offattn", _p(xcat), 2 * Cc, rows, lp + "cross_attn.offattn.weight", _p(oa), ncol,
+                    out_code=DP_F32)
+            fw.op(n + ".msda", lib.dp_msda, _p(self.memory), B, S, self.lvl_hw, len(shapes), _p(oa), _p(refs[l]),
+                  _p(xcat, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt, code | _lib.DP_MSDA_OFFATTN_F32)
+            # Gate (transformer.py:222-235)
+            G, gs, z = buf(rows, 2 * Cc), buf(rows, 2 * Cc), buf(rows, Cc)
+            eng.lin(fw, n + ".gate", _p(xcat), 2 * Cc, rows, lp + "gateway.gate.weight", _p(G), 2 * Cc)
+            fw.op(n + ".gate_fn", lib.dp_gate_fwd, _p(G), _p(xcat), _p(gs), _p(z), rows, Cc, code)
+            yg, s_g, st_g = buf(rows, Cc), buf(rows, Cc), f32(rows, 2)
+            fw.op(n + ".g_norm", lib.dp_ln_fwd, _p(yg), Cc, _p(z), None, _p(s_g), _p(st_g),
+                  _p(sd[lp + "gateway.norm.weight"]), _p(sd[lp + "gateway.norm.bias"]), C.c_float(1e-5), rows, Cc,
+                  None, 1, 0, code)
+            # FFN (transformer.py:371-385)
+            h, f = buf(rows, F), buf(rows, Cc)
+            eng.lin(fw, n + ".ffn1", _p(yg), Cc, rows, lp + "linear1.weight", _p(h), F, act=1)
+            eng.lin(fw, n + ".ffn2", _p(h), F, rows, lp + "linear2.weight", _p(f), Cc)
+            y, s_2, st_2 = buf(rows, Cc), buf(rows, Cc), f32(rows, 2)
+            fw.op(n + ".norm2", lib.dp_ln_fwd, _p(y), Cc, _p(yg), _p(f), _p(s_2), _p(st_2), _p(sd[lp + "norm2.weight"]),
+                  _p(sd[lp + "norm2.bias"]), C.c_float(1e-5), rows, Cc, None, 1, 0, code)
+            # ---- heads. u = output_pose (+ output_pose_detach: the previous output + this layer's
+            # pos, i.e. x0's keypoint rows: transformer.py:369/712/913 aliasing)
+            u = buf(krows, Cc)
+            fw.op(n + ".u", lib.dp_add_rows, _p(u), cr(Cc), _p(y), kp_map, _p(x0) if l > 0 else None, kp_map, krows, Cc,
+                  code)
+            if l == 0:
+                pp = f"{T_}pre_pose_embed.layers."
+                pre0, pre1 = buf(krows, Cc), buf(krows, Cc)
+                pre = f32(krows, 2)
+                eng.lin(fw, "pre0", _p(u), Cc, krows, pp + "0.weight", _p(pre0), Cc, act=1)
+                eng.lin(fw, "pre1", _p(pre0), Cc, krows, pp + "1.weight", _p(pre1), Cc, act=1)
+                eng.lin(fw, "pre2", _p(pre1), Cc, krows, pp + "2.weight", _p(pre), 2, out_code=DP_F32)
+                fw.op("pre_pose", lib.dp_pre_pose, _p(pre), _p(refs[0]), qrows, K, _p(self.pre_out))
+                eng.lin(fw, "pre_cls", _p(y), T * Cc, qrows, f"{T_}class_embed.0.weight", _p(self.pre_logits),
+                        eng.ncls, out_code=DP_F32)
+                S_.update(pre0=pre0, pre1=pre1)
+            pe = f"{T_}pose_embed.{l}.layers."
+            c0, c1 = buf(krows, Cc), buf(krows, Cc)
+            eng.lin(fw, n + ".pose0", _p(u), Cc, krows, pe + "0.weight", _p(c0), Cc, act=1)
+            eng.lin(fw, n + ".pose1", _p(c0), Cc, krows, pe + "1.weight", _p(c1), Cc, act=1)
+            if l > 0:   # + pred_corners_undetach (transformer.py:712)
+                fw.op(n + ".corners_prev", lib.dp_convert_rows, _p(corners[l - 1]), DP_F32, nb, _p(corners[l]), DP_F32,
+                      nb, krows, nb, C.c_float(1.0), 0)
+            eng.lin(fw, n + ".pose2", _p(c1), Cc, krows, pe + "2.weight", _p(corners[l]), nb, out_code=DP_F32,
+                    beta=1.0 if l > 0 else 0.0)
+            fw.op(n + ".refine", lib.dp_pose_refine, _p(corners[l]), _p(eng.project), eng.reg_max, _p(self.pre_out),
+                  C.c_float(eng.reg_scale), qrows, K, _p(kps[l]), _p(refs[l + 1]))
+            eng.lin(fw, n + ".cls", _p(y), T * Cc, qrows, f"{T_}class_embed.{l}.weight", _p(logits[l]), eng.ncls,
+                    out_code=DP_F32)
+            stt = f32(qrows, K * 5)
+            fw.op(n + ".lqe_stats", lib.dp_lqe_stats, _p(self.memory), S * Cc, lv0[0], lv0[1], Cc, _p(kps[l]), B, Qt, K,
+                  _p(stt), code)
+            hq = f32(qrows, nhid)
+            qe = f"{T_}lqe_embed.{l}.reg_conf.layers."
+            eng.lin(fw, n + ".lqe0", _p(stt), K * 5, qrows, qe + "0.weight", _p(hq), nhid, act=1, out_code=DP_F32,
+                    wt=sd[qe + "0.weight"], in_code=DP_F32)
+            # quality score (B, Q, 1) added to every class logit (transformer.py:288 broadcasts): the
+            # one output row of reg_conf's last layer read for each of the ncls columns (b_ns = 0)
+            w1 = sd[qe + "1.weight"]
+            b2 = sd[qe + "1.bias"].repeat(eng.ncls).contiguous()
+            self.arena.append(b2)
+            eng._gemm(fw, n + ".lqe1", _p(hq), nhid, 1, _p(w1), 1, 0, _p(logits[l]), eng.ncls, qrows, eng.ncls, nhid,
+                      DP_F32, DP_F32, bias=_p(b2), beta=1.0)
+            S_.update(se=se, ph=ph, pos=pos, x0=x0, qkv_w=qkv_w, att_w=att_w, P_w=P_w, x1=x1, s_w=s_w, st_w=st_w,
+                      qkv_a=qkv_a, att_a=att_a, P_a=P_a, xcat=xcat, s_a=s_a, st_a=st_a, oa=oa, gs=gs, yg=yg, s_g=s_g,
+                      st_g=st_g, h=h, y=y, s_2=s_2, st_2=st_2, u=u, c0=c0, c1=c1, stt=stt, hq=hq)
+            self.L_.append(S_)
+            prev_y = y
+        self.corners, self.kps, self.logits = corners, kps, logits
+
+        # ================= criterion (criterion.py:285-435) -> gradients of the head outputs
+        self._criterion_buffers()
+        # ================= backward
+        self._record_backward(tm, ep, delta)
+
+    # ------------------------------------------------------------------ criterion
+    def _criterion_buffers(self):
+        eng, B, P, nq, K, L = self.eng, self.B, self.P, self.eng.nq, self.eng.K, self.eng.L
+        dev = eng.device
+        ncls = eng.ncls
+        H = L + 2
+        self.H = H
+        self.hl = torch.empty(H, B, nq, ncls, dtype=torch.float32, device=dev)   # packed heads (match layout)
+        self.hk = torch.empty(H, B, nq, 2 * K, dtype=torch.float32, device=dev)
+        self.g_lg = torch.empty(H, B, nq, ncls, dtype=torch.float32, device=dev)
+        self.g_l1 = torch.empty(H, B, nq, 2 * K, dtype=torch.float32, device=dev)
+        self.g_oks = torch.empty(H, B, nq, 2 * K, dtype=torch.float32, device=dev)
+        self.losses = torch.empty(H, 3, dtype=torch.float32, device=dev)
+        self.match = torch.empty(H, B, nq, dtype=torch.int32, device=dev)
+        self.go = torch.empty(B, nq, dtype=torch.int32, device=dev)
+        self.n_go = torch.empty(1, dtype=torch.float32, device=dev)
+        self.n_boxes = torch.empty(1, dtype=torch.float32, device=dev)
+        if P:
+            Hd = L + 1
+            self.Hd = Hd
+            self.dl = torch.empty(Hd, B, P, ncls, dtype=torch.float32, device=dev)
+            self.dk = torch.empty(Hd, B, P, 2 * K, dtype=torch.float32, device=dev)
+            self.dg_lg = torch.empty(Hd, B, P, ncls, dtype=torch.float32, device=dev)
+            self.dg_l1 = torch.empty(Hd, B, P, 2 * K, dtype=torch.float32, device=dev)
+            self.dg_oks = torch.empty(Hd, B, P, 2 * K, dtype=torch.float32, device=dev)
+            self.dn_losses = torch.empty(Hd, 3, dtype=torch.float32, device=dev)
+            self.dn_m = torch.empty(B, P, dtype=torch.int32, device=dev)
+            self.n_dn = torch.empty(1, dtype=torch.float32, device=dev)
+        # gradients of the head outputs, assembled from the loss kernels
+        self.d_logits = [torch.zeros_like(t) for t in self.logits]
+        self.d_kps = [torch.zeros_like(t) for t in self.kps]
+        self.d_pre_logits = torch.zeros_like(self.pre_logits)
+        self.d_pre_out = torch.zeros_like(self.pre_out)
+        self.d_interm_logits = torch.zeros_like(self.interm_logits)
+        self.d_interm_kps = torch.empty(B, nq, 2 * K, dtype=torch.float32, device=dev)
+
+    def heads_pack(self):
+        """The H heads in the reference's matching order (final, aux 0..L-2, pre, interm) as
+        contiguous (B, nq, .) f32 blocks (their matching rows; DN rows separately)."""
+        eng, lib = self.eng, self.eng.lib
+        B, P, nq, K, L, Qt, T = self.B, self.P, eng.nq, eng.K, eng.L, self.Qt, eng.T
+        ncls = eng.ncls
+        s = C.c_void_p(torch.cuda.current_stream(eng.device).cuda_stream)
+        order = [L - 1] + list(range(L - 1))
+        chk = _lib.check
+        for h, l in enumerate(order):
+            chk(lib.dp_convert_rows(_p(self.logits[l], P * ncls), DP_F32, Qt * ncls, _p(self.hl[h]), DP_F32, nq * ncls,
+                                    B, nq * ncls, 1.0, 0, s), "pack")
+            chk(lib.dp_convert_rows(_p(self.kps[l], P * 2 * K), DP_F32, Qt * 2 * K, _p(self.hk[h]), DP_F32, nq * 2 * K,
+                                    B, nq * 2 * K, 1.0, 0, s), "pack")
+        chk(lib.dp_convert_rows(_p(self.pre_logits, P * ncls), DP_F32, Qt * ncls, _p(self.hl[L]), DP_F32, nq * ncls, B,
+                                nq * ncls, 1.0, 0, s), "pack")
+        chk(lib.dp_convert_rows(_p(self.pre_out, P * 2 * K), DP_F32, Qt * 2 * K, _p(self.hk[L]), DP_F32, nq * 2 * K, B,
+                                nq * 2 * K, 1.0, 0, s), "pack")
+        chk(lib.dp_convert_rows(_p(self.interm_logits), DP_F32, nq * ncls, _p(self.hl[L + 1]), DP_F32, nq * ncls, B,
+                                nq * ncls, 1.0, 0, s), "pack")
+        # interm keypoints = enc_outputs_pose_coord[:, :, 1:] (skip the centre)
+        chk(lib.dp_convert_rows(_p(self.ref0, 2), DP_F32, T * 2, _p(self.hk[L + 1]), DP_F32, 2 * K, B * nq, 2 * K, 1.0,
+                                0, s), "pack")
+        if P:
+            for l in range(L):
+                chk(lib.dp_convert_rows(_p(self.logits[l]), DP_F32, Qt * ncls, _p(self.dl[l]), DP_F32, P * ncls, B,
+                                        P * ncls, 1.0, 0, s), "pack")
+                chk(lib.dp_convert_rows(_p(self.kps[l]), DP_F32, Qt * 2 * K, _p(self.dk[l]), DP_F32, P * 2 * K, B,
+                                        P * 2 * K, 1.0, 0, s), "pack")
+            chk(lib.dp_convert_rows(_p(self.pre_logits), DP_F32, Qt * ncls, _p(self.dl[L]), DP_F32, P * ncls, B,
+                                    P * ncls, 1.0, 0, s), "pack")
+            chk(lib.dp_convert_rows(_p(self.pre_out), DP_F32, Qt * 2 * K, _p(self.dk[L]), DP_F32, P * 2 * K, B,
+                                    P * 2 * K, 1.0, 0, s), "pack")
+
+    def criterion(self, packed, sizes, num_group, weights=(2.0, 10.0, 4.0), cost=(2.0, 10.0, 4.0), alpha=0.25,
+                  gamma=2.0):
+        """Matching + losses + loss gradients (criterion.py:285-435) on the kernels of
+        detrpose_amd/criterion.py, then the hand-off into the head-output gradient buffers.
+        Returns (loss names, device loss values)."""
+        eng, lib = self.eng, self.eng.lib
+        B, P, nq, K, L, Qt, H = self.B, self.P, eng.nq, eng.K, eng.L, self.Qt, self.H
+        ncls = eng.ncls
+        dev = eng.device
+        s = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        chk = _lib.check
+        self.heads_pack()
+        sig = torch.tensor(COCO_SIGMAS if K == 17 else CROWDPOSE_SIGMAS, device=dev)
+        max_t = max([int(v) for v in sizes] + [1])
+        chk(lib.dp_hungarian_match(_p(self.hl), B * nq * ncls, nq * ncls, ncls, ncls, _p(self.hk), B * nq * 2 * K,
+                                   nq * 2 * K, 2 * K, K, _p(packed.off), _p(packed.label), _p(packed.kps),
+                                   _p(packed.area), H, B, nq, max_t, cost[0], cost[1], cost[2], alpha, _p(sig),
+                                   _p(self.match), None, s), "dp_hungarian_match")
+        chk(lib.dp_match_union(_p(self.match), H, B, nq, _p(self.go), _p(self.n_go), s), "dp_match_union")
+        self.n_boxes.fill_(float(max(sum(sizes), 0)))
+        heads = (_lib.LossHead * H)()
+        for h in range(H):
+            heads[h] = _lib.LossHead(_p(self.hl[h]), nq * ncls, ncls, _p(self.hk[h]), nq * 2 * K, 2 * K,
+                                     _p(self.match[h]))
+        chk(lib.dp_pose_loss(heads, H, B, nq, ncls, K, _p(self.go), _p(packed.off), _p(packed.label), _p(packed.kps),
+                             _p(packed.area), _p(sig), alpha, gamma, _p(self.n_boxes), _p(self.n_go), 1.0, weights[0],
+                             weights[1], weights[2], _p(self.losses), _p(self.g_lg), _p(self.g_l1), _p(self.g_oks), s),
+            "dp_pose_loss")
+        names = ["", *[f"_{i}" for i in range(L - 1)], "_pre", "_enc_0"]
+        if P:
+            Hd = self.Hd
+            self.dn_m.copy_(torch.from_numpy(dn_match(sizes, P, num_group)))
+            # num_boxes (clamped to >= 1, criterion.py:316-322) * num_dn_group (criterion.py:406)
+            self.n_dn.fill_(max(float(sum(sizes)), 1.0) * num_group)
+            dheads = (_lib.LossHead * Hd)()
+            for h in range(Hd):
+                dheads[h] = _lib.LossHead(_p(self.dl[h]), P * ncls, ncls, _p(self.dk[h]), P * 2 * K, 2 * K,
+                                          _p(self.dn_m))
+            chk(lib.dp_pose_loss(dheads, Hd, B, P, ncls, K, _p(self.dn_m), _p(packed.off), _p(packed.label),
+                                 _p(packed.kps), _p(packed.area), _p(sig), alpha, gamma, _p(self.n_dn), _p(self.n_dn),
+                                 1.0, weights[0], weights[1], weights[2], _p(self.dn_losses), _p(self.dg_lg),
+                                 _p(self.dg_l1), _p(self.dg_oks), s), "dp_pose_loss(dn)")
+        # ---- hand-off: d loss_total / d head outputs
+        order = [L - 1] + list(range(L - 1))
+
+        def put(dst, dst_off, ld_dst, src, n, acc=0):
+            chk(lib.dp_convert_rows(_p(src), DP_F32, n, _p(dst, dst_off), DP_F32, ld_dst, B, n, 1.0, acc, s), "hand-off")
+
+        for h, l in enumerate(order):
+            put(self.d_logits[l], P * ncls, Qt * ncls, self.g_lg[h], nq * ncls)
+            put(self.d_kps[l], P * 2 * K, Qt * 2 * K, self.g_l1[h], nq * 2 * K)
+            put(self.d_kps[l], P * 2 * K, Qt * 2 * K, self.g_oks[h], nq * 2 * K, 1)
+        put(self.d_pre_logits, P * ncls, Qt * ncls, self.g_lg[L], nq * ncls)
+        put(self.d_pre_out, P * 2 * K, Qt * 2 * K, self.g_l1[L], nq * 2 * K)
+        put(self.d_pre_out, P * 2 * K, Qt * 2 * K, self.g_oks[L], nq * 2 * K, 1)
+        put(self.d_interm_logits, 0, nq * ncls, self.g_lg[L + 1], nq * ncls)
+        put(self.d_interm_kps, 0, nq * 2 * K, self.g_l1[L + 1], nq * 2 * K)
+        put(self.d_interm_kps, 0, nq * 2 * K, self.g_oks[L + 1], nq * 2 * K, 1)
+        if P:
+            for l in range(L):
+                put(self.d_logits[l], 0, Qt * ncls, self.dg_lg[l], P * ncls)
+                put(self.d_kps[l], 0, Qt * 2 * K, self.dg_l1[l], P * 2 * K)
+                put(self.d_kps[l], 0, Qt * 2 * K, self.dg_oks[l], P * 2 * K, 1)
+            put(self.d_pre_logits, 0, Qt * ncls, self.dg_lg[L], P * ncls)
+            put(self.d_pre_out, 0, Qt * 2 * K, self.dg_l1[L], P * 2 * K)
+            put(self.d_pre_out, 0, Qt * 2 * K, self.dg_oks[L], P * 2 * K, 1)
+        keys = []
+        for n in names:
+            keys += ["loss_vfl" + n, "loss_keypoints" + n, "loss_oks" + n]
+        vals = [self.losses.reshape(-1)]
+        if P:
+            for n in [*[f"_dn_{i}" for i in range(L)], "_dn_pre"]:
+                keys += ["loss_vfl" + n, "loss_keypoints" + n, "loss_oks" + n]
+            vals.append(self.dn_losses.reshape(-1))
+        return keys, torch.cat(vals)
+
+    # ------------------------------------------------------------------ backward
+    def _record_backward(self, tm, ep, delta):
+        eng, lib = self.eng, self.eng.lib
+        bw = self.bw
+        B, P, nq, K, T, L, F, Qt = self.B, self.P, eng.nq, eng.K, eng.T, eng.L, eng.F, self.Qt
+        C_, nh = eng.C, eng.nh
+        Cc = C_
+        code = eng.code
+        dt = eng.tdtype
+        e = dt.itemsize
+        rows, krows, qrows = self.rows, self.krows, self.qrows
+        nb, ncol, ncls = eng.nb, nh * eng.nlev * eng.npnt * 3, eng.ncls
+        dev = eng.device
+        sd = eng.sd32
+        cr = contiguous_rows
+        kp_map = rowmap(Cc, K, T * Cc, Cc)
+        lv0 = self.shapes[0]
+        conv = code != DP_F32   # f32 gradients must be converted to dtype for the GEMMs
+
+        def buf(*shape, dtype=None):
+            t = torch.empty(*shape, dtype=dtype or dt, device=dev)
+            self.arena.append(t)
+            return t
+
+        def f32(*shape):
+            return buf(*shape, dtype=torch.float32)
+
+        def to_dt(name, src, rows_, n, ld=None):
+            """f32 gradient rows as the GEMM dtype (a copy in bf16 mode, the buffer itself in fp32)."""
+            if not conv:
+                return src, (ld or n)
+            d = buf(rows_, n)
+            bw.op(name, lib.dp_convert_rows, _p(src), DP_F32, ld or n, _p(d), code, n, rows_, n, C.c_float(1.0), 0)
+            return d, n
+
+        def mlp_bwd(name, dout_dt, ld_out, dout32, ld32, rows_, layers, ins, wkeys):
+            """Backward of an MLP chain: layers[i] output i (ReLU between); ins[i] input of layer i.
+            dout: gradient of the last layer's output. Returns the gradient of ins[0] (a buffer)."""
+            d, ldd, d32, l32 = dout_dt, ld_out, dout32, ld32
+            for i in range(len(wkeys) - 1, -1, -1):
+                x, ldx = ins[i]
+                eng.wgrad(bw, f"{name}.l{i}", _p(d), ldd, rows_, wkeys[i], _p(x), ldx, dy32=_p(d32) if d32 is not None
+                          else None, ld32=l32)
+                W = eng.w[wkeys[i]]
+                din = buf(rows_, W.shape[1])
+                gate = ins[i][0] if i > 0 else None
+                eng.dgrad(bw, f"{name}.l{i}.dx", _p(d), ldd, rows_, wkeys[i], _p(din), W.shape[1],
+                          gate=_p(gate) if gate is not None else None, ld_gate=ins[i][1] if i > 0 else 0)
+                d, ldd, d32, l32 = din, W.shape[1], None, None
+            return d
+
+        self.ones = torch.ones(ncls, dtype=torch.float32, device=dev)
+        bw.op("bw.zero", lib.dp_zero, _p(eng.grad_flat), eng.grad_flat.numel() * 4)
+        dY = buf(rows, Cc)
+        bw.op("bw.dY0", lib.dp_zero, _p(dY), rows * Cc * e)
+        dcorn = f32(krows, nb)
+        dpos = buf(krows, Cc)
+        for l in range(L - 1, -1, -1):
+            n = f"bw{l}"
+            lp = f"{T_}decoder.layers.{l}."
+            S_ = self.L_[l]
+            y = S_["y"]
+            # ---------------- heads of layer l
+            # LQE: logits = score + MLP(stats) (transformer.py:728, 275-288)
+            qe = f"{T_}lqe_embed.{l}.reg_conf.layers."
+            dlg = self.d_logits[l]
+            # d quality = sum over the class columns it was added to
+            dq = f32(qrows, 1)
+            eng._gemm(bw, n + ".lqe_dq", _p(dlg), ncls, 1, _p(self.ones), 1, 0, _p(dq), 1, qrows, 1, ncls, DP_F32,
+                      DP_F32)
+            eng.wgrad(bw, n + ".lqe1", _p(dq), 1, qrows, qe + "1.weight", _p(S_["hq"]), S_["hq"].shape[1],
+                      in_code=DP_F32)
+            nhid = S_["hq"].shape[1]
+            dhq = f32(qrows, nhid)
+            eng.dgrad(bw, n + ".lqe1.dx", _p(dq), 1, qrows, qe + "1.weight", _p(dhq), nhid, gate=_p(S_["hq"]),
+                      ld_gate=nhid, wt=sd[qe + "1.weight"], in_code=DP_F32, gate_code=DP_F32)
+            eng.wgrad(bw, n + ".lqe0", _p(dhq), nhid, qrows, qe + "0.weight", _p(S_["stt"]), K * 5, in_code=DP_F32)
+            dst = f32(qrows, K * 5)
+            eng.dgrad(bw, n + ".lqe0.dx", _p(dhq), nhid, qrows, qe + "0.weight", _p(dst), K * 5, wt=sd[qe + "0.weight"],
+                      in_code=DP_F32)
+            bw.op(n + ".lqe_stats_bwd", lib.dp_lqe_stats_bwd, _p(self.memory), self.S * Cc, lv0[0], lv0[1], Cc,
+                  _p(self.kps[l]), _p(dst), B, Qt, K, _p(self.d_kps[l]), code)
+            # class head on the instance token: score = class_embed[l](output[:, :, 0])
+            ck = f"{T_}class_embed.{l}.weight"
+            dlg_dt, ldl = to_dt(n + ".dlogits", dlg, qrows, ncls)
+            eng.wgrad(bw, n + ".cls", _p(dlg_dt), ldl, qrows, ck, _p(y), T * Cc, dy32=_p(dlg), ld32=ncls)
+            eng.dgrad(bw, n + ".cls.dx", _p(dlg_dt), ldl, qrows, ck, _p(dY), T * Cc, beta=1.0)
+            # Integral + distance2pose, then pred_corners = pose_head(u) + corners_{l-1} (kept
+            # undetached: d corners_{l-1} += d corners_l, carried in dcorn)
+            bw.op(n + ".refine_bwd", lib.dp_pose_refine_bwd, _p(self.corners[l]), _p(eng.project), eng.reg_max,
+                  C.c_float(eng.reg_scale), _p(self.d_kps[l]), qrows, K, _p(dcorn), 1 if l < L - 1 else 0)
+            dc_dt, ldc = to_dt(n + ".dcorn", dcorn, krows, nb)
+            pe = f"{T_}pose_embed.{l}.layers."
+            du = mlp_bwd(n + ".pose", dc_dt, ldc, dcorn, nb, krows, 3,
+                         [(S_["u"], Cc), (S_["c0"], Cc), (S_["c1"], Cc)], [pe + "0.weight", pe + "1.weight",
+                                                                         pe + "2.weight"])
+            bw.op(n + ".du", lib.dp_add_rows, _p(dY), kp_map, _p(dY), kp_map, _p(du), cr(Cc), krows, Cc, code)
+            if l == 0:
+                # pre head: pre_poses = sigmoid(MLP(output_pose) + inverse_sigmoid(ref)) (transformer.py:707)
+                dpre = f32(krows, 2)
+                bw.op("bw.pre_sig", lib.dp_sigmoid_bwd, _p(self.pre_out), _p(self.d_pre_out), _p(dpre), krows, 2, 2, 2,
+                      2)
+                dpre_dt, ldp = to_dt("bw.dpre", dpre, krows, 2)
+                pp = f"{T_}pre_pose_embed.layers."
+                du0 = mlp_bwd("bw.pre", dpre_dt, ldp, dpre, 2, krows, 3,
+                              [(S_["u"], Cc), (S_["pre0"], Cc), (S_["pre1"], Cc)],
+                              [pp + "0.weight", pp + "1.weight", pp + "2.weight"])
+                bw.op("bw.pre.du", lib.dp_add_rows, _p(dY), kp_map, _p(dY), kp_map, _p(du0), cr(Cc), krows, Cc, code)
+                dpl_dt, ldq = to_dt("bw.dpre_logits", self.d_pre_logits, qrows, ncls)
+                c0k = f"{T_}class_embed.0.weight"
+                eng.wgrad(bw, "bw.pre_cls", _p(dpl_dt), ldq, qrows, c0k, _p(y), T * Cc, dy32=_p(self.d_pre_logits),
+                          ld32=ncls)
+                eng.dgrad(bw, "bw.pre_cls.dx", _p(dpl_dt), ldq, qrows, c0k, _p(dY), T * Cc, beta=1.0)
+            # ---------------- the layer (transformer.py:387-442) in reverse
+            # FFN + norm2
+            ds2 = buf(rows, Cc)
+            bw.op(n + ".norm2", lib.dp_ln_bwd, _p(ds2), _p(dY), Cc, _p(S_["s_2"]), _p(S_["st_2"]),
+                  _p(sd[lp + "norm2.weight"]), rows, Cc, _p(eng.grads[lp + "norm2.weight"]),
+                  _p(eng.grads[lp + "norm2.bias"]), 0, code)
+            eng.wgrad(bw, n + ".ffn2", _p(ds2), Cc, rows, lp + "linear2.weight", _p(S_["h"]), F)
+            dh = buf(rows, F)
+            eng.dgrad(bw, n + ".ffn2.dx", _p(ds2), Cc, rows, lp + "linear2.weight", _p(dh), F, gate=_p(S_["h"]),
+                      ld_gate=F)
+            eng.wgrad(bw, n + ".ffn1", _p(dh), F, rows, lp + "linear1.weight", _p(S_["yg"]), Cc)
+            eng.dgrad(bw, n + ".ffn1.dx", _p(dh), F, rows, lp + "linear1.weight", _p(ds2), Cc, beta=1.0)   # d yg
+            # Gate + its norm
+            dz = buf(rows, Cc)
+            bw.op(n + ".g_norm", lib.dp_ln_bwd, _p(dz), _p(ds2), Cc, _p(S_["s_g"]), _p(S_["st_g"]),
+                  _p(sd[lp + "gateway.norm.weight"]), rows, Cc, _p(eng.grads[lp + "gateway.norm.weight"]),
+                  _p(eng.grads[lp + "gateway.norm.bias"]), 0, code)
+            dG, dx = buf(rows, 2 * Cc), buf(rows, 2 * Cc)
+            bw.op(n + ".gate_fn", lib.dp_gate_bwd, _p(dz), _p(S_["gs"]), _p(S_["xcat"]), _p(dG), _p(dx), rows, Cc, code)
+            eng.wgrad(bw, n + ".gate", _p(dG), 2 * Cc, rows, lp + "gateway.gate.weight", _p(S_["xcat"]), 2 * Cc)
+            eng.dgrad(bw, n + ".gate.dx", _p(dG), 2 * Cc, rows, lp + "gateway.gate.weight", _p(dx), 2 * Cc, beta=1.0)
+            # MSDA: d offsets / logits (dp_msda_bwd), then the offattn Linear
+            doa = f32(rows, ncol)
+            bw.op(n + ".msda_bwd", lib.dp_msda_bwd, _p(self.memory), B, self.S, self.lvl_hw, len(self.shapes),
+                  _p(S_["oa"]), _p(self.refs[l]), _p(dx, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt, None, _p(doa),
+                  None, code)
+            doa_dt, ldo = to_dt(n + ".doa", doa, rows, ncol)
+            ok = lp + "cross_attn.offattn.weight"
+            self._wgrad_offattn(bw, n, doa_dt, ldo, doa, rows, ok, S_["xcat"], lp)
+            eng.dgrad(bw, n + ".offattn.dx", _p(doa_dt), ldo, rows, ok, _p(dx), 2 * Cc, beta=1.0)
+            # x3 = LN_a(...) + pos on the keypoint rows (transformer.py:422): d pos
+            dx3_kp = rowmap(2 * Cc, K, T * 2 * Cc, 2 * Cc)
+            bw.op(n + ".dpos", lib.dp_add_rows, _p(dpos), cr(Cc), _p(dx), dx3_kp, None, cr(Cc), krows, Cc, code)
+            # across attention + its norm
+            da = buf(rows, Cc)
+            bw.op(n + ".a_norm", lib.dp_ln_bwd, _p(da), _p(dx), 2 * Cc, _p(S_["s_a"]), _p(S_["st_a"]),
+                  _p(sd[lp + "across_norm.weight"]), rows, Cc, _p(eng.grads[lp + "across_norm.weight"]),
+                  _p(eng.grads[lp + "across_norm.bias"]), 0, code)
+            self._mha_bwd(bw, n + ".a", lp + "across_attn.", da, S_["att_a"], S_["qkv_a"], S_["P_a"], S_["x1"],
+                          B, T, Qt * T, 1, T, Qt)
+            # within attention + its norm (da now holds d x1)
+            dw = buf(rows, Cc)
+            bw.op(n + ".w_norm", lib.dp_ln_bwd, _p(dw), _p(da), Cc, _p(S_["s_w"]), _p(S_["st_w"]),
+                  _p(sd[lp + "within_norm.weight"]), rows, Cc, _p(eng.grads[lp + "within_norm.weight"]),
+                  _p(eng.grads[lp + "within_norm.bias"]), 0, code)
+            self._mha_bwd(bw, n + ".w", lp + "within_attn.", dw, S_["att_w"], S_["qkv_w"], S_["P_w"], S_["x0"],
+                          qrows, 1, T, 0, 1, T)
+            # dw = d x0: x0 = y_{l-1} + pos on the keypoint rows (transformer.py:369)
+            bw.op(n + ".dpos2", lib.dp_add_rows, _p(dpos), cr(Cc), _p(dpos), cr(Cc), _p(dw), kp_map, krows, Cc, code)
+            hp = f"{T_}decoder.half_pose_ref_point_head.layers."
+            eng.wgrad(bw, n + ".pos1", _p(dpos), Cc, krows, hp + "1.weight", _p(S_["ph"]), Cc)
+            dph = buf(krows, Cc)
+            eng.dgrad(bw, n + ".pos1.dx", _p(dpos), Cc, krows, hp + "1.weight", _p(dph), Cc, gate=_p(S_["ph"]),
+                      ld_gate=Cc)
+            eng.wgrad(bw, n + ".pos0", _p(dph), Cc, krows, hp + "0.weight", _p(S_["se"]), Cc)
+            # the next (earlier) layer's output gradient starts as d x0
+            dY = dw
+        self.d_tgt0 = dY
+        bw.op("bw.query", lib.dp_query_build_bwd, _p(dY), _p(self.dn_label), B, P, nq, K, Cc,
+              _p(eng.grads[T_ + "tgt_embed.weight"]), _p(eng.grads[T_ + "keypoint_embedding.weight"]),
+              _p(eng.grads[T_ + "instance_embedding.weight"]), _p(eng.grads[T_ + "label_enc.weight"]),
+              eng.grads[T_ + "label_enc.weight"].shape[0], _p(eng.grads[T_ + "pose_enc.weight"]), code)
+        # ---------------- two-stage (transformer.py:1227-1250), selected rows only
+        ddelta = f32(B * nq, 2 * K)
+        bw.op("bw.ts.sig", lib.dp_sigmoid_bwd, _p(self.ref0, 2), _p(self.d_interm_kps), _p(ddelta), B * nq, 2 * K,
+              T * 2, 2 * K, 2 * K)
+        ddelta_dt, ldd = to_dt("bw.ts.ddelta", ddelta, B * nq, 2 * K)
+        epk = [f"{T_}enc_pose_embed.layers.{i}.weight" for i in range(4)]
+        dtm = mlp_bwd("bw.ts.pose", ddelta_dt, ldd, ddelta, 2 * K, B * nq, 4,
+                      [(tm, Cc)] + [(t, t.shape[1]) for t in ep], epk)
+        dil_dt, ldi = to_dt("bw.ts.dinterm", self.d_interm_logits, B * nq, ncls)
+        ck = f"{T_}enc_out_class_embed.weight"
+        eng.wgrad(bw, "bw.ts.cls", _p(dil_dt), ldi, B * nq, ck, _p(tm), Cc, dy32=_p(self.d_interm_logits), ld32=ncls)
+        eng.dgrad(bw, "bw.ts.cls.dx", _p(dil_dt), ldi, B * nq, ck, _p(dtm), Cc, beta=1.0)
+        xs = buf(B * nq, Cc)
+        bw.op("bw.ts.gather", lib.dp_gather_rows_masked, _p(self.memory), self.S * Cc, _p(self.topi), _p(eng.mask_u8),
+              self.S, B, nq, Cc, _p(xs), code)
+        ssel = buf(B * nq, Cc)
+        eng.lin(bw, "bw.ts.enc_output", _p(xs), Cc, B * nq, T_ + "enc_output.weight", _p(ssel), Cc)
+        ysel, stsel = buf(B * nq, Cc), f32(B * nq, 2)
+        bw.op("bw.ts.enc_norm_fwd", lib.dp_ln_fwd, _p(ysel), Cc, _p(ssel), None, None, _p(stsel),
+              _p(sd[T_ + "enc_output_norm.weight"]), _p(sd[T_ + "enc_output_norm.bias"]), C.c_float(1e-5), B * nq, Cc,
+              None, 1, 0, code)
+        dsel = buf(B * nq, Cc)
+        bw.op("bw.ts.enc_norm", lib.dp_ln_bwd, _p(dsel), _p(dtm), Cc, _p(ssel), _p(stsel),
+              _p(sd[T_ + "enc_output_norm.weight"]), B * nq, Cc, _p(eng.grads[T_ + "enc_output_norm.weight"]),
+              _p(eng.grads[T_ + "enc_output_norm.bias"]), 0, code)
+        eng.wgrad(bw, "bw.ts.enc_output", _p(dsel), Cc, B * nq, T_ + "enc_output.weight", _p(xs), Cc)
+
+    def _wgrad_offattn(self, bw, n, doa_dt, ldo, doa32, rows, okey, xcat, lp):
+        """The fused offsets | logits Linear's weight / bias gradients, written into the two
+        reference parameters (sampling_offsets, attention_weights)."""
+        eng, lib = self.eng, self.eng.lib
+        Cc = eng.C
+        no = eng.grads[lp + "cross_attn.sampling_offsets.weight"].shape[0]
+        na = eng.grads[lp + "cross_attn.attention_weights.weight"].shape[0]
+        for key, c0, nn in (("sampling_offsets", 0, no), ("attention_weights", no, na)):
+            G = eng.grads[lp + f"cross_attn.{key}.weight"]
+            eng._gemm(bw, f"{n}.{key}.dW", _p(doa_dt, c0), 1, ldo, _p(xcat), 2 * Cc, 1, _p(G), Cc, nn, Cc, rows,
+                      eng.code, DP_F32, beta=1.0)
+            bw.op(f"{n}.{key}.db", lib.dp_colsum, _p(doa32, c0), doa32.shape[1], rows, nn,
+                  _p(eng.grads[lp + f"cross_attn.{key}.bias"]), 1, DP_F32)
+
+    def _mha_bwd(self, bw, n, ap, dsum, att, qkv, Pbuf, xin, n_outer, n_inner, so, si, st, L):
+        """nn.MultiheadAttention backward (q = k = v = xin): dsum (the LN backward's output, d of
+        the residual sum) is the out_proj gradient; on return dsum holds d xin."""
+        eng, lib = self.eng, self.eng.lib
+        Cc, nh, code = eng.C, eng.nh, eng.code
+        rows = self.rows
+        eng.wgrad(bw, n + ".out", _p(dsum), Cc, rows, ap + "out_proj.weight", _p(att), Cc)
+        datt = self._scratch(("datt", rows, Cc), rows, Cc)
+        eng.dgrad(bw, n + ".out.dx", _p(dsum), Cc, rows, ap + "out_proj.weight", _p(datt), Cc)
+        dqkv = self._scratch(("dqkv", rows, 3 * Cc), rows, 3 * Cc)
+        bw.op(n + ".attn_bwd", lib.dp_attn_bwd, _p(qkv), 3 * Cc, _p(qkv, Cc), _p(qkv, 2 * Cc), 3 * Cc, _p(Pbuf),
+              _p(datt), Cc, _p(dqkv), 3 * Cc, _p(dqkv, Cc), _p(dqkv, 2 * Cc), 3 * Cc, n_outer, n_inner, so, si, st, L,
+              nh, Cc // nh, code)
+        eng.wgrad(bw, n + ".in", _p(dqkv), 3 * Cc, rows, ap + "in_proj_weight", _p(xin), Cc)
+        eng.dgrad(bw, n + ".in.dx", _p(dqkv), 3 * Cc, rows, ap + "in_proj_weight", _p(dsum), Cc, beta=1.0)
+
+    def _scratch(self, key, *shape):
+        if not hasattr(self, "_scr"):
+            self._scr = {}
+        if key not in self._scr:
+            t = torch.empty(*shape, dtype=self.eng.tdtype, device=self.eng.device)
+            self.arena.append(t)
+            self._scr[key] = t
+        return self._scr[key]
+
+    def cost(self, name, flops):
+        self.op_flops[name] = self.op_flops.get(name, 0.0) + flops
+
+    # ------------------------------------------------------------------ inputs / run
+    def set_inputs(self, memory, dn=None):
+        """memory (B, S, C) (encoder output levels flattened, any float dtype, on the device);
+        dn: {'label' (B, pad) int (-1 = padding), 'pose_unsig' (B, pad, 1+K, 2), 'attn_mask'
+        (pad+nq, pad+nq) bool} or None (pad must be 0)."""
+        self.memory.copy_(memory.to(self.memory.dtype))
+        if self.P:
+            self.dn_label.copy_(torch.as_tensor(dn["label"], dtype=torch.int32))
+            self.dn_ref.copy_(torch.sigmoid(torch.as_tensor(dn["pose_unsig"], dtype=torch.float32)))
+            self.mask.copy_(torch.as_tensor(dn["attn_mask"]).to(torch.uint8))
+
+    def forward(self, debug=None):
+        self.fw.run(debug=debug)
+
+    def backward(self, debug=None):
+        self.bw.run(debug=debug)
+
+
+def encoder_memory(eng_inf, images):
+    """The encoder output (B, S, C) of the inference engine's backbone + encoder for images:
+    the training transformer's input (frozen BN, detached)."""
+    plan = eng_inf.plan(images.shape[0])
+    plan.input.copy_(images)
+    plan.run()
+    return plan.bufs["memory"].view(images.shape[0], -1, eng_inf.tr.hidden_dim)

@@ -131,7 +131,7 @@ int dp_maxpool2x2_pad_rb(const void* in, int64_t in_bstride, int32_t in_pstride,
 int dp_conv2d_pool(const dp_conv_desc* d, void* pool_out, int64_t pool_bstride, int32_t pool_pstride,
                    void* stream);
 
-/* out[r] = a[r] + b[r] over `rows` rows of `c` elements (row maps as above). */
+/* out[r] = a[r] + b[r] over `rows` rows of `c` elements (row maps as above); b == NULL copies a. */
 int dp_add_rows(void* out, dp_rowmap om, const void* a, dp_rowmap am, const void* b, dp_rowmap bm,
                 int32_t rows, int32_t c, int32_t dtype, void* stream);
 
@@ -193,11 +193,12 @@ int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, const int32_t*
  * the module-level training op): offattn f32 [batch*lq][nhead*L*P*2 | nhead*L*P] = the raw
  * sampling_offsets | attention_weights Linear outputs, ref f32 [batch*lq][2]. Recomputes the
  * softmax and the sampling locations and applies the chain rule through them in the same pass:
- * grad_value f32 (zeroed here, f32 atomics), grad_offattn f32 (offattn layout), grad_ref f32
- * [batch*lq][2] or NULL (zeroed here; atomics over the heads). value / grad_out of dtype. */
+ * grad_value f32 (zeroed here, f32 atomics) or NULL (value not differentiated), grad_offattn f32
+ * (offattn layout), grad_ref f32 [batch*lq][2] or NULL (zeroed here; atomics over the heads).
+ * value / grad_out of dtype; grad_out rows ld_grad_out elements apart. */
 int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */,
-                int32_t nlevels, const float* offattn, const float* ref, const void* grad_out, int32_t lq,
-                int32_t nhead, int32_t dh, int32_t npoints, float* grad_value, float* grad_offattn,
+                int32_t nlevels, const float* offattn, const float* ref, const void* grad_out, int32_t ld_grad_out,
+                int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value, float* grad_offattn,
                 float* grad_ref, int32_t dtype, void* stream);
 
 /* Input pipeline of the reference benchmark (tools/benchmark/dataset.py:56-61) for one image
@@ -397,6 +398,120 @@ int dp_pose_loss(const dp_loss_head* heads /* host array of H */, int32_t H, int
                  const float* sigmas, float alpha, float gamma, const float* n_boxes,
                  const float* n_boxes_go, float world, float w_vfl, float w_kp, float w_oks,
                  float* losses, float* g_logits, float* g_kp_l1, float* g_kp_oks, void* stream);
+
+/* ---- Training step (BASELINE config 5): the transformer's training forward
+ * with OKS-denoising queries and its backward. Every nn.Linear forward / input gradient / weight
+ * gradient is a dp_gemm; the row ops have explicit forward (saving what the backward needs) and
+ * backward entry points. Activations and activation gradients are of `dtype`, LayerNorm
+ * statistics, parameter gradients and head tensors f32. Callers: detrpose_amd/train_engine.py. */
+
+/* C(b,m,n) = act(alpha * sum_k A(b,m,k) B(b,k,n) + bias[n] + beta * C(b,m,n)), then zeroed where
+ * gate(b,m,n) <= 0 (ReLU backward); A(b,m,k) = a[b*a_bs + m*a_rs + k*a_ks], B(b,k,n) =
+ * b[b*b_bs + k*b_ks + n*b_ns], C(b,m,n) = c[b*c_bs + m*c_rs + n]. A and B of in_dtype, C of
+ * out_dtype, f32 accumulation on MFMA. split_k 0 = automatic: a launch whose M x N grid cannot
+ * fill the chip (weight gradients) splits K and accumulates into f32 C with atomics (needs
+ * beta 1 and no bias / act / gate: C holds the initial value). Replaces nn.Linear and its
+ * autograd (F.linear's addmm / mm backward). */
+typedef struct dp_gemm_desc {
+  const void* a; int64_t a_bs, a_rs, a_ks;
+  const void* b; int64_t b_bs, b_ks, b_ns;
+  void* c;       int64_t c_bs, c_rs;
+  int32_t batch, m, n, k;
+  int32_t in_dtype, out_dtype;
+  const float* bias;
+  float alpha, beta;
+  int32_t act;
+  const void* gate; int64_t gate_bs, gate_rs; int32_t gate_dtype;
+  int32_t split_k;
+} dp_gemm_desc;
+int dp_gemm(const dp_gemm_desc* d, void* stream);
+
+/* y = LayerNorm(x [+ res]) over contiguous rows of c (nn.LayerNorm, eps): writes y, the pre-norm
+ * sum s = x + res (if s != NULL; the backward's input) and stats f32 [rows][2] = (mean, rstd);
+ * x / res / s rows contiguous, y rows ld_y apart.
+ * With post != NULL also y[r] += post[...] on the rows selected as in dp_layernorm (group /
+ * skip: row r of a group of `post_group` rows takes post row (r / group) * (group - skip) +
+ * (r % group - skip) when r % group >= skip): the decoder's second in-place pos add. */
+int dp_ln_fwd(void* y, int32_t ld_y, const void* x, const void* res, void* s, float* stats, const float* gamma,
+              const float* beta, float eps, int32_t rows, int32_t c, const void* post, int32_t post_group,
+              int32_t post_skip, int32_t dtype, void* stream);
+/* LayerNorm backward from the saved pre-norm input s and stats: dx (= or += when accumulate),
+ * dgamma / dbeta f32 [c] accumulated (+=, the caller zeroes them once per step). */
+int dp_ln_bwd(void* dx, const void* dy, int32_t ld_dy, const void* s, const float* stats, const float* gamma,
+              int32_t rows, int32_t c, float* dgamma, float* dbeta, int32_t accumulate, int32_t dtype, void* stream);
+
+/* out[n] (+)= sum over rows of x[r][n] (f32 out): bias gradients. x rows ld apart, of dtype. */
+int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, float* out, int32_t accumulate, int32_t dtype,
+              void* stream);
+
+/* Softmax attention core for the training step, with an optional bool mask (mask[i*seqlen + j]
+ * != 0: query i may not see key j; nn.MultiheadAttention attn_mask semantics). Sequences and
+ * rows addressed as dp_attention (row o*so + i*si + t*st; q / k / v columns h*dh of rows ld_q /
+ * ld_kv apart, out ld_o). Saves P f32 [seq][head][key][query] (softmax probabilities) for the
+ * backward. seqlen <= 256, dh <= 64. */
+int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out, int32_t ld_o,
+                float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
+                int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype, void* stream);
+/* Its backward: dq / dk / dv (same addressing as q / k / v, ld_dq / ld_dkv) from dout (ld_o). */
+int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, const float* p_save,
+                const void* dout, int32_t ld_o, void* dq, int32_t ld_dq, void* dk, void* dv, int32_t ld_dkv,
+                int32_t n_outer, int32_t n_inner, int64_t so, int64_t si, int64_t st, int32_t seqlen,
+                int32_t nhead, int32_t dh, int32_t dtype, void* stream);
+
+/* Gate.forward after its Linear (transformer.py:231-235): g = sigmoid(G) saved [rows][2c],
+ * z = g1 * x1 + g2 * x2 with xcat = [x1 | x2] rows of 2c. */
+int dp_gate_fwd(const void* G, const void* xcat, void* g, void* z, int32_t rows, int32_t c, int32_t dtype,
+                void* stream);
+/* Its backward from dz: dG = dg * g (1 - g) (pre-sigmoid) and dxcat = [dz g1 | dz g2] (the
+ * direct path; the Linear's dgrad is added by dp_gemm with beta 1). */
+int dp_gate_bwd(const void* dz, const void* g, const void* xcat, void* dG, void* dxcat, int32_t rows, int32_t c,
+                int32_t dtype, void* stream);
+
+/* Query construction of the training forward (transformer.py:1253-1261, 1278; DN queries of
+ * dn_component.py:132-153): tgt [B][pad + nq][1 + K][c] = DN slots [label_enc[dn_label] |
+ * pose_enc] (zero rows where dn_label < 0), then the matching queries [instance | tgt_embed[q] +
+ * keypoint_embedding]. Weights f32, tgt of dtype. */
+int dp_query_build(const float* tgt_embed, const float* kp_embed, const float* inst_embed, const float* label_enc,
+                   const float* pose_enc, const int32_t* dn_label, int32_t batch, int32_t pad, int32_t nq,
+                   int32_t nkp, int32_t c, void* tgt, int32_t dtype, void* stream);
+/* Its backward: gradients (+=, f32) of the five embedding tables from dtgt. */
+int dp_query_build_bwd(const void* dtgt, const int32_t* dn_label, int32_t batch, int32_t pad, int32_t nq,
+                       int32_t nkp, int32_t c, float* g_tgt_embed, float* g_kp_embed, float* g_inst_embed,
+                       float* g_label_enc, int32_t n_label, float* g_pose_enc, int32_t dtype, void* stream);
+
+/* Backward of dp_pose_refine's keypoint output (Integral softmax . project, distance2pose):
+ * dcorners [rows*nkp][2*(reg_max+1)] f32 (= or += when accumulate) from dkps [rows][nkp][2]. */
+int dp_pose_refine_bwd(const float* corners, const float* project, int32_t reg_max, float reg_scale,
+                       const float* dkps, int32_t rows, int32_t nkp, float* dcorners, int32_t accumulate,
+                       void* stream);
+/* pre_poses = sigmoid(pre + inverse_sigmoid(ref)) backward: dpre = dout * out * (1 - out). Also the
+ * two-stage keypoints sigmoid(delta + anchor) (transformer.py:1243): the same elementwise rule.
+ * out / dout / din f32 with element strides. */
+int dp_sigmoid_bwd(const float* out, const float* dout, float* din, int32_t rows, int32_t n, int64_t ld_out,
+                   int64_t ld_dout, int64_t ld_din, void* stream);
+/* LQE statistics backward (transformer.py:275-285): dkps (+=) [batch*nq][nkp][2] from
+ * dstats [batch*nq][nkp*5] through the top-4 / mean and the bilinear sampling coordinates
+ * (feats[0] is detached). */
+int dp_lqe_stats_bwd(const void* feat, int64_t feat_bstride, int32_t h, int32_t w, int32_t c, const float* kps,
+                     const float* dstats, int32_t batch, int32_t nq, int32_t nkp, float* dkps, int32_t dtype,
+                     void* stream);
+/* dst[idx[b][j]] (+)= src[b][j] rows of c (scatter of gathered rows; idx unique per image):
+ * the backward of dp_gather_rows. src rows contiguous, dst rows ld apart, f32 or dtype. */
+int dp_scatter_rows(const void* src, int32_t ld_src, const int64_t* idx, int32_t batch, int32_t k, int32_t c,
+                    void* dst, int64_t dst_bstride, int32_t ld_dst, int32_t accumulate, int32_t dtype,
+                    void* stream);
+/* dst[b][j] = src[b][idx[b][j]] rows of c, zero where row_mask[idx % mask_period] != 0: the
+ * masked memory rows the two-stage selection picked (memory.masked_fill(valid_mask, 0),
+ * transformer.py:1221), for the enc_output backward on the selected rows only. */
+int dp_gather_rows_masked(const void* src, int64_t src_bstride, const int64_t* idx, const uint8_t* row_mask,
+                          int32_t mask_period, int32_t batch, int32_t k, int32_t c, void* dst, int32_t dtype,
+                          void* stream);
+/* hipMemsetAsync(p, 0, bytes) on the stream (gradient buffers at the start of a step). */
+int dp_zero(void* p, int64_t bytes, void* stream);
+/* Element conversion / copy between f32 and dtype rows (the head outputs' f32 views, gradient
+ * hand-offs): dst[r][j] = src[r][j] (+ dst when accumulate) * scale. */
+int dp_convert_rows(const void* src, int32_t src_dtype, int64_t ld_src, void* dst, int32_t dst_dtype,
+                    int64_t ld_dst, int32_t rows, int32_t n, float scale, int32_t accumulate, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,190 @@
+"""Kernel-level tests of the training-step ops (include/detrpose_hip.h "Training step") against
+torch fp32 autograd of the same op on the same inputs (bf16 storage emulated on the torch side
+where the kernel stores bf16)."""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from detrpose_amd import _lib
+from detrpose_amd._lib import DP_BF16, DP_F32, GemmDesc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CODE = {torch.float32: DP_F32, torch.bfloat16: DP_BF16}
+
+
+def _s():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def gemm(a, a_st, b, b_st, c, c_rs, m, n, k, bias=None, alpha=1.0, beta=0.0, act=0, gate=None, gate_rs=0, split_k=0):
+    lib = _lib.load()
+    d = GemmDesc()
+    d.a, d.a_bs, d.a_rs, d.a_ks = a.data_ptr(), 0, a_st[0], a_st[1]
+    d.b, d.b_bs, d.b_ks, d.b_ns = b.data_ptr(), 0, b_st[0], b_st[1]
+    d.c, d.c_bs, d.c_rs = c.data_ptr(), 0, c_rs
+    d.batch, d.m, d.n, d.k = 1, m, n, k
+    d.in_dtype, d.out_dtype = CODE[a.dtype], CODE[c.dtype]
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.alpha, d.beta, d.act = alpha, beta, act
+    d.gate = gate.data_ptr() if gate is not None else None
+    d.gate_rs = gate_rs
+    d.gate_dtype = CODE[gate.dtype] if gate is not None else 0
+    d.split_k = split_k
+    _lib.check(lib.dp_gemm(C.byref(d), _s()), "dp_gemm")
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("m,n,k", [(300, 72, 256), (64, 64, 64), (1000, 288, 130), (7, 2, 256)])
+def test_gemm_linear_dgrad_wgrad(dt, m, n, k):
+    """y = x W^T + b (+relu), dx = dy W (relu gate), dW += dy^T x (split-K atomics)."""
+    torch.manual_seed(0)
+    x = torch.randn(m, k, device=DEV).to(dt)
+    W = torch.randn(n, k, device=DEV).to(dt)
+    b = torch.randn(n, device=DEV)
+    y = torch.empty(m, n, device=DEV, dtype=torch.float32)
+    gemm(x, (k, 1), W, (1, k), y, n, m, n, k, bias=b, act=1)
+    ref = torch.relu(x.float() @ W.float().t() + b)
+    tol = 1e-4 if dt == torch.float32 else 1e-3
+    assert (y - ref).abs().max() <= tol * max(1.0, ref.abs().max().item())
+    dy = torch.randn(m, n, device=DEV).to(dt)
+    dx = torch.empty(m, k, device=DEV, dtype=dt)
+    gate = torch.randn(m, k, device=DEV).to(dt)
+    gemm(dy, (n, 1), W, (k, 1), dx, k, m, k, n, gate=gate, gate_rs=k)
+    rdx = (dy.float() @ W.float()) * (gate.float() > 0)
+    assert (dx.float() - rdx).abs().max() <= (4e-3 if dt == torch.bfloat16 else 1e-4) * max(1.0, rdx.abs().max().item())
+    dW = torch.ones(n, k, device=DEV)
+    gemm(dy, (1, n), x, (k, 1), dW, k, n, k, m, beta=1.0)
+    rdW = 1.0 + dy.float().t() @ x.float()
+    assert (dW - rdW).abs().max() <= 1e-4 * max(1.0, rdW.abs().max().item())
+
+
+def test_gemm_generic_strides_and_forced_split():
+    torch.manual_seed(1)
+    A = torch.randn(50, 30, device=DEV)[:, ::3]      # (50, 10), strides (30, 3): generic
+    B = torch.randn(10, 70, device=DEV)               # (k, n) row-major: b_ks = 70, b_ns = 1 (mode 1)
+    Cm = torch.zeros(50, 70, device=DEV)
+    gemm(A, (30, 3), B, (70, 1), Cm, 70, 50, 70, 10, beta=1.0, split_k=2)
+    assert torch.allclose(Cm, A @ B, atol=1e-4)
+
+
+def test_layernorm_fwd_bwd():
+    lib = _lib.load()
+    torch.manual_seed(2)
+    rows, c = 333, 256
+    x, r = torch.randn(rows, c, device=DEV), torch.randn(rows, c, device=DEV)
+    g, b = torch.randn(c, device=DEV), torch.randn(c, device=DEV)
+    y = torch.empty(rows, 2 * c, device=DEV)
+    s = torch.empty(rows, c, device=DEV)
+    st = torch.empty(rows, 2, device=DEV)
+    post = torch.randn(rows // 3 * 2, c, device=DEV)
+    _lib.check(lib.dp_ln_fwd(y.data_ptr(), 2 * c, x.data_ptr(), r.data_ptr(), s.data_ptr(), st.data_ptr(), g.data_ptr(),
+                             b.data_ptr(), 1e-5, rows, c, post.data_ptr(), 3, 1, DP_F32, _s()), "ln")
+    xs = (x + r).requires_grad_(True)
+    gg, bb = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = F.layer_norm(xs, (c,), gg, bb, 1e-5)
+    add = torch.zeros(rows, c, device=DEV)
+    sel = torch.arange(rows, device=DEV) % 3 >= 1
+    add[sel] = post
+    assert torch.allclose(y[:, :c], ref + add, atol=1e-4)
+    dy = torch.randn(rows, 2 * c, device=DEV)
+    ref.backward(dy[:, :c])
+    dx = torch.empty(rows, c, device=DEV)
+    dg, db = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
+    _lib.check(lib.dp_ln_bwd(dx.data_ptr(), dy.data_ptr(), 2 * c, s.data_ptr(), st.data_ptr(), g.data_ptr(), rows, c,
+                             dg.data_ptr(), db.data_ptr(), 0, DP_F32, _s()), "ln_bwd")
+    assert torch.allclose(dx, xs.grad, atol=1e-4)
+    assert torch.allclose(dg, gg.grad, atol=1e-3) and torch.allclose(db, bb.grad, atol=1e-3)
+
+
+@pytest.mark.parametrize("L,dh,masked", [(18, 16, False), (96, 32, True), (150, 48, True)])
+def test_attention_fwd_bwd(L, dh, masked):
+    """Across-attention addressing (rows o*so + i*si + t*st) with an attn_mask."""
+    lib = _lib.load()
+    torch.manual_seed(3)
+    nh, B, Ti = 4, 2, 3
+    Cc = nh * dh
+    rows = B * Ti * L
+    qkv = torch.randn(rows, 3 * Cc, device=DEV)
+    mask = (torch.rand(L, L, device=DEV) < 0.3) if masked else torch.zeros(L, L, dtype=torch.bool, device=DEV)
+    mask.fill_diagonal_(False)
+    out = torch.empty(rows, Cc, device=DEV)
+    P = torch.empty(B * Ti * nh * L * L, device=DEV)
+    m8 = mask.to(torch.uint8).contiguous()
+    args = (B, Ti, L * Ti, 1, Ti, L, nh, dh, DP_F32)
+    _lib.check(lib.dp_attn_fwd(qkv.data_ptr(), 3 * Cc, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), 3 * Cc,
+                               out.data_ptr(), Cc, P.data_ptr(), m8.data_ptr() if masked else None, *args, _s()), "attn")
+    # torch reference: sequence (b, i) = rows b*L*Ti + i + t*Ti
+    q = qkv.detach().clone().requires_grad_(True)
+    x = q.view(B, L, Ti, 3, nh, dh).permute(3, 0, 2, 4, 1, 5)   # (3, B, Ti, nh, L, dh)
+    s = (x[0] / dh ** 0.5) @ x[1].transpose(-1, -2)
+    s = s.masked_fill(mask, float("-inf"))
+    o = torch.softmax(s, -1) @ x[2]                               # (B, Ti, nh, L, dh)
+    ref = o.permute(0, 3, 1, 2, 4).reshape(rows, Cc)
+    assert torch.allclose(out, ref, atol=1e-5)
+    dout = torch.randn(rows, Cc, device=DEV)
+    ref.backward(dout)
+    dqkv = torch.empty(rows, 3 * Cc, device=DEV)
+    _lib.check(lib.dp_attn_bwd(qkv.data_ptr(), 3 * Cc, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), 3 * Cc,
+                               P.data_ptr(), dout.data_ptr(), Cc, dqkv.data_ptr(), 3 * Cc, dqkv[:, Cc:].data_ptr(),
+                               dqkv[:, 2 * Cc:].data_ptr(), 3 * Cc, *args, _s()), "attn_bwd")
+    assert torch.allclose(dqkv, q.grad, atol=1e-4), (dqkv - q.grad).abs().max()
+
+
+def test_gate_fwd_bwd():
+    lib = _lib.load()
+    torch.manual_seed(4)
+    rows, c = 100, 64
+    G = torch.randn(rows, 2 * c, device=DEV, requires_grad=True)
+    xc = torch.randn(rows, 2 * c, device=DEV, requires_grad=True)
+    gs, z = torch.empty(rows, 2 * c, device=DEV), torch.empty(rows, c, device=DEV)
+    _lib.check(lib.dp_gate_fwd(G.data_ptr(), xc.data_ptr(), gs.data_ptr(), z.data_ptr(), rows, c, DP_F32, _s()), "g")
+    g = torch.sigmoid(G)
+    ref = g[:, :c] * xc[:, :c] + g[:, c:] * xc[:, c:]
+    assert torch.allclose(z, ref, atol=1e-5)
+    dz = torch.randn(rows, c, device=DEV)
+    ref.backward(dz)
+    dG, dx = torch.empty(rows, 2 * c, device=DEV), torch.empty(rows, 2 * c, device=DEV)
+    _lib.check(lib.dp_gate_bwd(dz.data_ptr(), gs.data_ptr(), xc.data_ptr(), dG.data_ptr(), dx.data_ptr(), rows, c,
+                               DP_F32, _s()), "gb")
+    assert torch.allclose(dG, G.grad, atol=1e-5) and torch.allclose(dx, xc.grad, atol=1e-5)
+
+
+def test_pose_refine_and_lqe_bwd():
+    """Integral + distance2pose backward and the LQE statistics backward vs autograd of the
+    oracle's restatements (transformer.py:238-260, 275-285)."""
+    from oracle.detrpose_cpu import bilinear_gather, weighting_function
+    lib = _lib.load()
+    torch.manual_seed(5)
+    rows, K, reg_max, s = 12, 17, 32, 4.0
+    nb = reg_max + 1
+    corners = torch.randn(rows * K, 2 * nb, device=DEV)
+    proj = weighting_function(reg_max, 0.5, s).to(DEV)
+    ref_init = torch.rand(rows, K, 2, device=DEV)
+    c_ = corners.clone().requires_grad_(True)
+    d = (torch.softmax(c_.reshape(-1, nb), 1) @ proj).reshape(rows, K, 2)
+    kps = ref_init + d / s
+    dk = torch.randn(rows, K, 2, device=DEV)
+    kps.backward(dk)
+    dc = torch.empty_like(corners)
+    _lib.check(lib.dp_pose_refine_bwd(corners.data_ptr(), proj.data_ptr(), reg_max, s, dk.data_ptr(), rows, K,
+                                      dc.data_ptr(), 0, _s()), "refine_bwd")
+    assert torch.allclose(dc, c_.grad, atol=1e-5)
+    # LQE stats backward (feat detached)
+    B, Q, h, w, c = 2, 6, 20, 20, 128
+    feat = torch.randn(B, h, w, c, device=DEV)
+    kp = (torch.rand(B, Q, K, 2, device=DEV) * 1.1 - 0.05).requires_grad_(True)
+    sv = bilinear_gather(feat.cpu(), kp.detach().cpu().reshape(B, Q * K, 2))   # value check helper
+    kpc = kp.detach().cpu().requires_grad_(True)
+    sv = bilinear_gather(feat.cpu(), kpc.reshape(B, Q * K, 2)).reshape(B, Q, K, c)
+    top = sv.topk(4, dim=-1)[0]
+    stat = torch.cat([top, top.mean(-1, keepdim=True)], -1)
+    dstat = torch.randn_like(stat)
+    stat.backward(dstat)
+    dkp = torch.zeros(B, Q, K, 2, device=DEV)
+    _lib.check(lib.dp_lqe_stats_bwd(feat.data_ptr(), h * w * c, h, w, c, kp.detach().contiguous().data_ptr(),
+                                    dstat.to(DEV).contiguous().data_ptr(), B, Q, K, dkp.data_ptr(), DP_F32, _s()),
+               "lqe_bwd")
+    assert torch.allclose(dkp.cpu(), kpc.grad, atol=1e-3), (dkp.cpu() - kpc.grad).abs().max()
