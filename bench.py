@@ -68,6 +68,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-train", action="store_true", help="skip the training-step leg (BASELINE configs[4])")
+    ap.add_argument("--train-batch", type=int, default=16, help="images per GPU of the training-step leg")
+    ap.add_argument("--train-steps", type=int, default=10)
     ap.add_argument("--latency-runs", type=int, default=1000)
     ap.add_argument("--latency-warmup", type=int, default=400)
     ap.add_argument("--profile-ops", type=str, default="", help="write per-op times (JSON) to this path")
@@ -233,6 +236,77 @@ def roofline_report(a, plan, op_ms, op_fn, peak):
                         for k, v in top],
     }
 
+
+
+def synthetic_targets(batch, K=17, seed=3, dev="cuda"):
+    """COCO-shaped synthetic targets: 1-6 persons per image, xyxy boxes, keypoints inside the box
+    with ~75 % visible, normalised area."""
+    g = torch.Generator().manual_seed(seed)
+    ts = []
+    for b in range(batch):
+        n = int(torch.randint(1, 7, (1,), generator=g))
+        c = torch.rand(n, 2, generator=g) * 0.6 + 0.2
+        wh = torch.rand(n, 2, generator=g) * 0.3 + 0.05
+        xy = (c[:, None] + (torch.rand(n, K, 2, generator=g) - 0.5) * wh[:, None]).clamp(0, 1)
+        vis = (torch.rand(n, K, generator=g) > 0.25).float()
+        ts.append({"labels": torch.zeros(n, dtype=torch.int64, device=dev),
+                   "boxes": torch.cat([c - wh / 2, c + wh / 2], 1).to(dev),
+                   "keypoints": torch.cat([xy.flatten(1), vis], 1).to(dev), "area": (wh.prod(1) * 0.53).to(dev)})
+    return ts
+
+
+def train_leg(size, dtype, dev, batch, steps, warmup=3):
+    """BASELINE configs[4] on one GPU, the part that is built: frozen backbone + encoder forward,
+    transformer training forward with OKS-denoising queries, criterion (matching, losses and
+    their gradients), transformer backward, clip_grad_norm_ + AdamW (detrpose_amd.train.Trainer).
+    Per-phase device times from HIP events on the same stream."""
+    from detrpose_amd import build_model
+    from detrpose_amd.synthetic import load_synthetic, synthetic_images
+    from detrpose_amd.train import Trainer
+    model, _ = build_model(size, dtype=dtype)
+    load_synthetic(model, 0)
+    tr = Trainer(model, dtype=dtype, device=dev)
+    images = synthetic_images(batch, seed=11).to(dev)
+    ts = synthetic_targets(batch, dev=dev)
+    for _ in range(warmup):
+        tr.step(images, ts)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        keys, vals = tr.step(images, ts)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    # phase split of one more step (HIP events around each phase)
+    plan = next(iter(tr.eng.plans.values()))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    ev[0].record()
+    tr._memory(images)
+    ev[1].record()
+    plan.forward()
+    ev[2].record()
+    from detrpose_amd.criterion import pack_targets
+    from detrpose_amd.train import dn_meta
+    packed = pack_targets(ts, 17, dev)
+    plan.criterion(packed, packed.sizes, dn_meta(packed.sizes)[1])
+    ev[3].record()
+    plan.backward()
+    ev[4].record()
+    tr.eng.optimizer_step(**tr.opt)
+    ev[5].record()
+    torch.cuda.synchronize()
+    names = ["encoder_fwd (frozen)", "transformer_fwd", "criterion", "transformer_bwd", "clip+adamw"]
+    phases = {n: round(ev[i].elapsed_time(ev[i + 1]), 3) for i, n in enumerate(names)}
+    flops = sum(plan.op_flops.values())
+    t_tr = phases["transformer_fwd"] + phases["transformer_bwd"]
+    return {"workload": f"DETRPose-{size.upper()} training step (BASELINE configs[4] on 1 GPU): frozen backbone + "
+                        f"encoder forward, transformer forward with OKS-denoising queries + criterion (incl. dn_* "
+                        f"losses) + transformer backward + clip_grad_norm_(0.1) + AdamW; {dtype}, batch {batch}, "
+                        f"synthetic targets (1-6 persons per image)",
+            "ms_per_step": round(ms, 3), "images_per_sec": round(batch / ms * 1e3, 2), "steps": steps,
+            "dn_pad": plan.P, "phase_ms": phases,
+            "transformer_gemm_tflops": round(flops / (t_tr * 1e-3) / 1e12, 2) if t_tr > 0 else None,
+            "losses_finite": bool(torch.isfinite(vals).all()),
+            "not_built": "backbone / encoder backward (frozen here), BatchNorm batch statistics"}
 
 
 def latency_bs1(model, pp, dev, runs, warmup):
@@ -432,6 +506,9 @@ def main():
                                          "value": round(v, 2), "unit": "images/sec", "outputs_finite": fin})
                 del ms
                 torch.cuda.empty_cache()
+        if world == 1 and not a.no_train:
+            out["train_step"] = train_leg(a.size, a.dtype, dev, a.train_batch, a.train_steps)
+            torch.cuda.empty_cache()
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.size, a.cpu_baseline_seconds)
         if not finite:

@@ -141,6 +141,9 @@ _SIGS = {
     "dp_gather_rows_masked": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, vp, i32, vp]),
     "dp_convert_rows": (i32, [vp, i32, i64, vp, i32, i64, i32, i32, f32, i32, vp]),
     "dp_zero": (i32, [vp, i64, vp]),
+    "dp_cdn_build": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, i32, f32, f32, C.c_uint64, vp, vp, vp]),
+    "dp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
+    "dp_adamw": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp]),
 }
 
 EXPORTED = tuple(k for k in _SIGS)

@@ -13,9 +13,10 @@ torch.distributed is initialised, criterion.py:306-323), so a criterion call nev
 synchronises with the host.
 
 Scope: the losses of the shipped configs, `['vfl', 'keypoints']` with weight_dict
-{loss_vfl, loss_keypoints, loss_oks} (configs/detrpose/include/detrpose_hgnetv2.py). The
-'labels', 'mal', 'local' and 'matching' losses and the denoising (dn_*) outputs raise
-NotImplementedError. There is no CPU path.
+{loss_vfl, loss_keypoints, loss_oks} (configs/detrpose/include/detrpose_hgnetv2.py), for the
+matched heads and the denoising heads (dn_aux_outputs / dn_aux_pre_outputs with their fixed
+positive matching, criterion.py:385-435). The 'labels', 'mal', 'local' and 'matching' losses
+raise NotImplementedError. There is no CPU path.
 
 Two deliberate departures from matcher.py: (1) the reference drops the keypoint costs of a head
 whose keypoints sum to <= 0 (matcher.py:70-93) and matches on the class cost alone; keypoints
@@ -63,6 +64,7 @@ class PackedTargets:
     area: torch.Tensor     # (T,) f32
     sizes: list
     max_t: int
+    boxes: torch.Tensor = None   # (T, 4) f32 xyxy (the DN queries' centre points) when given
 
 
 def pack_targets(targets, num_body_points: int, device) -> PackedTargets:
@@ -73,11 +75,15 @@ def pack_targets(targets, num_body_points: int, device) -> PackedTargets:
         label = torch.cat([t["labels"].reshape(-1) for t in targets]).to(device=device, dtype=torch.int32)
         kps = torch.cat([t["keypoints"].reshape(-1, K3) for t in targets]).to(device=device, dtype=torch.float32)
         area = torch.cat([t["area"].reshape(-1) for t in targets]).to(device=device, dtype=torch.float32)
+        boxes = (torch.cat([t["boxes"].reshape(-1, 4) for t in targets]).to(device=device, dtype=torch.float32)
+                 if all("boxes" in t for t in targets) else None)
     else:
         label = torch.zeros(1, dtype=torch.int32, device=device)
         kps = torch.zeros(1, K3, dtype=torch.float32, device=device)
         area = torch.ones(1, dtype=torch.float32, device=device)
-    return PackedTargets(off, label.contiguous(), kps.contiguous(), area.contiguous(), sizes, max(sizes or [0]))
+        boxes = torch.zeros(1, 4, dtype=torch.float32, device=device)
+    return PackedTargets(off, label.contiguous(), kps.contiguous(), area.contiguous(), sizes, max(sizes or [0]),
+                         boxes.contiguous() if boxes is not None else None)
 
 
 def _f32_rows(x: torch.Tensor, last: int) -> torch.Tensor:
@@ -200,8 +206,6 @@ class Criterion(nn.Module):
         self.last_match = None   # (match (H, B, Q), go (B, Q), head names) of the last call, for inspection
 
     def forward(self, outputs, targets):
-        if "dn_aux_outputs" in outputs or "dn_meta" in outputs:
-            raise NotImplementedError("denoising queries (prepare_for_cdn, dn_component.py:39-183) are not built")
         assert "aux_outputs" in outputs, ""   # criterion.py:313-314
         # heads in the reference's matching order (criterion.py:290-303)
         names = ["", *[f"_{i}" for i in range(len(outputs["aux_outputs"]))], "_pre",
@@ -256,6 +260,13 @@ class Criterion(nn.Module):
         src = [h["pred_logits"] for h in heads] + [h["pred_keypoints"] for h in heads]
         L = _PoseLoss.apply(run, *src)
         out = {}
+        self._put(out, names, L)
+        if "dn_aux_outputs" in outputs:
+            self._dn_losses(outputs, packed, n_boxes, world, sig, dev, out)
+        return dict(sorted(out.items()))
+
+    def _put(self, out, names, L):
+        wd = self.weight_dict
         for i, n in enumerate(names):
             if "vfl" in self.losses and "loss_vfl" in wd:
                 out["loss_vfl" + n] = L[i, 0]
@@ -264,4 +275,44 @@ class Criterion(nn.Module):
                     out["loss_keypoints" + n] = L[i, 1]
                 if "loss_oks" in wd:
                     out["loss_oks" + n] = L[i, 2]
-        return dict(sorted(out.items()))
+
+    def _dn_losses(self, outputs, packed, n_boxes, world, sig, dev, out):
+        """criterion.py:385-435: vfl + keypoints of every DN head with the fixed positive
+        matching (DN slot g * single_pad + t <-> target t), normalised by num_boxes * groups."""
+        from .train_engine import dn_match
+        meta = outputs["dn_meta"]
+        pad, groups = int(meta["pad_size"]), int(meta["num_dn_group"])
+        heads = [*outputs["dn_aux_outputs"], outputs["dn_aux_pre_outputs"]]
+        names = [*[f"_dn_{i}" for i in range(len(outputs["dn_aux_outputs"]))], "_dn_pre"]
+        K2 = 2 * self.num_body_points
+        logits = [_f32_rows(h["pred_logits"], outputs["pred_logits"].shape[-1]) for h in heads]
+        kps = [_f32_rows(h["pred_keypoints"], K2) for h in heads]
+        H = len(heads)
+        B, Q, ncls = logits[0].shape
+        assert Q == pad, (Q, pad)
+        m = torch.from_numpy(dn_match(packed.sizes, pad, groups)).to(dev)
+        # num_boxes (all-reduced, / world, >= 1) * groups; dp_pose_loss divides by world again
+        n_dn = torch.clamp(n_boxes / world, min=1.0) * groups * world
+        lib = _lib.load()
+        wd = self.weight_dict
+        w_vfl, w_kp, w_oks = (float(wd.get(k, 1.0)) for k in ("loss_vfl", "loss_keypoints", "loss_oks"))
+
+        def run():
+            losses = torch.empty(H, 3, dtype=torch.float32, device=dev)
+            g_lg = torch.empty(H, B, Q, ncls, dtype=torch.float32, device=dev)
+            g_l1 = torch.empty(H, B, Q, K2, dtype=torch.float32, device=dev)
+            g_oks = torch.empty(H, B, Q, K2, dtype=torch.float32, device=dev)
+            hs = (_lib.LossHead * H)()
+            for i in range(H):
+                hs[i] = _lib.LossHead(logits[i].data_ptr(), logits[i].stride(0), logits[i].stride(1), kps[i].data_ptr(),
+                                      kps[i].stride(0), kps[i].stride(1), m.data_ptr())
+            _lib.check(lib.dp_pose_loss(hs, H, B, Q, ncls, self.num_body_points, m.data_ptr(), packed.off.data_ptr(),
+                                        packed.label.data_ptr(), packed.kps.data_ptr(), packed.area.data_ptr(),
+                                        sig.data_ptr(), float(self.focal_alpha), float(self.gamma), n_dn.data_ptr(),
+                                        n_dn.data_ptr(), float(world), w_vfl, w_kp, w_oks, losses.data_ptr(),
+                                        g_lg.data_ptr(), g_l1.data_ptr(), g_oks.data_ptr(), _stream(dev)),
+                       "dp_pose_loss(dn)")
+            return losses, g_lg, g_l1, g_oks
+
+        src = [h["pred_logits"] for h in heads] + [h["pred_keypoints"] for h in heads]
+        self._put(out, names, _PoseLoss.apply(run, *src))

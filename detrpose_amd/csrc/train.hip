@@ -202,11 +202,12 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const T* __restrict__ q, i
   }
 }
 
-// Backward: dV_j = sum_i P_ij dO_i; dS_ij = P_ij (dO_i . V_j - sum_j' P_ij' dO_i . V_j');
-// dQ_i = scale sum_j dS_ij K_j; dK_j = scale sum_i dS_ij Q_i (q read unscaled). dS overwrites P.
+// Backward: dV_j = sum_i P_ij dO_i; dS_ij = P_ij (dO_i . V_j - D_i), D_i = sum_j P_ij dO_i . V_j;
+// dQ_i = scale sum_j dS_ij K_j; dK_j = scale sum_i dS_ij Q_i. P is only read (the step's backward
+// can be replayed); dS is recomputed where it is needed, D_i kept in LDS.
 template <typename T>
 __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, int ldq, const T* __restrict__ k,
-                                                      const T* __restrict__ v, int ldkv, float* __restrict__ psave,
+                                                      const T* __restrict__ v, int ldkv, const float* __restrict__ psave,
                                                       const T* __restrict__ dout, int ldo, T* __restrict__ dq, int lddq,
                                                       T* __restrict__ dk, T* __restrict__ dv, int lddkv, int n_inner,
                                                       int64_t so, int64_t si, int64_t st, int L, int nhead, int dh,
@@ -216,6 +217,7 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
   float* Ks = sm + L * dh;
   float* Vs = sm + 2 * L * dh;
   float* Ds = sm + 3 * L * dh;   // dO
+  float* Dr = sm + 4 * L * dh;   // D_i = sum_j P_ij dP_ij
   const int lane = threadIdx.x;
   const int h = blockIdx.x % nhead;
   const int seq = blockIdx.x / nhead;
@@ -230,8 +232,15 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
     Ds[e] = to_f32(dout[rr * ldo + h * dh + dd]);
   }
   __syncthreads();
-  float* P = psave + (int64_t)blockIdx.x * L * L;
-  // dV (lane = key j), before P is overwritten
+  const float* P = psave + (int64_t)blockIdx.x * L * L;
+  auto dpv = [&](int i, int j) {   // dP_ij = dO_i . V_j
+    float dp = 0.f;
+#pragma unroll
+    for (int dd = 0; dd < ATT_DH; ++dd)
+      if (dd < dh) dp = fmaf(Ds[i * dh + dd], Vs[j * dh + dd], dp);
+    return dp;
+  };
+  // dV (lane = key j)
   for (int j = lane; j < L; j += 64) {
     float acc[ATT_DH];
 #pragma unroll
@@ -247,29 +256,16 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
     for (int dd = 0; dd < ATT_DH; ++dd)
       if (dd < dh) dv[rj * lddkv + h * dh + dd] = from_f32<T>(acc[dd]);
   }
-  __syncthreads();   // every lane's P reads of this block are done before dS overwrites it
-  // dS and dQ (lane = query i)
+  // D and dQ (lane = query i)
   for (int i = lane; i < L; i += 64) {
     float di = 0.f;
-    for (int j = 0; j < L; ++j) {
-      const float p = P[(int64_t)j * L + i];
-      float dp = 0.f;
-#pragma unroll
-      for (int dd = 0; dd < ATT_DH; ++dd)
-        if (dd < dh) dp = fmaf(Ds[i * dh + dd], Vs[j * dh + dd], dp);
-      di = fmaf(p, dp, di);
-    }
+    for (int j = 0; j < L; ++j) di = fmaf(P[(int64_t)j * L + i], dpv(i, j), di);
+    Dr[i] = di;
     float acc[ATT_DH];
 #pragma unroll
     for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
     for (int j = 0; j < L; ++j) {
-      const float p = P[(int64_t)j * L + i];
-      float dp = 0.f;
-#pragma unroll
-      for (int dd = 0; dd < ATT_DH; ++dd)
-        if (dd < dh) dp = fmaf(Ds[i * dh + dd], Vs[j * dh + dd], dp);
-      const float ds = p * (dp - di);
-      P[(int64_t)j * L + i] = ds;
+      const float ds = P[(int64_t)j * L + i] * (dpv(i, j) - di);
 #pragma unroll
       for (int dd = 0; dd < ATT_DH; ++dd)
         if (dd < dh) acc[dd] = fmaf(ds, Ks[j * dh + dd], acc[dd]);
@@ -279,7 +275,6 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
     for (int dd = 0; dd < ATT_DH; ++dd)
       if (dd < dh) dq[ri * lddq + h * dh + dd] = from_f32<T>(acc[dd] * scale);
   }
-  __threadfence_block();
   __syncthreads();
   // dK (lane = key j)
   for (int j = lane; j < L; j += 64) {
@@ -287,7 +282,7 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
 #pragma unroll
     for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
     for (int i = 0; i < L; ++i) {
-      const float ds = P[(int64_t)j * L + i];
+      const float ds = P[(int64_t)j * L + i] * (dpv(i, j) - Dr[i]);
 #pragma unroll
       for (int dd = 0; dd < ATT_DH; ++dd)
         if (dd < dh) acc[dd] = fmaf(ds, Qs[i * dh + dd], acc[dd]);
@@ -554,6 +549,114 @@ __global__ void convert_kernel(const TS* __restrict__ src, int64_t lds, TD* __re
   *p = from_f32<TD>(v);
 }
 
+// ---------------------------------------------------------------- OKS-denoising draws
+// counter-based uniform [0, 1): splitmix64 finaliser of (seed, stream, index)
+__device__ __forceinline__ float urand(uint64_t seed, uint32_t stream, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1) + ((uint64_t)stream << 40);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// one thread per (image, DN slot, point): prepare_for_cdn's noised labels and keypoints
+// (dn_component.py:51-153) for slot = group * single_pad + t, t < targets of the image
+// (even groups positive, odd negative); padding slots get label -1 and ref 0.5.
+__global__ void cdn_build_kernel(const int* __restrict__ off, const int* __restrict__ labels,
+                                 const float* __restrict__ kps, const float* __restrict__ area,
+                                 const float* __restrict__ boxes, const float* __restrict__ sig, int B, int pad,
+                                 int single, int nkp, float label_noise, int num_classes, float img_h, float img_w,
+                                 uint64_t seed, int* __restrict__ dn_label, float* __restrict__ dn_ref) {
+  const int T = nkp + 1;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)B * pad * T) return;
+  const int pt = (int)(e % T);
+  const int64_t bs = e / T;
+  const int slot = (int)(bs % pad), b = (int)(bs / pad);
+  const int g = slot / single, t = slot - g * single;
+  const int n = off[b + 1] - off[b];
+  float* rf = dn_ref + e * 2;
+  if (t >= n) {
+    if (pt == 0) dn_label[bs] = -1;
+    rf[0] = rf[1] = 0.5f;   // sigmoid(0): the zero padding of input_query_pose
+    return;
+  }
+  const int tg = off[b] + t;
+  const uint64_t key = ((uint64_t)g * 1048576ull + (uint64_t)tg) * 64ull;   // (group, target) draw stream
+  if (pt == 0) {
+    int lab = labels[tg];
+    if (urand(seed, 1, key) < label_noise * 0.5f) lab = min((int)(urand(seed, 2, key) * num_classes), num_classes - 1);
+    dn_label[bs] = lab;
+  }
+  // point pt: 0 = centre of the xyxy box (dn_component.py:95), 1..K the keypoints
+  float x, y;
+  bool viz;
+  if (pt == 0) {
+    const float* bx = boxes + (int64_t)tg * 4;
+    x = (bx[0] + bx[2]) * 0.5f;
+    y = (bx[1] + bx[3]) * 0.5f;
+    viz = false;   // the centre is never noised (dn_component.py:104)
+  } else {
+    const float* kp = kps + (int64_t)tg * 3 * nkp;
+    x = kp[2 * (pt - 1)];
+    y = kp[2 * (pt - 1) + 1];
+    viz = kp[2 * nkp + pt - 1] != 0.f;
+  }
+  if (viz) {
+    // direction: normalize(rand_like) (first quadrant, dn_component.py:121-122); distance:
+    // alpha ~ U(0, ln 2) positive / U(ln 2, ln 10) negative, * 2 (area*h*w + eps) var, sqrt, / max(h, w)
+    const float u1 = urand(seed, 3, key + pt), u2 = urand(seed, 4, key + pt);
+    const float nrm = fmaxf(sqrtf(u1 * u1 + u2 * u2), 1e-12f);
+    const float ua = urand(seed, 5, key + pt);
+    const bool neg = g & 1;
+    const float lo = neg ? 0.69314718f : 0.f, hi = neg ? 2.30258509f : 0.69314718f;
+    float alpha = lo + (hi - lo) * ua;
+    const float s2 = 2.f * sig[pt];
+    alpha *= 2.f * (area[tg] * img_h * img_w + 1.1920929e-07f) * s2 * s2;
+    alpha = sqrtf(alpha) / fmaxf(img_h, img_w);
+    x += alpha * u1 / nrm;
+    y += alpha * u2 / nrm;
+  }
+  // inverse_sigmoid (utils.py:133-137) then the sigmoid of transformer.py:1279
+  auto isig = [](float v) {
+    v = fminf(fmaxf(v, 0.f), 1.f);
+    return logf(fmaxf(v, 1e-3f) / fmaxf(1.f - v, 1e-3f));
+  };
+  rf[0] = 1.f / (1.f + expf(-isig(x)));
+  rf[1] = 1.f / (1.f + expf(-isig(y)));
+}
+
+// ---------------------------------------------------------------- optimizer
+__global__ void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* __restrict__ out) {
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    acc = fmaf(g[i], g[i], acc);
+  acc = wave_sum(acc);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) unsafeAtomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+// torch.optim.AdamW step (decoupled weight decay, bias corrections) after
+// clip_grad_norm_(max_norm): g *= min(max_norm / (||g|| + 1e-6), 1) with ||g||^2 from sqnorm
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                             float bc1, float bc2, float max_norm, const float* __restrict__ sq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float scale = 1.f;
+  if (max_norm > 0.f) scale = fminf(max_norm / (sqrtf(*sq) + 1e-6f), 1.f);
+  const float gi = g[i] * scale;
+  float pi = p[i] * (1.f - lr * wd);
+  const float mi = b1 * m[i] + (1.f - b1) * gi;
+  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  pi -= (lr / bc1) * mi / (sqrtf(vi) / sqrtf(bc2) + eps);
+  p[i] = pi;
+}
+
 inline unsigned nblk(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
 // dynamic LDS above 64 KB needs the per-kernel attribute (once per instantiation)
@@ -652,11 +755,11 @@ extern "C" int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const voi
   DP_REQUIRE(q && k && v && p_save && dout && dq && dk && dv, "dp_attn_bwd: null pointer");
   DP_REQUIRE(seqlen > 0 && seqlen <= 256 && dh > 0 && dh <= ATT_DH && seqlen * dh <= 8192,
              "dp_attn_bwd: seqlen %d x dh %d (<= 256, <= 64, product <= 8192)", seqlen, dh);
-  const size_t lds = (size_t)4 * seqlen * dh * 4;
+  const size_t lds = (size_t)(4 * seqlen * dh + seqlen) * 4;
   const float scale = 1.f / sqrtf((float)dh);
   dim3 grid((unsigned)(n_outer * n_inner * nhead));
   hipStream_t s = as_stream(stream);
-  float* P = const_cast<float*>(p_save);   // overwritten with dS (the forward's P is consumed)
+  const float* P = p_save;
   if (lds > 64 * 1024) dtype == DP_BF16 ? allow_lds(attn_bwd_kernel<bf16_t>) : allow_lds(attn_bwd_kernel<float>);
   if (dtype == DP_BF16)
     hipLaunchKernelGGL(attn_bwd_kernel<bf16_t>, grid, dim3(64), lds, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
@@ -826,6 +929,40 @@ extern "C" int dp_convert_rows(const void* src, int32_t src_dtype, int64_t ld_sr
     hipLaunchKernelGGL((convert_kernel<float, float>), grid, block, 0, s, (const float*)src, ld_src, (float*)dst,
                        ld_dst, rows, n, scale, accumulate);
   return dp_check_launch("dp_convert_rows");
+}
+
+extern "C" int dp_cdn_build(const int32_t* tgt_off, const int32_t* tgt_label, const float* tgt_kps,
+                            const float* tgt_area, const float* tgt_boxes, const float* sigmas, int32_t batch,
+                            int32_t pad, int32_t single_pad, int32_t nkp, float label_noise_ratio, int32_t num_classes,
+                            float img_h, float img_w, uint64_t seed, int32_t* dn_label, float* dn_ref, void* stream) {
+  DP_REQUIRE(tgt_off && dn_label && dn_ref && sigmas && batch > 0 && pad > 0 && single_pad > 0 && pad % single_pad == 0,
+             "dp_cdn_build: bad arguments");
+  const int64_t total = (int64_t)batch * pad * (nkp + 1);
+  hipLaunchKernelGGL(cdn_build_kernel, dim3(nblk(total, 256)), dim3(256), 0, as_stream(stream), tgt_off, tgt_label,
+                     tgt_kps, tgt_area, tgt_boxes, sigmas, batch, pad, single_pad, nkp, label_noise_ratio, num_classes,
+                     img_h, img_w, seed, dn_label, dn_ref);
+  return dp_check_launch("dp_cdn_build");
+}
+
+extern "C" int dp_grad_sqnorm(const float* g, int64_t n, float* out, void* stream) {
+  DP_REQUIRE(g && out && n > 0, "dp_grad_sqnorm: bad arguments");
+  hipStream_t s = as_stream(stream);
+  if (hipMemsetAsync(out, 0, 4, s) != hipSuccess) return dp_check_launch("dp_grad_sqnorm");
+  int grid = (int)((n + 255) / 256);
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, s, g, n, out);
+  return dp_check_launch("dp_grad_sqnorm");
+}
+
+extern "C" int dp_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
+                        float beta1, float beta2, float eps, float weight_decay, int32_t step, float max_norm,
+                        const float* grad_sqnorm, void* stream) {
+  DP_REQUIRE(param && grad && exp_avg && exp_avg_sq && n > 0 && step > 0, "dp_adamw: bad arguments");
+  DP_REQUIRE(max_norm <= 0.f || grad_sqnorm, "dp_adamw: clipping needs the gradient's squared norm");
+  const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
+  hipLaunchKernelGGL(adamw_kernel, dim3(nblk(n, 256)), dim3(256), 0, as_stream(stream), param, grad, exp_avg,
+                     exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, bc1, bc2, max_norm, grad_sqnorm);
+  return dp_check_launch("dp_adamw");
 }
 
 extern "C" int dp_zero(void* p, int64_t bytes, void* stream) {

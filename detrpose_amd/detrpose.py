@@ -66,10 +66,13 @@ class DETRPose(nn.Module):
         self._engine = None  # weights changed: repack on next forward
         super()._load_from_state_dict(*args, **kw)
 
-    @torch.no_grad()
     def forward(self, samples, targets=None):
         if self.training:
             return self._forward_train(samples, targets)
+        with torch.no_grad():
+            return self._forward_eval(samples)
+
+    def _forward_eval(self, samples):
         if not samples.is_cuda:
             raise RuntimeError("DETRPose (MI355X) runs on the GPU only: move the images to a HIP device")
         hw = tuple(self.encoder.eval_spatial_size)
@@ -96,21 +99,28 @@ class DETRPose(nn.Module):
             raise ValueError(f"DETRPose expects images (B, 3, {hw[0]}, {hw[1]}), got {tuple(samples.shape)}")
 
     def _forward_train(self, samples, targets):
-        """The training-mode forward's outputs (transformer.py:1219-1385) without denoising:
-        every decoder layer's logits / keypoints / corners (aux_outputs), the first layer's
-        pre head (aux_pre_outputs) and the two-stage selection (aux_interm_outputs), in the
-        reference's dict layout, for Criterion. Values only: there is no backward through the
-        network on this path. Supported: targets=None (the reference's prepare_for_cdn needs
-        targets and .cuda(), dn_component.py:115) and BatchNorm layers in eval mode (frozen
-        BN; train-mode batch statistics / SyncBN are not built)."""
-        if targets is not None:
-            raise NotImplementedError("training forward with targets = OKS-denoising queries (prepare_for_cdn, "
-                                      "dn_component.py:39-183): not built; call with targets=None")
+        """The training-mode forward (transformer.py:1219-1387).
+
+        With targets: the full training forward with OKS-denoising queries through the HIP
+        training step (detrpose_amd.train.train_forward): the reference's output dict incl.
+        dn_aux_outputs / dn_aux_pre_outputs / dn_meta, differentiable w.r.t. the transformer's
+        parameters, so `criterion(outputs, targets)` then `loss.backward()` fills their .grad
+        (src/solver/engine.py:34-60). The backbone and encoder run frozen (their backward is
+        not built: they receive no gradient).
+
+        Without targets: every decoder layer's logits / keypoints / corners (aux_outputs), the
+        first layer's pre head and the two-stage selection, values only (the reference's own
+        non-DN training forward stops at transformer.py:1353).
+
+        BatchNorm layers must be in eval mode (frozen BN); train-mode batch statistics /
+        SyncBN are not built."""
         bn = [n for n, m in self.named_modules() if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.training]
         if bn:
             raise NotImplementedError(f"{len(bn)} BatchNorm layers are in train mode (batch statistics / SyncBN are not "
                                       f"built, e.g. {bn[0]}): put them in eval mode (frozen-BN training)")
         self._check_input(samples)
+        if targets is not None:
+            return self._forward_train_dn(samples, targets)
         eng = self.engine(samples.device)
         plan = eng.plan(samples.shape[0], aux=True)
         with torch.cuda.device(samples.device):
@@ -131,6 +141,18 @@ class DETRPose(nn.Module):
             out["aux_interm_outputs"] = [{"pred_logits": ao["interm_logits"].clone(),
                                           "pred_keypoints": ao["interm_ref"][:, :, 1:].clone().flatten(-2)}]
             out["aux_pre_outputs"] = {"pred_logits": ao["pre_logits"].clone(), "pred_keypoints": refs.clone()}
+        return out
+
+    def _forward_train_dn(self, samples, targets):
+        from .train import Trainer, train_forward
+        dev = samples.device
+        tr = getattr(self, "_trainer", None)
+        if tr is None or tr.device != dev or tr.eng.dtype_name != self.compute_dtype:
+            tr = Trainer(self, dtype=self.compute_dtype, device=dev)
+            object.__setattr__(self, "_trainer", tr)
+        with torch.cuda.device(dev), torch.enable_grad():
+            out = train_forward(tr, samples, targets)
+        tr.steps += 1
         return out
 
 

@@ -1,0 +1,213 @@
+"""One DETRPose training step on the HIP kernels (BASELINE config 5, the transformer half):
+
+    images -> frozen backbone + encoder (the inference plan's launches up to the memory)
+           -> OKS-denoising draws (dp_cdn_build)  -> transformer training forward (TrainPlan)
+           -> Hungarian matching + losses + their gradients (incl. dn_*)
+           -> transformer backward -> gradient all-reduce over RCCL (DDP, when initialised)
+           -> clip_grad_norm_(0.1) + AdamW (two launches over the flat parameter buffer)
+
+Reference: src/solver/engine.py:34-95 (train_one_epoch: model(samples, targets), criterion,
+sum of the loss dict, backward, clip_grad_norm_, optimizer.step), the DN construction of
+src/models/detrpose/dn_component.py:39-183 and DDP's all-reduce (src/misc/dist_utils.py:111-133).
+Scope: the encoder / backbone are frozen here (their backward is not built yet: the encoder
+memory is the transformer's input and receives no gradient); BatchNorm stays in eval mode.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .criterion import COCO_SIGMAS, CROWDPOSE_SIGMAS, pack_targets
+from .train_engine import TrainEngine, _p
+
+
+def dn_meta(sizes, dn_number=20):
+    """dn_component.py:54-63, 113-114: (pad_size, num_dn_group, single_pad) or None."""
+    known = max([int(s) for s in sizes] + [0])
+    if known == 0:
+        return None
+    groups = max((dn_number * 2) // (known * 2), 1)
+    return known * 2 * groups, groups, known
+
+
+def dn_attn_mask(pad, groups, single, nq):
+    """dn_component.py:155-167, the same loop (True = may not attend)."""
+    m = np.zeros((pad + nq, pad + nq), bool)
+    m[pad:, :pad] = True
+    for i in range(groups):
+        r = slice(single * 2 * i, single * 2 * (i + 1))
+        if i == 0:
+            m[r, single * 2 * (i + 1):pad] = True
+        if i == groups - 1:
+            m[r, :single * i * 2] = True
+        else:
+            m[r, single * 2 * (i + 1):pad] = True
+            m[r, :single * 2 * i] = True
+    return m
+
+
+class Trainer:
+    """The training step for a DETRPose module (reference parameter names), dtype 'bf16' or
+    'fp32'. Optimizer: AdamW(lr, betas, weight_decay) + clip_grad_norm_(max_norm), the configs'
+    values by default (configs/detrpose/detrpose_hgnetv2_*.py, include/detrpose_hgnetv2.py)."""
+
+    def __init__(self, model, dtype="bf16", device="cuda", lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4,
+                 max_norm=0.1, dn_number=20, label_noise_ratio=0.5, weights=(2.0, 10.0, 4.0), seed=0):
+        self.model = model
+        self.device = torch.device(device)
+        model.set_dtype(dtype)
+        self.inf = model.engine(self.device)
+        self.eng = TrainEngine(model, dtype, self.device)
+        self.opt = dict(lr=lr, betas=betas, weight_decay=weight_decay, max_norm=max_norm)
+        self.dn_number, self.label_noise_ratio = dn_number, label_noise_ratio
+        self.weights = weights
+        self.seed = seed
+        self.steps = 0
+        K = self.eng.K
+        sig = COCO_SIGMAS if K == 17 else CROWDPOSE_SIGMAS
+        self.dn_sigmas = torch.tensor(np.concatenate([[0.1], sig]).astype(np.float32), device=self.device)
+
+    def _memory(self, images):
+        """The frozen backbone + encoder: the inference plan's launches up to the memory."""
+        B = images.shape[0]
+        plan = self.inf.plan(B)
+        if images.data_ptr() != plan.input.data_ptr():
+            plan.input.copy_(images.to(torch.float32))
+        if not hasattr(plan, "encoder_ops"):
+            first = next(i for i, (n, _, _) in enumerate(plan.ops) if n.startswith("ts."))
+            plan.encoder_ops = plan.ops[:first]
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        for name, fn, args in plan.encoder_ops:
+            rc = fn(*args, s)
+            if rc:
+                _lib.check(rc, name)
+        shapes = [(f.H, f.W) for f in plan.bufs["encoder"]]
+        return plan.bufs["memory"], shapes
+
+    def _draw_dn(self, plan, packed, images, pad, groups, single):
+        """The step's OKS-denoising draws into the plan (dp_cdn_build) and its attention mask."""
+        if not pad:
+            return
+        eng, lib = self.eng, self.eng.lib
+        if packed.boxes is None:
+            raise ValueError("targets need 'boxes' (xyxy) for the denoising queries (dn_component.py:94-95)")
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        h, w = images.shape[-2:]
+        _lib.check(lib.dp_cdn_build(_p(packed.off), _p(packed.label), _p(packed.kps), _p(packed.area),
+                                    _p(packed.boxes), _p(self.dn_sigmas), images.shape[0], pad, single, eng.K,
+                                    self.label_noise_ratio, 80, float(h), float(w),
+                                    (self.seed * 1000003 + self.steps) & 0xFFFFFFFFFFFF, _p(plan.dn_label),
+                                    _p(plan.dn_ref), s), "dp_cdn_build")
+        if getattr(plan, "_mask_key", None) != (pad, groups, single):
+            plan.mask.copy_(torch.from_numpy(dn_attn_mask(pad, groups, single, eng.nq).astype(np.uint8)))
+            plan._mask_key = (pad, groups, single)
+
+    def step(self, images, targets, update=True):
+        """One step; returns (loss names, device tensor of the losses) (sum = the backward's loss)."""
+        eng, lib = self.eng, self.eng.lib
+        B = images.shape[0]
+        K, nq = eng.K, eng.nq
+        memory, shapes = self._memory(images)
+        packed = pack_targets(targets, K, self.device)
+        sizes = packed.sizes
+        meta = dn_meta(sizes, self.dn_number)
+        pad, groups, single = meta if meta else (0, 1, 1)
+        plan = eng.plan(B, pad, shapes, memory=memory)
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        self._draw_dn(plan, packed, images, pad, groups, single)
+        plan.forward()
+        keys, vals = plan.criterion(packed, sizes, groups, weights=self.weights)
+        plan.backward()
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            world = torch.distributed.get_world_size()
+            if world > 1:
+                # DDP: mean of the ranks' gradients (one all-reduce of the flat f32 buffer)
+                torch.distributed.all_reduce(eng.grad_flat)
+                _lib.check(lib.dp_convert_rows(_p(eng.grad_flat), 0, eng.grad_flat.numel(), _p(eng.grad_flat), 0,
+                                               eng.grad_flat.numel(), 1, eng.grad_flat.numel(), 1.0 / world, 0, s),
+                           "grad mean")
+        if update:
+            eng.optimizer_step(**self.opt)
+        self.steps += 1
+        return keys, vals
+
+
+class _TransformerStep(torch.autograd.Function):
+    """The TrainPlan's forward / backward as one autograd node: inputs are the transformer's
+    parameters (so `loss.backward()` lands their gradients in param.grad, as the reference's
+    autograd does), outputs the head tensors of every layer. The backward takes the gradients
+    autograd hands the outputs, runs the recorded backward tape and returns the parameter
+    gradients (copies: the engine's buffer is reused by the next step)."""
+
+    @staticmethod
+    def forward(ctx, trainer, plan, *params):
+        plan.forward()
+        ctx.trainer, ctx.plan = trainer, plan
+        outs = [t.clone() for t in plan.logits] + [t.clone() for t in plan.kps]
+        outs += [plan.pre_logits.clone(), plan.pre_out.clone(), plan.interm_logits.clone(),
+                 plan.ref0[:, :, 1:].clone().flatten(-2)]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        plan, eng = ctx.plan, ctx.trainer.eng
+        L = eng.L
+        dsts = plan.d_logits + plan.d_kps + [plan.d_pre_logits, plan.d_pre_out, plan.d_interm_logits,
+                                             plan.d_interm_kps]
+        with torch.no_grad():
+            for d, g in zip(dsts, grads):
+                if g is None:
+                    d.zero_()
+                else:
+                    d.copy_(g.reshape(d.shape))
+        plan.backward()
+        return (None, None, *[eng.grads[n].clone() for n in eng.pnames])
+
+
+def train_forward(trainer, images, targets):
+    """DETRPose.forward(samples, targets) in training mode (transformer.py:1219-1387): the
+    reference's output dict (final head, aux_outputs, aux_pre_outputs, aux_interm_outputs,
+    dn_aux_outputs, dn_aux_pre_outputs, dn_meta), differentiable w.r.t. the transformer's
+    parameters through _TransformerStep."""
+    eng = trainer.eng
+    model = trainer.model
+    eng.load_weights()          # the module's current parameter values (the user's optimizer owns them)
+    for p in eng.plans.values():
+        p.refresh_constants()
+    B = images.shape[0]
+    K, nq, L = eng.K, eng.nq, eng.L
+    memory, shapes = trainer._memory(images)
+    packed = pack_targets(targets, K, trainer.device)
+    meta = dn_meta(packed.sizes, trainer.dn_number)
+    pad, groups, single = meta if meta else (0, 1, 1)
+    plan = eng.plan(B, pad, shapes, memory=memory)
+    trainer._draw_dn(plan, packed, images, pad, groups, single)
+    params = [p for n, p in model.named_parameters() if n in eng.params]
+    assert len(params) == len(eng.pnames)
+    outs = _TransformerStep.apply(trainer, plan, *params)
+    logits, kps = outs[:L], outs[L:2 * L]
+    pre_lg, pre_kp, int_lg, int_kp = outs[2 * L:]
+    tr = model.transformer
+
+    def head(t_lg, t_kp, sl):
+        return {"pred_logits": t_lg[:, sl], "pred_keypoints": t_kp[:, sl].flatten(-2)}
+
+    m = slice(pad, None)
+    corners = [c.detach().view(B, pad + nq, K, -1) for c in plan.corners]
+    out = {**head(logits[-1], kps[-1], m), "pred_corners": corners[-1][:, m], "ref_points": plan.pre_out[:, m].detach(),
+           "up": tr.up, "reg_scale": tr.reg_scale, "reg_max": tr.reg_max}
+    out["aux_outputs"] = [{**head(logits[l], kps[l], m), "pred_corners": corners[l][:, m],
+                           "ref_points": plan.pre_out[:, m].detach(), "teacher_corners": corners[-1][:, m],
+                           "teacher_logits": logits[-1][:, m].detach()} for l in range(L - 1)]
+    out["aux_interm_outputs"] = [{"pred_logits": int_lg, "pred_keypoints": int_kp}]
+    out["aux_pre_outputs"] = head(pre_lg, pre_kp, m)
+    if pad:
+        d = slice(0, pad)
+        out["dn_aux_outputs"] = [{**head(logits[l], kps[l], d), "pred_corners": corners[l][:, d],
+                                  "ref_points": plan.pre_out[:, d].detach()} for l in range(L)]
+        out["dn_aux_pre_outputs"] = head(pre_lg, pre_kp, d)
+        out["dn_meta"] = {"pad_size": pad, "num_dn_group": groups}
+    return out

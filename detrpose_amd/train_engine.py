@@ -108,51 +108,127 @@ class TrainEngine:
         self.reg_max = tr.reg_max
         self.nb = 2 * (tr.reg_max + 1)
         self.ncls = tr.num_classes
-        # parameter gradients: one f32 arena, views under the reference names
+        # parameters: one f32 master buffer (the optimizer's), gradients and AdamW moments of
+        # the same layout, views under the reference names
         self.pnames = [n for n, p in model.named_parameters() if n.startswith(T_) and p.requires_grad]
         shapes = {n: tuple(p.shape) for n, p in model.named_parameters()}
-        total = sum(int(np.prod(shapes[n])) for n in self.pnames)
-        self.grad_flat = torch.zeros(total, dtype=torch.float32, device=self.device)
-        self.grads = {}
+        # each parameter starts on a 256-byte boundary (16-byte vector loads of any view)
+        sizes = [(int(np.prod(shapes[n])) + 63) // 64 * 64 for n in self.pnames]
+        total = sum(sizes)
+        dev = self.device
+        self.master = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.grad_flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.sqnorm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.opt_step = 0
+        self.grads, self.params = {}, {}
         o = 0
-        for n in self.pnames:
+        for n, sz in zip(self.pnames, sizes):
             k = int(np.prod(shapes[n]))
             self.grads[n] = self.grad_flat[o:o + k].view(shapes[n])
-            o += k
+            self.params[n] = self.master[o:o + k].view(shapes[n])
+            o += sz
         self.load_weights()
         self.plans = {}
 
     # ------------------------------------------------------------------ weights
     def load_weights(self):
-        """(Re)pack the module's current parameters: dtype copies for the GEMMs, f32 for
-        biases / norms / embeddings / the LQE MLP (f32 inputs)."""
+        """Copy the module's parameters into the f32 master and pack: dtype copies for the
+        GEMMs, f32 biases / norms / embeddings / the LQE MLP (f32 inputs). Later calls update
+        every packed buffer IN PLACE (recorded tapes hold their pointers)."""
         sd = {k: v.detach() for k, v in self.model.state_dict().items()}
-        dev, dt = self.device, self.tdtype
-        self.sd32 = {k: v.to(dev, torch.float32).contiguous() for k, v in sd.items() if k.startswith(T_)}
+        dev = self.device
+        with torch.no_grad():
+            for n in self.pnames:
+                self.params[n].copy_(sd[n].to(dev, torch.float32))
+        if getattr(self, "sd32", None) is not None:
+            with torch.no_grad():
+                for k, v in sd.items():
+                    if k.startswith(T_) and k not in self.params and k in self.sd32:
+                        self.sd32[k].copy_(v.to(dev, torch.float32))
+            self.refresh()
+            return
+        self.sd32 = {}
+        for k, v in sd.items():
+            if not k.startswith(T_):
+                continue
+            self.sd32[k] = self.params[k] if k in self.params else v.to(dev, torch.float32).contiguous()
         self.w = {}
         for k, v in self.sd32.items():
             if k.endswith("weight") and v.dim() == 2:
-                self.w[k] = v.to(dt).contiguous()
-        C = self.C
+                self.w[k] = v if self.tdtype == torch.float32 else v.to(self.tdtype).contiguous()
         for l in range(self.L):
             ca = f"{T_}decoder.layers.{l}.cross_attn."
             self.w[ca + "offattn.weight"] = torch.cat([self.sd32[ca + "sampling_offsets.weight"],
-                                                       self.sd32[ca + "attention_weights.weight"]], 0).to(dt).contiguous()
+                                                       self.sd32[ca + "attention_weights.weight"]], 0).to(
+                self.tdtype).contiguous()
             self.sd32[ca + "offattn.bias"] = torch.cat([self.sd32[ca + "sampling_offsets.bias"],
                                                         self.sd32[ca + "attention_weights.bias"]], 0).contiguous()
+        self._derived(sd)
+
+    def _derived(self, sd):
+        """Constants computed from the parameters (the masked-row LN value) and buffers."""
+        dev = self.device
         g, b = self.sd32[T_ + "enc_output_norm.weight"].double(), self.sd32[T_ + "enc_output_norm.bias"].double()
         bias = self.sd32[T_ + "enc_output.bias"].double()
         mr = (bias - bias.mean()) / torch.sqrt(bias.var(unbiased=False) + 1e-5) * g + b
-        self.masked_row = mr.float().contiguous()
-        self.mask_u8 = self.sd32[T_ + "valid_mask"].reshape(-1).to(torch.uint8).contiguous() \
-            if T_ + "valid_mask" in self.sd32 else sd[T_ + "valid_mask"].reshape(-1).to(dev, torch.uint8).contiguous()
+        if getattr(self, "masked_row", None) is None:
+            self.masked_row = mr.float().contiguous()
+        else:
+            self.masked_row.copy_(mr.float())
+        self.mask_u8 = sd[T_ + "valid_mask"].reshape(-1).to(dev, torch.uint8).contiguous()
         self.anchors = sd[T_ + "anchors"].reshape(-1, 2).to(dev, torch.float32).contiguous()
         tr = self.tr
         self.project = weighting_function(tr.reg_max, float(sd[T_ + "up"]), float(sd[T_ + "reg_scale"])).to(
             dev, torch.float32).contiguous()
         self.reg_scale = abs(float(sd[T_ + "reg_scale"]))
         self.dim_t = sd[T_ + "decoder.dim_t"].to(dev, torch.float32).contiguous()
-        assert self.masked_row.shape[0] == C
+
+    def refresh(self, stream=None):
+        """After an optimizer step on the master: the dtype GEMM copies (bf16 mode), the fused
+        offsets | logits weights and the masked-row constant follow the new values (in place:
+        the recorded tapes keep their pointers)."""
+        with torch.no_grad():
+            if self.tdtype != torch.float32:
+                for k, v in self.sd32.items():
+                    if k in self.w and self.w[k] is not v:
+                        self.w[k].copy_(v)
+            for l in range(self.L):
+                ca = f"{T_}decoder.layers.{l}.cross_attn."
+                no = self.sd32[ca + "sampling_offsets.weight"].shape[0]
+                self.w[ca + "offattn.weight"][:no].copy_(self.sd32[ca + "sampling_offsets.weight"])
+                self.w[ca + "offattn.weight"][no:].copy_(self.sd32[ca + "attention_weights.weight"])
+                self.sd32[ca + "offattn.bias"][:no].copy_(self.sd32[ca + "sampling_offsets.bias"])
+                self.sd32[ca + "offattn.bias"][no:].copy_(self.sd32[ca + "attention_weights.bias"])
+            g, b = self.sd32[T_ + "enc_output_norm.weight"].double(), self.sd32[T_ + "enc_output_norm.bias"].double()
+            bias = self.sd32[T_ + "enc_output.bias"].double()
+            self.masked_row.copy_(((bias - bias.mean()) / torch.sqrt(bias.var(unbiased=False) + 1e-5) * g + b).float())
+        for p in self.plans.values():
+            p.refresh_constants()
+
+    def optimizer_step(self, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4, max_norm=0.1):
+        """clip_grad_norm_(max_norm) + AdamW over every transformer parameter (src/solver/
+        engine.py:78-89, configs: AdamW lr 1e-4, wd 1e-4, clip 0.1) on the flat buffers: two
+        launches, no host synchronisation."""
+        lib = self.lib
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        n = self.master.numel()
+        self.opt_step += 1
+        if max_norm and max_norm > 0:
+            _lib.check(lib.dp_grad_sqnorm(_p(self.grad_flat), n, _p(self.sqnorm), s), "dp_grad_sqnorm")
+        _lib.check(lib.dp_adamw(_p(self.master), _p(self.grad_flat), _p(self.exp_avg), _p(self.exp_avg_sq), n, lr,
+                                betas[0], betas[1], eps, weight_decay, self.opt_step,
+                                max_norm if max_norm else 0.0, _p(self.sqnorm), s), "dp_adamw")
+        self.refresh()
+
+    def state_dict_update(self, module=None):
+        """Write the master parameters back into the module (reference names)."""
+        module = module or self.model
+        with torch.no_grad():
+            for n, p in module.named_parameters():
+                if n in self.params:
+                    p.copy_(self.params[n].to(p.device, p.dtype))
 
     # ------------------------------------------------------------------ launch helpers
     def _gemm(self, tape, name, a, a_rs, a_ks, b, b_ks, b_ns, c, c_rs, m, n, k, in_code, out_code, bias=None,
@@ -207,22 +283,25 @@ class TrainEngine:
             self.cur.cost(name + ".db", 4.0 * rows * N)
 
     # ------------------------------------------------------------------ plan
-    def plan(self, batch: int, pad: int, shapes) -> "TrainPlan":
-        key = (batch, pad, tuple(tuple(s) for s in shapes))
+    def plan(self, batch: int, pad: int, shapes, memory=None) -> "TrainPlan":
+        """memory: an existing (B, S, C) device buffer of dtype the plan reads the encoder memory
+        from (e.g. the inference plan's), instead of its own input buffer."""
+        key = (batch, pad, tuple(tuple(s) for s in shapes), memory.data_ptr() if memory is not None else None)
         if key not in self.plans:
-            self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes])
+            self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes], memory)
         return self.plans[key]
 
 
 class TrainPlan:
     """Buffers and tapes for one (batch, DN pad size, feature shapes)."""
 
-    def __init__(self, eng: TrainEngine, B: int, P: int, shapes):
+    def __init__(self, eng: TrainEngine, B: int, P: int, shapes, memory=None):
         self.eng = eng
         eng.cur = self
         self.B, self.P, self.shapes = B, P, shapes
         self.op_flops = {}
         self.arena = []
+        self._derived = []   # (buffer, parameter) pairs derived from parameters (refresh_constants)
         lib = eng.lib
         Cc, nh, nq, K, T, L, F = eng.C, eng.nh, eng.nq, eng.K, eng.T, eng.L, eng.F
         dt, code = eng.tdtype, eng.code
@@ -246,7 +325,11 @@ class TrainPlan:
             return buf(*shape, dtype=torch.float32)
 
         # ---------------- inputs
-        self.memory = buf(B, S, Cc)
+        if memory is not None:
+            assert memory.dtype == dt and memory.numel() == B * S * Cc and memory.is_contiguous()
+            self.memory = memory.view(B, S, Cc)
+        else:
+            self.memory = buf(B, S, Cc)
         self.dn_label = torch.full((B, max(P, 1)), -1, dtype=torch.int32, device=dev)
         self.dn_ref = f32(B, max(P, 1), T, 2)
         self.mask = torch.zeros(Qt, Qt, dtype=torch.uint8, device=dev)
@@ -415,6 +498,7 @@ class TrainPlan:
             w1 = sd[qe + "1.weight"]
             b2 = sd[qe + "1.bias"].repeat(eng.ncls).contiguous()
             self.arena.append(b2)
+            self._derived.append((b2, qe + "1.bias"))
             eng._gemm(fw, n + ".lqe1", _p(hq), nhid, 1, _p(w1), 1, 0, _p(logits[l]), eng.ncls, qrows, eng.ncls, nhid,
                       DP_F32, DP_F32, bias=_p(b2), beta=1.0)
             S_.update(se=se, ph=ph, pos=pos, x0=x0, qkv_w=qkv_w, att_w=att_w, P_w=P_w, x1=x1, s_w=s_w, st_w=st_w,
@@ -511,7 +595,9 @@ class TrainPlan:
         s = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         chk = _lib.check
         self.heads_pack()
-        sig = torch.tensor(COCO_SIGMAS if K == 17 else CROWDPOSE_SIGMAS, device=dev)
+        if getattr(self, "_sig", None) is None:
+            self._sig = torch.tensor(COCO_SIGMAS if K == 17 else CROWDPOSE_SIGMAS, device=dev)
+        sig = self._sig
         max_t = max([int(v) for v in sizes] + [1])
         chk(lib.dp_hungarian_match(_p(self.hl), B * nq * ncls, nq * ncls, ncls, ncls, _p(self.hk), B * nq * 2 * K,
                                    nq * 2 * K, 2 * K, K, _p(packed.off), _p(packed.label), _p(packed.kps),
@@ -519,27 +605,35 @@ class TrainPlan:
                                    _p(self.match), None, s), "dp_hungarian_match")
         chk(lib.dp_match_union(_p(self.match), H, B, nq, _p(self.go), _p(self.n_go), s), "dp_match_union")
         self.n_boxes.fill_(float(max(sum(sizes), 0)))
+        world = 1
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            # criterion.py:306-323: num_boxes / num_boxes_go summed over the ranks
+            torch.distributed.all_reduce(self.n_boxes)
+            torch.distributed.all_reduce(self.n_go)
+            world = torch.distributed.get_world_size()
         heads = (_lib.LossHead * H)()
         for h in range(H):
             heads[h] = _lib.LossHead(_p(self.hl[h]), nq * ncls, ncls, _p(self.hk[h]), nq * 2 * K, 2 * K,
                                      _p(self.match[h]))
         chk(lib.dp_pose_loss(heads, H, B, nq, ncls, K, _p(self.go), _p(packed.off), _p(packed.label), _p(packed.kps),
-                             _p(packed.area), _p(sig), alpha, gamma, _p(self.n_boxes), _p(self.n_go), 1.0, weights[0],
+                             _p(packed.area), _p(sig), alpha, gamma, _p(self.n_boxes), _p(self.n_go), float(world),
+                             weights[0],
                              weights[1], weights[2], _p(self.losses), _p(self.g_lg), _p(self.g_l1), _p(self.g_oks), s),
             "dp_pose_loss")
         names = ["", *[f"_{i}" for i in range(L - 1)], "_pre", "_enc_0"]
         if P:
             Hd = self.Hd
             self.dn_m.copy_(torch.from_numpy(dn_match(sizes, P, num_group)))
-            # num_boxes (clamped to >= 1, criterion.py:316-322) * num_dn_group (criterion.py:406)
-            self.n_dn.fill_(max(float(sum(sizes)), 1.0) * num_group)
+            # num_boxes (all-reduced, / world, clamped to >= 1: criterion.py:316-322) * num_dn_group
+            # (criterion.py:406); dp_pose_loss divides by `world` again, so pass it pre-multiplied
+            self.n_dn.copy_(torch.clamp(self.n_boxes / world, min=1.0) * num_group * world)
             dheads = (_lib.LossHead * Hd)()
             for h in range(Hd):
                 dheads[h] = _lib.LossHead(_p(self.dl[h]), P * ncls, ncls, _p(self.dk[h]), P * 2 * K, 2 * K,
                                           _p(self.dn_m))
             chk(lib.dp_pose_loss(dheads, Hd, B, P, ncls, K, _p(self.dn_m), _p(packed.off), _p(packed.label),
                                  _p(packed.kps), _p(packed.area), _p(sig), alpha, gamma, _p(self.n_dn), _p(self.n_dn),
-                                 1.0, weights[0], weights[1], weights[2], _p(self.dn_losses), _p(self.dg_lg),
+                                 float(world), weights[0], weights[1], weights[2], _p(self.dn_losses), _p(self.dg_lg),
                                  _p(self.dg_l1), _p(self.dg_oks), s), "dp_pose_loss(dn)")
         # ---- hand-off: d loss_total / d head outputs
         order = [L - 1] + list(range(L - 1))
@@ -829,6 +923,19 @@ class TrainPlan:
             self.dn_label.copy_(torch.as_tensor(dn["label"], dtype=torch.int32))
             self.dn_ref.copy_(torch.sigmoid(torch.as_tensor(dn["pose_unsig"], dtype=torch.float32)))
             self.mask.copy_(torch.as_tensor(dn["attn_mask"]).to(torch.uint8))
+
+    def set_dn(self, dn_label, dn_ref, mask):
+        """DN draws already on the device (dp_cdn_build): dn_label (B, pad) int32, dn_ref
+        (B, pad, 1+K, 2) f32 reference points, mask (Qt, Qt) uint8."""
+        if self.P:
+            self.dn_label.copy_(dn_label)
+            self.dn_ref.copy_(dn_ref)
+            self.mask.copy_(mask)
+
+    def refresh_constants(self):
+        with torch.no_grad():
+            for buf_, key in self._derived:
+                buf_.copy_(self.eng.sd32[key].repeat(buf_.numel() // self.eng.sd32[key].numel()))
 
     def forward(self, debug=None):
         self.fw.run(debug=debug)

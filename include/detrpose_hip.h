@@ -452,7 +452,8 @@ int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, float* out, in
 int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out, int32_t ld_o,
                 float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
                 int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype, void* stream);
-/* Its backward: dq / dk / dv (same addressing as q / k / v, ld_dq / ld_dkv) from dout (ld_o). */
+/* Its backward: dq / dk / dv (same addressing as q / k / v, ld_dq / ld_dkv) from dout (ld_o);
+ * p_save is only read (the backward can be replayed on the same forward). */
 int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, const float* p_save,
                 const void* dout, int32_t ld_o, void* dq, int32_t ld_dq, void* dk, void* dv, int32_t ld_dkv,
                 int32_t n_outer, int32_t n_inner, int64_t so, int64_t si, int64_t st, int32_t seqlen,
@@ -506,6 +507,27 @@ int dp_scatter_rows(const void* src, int32_t ld_src, const int64_t* idx, int32_t
 int dp_gather_rows_masked(const void* src, int64_t src_bstride, const int64_t* idx, const uint8_t* row_mask,
                           int32_t mask_period, int32_t batch, int32_t k, int32_t c, void* dst, int32_t dtype,
                           void* stream);
+/* prepare_for_cdn's random part (dn_component.py:51-153) on the device: for DN slot
+ * group * single_pad + t (t < targets of the image; even groups positive, odd negative) the
+ * target's label, replaced with probability label_noise_ratio / 2 by a uniform class <
+ * num_classes, and its 1 + K points (xyxy-box centre, keypoints) with visible keypoints moved
+ * along a first-quadrant unit direction by sqrt(alpha * 2 (area h w + eps) (2 sigma)^2) / max(h, w),
+ * alpha ~ U(0, ln 2) (positive) / U(ln 2, ln 10) (negative); out dn_label [B][pad] (-1 padding)
+ * and dn_ref [B][pad][1+K][2] = sigmoid(inverse_sigmoid(point)) (0.5 padding). sigmas [1+K]
+ * (0.1 for the centre, then the keypoint sigmas). Counter-based RNG (seed): the draws are
+ * distributed as the reference's torch.rand draws, not the same numbers. */
+int dp_cdn_build(const int32_t* tgt_off, const int32_t* tgt_label, const float* tgt_kps, const float* tgt_area,
+                 const float* tgt_boxes, const float* sigmas, int32_t batch, int32_t pad, int32_t single_pad,
+                 int32_t nkp, float label_noise_ratio, int32_t num_classes, float img_h, float img_w, uint64_t seed,
+                 int32_t* dn_label, float* dn_ref, void* stream);
+/* Squared L2 norm of a gradient buffer (f32 scalar out, zeroed here): clip_grad_norm_'s norm. */
+int dp_grad_sqnorm(const float* g, int64_t n, float* out, void* stream);
+/* torch.optim.AdamW step over a flat f32 parameter buffer (decoupled weight decay, bias
+ * correction for `step`), after clip_grad_norm_(max_norm) (src/solver/engine.py:78-89) read
+ * from grad_sqnorm on the device (max_norm <= 0: no clipping). */
+int dp_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
+             float beta2, float eps, float weight_decay, int32_t step, float max_norm, const float* grad_sqnorm,
+             void* stream);
 /* hipMemsetAsync(p, 0, bytes) on the stream (gradient buffers at the start of a step). */
 int dp_zero(void* p, int64_t bytes, void* stream);
 /* Element conversion / copy between f32 and dtype rows (the head outputs' f32 views, gradient

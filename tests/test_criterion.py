@@ -107,7 +107,7 @@ def test_criterion_scope_errors():
     with pytest.raises(NotImplementedError):
         Criterion(2, m, {"loss_vfl": 2.0}, ["vfl", "local"], 17)
     c = Criterion(2, m, {"loss_vfl": 2.0}, ["vfl"], 17)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(AssertionError):   # criterion.py:313-314: the aux heads are required
         c({"pred_logits": None, "dn_meta": {}}, [])
     with pytest.raises(NotImplementedError):
         HungarianMatcher(num_body_points=5)

@@ -70,8 +70,9 @@ def test_train_forward_refusals(golden_dir):
     with pytest.raises(NotImplementedError):
         model(img)
     _frozen_bn_train(model)
-    with pytest.raises(NotImplementedError):   # targets -> denoising queries
-        model(img, [{"labels": torch.zeros(1, dtype=torch.int64), "keypoints": torch.rand(1, 51)}])
+    with pytest.raises(ValueError):   # targets -> denoising queries, which need the xyxy boxes
+        model(img, [{"labels": torch.zeros(1, dtype=torch.int64).cuda(), "keypoints": torch.rand(1, 51).cuda(),
+                     "area": torch.rand(1).cuda()}])
 
 
 def test_train_forward_bf16_and_criterion(golden_dir):
@@ -96,3 +97,51 @@ def test_train_forward_bf16_and_criterion(golden_dir):
     assert len(losses) == 3 * (1 + 5 + 1 + 1)
     vals = torch.stack(list(losses.values()))
     assert torch.isfinite(vals).all() and (vals >= 0).all()
+
+
+def test_train_forward_with_targets_autograd(golden_dir):
+    """The reference's training loop on the drop-in API (src/solver/engine.py:34-60):
+    outputs = model(samples, targets) with OKS-denoising queries, loss = sum(criterion(outputs,
+    targets).values()), loss.backward() -> every transformer parameter has a .grad, equal to the
+    training plan's own gradient for the same DN draws (the autograd glue hands the Criterion's
+    gradients to the recorded backward unchanged)."""
+    from detrpose_amd.criterion import Criterion, HungarianMatcher, pack_targets
+    model = _model(golden_dir, "n", 0, "fp32").cuda()
+    _frozen_bn_train(model)
+    img = synthetic_images(2, seed=1).cuda()
+    gen = torch.Generator().manual_seed(4)
+    targets = []
+    for n in (3, 2):
+        c = torch.rand(n, 2, generator=gen) * 0.6 + 0.2
+        wh = torch.rand(n, 2, generator=gen) * 0.3 + 0.05
+        kp = torch.cat([torch.rand(n, 34, generator=gen), (torch.rand(n, 17, generator=gen) > 0.3).float()], 1)
+        targets.append({"labels": torch.tensor([i % 2 for i in range(n)]).cuda(), "keypoints": kp.cuda(),
+                        "boxes": torch.cat([c - wh / 2, c + wh / 2], 1).cuda(), "area": (wh.prod(1) * 0.53).cuda()})
+    crit = Criterion(2, HungarianMatcher(2.0, 0.25, 10.0, 4.0), {"loss_vfl": 2.0, "loss_keypoints": 10.0,
+                                                                 "loss_oks": 4.0}, ["vfl", "keypoints"], 17)
+    out = model(img, targets)
+    assert out["dn_meta"] == {"pad_size": 36, "num_dn_group": 6}   # 3 targets at most: 40 // 6 groups
+    assert len(out["dn_aux_outputs"]) == 3 and out["dn_aux_outputs"][0]["pred_logits"].shape == (2, 36, 2)
+    losses = crit(out, targets)
+    assert len(losses) == 27 and any(k.endswith("_dn_pre") for k in losses)
+    loss = sum(losses.values())
+    assert torch.isfinite(loss)
+    loss.backward()
+    tr = model._trainer
+    names = [n for n, p in model.named_parameters() if n.startswith("transformer.") and p.requires_grad]
+    assert all(dict(model.named_parameters())[n].grad is not None for n in names)
+    # the plan's own hand-off on the same draws
+    plan = next(p for p in tr.eng.plans.values() if p.P == 36)
+    packed = pack_targets(targets, 17, img.device)
+    keys, vals = plan.criterion(packed, packed.sizes, 6)
+    ref_losses = dict(zip(keys, vals.cpu().tolist()))
+    for k, v in losses.items():
+        assert abs(float(v) - ref_losses[k]) <= 1e-5 * max(1.0, abs(ref_losses[k])), k
+    plan.backward()
+    torch.cuda.synchronize()
+    params = dict(model.named_parameters())
+    rows = sorted(((float((params[n].grad - tr.eng.grads[n]).abs().max()) /
+                    max(float(tr.eng.grads[n].abs().max()), 1e-12), n, float(tr.eng.grads[n].abs().max()),
+                    float(params[n].grad.abs().max())) for n in names), reverse=True)
+    print("autograd vs plan gradient: worst relative differences", rows[:6])
+    assert rows[0][0] <= 1e-5

@@ -91,3 +91,15 @@ def test_oracle_dn_gradients_match_reference(dn_case):
         assert err <= 1e-4, (k, err)
     worst.sort(reverse=True)
     print("worst relative gradient errors:", worst[:5])
+
+
+def test_dn_meta_and_attn_mask_match_reference(golden_dir):
+    """detrpose_amd.train.dn_meta / dn_attn_mask (dn_component.py:54-63, 113-114, 155-167)
+    reproduce the reference's pad size, group count and attention mask."""
+    from detrpose_amd.train import dn_attn_mask, dn_meta
+    g = np.load(os.path.join(golden_dir, "train_dn_n_b2.npz"))
+    pad, groups, single = dn_meta([int(v) for v in g["sizes"]])
+    assert pad == int(g["dn_pad_size"]) and groups == int(g["dn_num_group"])
+    np.testing.assert_array_equal(dn_attn_mask(pad, groups, single, 60), g["dn_attn_mask"])
+    assert dn_meta([0, 0]) is None
+    assert dn_meta([25, 3])[:2] == (50, 1)   # more targets than dn_number: one group
