@@ -226,58 +226,36 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
       pbase = pbase0;
     }
 
-    // one K-step; the first of a tile starts the MFMA chain from a zero C operand
-    auto step = [&](int kt, auto first_tag) {
-      constexpr bool FIRST = decltype(first_tag)::value;
-      const char* wsl;
-      if (RESW) {
-        wsl = wbase + kt * BN * 128;
-      } else {
-        if (!FIRST) {
-          if (!(DP_HALO_ABL & 1)) wait_vmcnt<0>();
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (!(DP_HALO_ABL & 2)) __builtin_amdgcn_s_barrier();
-        }
-        if (kt + 1 < nk) issue_w(kt + 1, wbase + ((kt + 1) & 1) * BN * 128);
-        wsl = wbase + (kt & 1) * BN * 128;
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    // pixel fragments of K-step kt from the patch (this lane's 8 channels of k = 64 kt + 32 ks
+    // + 8 g -> tap, channel); the patch is complete for the whole tile, so step kt+1's are
+    // read during step kt, before its barrier: after a barrier only the weight fragments wait
+    auto tab_e = [&](int kt, int (&te)[2]) {
+#if DP_HALO_TAB
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) te[ks] = tab[kt * 8 + 4 * ks + g];
+#else
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int cc = 4 * ks + g;
-        // this lane's 8 channels of K: k = kt*64 + 32 ks + 8 g -> (tap, ci)
-#if DP_HALO_TAB
-        const int te = tab[kt * 8 + cc];
-        const int toff = te & 127, c8 = (te >> 7) & 7;
-        const char* pl = pbase + (te >> 10) * Gm::PLANE;
-#else
-        const int k = kt * 64 + cc * 8;
+        const int k = kt * 64 + (4 * ks + g) * 8;
         int tap = (unsigned)k / (unsigned)cin;
         int ci = k - tap * cin;
         if (tap >= ktaps) tap = 0, ci = 0;           // kpad tail: weights are zero there
         const int ky = tap / KW, kx = tap - ky * KW;
-        const int toff = ky * Gm::PW + kx;
-        const char* pl = pbase + (ci >> 6) * Gm::PLANE;
-        const int c8 = (ci >> 3) & 7;
+        te[ks] = (ky * Gm::PW + kx) | (((ci >> 3) & 7) << 7) | ((ci >> 6) << 10);
+      }
 #endif
-        bf16x8 wf[TN], pf[TM];
+    };
+    auto read_pf = [&](const int (&te)[2], bf16x8 (&pf)[2][TM]) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int r = 16 * j + (lane & 15);
-          wf[j] = *reinterpret_cast<const bf16x8*>(wsl + r * 128 + ((cc ^ (r & 7)) << 4));
-        }
+      for (int ks = 0; ks < 2; ++ks) {
+        const int toff = te[ks] & 127, c8 = (te[ks] >> 7) & 7;
+        const char* pl = pbase + (te[ks] >> 10) * Gm::PLANE;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int yq = wm * TM + i;
           const int pr = yq * S * Gm::PW + q * S + toff;
-          pf[i] = *reinterpret_cast<const bf16x8*>(pl + pr * 128 + ((c8 ^ (pr & 7)) << 4));
+          pf[ks][i] = *reinterpret_cast<const bf16x8*>(pl + pr * 128 + ((c8 ^ (pr & 7)) << 4));
         }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                wf[j], pf[i], (FIRST && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
       }
     };
     if constexpr (NKC > 0) {
@@ -304,8 +282,59 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
         }
       }
     } else {
-      step(0, std::true_type{});
-      for (int kt = 1; kt < nk; ++kt) step(kt, std::false_type{});
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // tap-table entries two K-steps ahead, pixel fragments one step ahead
+      bf16x8 pfc[2][TM], pfn[2][TM];
+      int te[2];
+      tab_e(0, te);
+      read_pf(te, pfc);
+      tab_e(nk > 1 ? 1 : 0, te);
+      for (int kt = 0; kt < nk; ++kt) {
+        const char* wsl;
+        if (RESW) {
+          wsl = wbase + kt * BN * 128;
+        } else {
+          if (kt > 0) {
+            if (!(DP_HALO_ABL & 1)) wait_vmcnt<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (!(DP_HALO_ABL & 2)) __builtin_amdgcn_s_barrier();
+          }
+          if (kt + 1 < nk) issue_w(kt + 1, wbase + ((kt + 1) & 1) * BN * 128);
+          wsl = wbase + (kt & 1) * BN * 128;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 wf[2][TN];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int r = 16 * j + (lane & 15);
+            wf[ks][j] = *reinterpret_cast<const bf16x8*>(wsl + r * 128 + (((4 * ks + g) ^ (r & 7)) << 4));
+          }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0][j], pfc[0][i], acc[i][j], 0, 0, 0);
+        // unconditional (the last steps re-read valid entries): a branch here would merge the
+        // wait-count states and make the MFMAs below wait for these reads
+        __builtin_amdgcn_sched_barrier(0);   // keep these reads between the two MFMA groups
+        read_pf(te, pfn);
+        tab_e(kt + 2 < nk ? kt + 2 : nk - 1, te);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1][j], pfc[1][i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) pfc[ks][i] = pfn[ks][i];
+      }
     }
     if constexpr (EARLY) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
