@@ -236,3 +236,102 @@ def losses(res, sizes, tgt_labels, tgt_kps, tgt_area, K, ncls, weights=(2.0, 10.
             out["loss_keypoints" + n] = weights[1] * l1
             out["loss_oks" + n] = weights[2] * lo
     return dict(sorted(out.items())), matches, go
+
+
+# ----------------------------------------------------------------------------- encoder (training)
+
+def _bn_train(x, P, p, stats=None):
+    """nn.BatchNorm2d in training mode (hybrid_encoder.py:68, 124): batch statistics over
+    (N, H, W), biased variance for the normalisation; running statistics updated with momentum
+    0.1 and the unbiased variance (F.batch_norm). stats: name -> running tensor (updated in
+    place) or None."""
+    rm = rv = None
+    if stats is not None:
+        rm, rv = stats[p + ".running_mean"], stats[p + ".running_var"]
+    return F.batch_norm(x, rm, rv, P[p + ".weight"], P[p + ".bias"], True, 0.1, 1e-5)
+
+
+def _act(x, name):
+    if name is None:
+        return x
+    return {"relu": F.relu, "silu": F.silu, "gelu": F.gelu}[name](x)
+
+
+def _conv_norm_t(x, P, p, stats, stride=1, groups=1, act=None):
+    """ConvNormLayer_fuse.forward before deploy (hybrid_encoder.py:100-128), training mode."""
+    w = P[p + ".conv.weight"]
+    k = w.shape[-1]
+    x = F.conv2d(x, w, P.get(p + ".conv.bias"), stride, (k - 1) // 2, 1, groups)
+    return _act(_bn_train(x, P, p + ".norm", stats), act)
+
+
+def _vgg_t(x, P, p, stats, act):
+    """VGGBlock.forward, training (hybrid_encoder.py:139-154): act(BN(conv3x3) + BN(conv1x1))."""
+    return _act(_conv_norm_t(x, P, p + ".conv1", stats) + _conv_norm_t(x, P, p + ".conv2", stats), act)
+
+
+def _csp_t(x, P, p, stats, nblk, act):
+    """CSPLayer.forward (hybrid_encoder.py:215-240)."""
+    x1 = _conv_norm_t(x, P, p + ".conv1", stats, act=act)
+    for i in range(nblk):
+        x1 = _vgg_t(x1, P, f"{p}.bottlenecks.{i}", stats, act)
+    return x1 + _conv_norm_t(x, P, p + ".conv2", stats, act=act)
+
+
+def _elan_t(x, P, p, stats, nblk, act="silu"):
+    """RepNCSPELAN4.forward (hybrid_encoder.py:192-212)."""
+    y = _conv_norm_t(x, P, p + ".cv1", stats, act=act)
+    c = y.shape[1] // 2
+    ys = [y[:, :c], y[:, c:]]
+    z = _csp_t(ys[-1], P, p + ".cv2.0", stats, nblk, act)
+    ys.append(_conv_norm_t(z, P, p + ".cv2.1", stats, act=act))
+    z = _csp_t(ys[-1], P, p + ".cv3.0", stats, nblk, act)
+    ys.append(_conv_norm_t(z, P, p + ".cv3.1", stats, act=act))
+    return _conv_norm_t(torch.cat(ys, 1), P, p + ".cv4", stats, act=act)
+
+
+def train_encoder(feats, P, cfg, stats=None):
+    """HybridEncoder.forward in training mode (hybrid_encoder.py:462-507): BatchNorm2d on batch
+    statistics (sync_bn over one process), the AIFI TransformerEncoderLayer (270-296, post-norm,
+    dropout 0), FPN / PAN as oracle.detrpose_cpu.encoder. feats: backbone outputs (leaves or
+    detached); P: name -> tensor, encoder parameters as autograd leaves; stats: running
+    statistics updated in place (optional)."""
+    from oracle.detrpose_cpu import sine_pos_embed_2d
+    C = cfg["hidden_dim"]
+    nlev = cfg["n_levels"]
+    nblk = round(3 * cfg["depth_mult"])
+    enc_idx = cfg.get("use_encoder_idx", [2])
+    E = "encoder."
+    proj = [_bn_train(F.conv2d(f, P[f"{E}input_proj.{i}.conv.weight"]), P, f"{E}input_proj.{i}.norm", stats)
+            for i, f in enumerate(feats)]
+    for i, ei in enumerate(enc_idx):
+        B, _, H, W = proj[ei].shape
+        src = proj[ei].flatten(2).permute(0, 2, 1)
+        pos = sine_pos_embed_2d(W, H, C // 2, cfg["temperatureW"])
+        p = f"{E}encoder.{i}.layers.0"
+        q = src + pos
+        Wi, bi = P[p + ".self_attn.in_proj_weight"], P[p + ".self_attn.in_proj_bias"]
+        nh = cfg["nhead"]
+        dh = C // nh
+        Q = F.linear(q, Wi[:C], bi[:C]).reshape(B, -1, nh, dh).transpose(1, 2)
+        K = F.linear(q, Wi[C:2 * C], bi[C:2 * C]).reshape(B, -1, nh, dh).transpose(1, 2)
+        V = F.linear(src, Wi[2 * C:], bi[2 * C:]).reshape(B, -1, nh, dh).transpose(1, 2)
+        o = (torch.softmax((Q / math.sqrt(dh)) @ K.transpose(-1, -2), -1) @ V).transpose(1, 2).reshape(B, -1, C)
+        s2 = F.linear(o, P[p + ".self_attn.out_proj.weight"], P[p + ".self_attn.out_proj.bias"])
+        src = _ln(src + s2, P, p + ".norm1")
+        s2 = _lin(_act(_lin(src, P, p + ".linear1"), cfg["enc_act"]), P, p + ".linear2")
+        src = _ln(src + s2, P, p + ".norm2")
+        proj[ei] = src.permute(0, 2, 1).reshape(B, C, H, W)
+    inner = [proj[-1]]
+    for idx in range(nlev - 1, 0, -1):
+        j = nlev - 1 - idx
+        high = _conv_norm_t(inner[0], P, f"{E}lateral_convs.{j}", stats, act=cfg["act"])
+        inner[0] = high
+        up = F.interpolate(high, scale_factor=2.0, mode="nearest")
+        inner.insert(0, _elan_t(torch.cat([up, proj[idx - 1]], 1), P, f"{E}fpn_blocks.{j}", stats, nblk))
+    outs = [inner[0]]
+    for idx in range(nlev - 1):
+        d = _conv_norm_t(outs[-1], P, f"{E}downsample_convs.{idx}.0.cv1", stats)
+        d = _conv_norm_t(d, P, f"{E}downsample_convs.{idx}.0.cv2", stats, stride=2, groups=d.shape[1])
+        outs.append(_elan_t(torch.cat([d, inner[idx + 1]], 1), P, f"{E}pan_blocks.{idx}", stats, nblk))
+    return outs

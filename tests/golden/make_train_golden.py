@@ -241,7 +241,7 @@ def dn_targets(B, K, sizes, seed):
     return out
 
 
-def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5):
+def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_train=False):
     """The reference's full training step with OKS-denoising queries (transformer.py:1265-1385,
     dn_component.py:39-183) on CPU: training-mode forward WITH targets, the Criterion with its
     dn_* losses (criterion.py:385-435), loss.backward(). BatchNorm layers in eval mode (frozen
@@ -261,7 +261,15 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5):
         are never modified, so the copy changes no value or gradient. It is what the
         reference's AMP training run does anyway (autocast's casts are copies).
     Stored: targets, DN inputs, every loss, the outputs of every head, and for every
-    transformer parameter its gradient (full, f32)."""
+    transformer parameter its gradient (full, f32).
+
+    enc_train=True (the encoder half of config 5): the HybridEncoder runs in training mode as
+    the reference trains it (its BatchNorm2d layers on batch statistics, sync_bn on one
+    process), the backbone (FrozenBatchNorm2d, freeze_norm=True) is evaluated without
+    gradient and its outputs enter the encoder as leaves, so the gradients stored are the
+    encoder's and the transformer's parameters' plus d loss / d backbone-output ("dfeat.*"),
+    and the encoder outputs ("enc.*") and every encoder BN's running statistics after the
+    step's update ("bn.*") are stored too."""
     from detrpose_amd.synthetic import load_synthetic, synthetic_images
     import src.models.detrpose.transformer as tmod
     Criterion, HungarianMatcher = _import_criterion()
@@ -269,13 +277,24 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5):
     model, _ = make_golden.build_reference(ref, size)
     load_synthetic(model, seed=wseed)
     model.train()
-    for m in model.modules():
+    for m in (model.backbone if enc_train else model).modules():
         if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
             m.eval()
     K = model.transformer.num_body_points
     images = synthetic_images(batch, seed=1)
     targets = dn_targets(batch, K, sizes, tseed)
-    hk = model.encoder.register_forward_hook(lambda mod, a, out: [o.detach() for o in out])
+    feats_cap, enc_cap = [], []
+    if enc_train:
+        model.backbone.eval()
+
+        def leaf_feats(mod, a, out):
+            feats_cap.extend(o.detach().requires_grad_(True) for o in out)
+            return list(feats_cap)
+
+        hk = model.backbone.register_forward_hook(leaf_feats)
+        he = model.encoder.register_forward_hook(lambda mod, a, out: enc_cap.extend(o.detach() for o in out))
+    else:
+        hk = model.encoder.register_forward_hook(lambda mod, a, out: [o.detach() for o in out])
     hcls = [m.register_forward_pre_hook(lambda mod, a: (a[0].clone(),) + tuple(a[1:]))
             for m in model.transformer.class_embed]
     cap = {}
@@ -309,6 +328,8 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5):
         torch.Tensor.cuda = orig_cuda
         torch.argsort = orig_argsort
         hk.remove()
+        if enc_train:
+            he.remove()
         for h in hcls:
             h.remove()
     label, pose, mask, meta = cap["cdn"]
@@ -348,10 +369,27 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5):
         head(f"dn{i}", o)
     head("dn_pre", out["dn_aux_pre_outputs"])
     ng = 0
+    # enc_train: sampled (make_golden._sample: seeded indices + values, sum, |sum|) to keep the
+    # fixture small; the backbone features are not stored (the checker recomputes them)
+    put = (lambda name, t: make_golden._sample(st, name, t)) if enc_train else \
+        (lambda name, t: st.__setitem__(name, t.detach().numpy()))
     for n, p in model.transformer.named_parameters():
         if p.grad is not None:
-            st["grad." + n] = p.grad.numpy()
+            put("grad." + n, p.grad)
             ng += 1
+    if enc_train:
+        for n, p in model.encoder.named_parameters():
+            if p.grad is not None:
+                put("grad.encoder." + n, p.grad)
+                ng += 1
+        for i, f in enumerate(feats_cap):
+            put(f"dfeat{i}", f.grad)
+        for i, e in enumerate(enc_cap):
+            put(f"enc{i}", e)
+        for n, m in model.encoder.named_modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+                st[f"bn.encoder.{n}.running_mean"] = m.running_mean.numpy()
+                st[f"bn.encoder.{n}.running_var"] = m.running_var.numpy()
     print(f"  [{size}] DN train step b{batch} targets {sizes}: pad {meta['pad_size']} groups {meta['num_dn_group']}, "
           f"{len(keys)} losses, total {float(total):.6f}, {ng} parameter gradients")
     return st
@@ -361,6 +399,11 @@ def main():
     torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
     Criterion, HungarianMatcher = _import_criterion()
     ref = make_golden._import_reference()
+    if os.environ.get("ONLY_DN_ENC"):
+        st = golden_train_dn(ref, "n", 2, [3, 1], enc_train=True)
+        np.savez_compressed(os.path.join(HERE, "train_dn_enc_n_b2.npz"), **st)
+        print("wrote train_dn_enc_n_b2.npz")
+        return
     if os.environ.get("ONLY_DN"):
         st = golden_train_dn(ref, "n", 2, [3, 1])
         np.savez_compressed(os.path.join(HERE, "train_dn_n_b2.npz"), **st)

@@ -103,3 +103,85 @@ def test_dn_meta_and_attn_mask_match_reference(golden_dir):
     np.testing.assert_array_equal(dn_attn_mask(pad, groups, single, 60), g["dn_attn_mask"])
     assert dn_meta([0, 0]) is None
     assert dn_meta([25, 3])[:2] == (50, 1)   # more targets than dn_number: one group
+
+
+def _sampled(g, name):
+    return g[name + "__idx"], g[name + "__val"], float(g[name + "__sum"]), float(g[name + "__abssum"])
+
+
+def oracle_train_step_enc(size, g):
+    """The encoder half of config 5 on the oracle: backbone features of the golden images as
+    leaves, the encoder in training mode (BatchNorm on batch statistics, running statistics
+    updated), the training transformer with the golden DN draws, the criterion, backward.
+    Returns (losses, grads keyed like the golden, d feats, encoder outputs, running stats)."""
+    from oracle.detrpose_cpu import backbone
+    from oracle.train_cpu import losses, train_encoder, train_transformer
+    cfg = get_config(size)
+    model, _ = build_model(size)
+    params = {k for k, v in model.named_parameters() if v.requires_grad}
+    load_synthetic(model, seed=int(g["meta"][1]))
+    sd = {k: v.detach().float() for k, v in model.state_dict().items()}
+    B = int(g["meta"][0])
+    images = synthetic_images(B, seed=int(g["meta"][2]))
+    bc = cfg["backbone"]
+    with torch.no_grad():
+        feats = [f.clone().requires_grad_(True) for f in backbone(images, sd, bc["name"], bc["return_idx"],
+                                                                   bc["use_lab"])]
+    P = {k: (v.clone().requires_grad_(True) if k in params and (k.startswith("transformer.") or
+                                                               k.startswith("encoder.")) else v)
+         for k, v in sd.items()}
+    stats = {k: v.clone() for k, v in sd.items() if k.endswith("running_mean") or k.endswith("running_var")}
+    enc = train_encoder(feats, P, cfg["encoder"], stats)
+    res = train_transformer(enc, P, cfg["transformer"], dn=dn_inputs(g))
+    sizes, lab, kps, area = targets_of(g)
+    ld, _, _ = losses(res, sizes, lab, kps, area, cfg["transformer"]["num_body_points"],
+                      cfg["transformer"]["num_classes"])
+    sum(ld.values()).backward()
+    grads = {}
+    for k, v in P.items():
+        if isinstance(v, torch.Tensor) and v.requires_grad and v.grad is not None:
+            grads["grad." + (k[len("transformer."):] if k.startswith("transformer.") else k)] = v.grad
+    return ld, grads, [f.grad for f in feats], [e.detach() for e in enc], stats
+
+
+@pytest.fixture(scope="module")
+def enc_case(golden_dir):
+    g = np.load(os.path.join(golden_dir, "train_dn_enc_n_b2.npz"))
+    return g, oracle_train_step_enc("n", g)
+
+
+def test_oracle_encoder_step_losses_match_reference(enc_case):
+    g, (ld, _, _, _, _) = enc_case
+    assert list(ld) == [str(k) for k in g["loss_keys"]]
+    np.testing.assert_allclose([float(v) for v in ld.values()], g["loss_vals"], rtol=1e-5, atol=1e-6)
+
+
+def test_oracle_encoder_step_gradients_match_reference(enc_case):
+    """Every transformer AND encoder parameter gradient (sampled entries) within 1e-4 of its
+    scale, d loss / d backbone features and the encoder outputs likewise, and the encoder
+    BatchNorm running statistics after the step's update within 1e-5."""
+    g, (_, grads, dfeat, enc, stats) = enc_case
+    names = sorted(k[:-len("__idx")] for k in g.files if k.startswith("grad.") and k.endswith("__idx"))
+    assert names == sorted(grads), set(names) ^ set(grads)
+    assert sum(n.startswith("grad.encoder.") for n in names) > 50
+    worst = []
+    checks = [(n, grads[n]) for n in names] + [(f"dfeat{i}", t) for i, t in enumerate(dfeat)] + \
+        [(f"enc{i}", t) for i, t in enumerate(enc)]
+    for n, t in checks:
+        idx, val, s, a = _sampled(g, n)
+        got = t.detach().double().reshape(-1).numpy()
+        scale = max(float(np.abs(val).max()), a / got.size)
+        if scale < 1e-5:
+            # analytically zero: a BN bias whose output reaches the loss only through another
+            # training-mode BN, which removes any per-channel shift (rounding noise ~1e-7)
+            assert float(np.abs(got).max()) < 1e-5, (n, float(np.abs(got).max()))
+            continue
+        err = float(np.abs(got[idx] - val).max()) / scale
+        worst.append((err, n))
+        assert err <= 1e-4, (n, err)
+        assert abs(got.sum() - s) <= 1e-4 * a + 1e-9, (n, got.sum(), s)
+    for k in g.files:
+        if k.startswith("bn."):
+            np.testing.assert_allclose(stats[k[3:]].numpy(), g[k], rtol=1e-5, atol=1e-6, err_msg=k)
+    worst.sort(reverse=True)
+    print("worst relative errors:", worst[:5])
