@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DETRPOSE_HIP_LIB", os.path.join(_HERE, "lib", "libdetrpose_hip.so"))
 
 DP_F32, DP_BF16 = 0, 1
+DP_ACT_NONE, DP_ACT_RELU, DP_ACT_SILU, DP_ACT_GELU = 0, 1, 2, 3
 DP_MSDA_OFFATTN_F32 = 0x100
 ACT = {None: 0, "none": 0, "relu": 1, "silu": 2, "gelu": 3}
 
@@ -96,7 +97,7 @@ _SIGS = {
     "dp_resize_pad": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, f32, vp]),
     "dp_msda_core_fwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "dp_msda_core_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, i32, vp]),
-    "dp_msda_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp]),
+    "dp_msda_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, i32, vp]),
     "dp_topk": (i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
     "dp_class_max": (i32, [vp, i32, i32, vp, vp, i32, vp, i32, vp]),
     "dp_gather_rows": (i32, [vp, i64, vp, i32, i32, i32, vp, i32, vp]),
@@ -136,7 +137,7 @@ _SIGS = {
     "dp_query_build_bwd": (i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, i32, vp]),
     "dp_pose_refine_bwd": (i32, [vp, vp, i32, f32, vp, i32, i32, vp, i32, vp]),
     "dp_sigmoid_bwd": (i32, [vp, vp, vp, i32, i32, i64, i64, i64, vp]),
-    "dp_lqe_stats_bwd": (i32, [vp, i64, i32, i32, i32, vp, vp, i32, i32, i32, vp, i32, vp]),
+    "dp_lqe_stats_bwd": (i32, [vp, i64, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp, i64, i32, vp]),
     "dp_scatter_rows": (i32, [vp, i32, vp, i32, i32, i32, vp, i64, i32, i32, i32, vp]),
     "dp_gather_rows_masked": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, vp, i32, vp]),
     "dp_convert_rows": (i32, [vp, i32, i64, vp, i32, i64, i32, i32, f32, i32, vp]),
@@ -144,6 +145,21 @@ _SIGS = {
     "dp_cdn_build": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, i32, f32, f32, C.c_uint64, vp, vp, vp]),
     "dp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
     "dp_adamw": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp]),
+    # HybridEncoder training (csrc/encoder_train.hip)
+    "dp_bn_stats": (i32, [vp, i64, i32, i32, vp, i32, vp]),
+    "dp_bn_finalize": (i32, [vp, i32, f32, i32, f32, f32, vp, vp, vp, vp]),
+    "dp_bn_act_fwd": (i32, [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
+    "dp_bn_act_bwd_reduce": (i32, [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp,
+                                   vp, i32, vp]),
+    "dp_bn_act_bwd_apply": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32,
+                                  vp, f32, i32, vp]),
+    "dp_im2col": (i32, [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
+    "dp_conv_pack": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, vp]),
+    "dp_dwconv_bwd": (i32, [vp, i64, i32, vp, i64, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, i32,
+                            vp, i32, vp]),
+    "dp_upsample2x": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, i32, vp]),
+    "dp_axpby_rows": (i32, [vp, i64, vp, i64, f32, vp, i64, f32, i32, i32, i32, i32, vp]),
+    "dp_act_bwd": (i32, [vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, vp]),
 }
 
 EXPORTED = tuple(k for k in _SIGS)

@@ -1,0 +1,502 @@
+// Row ops of the HybridEncoder's training step (BASELINE config 5): the
+// encoder's BatchNorm2d layers on batch statistics (sync_bn), the ConvNormLayer / VGGBlock
+// epilogues with their backward, the pieces of conv backward that are not GEMMs or convs
+// themselves, and the nearest-x2 / activation / add rows. Convolutions run on dp_conv2d
+// (forward and 3x3 input gradient with flipped weights) and dp_gemm (1x1 input gradient,
+// every weight gradient over an im2col); see detrpose_amd/encoder_train.py for the tape.
+//
+// Layout: NHWC activations as [rows][c] with a row stride (channel slices of concat buffers),
+// rows = batch * h * w. f32 statistics. Activations / activation gradients of dtype.
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ float ld_(const T* p) {
+  return to_f32(*p);
+}
+
+// act(pre) and d act / d pre (hybrid_encoder.py get_activation: silu / relu / gelu (erf))
+__device__ __forceinline__ float act_f(float x, int act) {
+  if (act == DP_ACT_RELU) return fmaxf(x, 0.f);
+  if (act == DP_ACT_SILU) return x / (1.f + __expf(-x));
+  if (act == DP_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  return x;
+}
+__device__ __forceinline__ float act_d(float x, int act) {
+  if (act == DP_ACT_RELU) return x > 0.f ? 1.f : 0.f;
+  if (act == DP_ACT_SILU) {
+    const float s = 1.f / (1.f + __expf(-x));
+    return s * (1.f + x * (1.f - s));
+  }
+  if (act == DP_ACT_GELU)
+    return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+  return 1.f;
+}
+
+// ---------------------------------------------------------------- BatchNorm statistics
+// Column sums over a block of rows, shifted by the column's first-row value K (single-pass
+// variance without the E[x^2] - mean^2 cancellation): out[0] = K, out[1] += sum (x - K),
+// out[2] += sum (x - K)^2. Block: 64 channels (lane) x 4 row phases (wave), 256 rows.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, int64_t ld, int rows, int c,
+                                                       float* __restrict__ out) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * 256;
+  float s1 = 0.f, s2 = 0.f;
+  if (ch < c) {
+    const float k = ld_(x + ch);
+    const int r1 = min(r0 + 256, rows);
+    for (int r = r0 + wv; r < r1; r += 4) {
+      const float d = ld_(x + (int64_t)r * ld + ch) - k;
+      s1 += d;
+      s2 = fmaf(d, d, s2);
+    }
+    if (blockIdx.y == 0 && wv == 0) out[ch] = k;
+  }
+  red[0][wv][lane] = s1;
+  red[1][wv][lane] = s2;
+  __syncthreads();
+  if (wv == 0 && ch < c) {
+    atomicAdd(out + c + ch, red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane]);
+    atomicAdd(out + 2 * c + ch, red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane]);
+  }
+}
+
+// parts [np][3][c] (one per rank: K, S1, S2 over `count` rows each) -> mr [2][c] = (mean, rstd)
+// of the union (Chan's parallel combination), biased variance; running statistics updated as
+// F.batch_norm does (momentum, unbiased variance)
+__global__ void bn_finalize_kernel(const float* __restrict__ parts, int np, float count, int c, float eps,
+                                   float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
+                                   float* __restrict__ mr) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int p = 0; p < np; ++p) {
+    const float* q = parts + (int64_t)p * 3 * c;
+    const double k = q[ch], s1 = q[c + ch], s2 = q[2 * c + ch];
+    const double mi = k + s1 / count, m2i = s2 - s1 * s1 / count;
+    const double nn = n + count, delta = mi - mean;
+    mean += delta * count / nn;
+    m2 += m2i + delta * delta * n * count / nn;
+    n = nn;
+  }
+  const double var = m2 / n;
+  mr[ch] = (float)mean;
+  mr[c + ch] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) {
+    rmean[ch] = (float)((1.0 - momentum) * rmean[ch] + momentum * mean);
+    rvar[ch] = (float)((1.0 - momentum) * rvar[ch] + momentum * (n > 1.0 ? m2 / (n - 1.0) : var));
+  }
+}
+
+struct BnBranch {
+  const void* z;
+  int64_t ld;
+  const float* mr;   // [2][c] mean, rstd
+  const float* g;
+  const float* b;
+};
+
+template <typename T>
+__device__ __forceinline__ float bn_of(const BnBranch& p, int64_t r, int ch, int c, float* xh) {
+  const float x = ld_(reinterpret_cast<const T*>(p.z) + r * p.ld + ch);
+  const float h = (x - p.mr[ch]) * p.mr[c + ch];
+  *xh = h;
+  return fmaf(p.g[ch], h, p.b[ch]);
+}
+
+// y = act(bn1(z1) [+ bn2(z2)]) (+ res when res != NULL)
+template <typename T>
+__global__ void bn_act_fwd_kernel(T* __restrict__ y, int64_t ldy, BnBranch p1, BnBranch p2, const T* __restrict__ res,
+                                  int64_t ldr, int rows, int c, int act) {
+  const int64_t total = (int64_t)rows * c;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / c;
+    const int ch = (int)(e - r * c);
+    float h;
+    float v = bn_of<T>(p1, r, ch, c, &h);
+    if (p2.z) v += bn_of<T>(p2, r, ch, c, &h);
+    v = act_f(v, act);
+    if (res) v += ld_(res + r * ldr + ch);
+    y[r * ldy + ch] = from_f32<T>(v);
+  }
+}
+
+// dp = dy * act'(pre): column sums sums[0] += sum dp, sums[1] += sum dp xh1, sums[2] += sum dp
+// xh2, and the parameter gradients dg1 += sum dp xh1, db1 += sum dp (dg2 / db2 likewise)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restrict__ dy, int64_t ldy, BnBranch p1,
+                                                                BnBranch p2, int rows, int c, int act,
+                                                                float* __restrict__ sums, float* __restrict__ dg1,
+                                                                float* __restrict__ db1, float* __restrict__ dg2,
+                                                                float* __restrict__ db2) {
+  __shared__ float red[3][4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * 256;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  if (ch < c) {
+    const int r1 = min(r0 + 256, rows);
+    for (int r = r0 + wv; r < r1; r += 4) {
+      float h1, h2 = 0.f;
+      float pre = bn_of<T>(p1, r, ch, c, &h1);
+      if (p2.z) pre += bn_of<T>(p2, r, ch, c, &h2);
+      const float dp = ld_(dy + (int64_t)r * ldy + ch) * act_d(pre, act);
+      a0 += dp;
+      a1 = fmaf(dp, h1, a1);
+      a2 = fmaf(dp, h2, a2);
+    }
+  }
+  red[0][wv][lane] = a0;
+  red[1][wv][lane] = a1;
+  red[2][wv][lane] = a2;
+  __syncthreads();
+  if (wv == 0 && ch < c) {
+    const float s0 = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+    const float s1 = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+    const float s2 = red[2][0][lane] + red[2][1][lane] + red[2][2][lane] + red[2][3][lane];
+    atomicAdd(sums + ch, s0);
+    atomicAdd(sums + c + ch, s1);
+    atomicAdd(sums + 2 * c + ch, s2);
+    if (dg1) atomicAdd(dg1 + ch, s1);
+    if (db1) atomicAdd(db1 + ch, s0);
+    if (dg2) atomicAdd(dg2 + ch, s2);
+    if (db2) atomicAdd(db2 + ch, s0);
+  }
+}
+
+// dz_k = g_k rstd_k (dp - sum dp / N - xh_k sum (dp xh_k) / N) (torch batch_norm_backward with
+// the synced sums)
+template <typename T>
+__global__ void bn_act_bwd_apply_kernel(T* __restrict__ dz1, int64_t ld1, T* __restrict__ dz2, int64_t ld2,
+                                        const T* __restrict__ dy, int64_t ldy, BnBranch p1, BnBranch p2, int rows,
+                                        int c, int act, const float* __restrict__ sums, float inv_n) {
+  const int64_t total = (int64_t)rows * c;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / c;
+    const int ch = (int)(e - r * c);
+    float h1, h2 = 0.f;
+    float pre = bn_of<T>(p1, r, ch, c, &h1);
+    if (p2.z) pre += bn_of<T>(p2, r, ch, c, &h2);
+    const float dp = ld_(dy + r * ldy + ch) * act_d(pre, act);
+    const float m0 = sums[ch] * inv_n;
+    dz1[r * ld1 + ch] = from_f32<T>(p1.g[ch] * p1.mr[c + ch] * (dp - m0 - h1 * sums[c + ch] * inv_n));
+    if (dz2) dz2[r * ld2 + ch] = from_f32<T>(p2.g[ch] * p2.mr[c + ch] * (dp - m0 - h2 * sums[2 * c + ch] * inv_n));
+  }
+}
+
+// ---------------------------------------------------------------- conv backward pieces
+// col[row][ci * kh * kw + ky * kw + kx] = x[b][oy * s - pad + ky][ox * s - pad + kx][ci] (0 outside):
+// the [rows][cin][kh][kw] operand whose product with dz^T is the weight gradient in the
+// reference layout [cout][cin][kh][kw]
+template <typename T>
+__global__ void im2col_kernel(const T* __restrict__ x, int64_t bs, int ps, int h, int w, int cin, int kh, int kw,
+                              int stride, int pad, int oh, int ow, T* __restrict__ col, int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (row, ci)
+  if (e >= total) return;
+  const int ci = (int)(e % cin);
+  const int64_t row = e / cin;
+  const int ox = (int)(row % ow);
+  const int64_t t = row / ow;
+  const int oy = (int)(t % oh), b = (int)(t / oh);
+  T* o = col + row * ((int64_t)cin * kh * kw) + (int64_t)ci * kh * kw;
+  for (int ky = 0; ky < kh; ++ky)
+    for (int kx = 0; kx < kw; ++kx) {
+      const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+      const bool ok = (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+      o[ky * kw + kx] = ok ? x[(int64_t)b * bs + ((int64_t)iy * w + ix) * ps + ci] : from_f32<T>(0.f);
+    }
+}
+
+// f32 master weights [cout][cin][kh][kw] -> the conv kernels' packed [rows][kpad] (K = ky, kx, ci):
+// mode 0 forward (rows = cout), mode 1 input gradient (rows = cin, K over cout, taps flipped),
+// mode 2 depthwise taps [kh*kw][c] f32 (cin = 1)
+template <typename T>
+__global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin, int kh, int kw, void* __restrict__ out,
+                                 int kpad, int mode) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (mode == 2) {
+    if (e >= (int64_t)cout * kh * kw) return;
+    const int tap = (int)(e / cout), ch = (int)(e % cout);
+    reinterpret_cast<float*>(out)[e] = w[(int64_t)ch * kh * kw + tap];
+    return;
+  }
+  const int rows = mode == 0 ? cout : cin;
+  const int inner = mode == 0 ? cin : cout;
+  if (e >= (int64_t)rows * kpad) return;
+  const int r = (int)(e / kpad), k = (int)(e % kpad);
+  float v = 0.f;
+  if (k < kh * kw * inner) {
+    const int tap = k / inner, j = k - tap * inner;
+    const int ky = tap / kw, kx = tap - ky * kw;
+    v = mode == 0 ? w[(((int64_t)r * cin + j) * kh + ky) * kw + kx]
+                  : w[(((int64_t)j * cin + r) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)];
+  }
+  reinterpret_cast<T*>(out)[e] = from_f32<T>(v);
+}
+
+// depthwise conv backward (SCDown's 3x3 s2, hybrid_encoder.py:156-170): dx (+=) by gathering the
+// output positions each input pixel feeds, dw [c][kh][kw] (+=, f32 atomics) by column sums over
+// the output pixels of a 256-pixel chunk
+template <typename T>
+__global__ void dw_bwd_data_kernel(const T* __restrict__ dz, int64_t zbs, int zps, const float* __restrict__ wt,
+                                   int h, int w, int c, int k, int s, int pad, int oh, int ow, T* __restrict__ dx,
+                                   int64_t xbs, int xps, int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int ch = (int)(e % c);
+  const int64_t p = e / c;
+  const int x = (int)(p % w);
+  const int64_t t = p / w;
+  const int y = (int)(t % h), b = (int)(t / h);
+  float acc = 0.f;
+  for (int ky = 0; ky < k; ++ky) {
+    const int ny = y + pad - ky;
+    if (ny < 0 || ny % s) continue;
+    const int oy = ny / s;
+    if (oy >= oh) continue;
+    for (int kx = 0; kx < k; ++kx) {
+      const int nx = x + pad - kx;
+      if (nx < 0 || nx % s) continue;
+      const int ox = nx / s;
+      if (ox >= ow) continue;
+      acc = fmaf(ld_(dz + (int64_t)b * zbs + ((int64_t)oy * ow + ox) * zps + ch), wt[(ky * k + kx) * c + ch], acc);
+    }
+  }
+  T* o = dx + (int64_t)b * xbs + ((int64_t)y * w + x) * xps + ch;
+  *o = from_f32<T>(ld_(o) + acc);
+}
+
+template <typename T>
+__global__ void dw_bwd_weight_kernel(const T* __restrict__ x, int64_t xbs, int xps, const T* __restrict__ dz,
+                                     int64_t zbs, int zps, int h, int w, int c, int k, int s, int pad, int oh, int ow,
+                                     int opix, float* __restrict__ dw) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  const int p0 = blockIdx.y * 256, p1 = min(p0 + 256, opix);
+  float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = p0; p < p1; ++p) {
+    const int ox = p % ow, t = p / ow, oy = t % oh, b = t / oh;
+    const float g = ld_(dz + (int64_t)b * zbs + ((int64_t)oy * ow + ox) * zps + ch);
+    for (int ky = 0; ky < k; ++ky)
+      for (int kx = 0; kx < k; ++kx) {
+        const int iy = oy * s - pad + ky, ix = ox * s - pad + kx;
+        if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w)
+          acc[ky * k + kx] = fmaf(g, ld_(x + (int64_t)b * xbs + ((int64_t)iy * w + ix) * xps + ch), acc[ky * k + kx]);
+      }
+  }
+  for (int t = 0; t < k * k; ++t) atomicAdd(dw + (int64_t)ch * k * k + t, acc[t]);
+}
+
+// ---------------------------------------------------------------- rows
+// nearest x2 (F.interpolate(scale_factor=2, nearest), hybrid_encoder.py:487): forward copy and
+// its backward (2x2 sum, +=)
+template <typename T>
+__global__ void up2_kernel(const T* __restrict__ src, int64_t sbs, int sps, int h, int w, int c, T* __restrict__ dst,
+                           int64_t dbs, int dps, int bwd, int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over the small map
+  if (e >= total) return;
+  const int ch = (int)(e % c);
+  const int64_t p = e / c;
+  const int x = (int)(p % w);
+  const int64_t t = p / w;
+  const int y = (int)(t % h), b = (int)(t / h);
+  const int64_t big[4] = {((int64_t)(2 * y) * (2 * w) + 2 * x), ((int64_t)(2 * y) * (2 * w) + 2 * x + 1),
+                          ((int64_t)(2 * y + 1) * (2 * w) + 2 * x), ((int64_t)(2 * y + 1) * (2 * w) + 2 * x + 1)};
+  if (!bwd) {
+    const T v = src[(int64_t)b * sbs + ((int64_t)y * w + x) * sps + ch];
+    for (int q = 0; q < 4; ++q) dst[(int64_t)b * dbs + big[q] * dps + ch] = v;
+  } else {   // src = d big map, dst = d small map (+=)
+    float acc = 0.f;
+    for (int q = 0; q < 4; ++q) acc += ld_(src + (int64_t)b * sbs + big[q] * sps + ch);
+    T* o = dst + (int64_t)b * dbs + ((int64_t)y * w + x) * dps + ch;
+    *o = from_f32<T>(ld_(o) + acc);
+  }
+}
+
+// y (=|+=) alpha a [+ beta b]: residual adds and their backward (gradient fan-out)
+template <typename T>
+__global__ void axpby_kernel(T* __restrict__ y, int64_t ldy, const T* __restrict__ a, int64_t lda, float alpha,
+                             const T* __restrict__ b, int64_t ldb, float beta, int rows, int c, int acc) {
+  const int64_t total = (int64_t)rows * c;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / c;
+    const int ch = (int)(e - r * c);
+    float v = alpha * ld_(a + r * lda + ch);
+    if (b) v = fmaf(beta, ld_(b + r * ldb + ch), v);
+    T* o = y + r * ldy + ch;
+    *o = from_f32<T>(acc ? ld_(o) + v : v);
+  }
+}
+
+// dx = dy * act'(pre) (the AIFI FFN's GELU, hybrid_encoder.py:292)
+template <typename T>
+__global__ void act_bwd_kernel(const T* __restrict__ pre, int64_t ldp, const T* __restrict__ dy, int64_t ldy,
+                               T* __restrict__ dx, int64_t ldx, int rows, int c, int act) {
+  const int64_t total = (int64_t)rows * c;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / c;
+    const int ch = (int)(e - r * c);
+    dx[r * ldx + ch] = from_f32<T>(ld_(dy + r * ldy + ch) * act_d(ld_(pre + r * ldp + ch), act));
+  }
+}
+
+int grid_for(int64_t total) {
+  int64_t g = (total + 255) / 256;
+  return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+#define DP_DT(CALL)                    \
+  do {                                 \
+    if (dtype == DP_BF16) {            \
+      using T = bf16_t;                \
+      CALL;                            \
+    } else {                           \
+      using T = float;                 \
+      CALL;                            \
+    }                                  \
+  } while (0)
+
+extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, int32_t dtype,
+                           void* stream) {
+  DP_REQUIRE(x && out && rows > 0 && c > 0 && ld >= c, "dp_bn_stats: bad arguments");
+  hipStream_t s = as_stream(stream);
+  if (hipMemsetAsync(out + c, 0, 2 * (size_t)c * sizeof(float), s) != hipSuccess) {
+    dp_set_error("dp_bn_stats: memset failed");
+    return DP_EINVAL;
+  }
+  dim3 grid((c + 63) / 64, (rows + 255) / 256);
+  DP_DT(hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ld, rows, c, out));
+  return dp_check_launch("dp_bn_stats");
+}
+
+extern "C" int dp_bn_finalize(const float* parts, int32_t nparts, float count, int32_t c, float eps, float momentum,
+                              float* running_mean, float* running_var, float* mean_rstd, void* stream) {
+  DP_REQUIRE(parts && nparts > 0 && count > 0.f && c > 0 && mean_rstd && (!running_mean == !running_var),
+             "dp_bn_finalize: bad arguments");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((c + 255) / 256), dim3(256), 0, as_stream(stream), parts, nparts, count,
+                     c, eps, momentum, running_mean, running_var, mean_rstd);
+  return dp_check_launch("dp_bn_finalize");
+}
+
+extern "C" int dp_bn_act_fwd(void* y, int64_t ld_y, const void* z1, int64_t ld1, const float* mr1, const float* g1,
+                             const float* b1, const void* z2, int64_t ld2, const float* mr2, const float* g2,
+                             const float* b2, const void* res, int64_t ld_res, int32_t rows, int32_t c, int32_t act,
+                             int32_t dtype, void* stream) {
+  DP_REQUIRE(y && z1 && mr1 && g1 && b1 && rows > 0 && c > 0 && (!z2 || (mr2 && g2 && b2)),
+             "dp_bn_act_fwd: bad arguments");
+  const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
+  DP_DT(hipLaunchKernelGGL(bn_act_fwd_kernel<T>, dim3(grid_for((int64_t)rows * c)), dim3(256), 0, as_stream(stream),
+                           (T*)y, ld_y, p1, p2, (const T*)res, ld_res, rows, c, act));
+  return dp_check_launch("dp_bn_act_fwd");
+}
+
+extern "C" int dp_bn_act_bwd_reduce(const void* dy, int64_t ld_dy, const void* z1, int64_t ld1, const float* mr1,
+                                    const float* g1, const float* b1, const void* z2, int64_t ld2, const float* mr2,
+                                    const float* g2, const float* b2, int32_t rows, int32_t c, int32_t act,
+                                    float* sums, float* dg1, float* db1, float* dg2, float* db2, int32_t dtype,
+                                    void* stream) {
+  DP_REQUIRE(dy && z1 && mr1 && g1 && b1 && sums && rows > 0 && c > 0 && (!z2 || (mr2 && g2 && b2)),
+             "dp_bn_act_bwd_reduce: bad arguments");
+  hipStream_t s = as_stream(stream);
+  if (hipMemsetAsync(sums, 0, 3 * (size_t)c * sizeof(float), s) != hipSuccess) {
+    dp_set_error("dp_bn_act_bwd_reduce: memset failed");
+    return DP_EINVAL;
+  }
+  const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
+  dim3 grid((c + 63) / 64, (rows + 255) / 256);
+  DP_DT(hipLaunchKernelGGL(bn_act_bwd_reduce_kernel<T>, grid, dim3(256), 0, s, (const T*)dy, ld_dy, p1, p2, rows, c,
+                           act, sums, dg1, db1, dg2, db2));
+  return dp_check_launch("dp_bn_act_bwd_reduce");
+}
+
+extern "C" int dp_bn_act_bwd_apply(void* dz1, int64_t ld_dz1, void* dz2, int64_t ld_dz2, const void* dy, int64_t ld_dy,
+                                   const void* z1, int64_t ld1, const float* mr1, const float* g1, const float* b1,
+                                   const void* z2, int64_t ld2, const float* mr2, const float* g2, const float* b2,
+                                   int32_t rows, int32_t c, int32_t act, const float* sums, float count, int32_t dtype,
+                                   void* stream) {
+  DP_REQUIRE(dz1 && dy && z1 && mr1 && g1 && b1 && sums && rows > 0 && c > 0 && count > 0.f &&
+                 (!z2 || (mr2 && g2 && b2 && dz2)),
+             "dp_bn_act_bwd_apply: bad arguments");
+  const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
+  DP_DT(hipLaunchKernelGGL(bn_act_bwd_apply_kernel<T>, dim3(grid_for((int64_t)rows * c)), dim3(256), 0,
+                           as_stream(stream), (T*)dz1, ld_dz1, (T*)(z2 ? dz2 : nullptr), ld_dz2, (const T*)dy, ld_dy,
+                           p1, p2, rows, c, act, sums, 1.f / count));
+  return dp_check_launch("dp_bn_act_bwd_apply");
+}
+
+extern "C" int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int32_t batch, int32_t h, int32_t w,
+                         int32_t cin, int32_t kh, int32_t kw, int32_t stride, int32_t pad, int32_t oh, int32_t ow,
+                         void* col, int32_t dtype, void* stream) {
+  DP_REQUIRE(x && col && batch > 0 && cin > 0 && kh > 0 && kw > 0 && stride > 0 && oh > 0 && ow > 0,
+             "dp_im2col: bad arguments");
+  const int64_t total = (int64_t)batch * oh * ow * cin;
+  DP_DT(hipLaunchKernelGGL(im2col_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
+                           (const T*)x, bstride, pstride, h, w, cin, kh, kw, stride, pad, oh, ow, (T*)col, total));
+  return dp_check_launch("dp_im2col");
+}
+
+extern "C" int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out, int32_t kpad,
+                            int32_t mode, int32_t dtype, void* stream) {
+  DP_REQUIRE(w && out && cout > 0 && cin > 0 && mode >= 0 && mode <= 2 &&
+                 (mode == 2 ? cin == 1 : kpad >= kh * kw * (mode == 0 ? cin : cout)),
+             "dp_conv_pack: bad arguments");
+  const int64_t total = mode == 2 ? (int64_t)cout * kh * kw : (int64_t)(mode == 0 ? cout : cin) * kpad;
+  DP_DT(hipLaunchKernelGGL(conv_pack_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
+                           w, cout, cin, kh, kw, out, kpad, mode));
+  return dp_check_launch("dp_conv_pack");
+}
+
+extern "C" int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride, const void* dz, int64_t z_bstride,
+                             int32_t z_pstride, const float* wt, int32_t batch, int32_t h, int32_t w, int32_t c,
+                             int32_t k, int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* dx,
+                             int64_t dx_bstride, int32_t dx_pstride, float* dw, int32_t dtype, void* stream) {
+  DP_REQUIRE(x && dz && wt && batch > 0 && c > 0 && k > 0 && k <= 3 && stride > 0, "dp_dwconv_bwd: bad arguments");
+  hipStream_t s = as_stream(stream);
+  if (dx) {
+    const int64_t total = (int64_t)batch * h * w * c;
+    DP_DT(hipLaunchKernelGGL(dw_bwd_data_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                             (const T*)dz, z_bstride, z_pstride, wt, h, w, c, k, stride, pad, oh, ow, (T*)dx,
+                             dx_bstride, dx_pstride, total));
+  }
+  if (dw) {
+    const int opix = batch * oh * ow;
+    dim3 grid((c + 63) / 64, (opix + 255) / 256);
+    DP_DT(hipLaunchKernelGGL(dw_bwd_weight_kernel<T>, grid, dim3(64), 0, s, (const T*)x, x_bstride, x_pstride,
+                             (const T*)dz, z_bstride, z_pstride, h, w, c, k, stride, pad, oh, ow, opix, dw));
+  }
+  return dp_check_launch("dp_dwconv_bwd");
+}
+
+extern "C" int dp_upsample2x(const void* src, int64_t src_bstride, int32_t src_pstride, int32_t batch, int32_t h,
+                             int32_t w, int32_t c, void* dst, int64_t dst_bstride, int32_t dst_pstride,
+                             int32_t backward, int32_t dtype, void* stream) {
+  DP_REQUIRE(src && dst && batch > 0 && h > 0 && w > 0 && c > 0, "dp_upsample2x: bad arguments");
+  const int64_t total = (int64_t)batch * h * w * c;
+  DP_DT(hipLaunchKernelGGL(up2_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
+                           (const T*)src, src_bstride, src_pstride, h, w, c, (T*)dst, dst_bstride, dst_pstride,
+                           backward, total));
+  return dp_check_launch("dp_upsample2x");
+}
+
+extern "C" int dp_axpby_rows(void* y, int64_t ld_y, const void* a, int64_t ld_a, float alpha, const void* b,
+                             int64_t ld_b, float beta, int32_t rows, int32_t c, int32_t accumulate, int32_t dtype,
+                             void* stream) {
+  DP_REQUIRE(y && a && rows > 0 && c > 0, "dp_axpby_rows: bad arguments");
+  DP_DT(hipLaunchKernelGGL(axpby_kernel<T>, dim3(grid_for((int64_t)rows * c)), dim3(256), 0, as_stream(stream), (T*)y,
+                           ld_y, (const T*)a, ld_a, alpha, (const T*)b, ld_b, beta, rows, c, accumulate));
+  return dp_check_launch("dp_axpby_rows");
+}
+
+extern "C" int dp_act_bwd(const void* pre, int64_t ld_pre, const void* dy, int64_t ld_dy, void* dx, int64_t ld_dx,
+                          int32_t rows, int32_t c, int32_t act, int32_t dtype, void* stream) {
+  DP_REQUIRE(pre && dy && dx && rows > 0 && c > 0, "dp_act_bwd: bad arguments");
+  DP_DT(hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(grid_for((int64_t)rows * c)), dim3(256), 0, as_stream(stream),
+                           (const T*)pre, ld_pre, (const T*)dy, ld_dy, (T*)dx, ld_dx, rows, c, act));
+  return dp_check_launch("dp_act_bwd");
+}

@@ -235,6 +235,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs g) {
         if (g.bias) v += g.bias[n];
         if (g.beta != 0.f) v += g.beta * (g.cf ? g.cf[o] : (float)g.cb[o]);
         if (g.act == DP_ACT_RELU) v = fmaxf(v, 0.f);
+        else if (g.act == DP_ACT_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
         if (g.gate) {
           const int64_t go = (int64_t)bidx * g.g_bs + (int64_t)m * g.g_rs + n;
           const float gv = g.gate_bf16 ? (float)reinterpret_cast<const bf16_t*>(g.gate)[go]
@@ -263,7 +264,8 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
              d.k, d.batch);
   DP_REQUIRE(d.in_dtype == DP_BF16 || d.in_dtype == DP_F32, "dp_gemm: bad input dtype %d", d.in_dtype);
   DP_REQUIRE(d.out_dtype == DP_BF16 || d.out_dtype == DP_F32, "dp_gemm: bad output dtype %d", d.out_dtype);
-  DP_REQUIRE(d.act == DP_ACT_NONE || d.act == DP_ACT_RELU, "dp_gemm: act %d (none / relu)", d.act);
+  DP_REQUIRE(d.act == DP_ACT_NONE || d.act == DP_ACT_RELU || d.act == DP_ACT_GELU, "dp_gemm: act %d (none / relu / gelu)",
+             d.act);
   DP_REQUIRE(d.split_k >= 0, "dp_gemm: split_k %d", d.split_k);
   const int es = d.in_dtype == DP_BF16 ? 2 : 4;
   const int vec = 16 / es;

@@ -309,7 +309,8 @@ extern "C" int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, con
 extern "C" int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
                            const float* offattn, const float* ref, const void* grad_out, int32_t ld_grad_out,
                            int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value,
-                           float* grad_offattn, float* grad_ref, int32_t dtype, void* stream) {
+                           int32_t accumulate_value, float* grad_offattn, float* grad_ref, int32_t dtype,
+                           void* stream) {
   TLevels lv;
   const int rc = check_core(value, batch, S, lvl_hw, nlevels, offattn, ref, lq, nhead, dh, npoints, dtype, &lv);
   if (rc) return rc;
@@ -319,7 +320,8 @@ extern "C" int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const in
              "dp_msda_bwd: grad_out must be 16-byte aligned per row (ld %d)", ld_grad_out);
   hipStream_t s = as_stream(stream);
   // grad_value (and grad_ref) are accumulated by atomics: clear them on the stream first
-  if ((grad_value && hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess) ||
+  if ((grad_value && !accumulate_value &&
+       hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess) ||
       (grad_ref && hipMemsetAsync(grad_ref, 0, (size_t)batch * lq * 2 * sizeof(float), s) != hipSuccess))
     return dp_check_launch("dp_msda_bwd(memset)");
   const int ppw = 64 / (dh / VEC);

@@ -212,12 +212,13 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
                                                       T* __restrict__ dk, T* __restrict__ dv, int lddkv, int n_inner,
                                                       int64_t so, int64_t si, int64_t st, int L, int nhead, int dh,
                                                       float scale) {
+  // Q is read from global memory in the dK phase (every lane the same row: broadcast loads),
+  // which keeps a 400-token sequence (the AIFI layer, dh 32) within 160 KB of LDS
   extern __shared__ float sm[];
-  float* Qs = sm;
-  float* Ks = sm + L * dh;
-  float* Vs = sm + 2 * L * dh;
-  float* Ds = sm + 3 * L * dh;   // dO
-  float* Dr = sm + 4 * L * dh;   // D_i = sum_j P_ij dP_ij
+  float* Ks = sm;
+  float* Vs = sm + L * dh;
+  float* Ds = sm + 2 * L * dh;   // dO
+  float* Dr = sm + 3 * L * dh;   // D_i = sum_j P_ij dP_ij
   const int lane = threadIdx.x;
   const int h = blockIdx.x % nhead;
   const int seq = blockIdx.x / nhead;
@@ -226,7 +227,6 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
   for (int e = lane; e < L * dh; e += 64) {
     const int t = e / dh, dd = e - t * dh;
     const int64_t rr = row0 + t * st;
-    Qs[e] = to_f32(q[rr * ldq + h * dh + dd]);
     Ks[e] = to_f32(k[rr * ldkv + h * dh + dd]);
     Vs[e] = to_f32(v[rr * ldkv + h * dh + dd]);
     Ds[e] = to_f32(dout[rr * ldo + h * dh + dd]);
@@ -283,9 +283,10 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
     for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
     for (int i = 0; i < L; ++i) {
       const float ds = P[(int64_t)j * L + i] * (dpv(i, j) - Dr[i]);
+      const T* qi = q + (row0 + i * st) * ldq + h * dh;
 #pragma unroll
       for (int dd = 0; dd < ATT_DH; ++dd)
-        if (dd < dh) acc[dd] = fmaf(ds, Qs[i * dh + dd], acc[dd]);
+        if (dd < dh) acc[dd] = fmaf(ds, to_f32(qi[dd]), acc[dd]);
     }
     const int64_t rj = row0 + j * st;
 #pragma unroll
@@ -440,7 +441,8 @@ __global__ void sigmoid_bwd_kernel(const float* __restrict__ y, const float* __r
 template <typename T, int E>
 __global__ __launch_bounds__(256) void lqe_bwd_kernel(const T* __restrict__ feat, int64_t fbs, int h, int w, int c,
                                                       const float* __restrict__ kps, const float* __restrict__ dst,
-                                                      int nq, int nkp, int total, float* __restrict__ dkps) {
+                                                      int nq, int nkp, int total, float* __restrict__ dkps,
+                                                      float* __restrict__ dfeat, int64_t dfbs) {
   const int lane = threadIdx.x & 63;
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= total) return;
@@ -490,6 +492,14 @@ __global__ __launch_bounds__(256) void lqe_bwd_kernel(const T* __restrict__ feat
     if (lane == winner) {
       used |= 1u << li;
       const float coef = ds[s] + dmean;
+      if (dfeat) {   // d feat: the bilinear weights of the selected channel's four corners
+        float* df = dfeat + (int64_t)b * dfbs + lane * E + li;
+#pragma unroll
+        for (int cn = 0; cn < 4; ++cn) {
+          const int xi = x0 + (cn & 1), yi = y0 + (cn >> 1);
+          if (xi >= 0 && xi < w && yi >= 0 && yi < h) atomicAdd(df + ((int64_t)yi * w + xi) * c, coef * wt[cn]);
+        }
+      }
 #pragma unroll
       for (int t = 0; t < E; ++t)
         if (t == li) {
@@ -729,8 +739,8 @@ extern "C" int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const voi
                            int64_t so, int64_t si, int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype,
                            void* stream) {
   DP_REQUIRE(q && k && v && out && p_save, "dp_attn_fwd: null pointer");
-  DP_REQUIRE(seqlen > 0 && seqlen <= 256 && dh > 0 && dh <= ATT_DH && seqlen * dh <= 8192,
-             "dp_attn_fwd: seqlen %d x dh %d (<= 256, <= 64, product <= 8192)", seqlen, dh);
+  DP_REQUIRE(seqlen > 0 && seqlen <= 1024 && dh > 0 && dh <= ATT_DH && (size_t)2 * seqlen * dh * 4 <= 160 * 1024,
+             "dp_attn_fwd: seqlen %d x dh %d (<= 1024, <= 64, K and V in 160 KB of LDS)", seqlen, dh);
   DP_REQUIRE((int64_t)n_outer * n_inner * nhead < (1ll << 31), "dp_attn_fwd: too many sequences");
   const size_t lds = (size_t)2 * seqlen * dh * 4;
   const float scale = 1.f / sqrtf((float)dh);
@@ -753,9 +763,10 @@ extern "C" int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const voi
                            void* dv, int32_t ld_dkv, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
                            int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype, void* stream) {
   DP_REQUIRE(q && k && v && p_save && dout && dq && dk && dv, "dp_attn_bwd: null pointer");
-  DP_REQUIRE(seqlen > 0 && seqlen <= 256 && dh > 0 && dh <= ATT_DH && seqlen * dh <= 8192,
-             "dp_attn_bwd: seqlen %d x dh %d (<= 256, <= 64, product <= 8192)", seqlen, dh);
-  const size_t lds = (size_t)(4 * seqlen * dh + seqlen) * 4;
+  DP_REQUIRE(seqlen > 0 && seqlen <= 1024 && dh > 0 && dh <= ATT_DH &&
+                 (size_t)(3 * seqlen * dh + seqlen) * 4 <= 160 * 1024,
+             "dp_attn_bwd: seqlen %d x dh %d (<= 1024, <= 64, K, V, dO in 160 KB of LDS)", seqlen, dh);
+  const size_t lds = (size_t)(3 * seqlen * dh + seqlen) * 4;
   const float scale = 1.f / sqrtf((float)dh);
   dim3 grid((unsigned)(n_outer * n_inner * nhead));
   hipStream_t s = as_stream(stream);
@@ -858,7 +869,7 @@ extern "C" int dp_sigmoid_bwd(const float* out, const float* dout, float* din, i
 
 extern "C" int dp_lqe_stats_bwd(const void* feat, int64_t feat_bstride, int32_t h, int32_t w, int32_t c,
                                 const float* kps, const float* dstats, int32_t batch, int32_t nq, int32_t nkp,
-                                float* dkps, int32_t dtype, void* stream) {
+                                float* dkps, float* dfeat, int64_t dfeat_bstride, int32_t dtype, void* stream) {
   DP_REQUIRE(feat && kps && dstats && dkps, "dp_lqe_stats_bwd: null pointer");
   DP_REQUIRE(c % 64 == 0 && c / 64 >= 1 && c / 64 <= 8, "dp_lqe_stats_bwd: c=%d (64..512, multiple of 64)", c);
   const int total = batch * nq * nkp;
@@ -866,7 +877,7 @@ extern "C" int dp_lqe_stats_bwd(const void* feat, int64_t feat_bstride, int32_t 
 #define DP_LQEB(T_, E_)                                                                                         \
   case E_:                                                                                                      \
     hipLaunchKernelGGL((lqe_bwd_kernel<T_, E_>), dim3(nblk(total, 4)), dim3(256), 0, s, (const T_*)feat,        \
-                       feat_bstride, h, w, c, kps, dstats, nq, nkp, total, dkps);                               \
+                       feat_bstride, h, w, c, kps, dstats, nq, nkp, total, dkps, dfeat, dfeat_bstride);         \
     break;
   if (dtype == DP_BF16) {
     switch (c / 64) { DP_LQEB(bf16_t, 1) DP_LQEB(bf16_t, 2) DP_LQEB(bf16_t, 3) DP_LQEB(bf16_t, 4) DP_LQEB(bf16_t, 5)

@@ -140,7 +140,7 @@ class MSDeformAttnFunction(torch.autograd.Function):
         lib = _lib.load()
         s = torch.cuda.current_stream(value.device).cuda_stream
         _lib.check(lib.dp_msda_bwd(value.data_ptr(), N, S, hw, nl, oa32.data_ptr(), ref.data_ptr(), go.data_ptr(), Cc,
-                                   rows // N, ctx.n_heads, Cc // ctx.n_heads, ctx.n_points, gv.data_ptr(),
+                                   rows // N, ctx.n_heads, Cc // ctx.n_heads, ctx.n_points, gv.data_ptr(), 0,
                                    goa.data_ptr(), gref.data_ptr() if gref is not None else None,
                                    _DT[value.dtype], C.c_void_p(s)), "dp_msda_bwd")
         return gv.to(value.dtype), None, goa, gref, None, None

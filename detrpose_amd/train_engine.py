@@ -750,7 +750,7 @@ class TrainPlan:
             eng.dgrad(bw, n + ".lqe0.dx", _p(dhq), nhid, qrows, qe + "0.weight", _p(dst), K * 5, wt=sd[qe + "0.weight"],
                       in_code=DP_F32)
             bw.op(n + ".lqe_stats_bwd", lib.dp_lqe_stats_bwd, _p(self.memory), self.S * Cc, lv0[0], lv0[1], Cc,
-                  _p(self.kps[l]), _p(dst), B, Qt, K, _p(self.d_kps[l]), code)
+                  _p(self.kps[l]), _p(dst), B, Qt, K, _p(self.d_kps[l]), None, 0, code)
             # class head on the instance token: score = class_embed[l](output[:, :, 0])
             ck = f"{T_}class_embed.{l}.weight"
             dlg_dt, ldl = to_dt(n + ".dlogits", dlg, qrows, ncls)
@@ -806,8 +806,8 @@ class TrainPlan:
             # MSDA: d offsets / logits (dp_msda_bwd), then the offattn Linear
             doa = f32(rows, ncol)
             bw.op(n + ".msda_bwd", lib.dp_msda_bwd, _p(self.memory), B, self.S, self.lvl_hw, len(self.shapes),
-                  _p(S_["oa"]), _p(self.refs[l]), _p(dx, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt, None, _p(doa),
-                  None, code)
+                  _p(S_["oa"]), _p(self.refs[l]), _p(dx, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt, None, 0,
+                  _p(doa), None, code)
             doa_dt, ldo = to_dt(n + ".doa", doa, rows, ncol)
             ok = lp + "cross_attn.offattn.weight"
             self._wgrad_offattn(bw, n, doa_dt, ldo, doa, rows, ok, S_["xcat"], lp)

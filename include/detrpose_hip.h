@@ -193,13 +193,13 @@ int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, const int32_t*
  * the module-level training op): offattn f32 [batch*lq][nhead*L*P*2 | nhead*L*P] = the raw
  * sampling_offsets | attention_weights Linear outputs, ref f32 [batch*lq][2]. Recomputes the
  * softmax and the sampling locations and applies the chain rule through them in the same pass:
- * grad_value f32 (zeroed here, f32 atomics) or NULL (value not differentiated), grad_offattn f32
- * (offattn layout), grad_ref f32 [batch*lq][2] or NULL (zeroed here; atomics over the heads).
- * value / grad_out of dtype; grad_out rows ld_grad_out elements apart. */
+ * grad_value f32 (f32 atomics; zeroed here first unless accumulate_value) or NULL (value not
+ * differentiated), grad_offattn f32 (offattn layout), grad_ref f32 [batch*lq][2] or NULL (zeroed
+ * here; atomics over the heads). value / grad_out of dtype; grad_out rows ld_grad_out apart. */
 int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */,
                 int32_t nlevels, const float* offattn, const float* ref, const void* grad_out, int32_t ld_grad_out,
-                int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value, float* grad_offattn,
-                float* grad_ref, int32_t dtype, void* stream);
+                int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value, int32_t accumulate_value,
+                float* grad_offattn, float* grad_ref, int32_t dtype, void* stream);
 
 /* Input pipeline of the reference benchmark (tools/benchmark/dataset.py:56-61) for one image
  * decoded to uint8 RGB (3, h, w) on the device: T.Resize to (new_h, new_w) (bilinear with
@@ -405,7 +405,8 @@ int dp_pose_loss(const dp_loss_head* heads /* host array of H */, int32_t H, int
  * backward entry points. Activations and activation gradients are of `dtype`, LayerNorm
  * statistics, parameter gradients and head tensors f32. Callers: detrpose_amd/train_engine.py. */
 
-/* C(b,m,n) = act(alpha * sum_k A(b,m,k) B(b,k,n) + bias[n] + beta * C(b,m,n)), then zeroed where
+/* C(b,m,n) = act(alpha * sum_k A(b,m,k) B(b,k,n) + bias[n] + beta * C(b,m,n)) (act: none / ReLU / GELU
+ * (erf)), then zeroed where
  * gate(b,m,n) <= 0 (ReLU backward); A(b,m,k) = a[b*a_bs + m*a_rs + k*a_ks], B(b,k,n) =
  * b[b*b_bs + k*b_ks + n*b_ns], C(b,m,n) = c[b*c_bs + m*c_rs + n]. A and B of in_dtype, C of
  * out_dtype, f32 accumulation on MFMA. split_k 0 = automatic: a launch whose M x N grid cannot
@@ -448,12 +449,14 @@ int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, float* out, in
  * != 0: query i may not see key j; nn.MultiheadAttention attn_mask semantics). Sequences and
  * rows addressed as dp_attention (row o*so + i*si + t*st; q / k / v columns h*dh of rows ld_q /
  * ld_kv apart, out ld_o). Saves P f32 [seq][head][key][query] (softmax probabilities) for the
- * backward. seqlen <= 256, dh <= 64. */
+ * backward. seqlen <= 1024, dh <= 64, K and V of a sequence within 160 KB of LDS (the decoder's
+ * 18 / 60 + DN tokens, the AIFI layer's 400: hybrid_encoder.py:276-279). */
 int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out, int32_t ld_o,
                 float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
                 int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype, void* stream);
 /* Its backward: dq / dk / dv (same addressing as q / k / v, ld_dq / ld_dkv) from dout (ld_o);
- * p_save is only read (the backward can be replayed on the same forward). */
+ * p_save is only read (the backward can be replayed on the same forward). K, V, dout of a
+ * sequence within 160 KB of LDS. */
 int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, const float* p_save,
                 const void* dout, int32_t ld_o, void* dq, int32_t ld_dq, void* dk, void* dv, int32_t ld_dkv,
                 int32_t n_outer, int32_t n_inner, int64_t so, int64_t si, int64_t st, int32_t seqlen,
@@ -491,11 +494,12 @@ int dp_pose_refine_bwd(const float* corners, const float* project, int32_t reg_m
 int dp_sigmoid_bwd(const float* out, const float* dout, float* din, int32_t rows, int32_t n, int64_t ld_out,
                    int64_t ld_dout, int64_t ld_din, void* stream);
 /* LQE statistics backward (transformer.py:275-285): dkps (+=) [batch*nq][nkp][2] from
- * dstats [batch*nq][nkp*5] through the top-4 / mean and the bilinear sampling coordinates
- * (feats[0] is detached). */
+ * dstats [batch*nq][nkp*5] through the top-4 / mean and the bilinear sampling coordinates;
+ * with dfeat != NULL also d feats[0] (+=, f32 atomics, NHWC rows of c, images dfeat_bstride
+ * apart: F.grid_sample's input gradient at the selected channels), else feats[0] is detached. */
 int dp_lqe_stats_bwd(const void* feat, int64_t feat_bstride, int32_t h, int32_t w, int32_t c, const float* kps,
-                     const float* dstats, int32_t batch, int32_t nq, int32_t nkp, float* dkps, int32_t dtype,
-                     void* stream);
+                     const float* dstats, int32_t batch, int32_t nq, int32_t nkp, float* dkps, float* dfeat,
+                     int64_t dfeat_bstride, int32_t dtype, void* stream);
 /* dst[idx[b][j]] (+)= src[b][j] rows of c (scatter of gathered rows; idx unique per image):
  * the backward of dp_gather_rows. src rows contiguous, dst rows ld apart, f32 or dtype. */
 int dp_scatter_rows(const void* src, int32_t ld_src, const int64_t* idx, int32_t batch, int32_t k, int32_t c,
@@ -534,6 +538,70 @@ int dp_zero(void* p, int64_t bytes, void* stream);
  * hand-offs): dst[r][j] = src[r][j] (+ dst when accumulate) * scale. */
 int dp_convert_rows(const void* src, int32_t src_dtype, int64_t ld_src, void* dst, int32_t dst_dtype,
                     int64_t ld_dst, int32_t rows, int32_t n, float scale, int32_t accumulate, void* stream);
+
+/* ---- HybridEncoder training step (BASELINE config 5; hybrid_encoder.py:56-212, 246-296,
+ * 462-507 in training mode). Activations are NHWC rows [rows = batch*h*w][c] with a row stride
+ * (ld, elements: channel slices of concat buffers), of dtype; statistics / parameter gradients
+ * f32. Callers: detrpose_amd/encoder_train.py. */
+
+/* nn.BatchNorm2d batch statistics, per rank: out [3][c] = (K = x[0][ch], sum (x - K), sum (x - K)^2)
+ * over the rows (single pass, shifted by the first row against cancellation). */
+int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, int32_t dtype, void* stream);
+/* Combines nparts per-rank dp_bn_stats outputs (all-gathered: SyncBatchNorm, dist_utils.py:122;
+ * `count` rows each) into mean_rstd [2][c] = (mean, 1/sqrt(biased var + eps)) and updates the
+ * running statistics as F.batch_norm does (momentum, unbiased variance; NULL: no update). */
+int dp_bn_finalize(const float* parts, int32_t nparts, float count, int32_t c, float eps, float momentum,
+                   float* running_mean, float* running_var, float* mean_rstd, void* stream);
+/* y = act(g1 (z1 - mean1) rstd1 + b1 [+ g2 (z2 - mean2) rstd2 + b2]) [+ res]: ConvNormLayer's
+ * norm + act (one branch) and VGGBlock's act(BN(conv3x3) + BN(conv1x1)) (two branches); res is
+ * the CSP sum's other operand when fused. act: DP_ACT_*. */
+int dp_bn_act_fwd(void* y, int64_t ld_y, const void* z1, int64_t ld1, const float* mr1, const float* g1,
+                  const float* b1, const void* z2, int64_t ld2, const float* mr2, const float* g2, const float* b2,
+                  const void* res, int64_t ld_res, int32_t rows, int32_t c, int32_t act, int32_t dtype, void* stream);
+/* Its backward, first pass: dp = dy * act'(pre) (pre recomputed from z / statistics); sums [3][c] =
+ * (sum dp, sum dp xhat1, sum dp xhat2) over this rank's rows (zeroed here; all-reduce them for
+ * SyncBN before the second pass) and, from the LOCAL sums, dg_k += sum dp xhat_k, db_k += sum dp
+ * (NULL to skip). */
+int dp_bn_act_bwd_reduce(const void* dy, int64_t ld_dy, const void* z1, int64_t ld1, const float* mr1,
+                         const float* g1, const float* b1, const void* z2, int64_t ld2, const float* mr2,
+                         const float* g2, const float* b2, int32_t rows, int32_t c, int32_t act, float* sums,
+                         float* dg1, float* db1, float* dg2, float* db2, int32_t dtype, void* stream);
+/* Second pass: dz_k = g_k rstd_k (dp - sum dp / count - xhat_k sum (dp xhat_k) / count), count =
+ * the rows of all ranks (batch_norm_backward_elemt). */
+int dp_bn_act_bwd_apply(void* dz1, int64_t ld_dz1, void* dz2, int64_t ld_dz2, const void* dy, int64_t ld_dy,
+                        const void* z1, int64_t ld1, const float* mr1, const float* g1, const float* b1,
+                        const void* z2, int64_t ld2, const float* mr2, const float* g2, const float* b2,
+                        int32_t rows, int32_t c, int32_t act, const float* sums, float count, int32_t dtype,
+                        void* stream);
+/* col [batch*oh*ow][cin*kh*kw] = the conv's input patches, K order (cin, ky, kx): dp_gemm of dz^T
+ * with it is the weight gradient in the reference layout [cout][cin][kh][kw]. */
+int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int32_t batch, int32_t h, int32_t w, int32_t cin,
+              int32_t kh, int32_t kw, int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* col, int32_t dtype,
+              void* stream);
+/* f32 master conv weights [cout][cin][kh][kw] -> dp_conv2d's packed layout: mode 0 [cout][kpad]
+ * (K = ky, kx, cin; the forward), mode 1 [cin][kpad] (K = ky, kx, cout, taps rotated by 180
+ * degrees: the stride-1 input gradient as a conv of dz), mode 2 depthwise taps f32 [kh*kw][cout]
+ * (cin = 1, dp_dwconv2d's layout). */
+int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out, int32_t kpad,
+                 int32_t mode, int32_t dtype, void* stream);
+/* Depthwise conv backward (k <= 3, any stride / pad): dx (+=, NULL to skip) and dw f32
+ * [c][k][k] (+=, NULL to skip) from dz. x / dz / dx: NHWC with image and pixel strides. */
+int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride, const void* dz, int64_t z_bstride,
+                  int32_t z_pstride, const float* wt, int32_t batch, int32_t h, int32_t w, int32_t c, int32_t k,
+                  int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* dx, int64_t dx_bstride,
+                  int32_t dx_pstride, float* dw, int32_t dtype, void* stream);
+/* Nearest x2 upsample of an h x w map (F.interpolate(scale_factor=2.), hybrid_encoder.py:487):
+ * backward == 0: dst (2h x 2w) = copy; backward != 0: src is the 2h x 2w gradient and dst
+ * (h x w) += its 2x2 sums. */
+int dp_upsample2x(const void* src, int64_t src_bstride, int32_t src_pstride, int32_t batch, int32_t h, int32_t w,
+                  int32_t c, void* dst, int64_t dst_bstride, int32_t dst_pstride, int32_t backward, int32_t dtype,
+                  void* stream);
+/* y (= or +=) alpha a + beta b (b may be NULL): residual sums and gradient fan-out. */
+int dp_axpby_rows(void* y, int64_t ld_y, const void* a, int64_t ld_a, float alpha, const void* b, int64_t ld_b,
+                  float beta, int32_t rows, int32_t c, int32_t accumulate, int32_t dtype, void* stream);
+/* dx = dy * act'(pre) (elementwise; the AIFI FFN's GELU backward). */
+int dp_act_bwd(const void* pre, int64_t ld_pre, const void* dy, int64_t ld_dy, void* dx, int64_t ld_dx, int32_t rows,
+               int32_t c, int32_t act, int32_t dtype, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,276 @@
+"""The HybridEncoder training kernels (csrc/encoder_train.hip, the AIFI attention in
+csrc/train.hip) through the C ABI vs torch fp32 autograd of the same ops: BatchNorm2d in
+training mode (one and two branches, SyncBN's per-rank combination, running statistics),
+its backward, the conv weight gradient via im2col + dp_gemm, the flipped-weight input
+gradient as a dp_conv2d, depthwise conv backward, nearest x2, GELU backward and 400-token
+attention (hybrid_encoder.py:56-212, 246-296). fp32 bound: 2e-4 of the output scale."""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from detrpose_amd import _lib
+from detrpose_amd._lib import DP_F32, ConvDesc, GemmDesc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+ACTS = {"silu": _lib.DP_ACT_SILU, "relu": _lib.DP_ACT_RELU, None: _lib.DP_ACT_NONE}
+
+
+def _s():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _close(got, ref, what, tol=2e-4):
+    got, ref = got.float().cpu(), ref.float().cpu()
+    scale = max(1.0, float(ref.abs().max()))
+    err = float((got - ref).abs().max())
+    print(f"{what}: max err {err:.3g} (scale {scale:.3g})")
+    assert err <= tol * scale, (what, err, scale)
+
+
+def _act(x, a):
+    return {"silu": F.silu, "relu": F.relu, None: lambda t: t}[a](x)
+
+
+def bn_stats(lib, z, count_parts=1):
+    """per-part dp_bn_stats over row splits, then dp_bn_finalize: (mean_rstd, parts)."""
+    rows, c = z.shape
+    parts = torch.zeros(count_parts, 3, c, device=DEV)
+    per = rows // count_parts
+    for p in range(count_parts):
+        zp = z[p * per:(p + 1) * per]
+        _lib.check(lib.dp_bn_stats(zp.data_ptr(), c, per, c, parts[p].data_ptr(), DP_F32, _s()), "bn_stats")
+    return parts, per
+
+
+@pytest.mark.parametrize("two,act,nparts", [(False, "silu", 1), (True, "relu", 1), (False, None, 2), (True, "silu", 2)])
+def test_bn_act_train_forward_backward(two, act, nparts):
+    lib = _lib.load()
+    torch.manual_seed(3 + nparts)
+    B, H, W, c = 4, 9, 7, 96
+    rows = B * H * W
+    z1 = (torch.randn(rows, c, device=DEV) * 2 + 3).requires_grad_(True)
+    z2 = (torch.randn(rows, c, device=DEV) - 1).requires_grad_(True)
+    g1, b1 = torch.randn(c, device=DEV).requires_grad_(True), torch.randn(c, device=DEV).requires_grad_(True)
+    g2, b2 = torch.randn(c, device=DEV).requires_grad_(True), torch.randn(c, device=DEV).requires_grad_(True)
+    rm1, rv1 = torch.randn(c, device=DEV), torch.rand(c, device=DEV) + 0.5
+    rm1_ref, rv1_ref = rm1.clone(), rv1.clone()
+    pre = F.batch_norm(z1, rm1_ref, rv1_ref, g1, b1, True, 0.1, 1e-5)
+    if two:
+        pre = pre + F.batch_norm(z2, None, None, g2, b2, True, 0.1, 1e-5)
+    y_ref = _act(pre, act)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    # forward on the kernels (SyncBN: per-part statistics combined)
+    mr1, mr2 = torch.empty(2, c, device=DEV), torch.empty(2, c, device=DEV)
+    parts, per = bn_stats(lib, z1.detach(), nparts)
+    _lib.check(lib.dp_bn_finalize(parts.data_ptr(), nparts, float(per), c, 1e-5, 0.1, rm1.data_ptr(), rv1.data_ptr(),
+                                  mr1.data_ptr(), _s()), "finalize")
+    if two:
+        parts2, _ = bn_stats(lib, z2.detach(), nparts)
+        _lib.check(lib.dp_bn_finalize(parts2.data_ptr(), nparts, float(per), c, 1e-5, 0.1, None, None,
+                                      mr2.data_ptr(), _s()), "finalize2")
+    y = torch.empty(rows, c, device=DEV)
+    zp2 = z2.detach() if two else None
+    _lib.check(lib.dp_bn_act_fwd(y.data_ptr(), c, z1.detach().data_ptr(), c, mr1.data_ptr(), g1.detach().data_ptr(),
+                                 b1.detach().data_ptr(), zp2.data_ptr() if two else None, c,
+                                 mr2.data_ptr() if two else None, g2.detach().data_ptr() if two else None,
+                                 b2.detach().data_ptr() if two else None, None, 0, rows, c, ACTS[act], DP_F32, _s()),
+               "bn_act_fwd")
+    torch.cuda.synchronize()
+    _close(y, y_ref, f"bn fwd two={two} {act}")
+    _close(rm1, rm1_ref, "running mean", 1e-5)
+    _close(rv1, rv1_ref, "running var", 1e-5)
+    # backward: reduce (+ the SyncBN all-reduce, here one rank) then apply
+    sums = torch.empty(3, c, device=DEV)
+    dg1, db1, dg2, db2 = (torch.zeros(c, device=DEV) for _ in range(4))
+    _lib.check(lib.dp_bn_act_bwd_reduce(dy.data_ptr(), c, z1.detach().data_ptr(), c, mr1.data_ptr(),
+                                        g1.detach().data_ptr(), b1.detach().data_ptr(),
+                                        zp2.data_ptr() if two else None, c, mr2.data_ptr() if two else None,
+                                        g2.detach().data_ptr() if two else None,
+                                        b2.detach().data_ptr() if two else None, rows, c, ACTS[act], sums.data_ptr(),
+                                        dg1.data_ptr(), db1.data_ptr(), dg2.data_ptr() if two else None,
+                                        db2.data_ptr() if two else None, DP_F32, _s()), "bn_bwd_reduce")
+    dz1, dz2 = torch.empty(rows, c, device=DEV), torch.empty(rows, c, device=DEV)
+    _lib.check(lib.dp_bn_act_bwd_apply(dz1.data_ptr(), c, dz2.data_ptr() if two else None, c, dy.data_ptr(), c,
+                                       z1.detach().data_ptr(), c, mr1.data_ptr(), g1.detach().data_ptr(),
+                                       b1.detach().data_ptr(), zp2.data_ptr() if two else None, c,
+                                       mr2.data_ptr() if two else None, g2.detach().data_ptr() if two else None,
+                                       b2.detach().data_ptr() if two else None, rows, c, ACTS[act], sums.data_ptr(),
+                                       float(rows), DP_F32, _s()), "bn_bwd_apply")
+    torch.cuda.synchronize()
+    _close(dz1, z1.grad, "dz1")
+    _close(dg1, g1.grad, "dgamma1")
+    _close(db1, b1.grad, "dbeta1")
+    if two:
+        _close(dz2, z2.grad, "dz2")
+        _close(dg2, g2.grad, "dgamma2")
+        _close(db2, b2.grad, "dbeta2")
+
+
+def _conv_desc(x, w_packed, kpad, cin, cout, h, w, k, out, res=None, B=2):
+    d = ConvDesc()
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = x.data_ptr(), h * w * cin, cin, h, w, cin
+    d.weight, d.kpad, d.bias = w_packed.data_ptr(), kpad, None
+    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = k, k, 1, (k - 1) // 2, (k - 1) // 2
+    d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out.data_ptr(), h * w * cout, cout, h, w, cout
+    if res is not None:
+        d.res, d.res_bstride, d.res_pstride = res.data_ptr(), h * w * cout, cout
+    d.batch, d.act, d.dtype = B, 0, DP_F32
+    return d
+
+
+@pytest.mark.parametrize("k,cin,cout", [(3, 64, 96), (1, 128, 64), (3, 32, 32)])
+def test_conv_pack_forward_dgrad_wgrad(k, cin, cout):
+    """Packed forward == F.conv2d; the 180-degree-rotated packing run as a conv of dz == the input
+    gradient (accumulated through the residual input); im2col (cin, ky, kx) + dp_gemm == the
+    weight gradient in the reference layout."""
+    lib = _lib.load()
+    torch.manual_seed(k * cin)
+    B, h, w = 2, 11, 13
+    wt = torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5
+    x = torch.randn(B, cin, h, w, device=DEV).requires_grad_(True)
+    wr = wt.clone().requires_grad_(True)
+    y = F.conv2d(x, wr, None, 1, (k - 1) // 2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xn = x.detach().permute(0, 2, 3, 1).contiguous()
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    kpad = (k * k * cin + 31) // 32 * 32
+    wp = torch.empty(cout, kpad, device=DEV)
+    _lib.check(lib.dp_conv_pack(wt.data_ptr(), cout, cin, k, k, wp.data_ptr(), kpad, 0, DP_F32, _s()), "pack")
+    out = torch.empty(B, h, w, cout, device=DEV)
+    d = _conv_desc(xn, wp, kpad, cin, cout, h, w, k, out)
+    _lib.check(lib.dp_conv2d(C.byref(d), _s()), "fwd")
+    torch.cuda.synchronize()
+    _close(out, y.detach().permute(0, 2, 3, 1), f"conv{k} fwd")
+    # input gradient: conv of dz with the rotated packing, accumulated onto a prior value
+    kpad2 = (k * k * cout + 31) // 32 * 32
+    wf = torch.empty(cin, kpad2, device=DEV)
+    _lib.check(lib.dp_conv_pack(wt.data_ptr(), cout, cin, k, k, wf.data_ptr(), kpad2, 1, DP_F32, _s()), "flip")
+    prior = torch.randn(B, h, w, cin, device=DEV)
+    dx = prior.clone()
+    d2 = _conv_desc(dyn, wf, kpad2, cout, cin, h, w, k, dx, res=dx)
+    _lib.check(lib.dp_conv2d(C.byref(d2), _s()), "dgrad")
+    torch.cuda.synchronize()
+    _close(dx, prior + x.grad.permute(0, 2, 3, 1), f"conv{k} dgrad")
+    # weight gradient
+    rows, K = B * h * w, cin * k * k
+    col = torch.empty(rows, K, device=DEV)
+    _lib.check(lib.dp_im2col(xn.data_ptr(), h * w * cin, cin, B, h, w, cin, k, k, 1, (k - 1) // 2, h, w,
+                             col.data_ptr(), DP_F32, _s()), "im2col")
+    dW = torch.zeros(cout, K, device=DEV)
+    g = GemmDesc()
+    g.a, g.a_bs, g.a_rs, g.a_ks = dyn.data_ptr(), 0, 1, cout
+    g.b, g.b_bs, g.b_ks, g.b_ns = col.data_ptr(), 0, K, 1
+    g.c, g.c_bs, g.c_rs = dW.data_ptr(), 0, K
+    g.batch, g.m, g.n, g.k = 1, cout, K, rows
+    g.in_dtype, g.out_dtype = DP_F32, DP_F32
+    g.alpha, g.beta = 1.0, 1.0
+    _lib.check(lib.dp_gemm(C.byref(g), _s()), "wgrad")
+    torch.cuda.synchronize()
+    _close(dW.view(cout, cin, k, k), wr.grad, f"conv{k} wgrad")
+
+
+def test_depthwise_s2_backward_and_pack():
+    """SCDown's depthwise 3x3 stride-2 conv (hybrid_encoder.py:156-170): dp_conv_pack mode 2 +
+    dp_dwconv2d forward, dp_dwconv_bwd input and weight gradients vs autograd."""
+    lib = _lib.load()
+    torch.manual_seed(9)
+    B, c, h, w = 2, 64, 17, 12
+    wt = torch.randn(c, 1, 3, 3, device=DEV)
+    x = torch.randn(B, c, h, w, device=DEV).requires_grad_(True)
+    wr = wt.clone().requires_grad_(True)
+    y = F.conv2d(x, wr, None, 2, 1, 1, c)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    oh, ow = y.shape[2:]
+    taps = torch.empty(9, c, device=DEV)
+    _lib.check(lib.dp_conv_pack(wt.data_ptr(), c, 1, 3, 3, taps.data_ptr(), 0, 2, DP_F32, _s()), "pack dw")
+    xn = x.detach().permute(0, 2, 3, 1).contiguous()
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    d = ConvDesc()
+    out = torch.empty(B, oh, ow, c, device=DEV)
+    d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = xn.data_ptr(), h * w * c, c, h, w, c
+    d.weight, d.kpad, d.bias = taps.data_ptr(), 0, None
+    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = 3, 3, 2, 1, 1
+    d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out.data_ptr(), oh * ow * c, c, oh, ow, c
+    d.batch, d.act, d.dtype = B, 0, DP_F32
+    _lib.check(lib.dp_dwconv2d(C.byref(d), _s()), "dw fwd")
+    dx = torch.zeros(B, h, w, c, device=DEV)
+    dw = torch.zeros(c, 3, 3, device=DEV)
+    _lib.check(lib.dp_dwconv_bwd(xn.data_ptr(), h * w * c, c, dyn.data_ptr(), oh * ow * c, c, taps.data_ptr(), B, h, w,
+                                 c, 3, 2, 1, oh, ow, dx.data_ptr(), h * w * c, c, dw.data_ptr(), DP_F32, _s()), "dw bwd")
+    torch.cuda.synchronize()
+    _close(out, y.detach().permute(0, 2, 3, 1), "dw fwd")
+    _close(dx, x.grad.permute(0, 2, 3, 1), "dw dx")
+    _close(dw, wr.grad.view(c, 3, 3), "dw dw")
+
+
+def test_upsample_axpby_gelu_backward():
+    lib = _lib.load()
+    torch.manual_seed(2)
+    B, h, w, c, ld = 2, 5, 6, 32, 80
+    x = torch.randn(B, h, w, c, device=DEV)
+    big = torch.zeros(B, 2 * h, 2 * w, ld, device=DEV)
+    _lib.check(lib.dp_upsample2x(x.data_ptr(), h * w * c, c, B, h, w, c, big[..., 16:].data_ptr(), 4 * h * w * ld, ld,
+                                 0, DP_F32, _s()), "up fwd")
+    ref = F.interpolate(x.permute(0, 3, 1, 2), scale_factor=2.0, mode="nearest").permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    _close(big[..., 16:16 + c], ref, "up fwd")
+    dbig = torch.randn(B, 2 * h, 2 * w, c, device=DEV)
+    dx = torch.ones(B, h, w, c, device=DEV)
+    _lib.check(lib.dp_upsample2x(dbig.data_ptr(), 4 * h * w * c, c, B, h, w, c, dx.data_ptr(), h * w * c, c, 1, DP_F32,
+                                 _s()), "up bwd")
+    want = 1 + F.avg_pool2d(dbig.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1) * 4
+    torch.cuda.synchronize()
+    _close(dx, want, "up bwd")
+    rows = B * h * w
+    a, b = torch.randn(rows, c, device=DEV), torch.randn(rows, c, device=DEV)
+    y = torch.randn(rows, c, device=DEV)
+    y0 = y.clone()
+    _lib.check(lib.dp_axpby_rows(y.data_ptr(), c, a.data_ptr(), c, 2.0, b.data_ptr(), c, -0.5, rows, c, 1, DP_F32, _s()),
+               "axpby")
+    torch.cuda.synchronize()
+    _close(y, y0 + 2 * a - 0.5 * b, "axpby")
+    pre = torch.randn(rows, c, device=DEV).requires_grad_(True)
+    g = F.gelu(pre)
+    dyy = torch.randn_like(g)
+    g.backward(dyy)
+    dxx = torch.empty(rows, c, device=DEV)
+    _lib.check(lib.dp_act_bwd(pre.detach().data_ptr(), c, dyy.data_ptr(), c, dxx.data_ptr(), c, rows, c, _lib.DP_ACT_GELU, DP_F32,
+                              _s()), "gelu bwd")
+    torch.cuda.synchronize()
+    _close(dxx, pre.grad, "gelu bwd")
+
+
+@pytest.mark.parametrize("C_,nh", [(128, 8), (256, 8)])
+def test_attention_400_tokens(C_, nh):
+    """The AIFI self-attention core (400 tokens of a 20 x 20 map, hybrid_encoder.py:276-279):
+    dp_attn_fwd / dp_attn_bwd vs autograd, q / k / v slices of one [rows][3C] buffer."""
+    lib = _lib.load()
+    torch.manual_seed(C_)
+    B, L = 2, 400
+    dh = C_ // nh
+    qkv = torch.randn(B, L, 3 * C_, device=DEV)
+    t = qkv.clone().requires_grad_(True)
+    q, k, v = t.split(C_, -1)
+    sh = lambda z: z.reshape(B, L, nh, dh).transpose(1, 2)   # noqa: E731
+    o = (torch.softmax(sh(q) @ sh(k).transpose(-1, -2) / dh ** 0.5, -1) @ sh(v)).transpose(1, 2).reshape(B, L, C_)
+    do = torch.randn_like(o)
+    o.backward(do)
+    out = torch.empty(B, L, C_, device=DEV)
+    P = torch.empty(B * nh, L, L, device=DEV)
+    base = qkv.data_ptr()
+    _lib.check(lib.dp_attn_fwd(base, 3 * C_, base + 4 * C_, base + 8 * C_, 3 * C_, out.data_ptr(), C_, P.data_ptr(), None,
+                               B, 1, L, 0, 1, L, nh, dh, DP_F32, _s()), "attn fwd")
+    d = torch.zeros(B, L, 3 * C_, device=DEV)
+    db = d.data_ptr()
+    _lib.check(lib.dp_attn_bwd(base, 3 * C_, base + 4 * C_, base + 8 * C_, 3 * C_, P.data_ptr(), do.data_ptr(), C_, db,
+                               3 * C_, db + 4 * C_, db + 8 * C_, 3 * C_, B, 1, L, 0, 1, L, nh, dh, DP_F32, _s()),
+               "attn bwd")
+    torch.cuda.synchronize()
+    _close(out, o.detach(), "attn400 fwd")
+    _close(d, t.grad, "attn400 bwd")

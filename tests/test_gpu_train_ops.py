@@ -172,19 +172,21 @@ def test_pose_refine_and_lqe_bwd():
     _lib.check(lib.dp_pose_refine_bwd(corners.data_ptr(), proj.data_ptr(), reg_max, s, dk.data_ptr(), rows, K,
                                       dc.data_ptr(), 0, _s()), "refine_bwd")
     assert torch.allclose(dc, c_.grad, atol=1e-5)
-    # LQE stats backward (feat detached)
+    # LQE stats backward: d keypoints, and d feats[0] (F.grid_sample's input gradient)
     B, Q, h, w, c = 2, 6, 20, 20, 128
     feat = torch.randn(B, h, w, c, device=DEV)
     kp = (torch.rand(B, Q, K, 2, device=DEV) * 1.1 - 0.05).requires_grad_(True)
-    sv = bilinear_gather(feat.cpu(), kp.detach().cpu().reshape(B, Q * K, 2))   # value check helper
     kpc = kp.detach().cpu().requires_grad_(True)
-    sv = bilinear_gather(feat.cpu(), kpc.reshape(B, Q * K, 2)).reshape(B, Q, K, c)
+    featc = feat.cpu().requires_grad_(True)
+    sv = bilinear_gather(featc, kpc.reshape(B, Q * K, 2)).reshape(B, Q, K, c)
     top = sv.topk(4, dim=-1)[0]
     stat = torch.cat([top, top.mean(-1, keepdim=True)], -1)
     dstat = torch.randn_like(stat)
     stat.backward(dstat)
     dkp = torch.zeros(B, Q, K, 2, device=DEV)
+    dfeat = torch.zeros(B, h, w, c, device=DEV)
     _lib.check(lib.dp_lqe_stats_bwd(feat.data_ptr(), h * w * c, h, w, c, kp.detach().contiguous().data_ptr(),
-                                    dstat.to(DEV).contiguous().data_ptr(), B, Q, K, dkp.data_ptr(), DP_F32, _s()),
-               "lqe_bwd")
+                                    dstat.to(DEV).contiguous().data_ptr(), B, Q, K, dkp.data_ptr(), dfeat.data_ptr(),
+                                    h * w * c, DP_F32, _s()), "lqe_bwd")
     assert torch.allclose(dkp.cpu(), kpc.grad, atol=1e-3), (dkp.cpu() - kpc.grad).abs().max()
+    assert torch.allclose(dfeat.cpu(), featc.grad, atol=1e-5), (dfeat.cpu() - featc.grad).abs().max()
