@@ -138,7 +138,7 @@ _SIGS = {
     "dp_pose_refine_bwd": (i32, [vp, vp, i32, f32, vp, i32, i32, vp, i32, vp]),
     "dp_sigmoid_bwd": (i32, [vp, vp, vp, i32, i32, i64, i64, i64, vp]),
     "dp_lqe_stats_bwd": (i32, [vp, i64, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp, i64, i32, vp]),
-    "dp_scatter_rows": (i32, [vp, i32, vp, i32, i32, i32, vp, i64, i32, i32, i32, vp]),
+    "dp_scatter_rows": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, vp, i64, i32, i32, i32, vp]),
     "dp_gather_rows_masked": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, vp, i32, vp]),
     "dp_convert_rows": (i32, [vp, i32, i64, vp, i32, i64, i32, i32, f32, i32, vp]),
     "dp_zero": (i32, [vp, i64, vp]),
@@ -154,7 +154,7 @@ _SIGS = {
     "dp_bn_act_bwd_apply": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32,
                                   vp, f32, i32, vp]),
     "dp_im2col": (i32, [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
-    "dp_conv_pack": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, vp]),
+    "dp_conv_pack": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, i32, vp]),
     "dp_dwconv_bwd": (i32, [vp, i64, i32, vp, i64, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, i32,
                             vp, i32, vp]),
     "dp_upsample2x": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, i32, vp]),

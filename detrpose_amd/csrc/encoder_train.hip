@@ -213,10 +213,11 @@ __global__ void im2col_kernel(const T* __restrict__ x, int64_t bs, int ps, int h
 
 // f32 master weights [cout][cin][kh][kw] -> the conv kernels' packed [rows][kpad] (K = ky, kx, ci):
 // mode 0 forward (rows = cout), mode 1 input gradient (rows = cin, K over cout, taps flipped),
-// mode 2 depthwise taps [kh*kw][c] f32 (cin = 1)
+// mode 2 depthwise taps [kh*kw][c] f32 (cin = 1). kc: the K dimension's channel stride (>= the
+// real channel count: maps whose channels are padded to a vector multiple), zero in the pads
 template <typename T>
 __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin, int kh, int kw, void* __restrict__ out,
-                                 int kpad, int mode) {
+                                 int kpad, int kc, int mode) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (mode == 2) {
     if (e >= (int64_t)cout * kh * kw) return;
@@ -229,8 +230,8 @@ __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin,
   if (e >= (int64_t)rows * kpad) return;
   const int r = (int)(e / kpad), k = (int)(e % kpad);
   float v = 0.f;
-  if (k < kh * kw * inner) {
-    const int tap = k / inner, j = k - tap * inner;
+  const int tap = k / kc, j = k - tap * kc;
+  if (tap < kh * kw && j < inner) {
     const int ky = tap / kw, kx = tap - ky * kw;
     v = mode == 0 ? w[(((int64_t)r * cin + j) * kh + ky) * kw + kx]
                   : w[(((int64_t)j * cin + r) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)];
@@ -442,13 +443,14 @@ extern "C" int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int32_
 }
 
 extern "C" int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out, int32_t kpad,
-                            int32_t mode, int32_t dtype, void* stream) {
+                            int32_t kc, int32_t mode, int32_t dtype, void* stream) {
+  if (kc <= 0) kc = mode == 0 ? cin : cout;
   DP_REQUIRE(w && out && cout > 0 && cin > 0 && mode >= 0 && mode <= 2 &&
-                 (mode == 2 ? cin == 1 : kpad >= kh * kw * (mode == 0 ? cin : cout)),
+                 (mode == 2 ? cin == 1 : (kc >= (mode == 0 ? cin : cout) && kpad >= kh * kw * kc)),
              "dp_conv_pack: bad arguments");
   const int64_t total = mode == 2 ? (int64_t)cout * kh * kw : (int64_t)(mode == 0 ? cout : cin) * kpad;
   DP_DT(hipLaunchKernelGGL(conv_pack_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
-                           w, cout, cin, kh, kw, out, kpad, mode));
+                           w, cout, cin, kh, kw, out, kpad, kc, mode));
   return dp_check_launch("dp_conv_pack");
 }
 

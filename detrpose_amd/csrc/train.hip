@@ -518,14 +518,16 @@ __global__ __launch_bounds__(256) void lqe_bwd_kernel(const T* __restrict__ feat
 
 // ---------------------------------------------------------------- row moves
 template <typename T>
-__global__ void scatter_rows_kernel(const T* __restrict__ src, int lds, const int64_t* __restrict__ idx, int k, int c,
-                                    T* __restrict__ dst, int64_t dbs, int ldd, int acc, int64_t total) {
+__global__ void scatter_rows_kernel(const T* __restrict__ src, int lds, const int64_t* __restrict__ idx,
+                                    const uint8_t* __restrict__ mask, int period, int k, int c, T* __restrict__ dst,
+                                    int64_t dbs, int ldd, int acc, int64_t total) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int ch = (int)(e % c);
   const int64_t rj = e / c;   // b * k + j
   const int b = (int)(rj / k);
   const int64_t dr = idx[rj];
+  if (mask && mask[dr % period]) return;   // masked_fill'ed row: no gradient reaches it
   T* p = dst + (int64_t)b * dbs + dr * ldd + ch;
   float v = to_f32(src[rj * lds + ch]);
   if (acc) v += to_f32(*p);
@@ -890,18 +892,19 @@ extern "C" int dp_lqe_stats_bwd(const void* feat, int64_t feat_bstride, int32_t 
   return dp_check_launch("dp_lqe_stats_bwd");
 }
 
-extern "C" int dp_scatter_rows(const void* src, int32_t ld_src, const int64_t* idx, int32_t batch, int32_t k,
-                               int32_t c, void* dst, int64_t dst_bstride, int32_t ld_dst, int32_t accumulate,
-                               int32_t dtype, void* stream) {
-  DP_REQUIRE(src && idx && dst && batch > 0 && k > 0 && c > 0, "dp_scatter_rows: bad arguments");
+extern "C" int dp_scatter_rows(const void* src, int32_t ld_src, const int64_t* idx, const uint8_t* row_mask,
+                               int32_t mask_period, int32_t batch, int32_t k, int32_t c, void* dst,
+                               int64_t dst_bstride, int32_t ld_dst, int32_t accumulate, int32_t dtype, void* stream) {
+  DP_REQUIRE(src && idx && dst && batch > 0 && k > 0 && c > 0 && (!row_mask || mask_period > 0),
+             "dp_scatter_rows: bad arguments");
   const int64_t total = (int64_t)batch * k * c;
   hipStream_t s = as_stream(stream);
   if (dtype == DP_BF16)
     hipLaunchKernelGGL(scatter_rows_kernel<bf16_t>, dim3(nblk(total, 256)), dim3(256), 0, s, (const bf16_t*)src, ld_src,
-                       idx, k, c, (bf16_t*)dst, dst_bstride, ld_dst, accumulate, total);
+                       idx, row_mask, mask_period, k, c, (bf16_t*)dst, dst_bstride, ld_dst, accumulate, total);
   else
     hipLaunchKernelGGL(scatter_rows_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, (const float*)src, ld_src,
-                       idx, k, c, (float*)dst, dst_bstride, ld_dst, accumulate, total);
+                       idx, row_mask, mask_period, k, c, (float*)dst, dst_bstride, ld_dst, accumulate, total);
   return dp_check_launch("dp_scatter_rows");
 }
 

@@ -89,8 +89,9 @@ class TrainEngine:
     dtype 'fp32' (parity mode) or 'bf16' (bf16 activations and activation gradients, f32
     accumulation, f32 LayerNorm statistics, f32 heads and parameter gradients)."""
 
-    def __init__(self, model, dtype="fp32", device="cuda"):
+    def __init__(self, model, dtype="fp32", device="cuda", train_encoder=False):
         self.lib = _lib.load()
+        self.train_encoder = train_encoder
         self.model = model
         self.tr = tr = model.transformer
         self.dtype_name = dtype
@@ -110,7 +111,10 @@ class TrainEngine:
         self.ncls = tr.num_classes
         # parameters: one f32 master buffer (the optimizer's), gradients and AdamW moments of
         # the same layout, views under the reference names
-        self.pnames = [n for n, p in model.named_parameters() if n.startswith(T_) and p.requires_grad]
+        # the transformer's parameters; with train_encoder also the HybridEncoder's
+        # (detrpose_amd/encoder_train.py), whose BatchNorm running statistics live in `running`
+        pref = (T_, "encoder.") if train_encoder else (T_,)
+        self.pnames = [n for n, p in model.named_parameters() if n.startswith(pref) and p.requires_grad]
         shapes = {n: tuple(p.shape) for n, p in model.named_parameters()}
         # each parameter starts on a 256-byte boundary (16-byte vector loads of any view)
         sizes = [(int(np.prod(shapes[n])) + 63) // 64 * 64 for n in self.pnames]
@@ -129,8 +133,14 @@ class TrainEngine:
             self.grads[n] = self.grad_flat[o:o + k].view(shapes[n])
             self.params[n] = self.master[o:o + k].view(shapes[n])
             o += sz
+        self.running = {}
+        if train_encoder:
+            for n, b in model.named_buffers():
+                if n.startswith("encoder.") and (n.endswith(".running_mean") or n.endswith(".running_var")):
+                    self.running[n] = b.detach().to(dev, torch.float32).clone()
         self.load_weights()
         self.plans = {}
+        self.enc_plans = {}
 
     # ------------------------------------------------------------------ weights
     def load_weights(self):
@@ -229,6 +239,9 @@ class TrainEngine:
             for n, p in module.named_parameters():
                 if n in self.params:
                     p.copy_(self.params[n].to(p.device, p.dtype))
+            for n, b in module.named_buffers():
+                if n in self.running:
+                    b.copy_(self.running[n].to(b.device, b.dtype))
 
     # ------------------------------------------------------------------ launch helpers
     def _gemm(self, tape, name, a, a_rs, a_ks, b, b_ks, b_ns, c, c_rs, m, n, k, in_code, out_code, bias=None,
@@ -283,20 +296,32 @@ class TrainEngine:
             self.cur.cost(name + ".db", 4.0 * rows * N)
 
     # ------------------------------------------------------------------ plan
-    def plan(self, batch: int, pad: int, shapes, memory=None) -> "TrainPlan":
+    def plan(self, batch: int, pad: int, shapes, memory=None, d_memory=None) -> "TrainPlan":
         """memory: an existing (B, S, C) device buffer of dtype the plan reads the encoder memory
-        from (e.g. the inference plan's), instead of its own input buffer."""
-        key = (batch, pad, tuple(tuple(s) for s in shapes), memory.data_ptr() if memory is not None else None)
+        from (e.g. the inference plan's), instead of its own input buffer. d_memory: a (B, S, C)
+        f32 buffer the backward writes d loss / d memory into (the encoder's training step)."""
+        key = (batch, pad, tuple(tuple(s) for s in shapes), memory.data_ptr() if memory is not None else None,
+               d_memory.data_ptr() if d_memory is not None else None)
         if key not in self.plans:
-            self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes], memory)
+            self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes], memory, d_memory)
         return self.plans[key]
+
+    def encoder_plan(self, batch: int, feat_shapes):
+        """The HybridEncoder's training forward / backward (encoder_train.EncoderTrainPlan)."""
+        assert self.train_encoder, "TrainEngine(train_encoder=True) trains the encoder"
+        from .encoder_train import EncoderTrainPlan
+        key = (batch, tuple(tuple(s) for s in feat_shapes))
+        if key not in self.enc_plans:
+            self.enc_plans[key] = EncoderTrainPlan(self, batch, feat_shapes)
+        return self.enc_plans[key]
 
 
 class TrainPlan:
     """Buffers and tapes for one (batch, DN pad size, feature shapes)."""
 
-    def __init__(self, eng: TrainEngine, B: int, P: int, shapes, memory=None):
+    def __init__(self, eng: TrainEngine, B: int, P: int, shapes, memory=None, d_memory=None):
         self.eng = eng
+        self.d_memory = d_memory
         eng.cur = self
         self.B, self.P, self.shapes = B, P, shapes
         self.op_flops = {}
@@ -722,6 +747,10 @@ class TrainPlan:
 
         self.ones = torch.ones(ncls, dtype=torch.float32, device=dev)
         bw.op("bw.zero", lib.dp_zero, _p(eng.grad_flat), eng.grad_flat.numel() * 4)
+        dm = self.d_memory   # d loss / d memory (f32): MSDA value, LQE feats[0], two-stage rows
+        if dm is not None:
+            assert dm.dtype == torch.float32 and dm.numel() == B * self.S * Cc
+            bw.op("bw.zero_dmem", lib.dp_zero, _p(dm), dm.numel() * 4)
         dY = buf(rows, Cc)
         bw.op("bw.dY0", lib.dp_zero, _p(dY), rows * Cc * e)
         dcorn = f32(krows, nb)
@@ -750,7 +779,8 @@ class TrainPlan:
             eng.dgrad(bw, n + ".lqe0.dx", _p(dhq), nhid, qrows, qe + "0.weight", _p(dst), K * 5, wt=sd[qe + "0.weight"],
                       in_code=DP_F32)
             bw.op(n + ".lqe_stats_bwd", lib.dp_lqe_stats_bwd, _p(self.memory), self.S * Cc, lv0[0], lv0[1], Cc,
-                  _p(self.kps[l]), _p(dst), B, Qt, K, _p(self.d_kps[l]), None, 0, code)
+                  _p(self.kps[l]), _p(dst), B, Qt, K, _p(self.d_kps[l]), _p(dm) if dm is not None else None,
+                  self.S * Cc, code)
             # class head on the instance token: score = class_embed[l](output[:, :, 0])
             ck = f"{T_}class_embed.{l}.weight"
             dlg_dt, ldl = to_dt(n + ".dlogits", dlg, qrows, ncls)
@@ -806,8 +836,8 @@ class TrainPlan:
             # MSDA: d offsets / logits (dp_msda_bwd), then the offattn Linear
             doa = f32(rows, ncol)
             bw.op(n + ".msda_bwd", lib.dp_msda_bwd, _p(self.memory), B, self.S, self.lvl_hw, len(self.shapes),
-                  _p(S_["oa"]), _p(self.refs[l]), _p(dx, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt, None, 0,
-                  _p(doa), None, code)
+                  _p(S_["oa"]), _p(self.refs[l]), _p(dx, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt,
+                  _p(dm) if dm is not None else None, 1, _p(doa), None, code)
             doa_dt, ldo = to_dt(n + ".doa", doa, rows, ncol)
             ok = lp + "cross_attn.offattn.weight"
             self._wgrad_offattn(bw, n, doa_dt, ldo, doa, rows, ok, S_["xcat"], lp)
@@ -870,6 +900,14 @@ class TrainPlan:
               _p(sd[T_ + "enc_output_norm.weight"]), B * nq, Cc, _p(eng.grads[T_ + "enc_output_norm.weight"]),
               _p(eng.grads[T_ + "enc_output_norm.bias"]), 0, code)
         eng.wgrad(bw, "bw.ts.enc_output", _p(dsel), Cc, B * nq, T_ + "enc_output.weight", _p(xs), Cc)
+        if dm is not None:
+            # d memory on the selected rows (memory.masked_fill(~valid_mask, 0): none to masked rows)
+            dxs = f32(B * nq, Cc)
+            W = eng.w[T_ + "enc_output.weight"]
+            eng._gemm(bw, "bw.ts.enc_output.dx", _p(dsel), Cc, 1, _p(W), Cc, 1, _p(dxs), Cc, B * nq, Cc, Cc, code,
+                      DP_F32)
+            bw.op("bw.ts.dmem", lib.dp_scatter_rows, _p(dxs), Cc, _p(self.topi), _p(eng.mask_u8), self.S, B, nq, Cc,
+                  _p(dm), self.S * Cc, Cc, 1, DP_F32)
 
     def _wgrad_offattn(self, bw, n, doa_dt, ldo, doa32, rows, okey, xcat, lp):
         """The fused offsets | logits Linear's weight / bias gradients, written into the two

@@ -501,10 +501,12 @@ int dp_lqe_stats_bwd(const void* feat, int64_t feat_bstride, int32_t h, int32_t 
                      const float* dstats, int32_t batch, int32_t nq, int32_t nkp, float* dkps, float* dfeat,
                      int64_t dfeat_bstride, int32_t dtype, void* stream);
 /* dst[idx[b][j]] (+)= src[b][j] rows of c (scatter of gathered rows; idx unique per image):
- * the backward of dp_gather_rows. src rows contiguous, dst rows ld apart, f32 or dtype. */
-int dp_scatter_rows(const void* src, int32_t ld_src, const int64_t* idx, int32_t batch, int32_t k, int32_t c,
-                    void* dst, int64_t dst_bstride, int32_t ld_dst, int32_t accumulate, int32_t dtype,
-                    void* stream);
+ * the backward of dp_gather_rows (of dp_gather_rows_masked with row_mask: rows whose
+ * row_mask[idx % mask_period] != 0 receive nothing, memory.masked_fill's gradient). src rows
+ * ld_src apart, dst rows ld apart, f32 or dtype. */
+int dp_scatter_rows(const void* src, int32_t ld_src, const int64_t* idx, const uint8_t* row_mask,
+                    int32_t mask_period, int32_t batch, int32_t k, int32_t c, void* dst, int64_t dst_bstride,
+                    int32_t ld_dst, int32_t accumulate, int32_t dtype, void* stream);
 /* dst[b][j] = src[b][idx[b][j]] rows of c, zero where row_mask[idx % mask_period] != 0: the
  * masked memory rows the two-stage selection picked (memory.masked_fill(valid_mask, 0),
  * transformer.py:1221), for the enc_output backward on the selected rows only. */
@@ -581,9 +583,10 @@ int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int32_t batch, in
 /* f32 master conv weights [cout][cin][kh][kw] -> dp_conv2d's packed layout: mode 0 [cout][kpad]
  * (K = ky, kx, cin; the forward), mode 1 [cin][kpad] (K = ky, kx, cout, taps rotated by 180
  * degrees: the stride-1 input gradient as a conv of dz), mode 2 depthwise taps f32 [kh*kw][cout]
- * (cin = 1, dp_dwconv2d's layout). */
+ * (cin = 1, dp_dwconv2d's layout). kc: channel stride of K (the padded channel count of the map
+ * the packed conv reads, zero weights in the pads; 0 = unpadded). */
 int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out, int32_t kpad,
-                 int32_t mode, int32_t dtype, void* stream);
+                 int32_t kc, int32_t mode, int32_t dtype, void* stream);
 /* Depthwise conv backward (k <= 3, any stride / pad): dx (+=, NULL to skip) and dw f32
  * [c][k][k] (+=, NULL to skip) from dz. x / dz / dx: NHWC with image and pixel strides. */
 int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride, const void* dz, int64_t z_bstride,

@@ -1,0 +1,153 @@
+"""The encoder half of the training step (BASELINE config 5) on the HIP kernels
+(detrpose_amd/encoder_train.py + train_engine.py with train_encoder=True) against the reference's
+own DN training step with a trainable HybridEncoder (tests/golden/train_dn_enc_n_b2.npz, made by
+tests/golden/make_train_golden.py, oracle pinned in tests/test_train_oracle.py): the encoder's
+training-mode outputs (BatchNorm on batch statistics), all 27 losses, the gradient of every
+transformer AND encoder parameter, d loss / d backbone features and the BatchNorm running
+statistics after the step. fp32 mode, DETRPose-N at batch 2, the reference's DN draws; the
+backbone features are the pinned oracle's (the backbone is an input here)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from detrpose_amd import build_model
+from detrpose_amd.configs import get_config
+from detrpose_amd.criterion import pack_targets
+from detrpose_amd.synthetic import load_synthetic, synthetic_images
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _targets(g, dev):
+    sizes = [int(v) for v in g["sizes"]]
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    ts = []
+    for b in range(len(sizes)):
+        sl = slice(off[b], off[b + 1])
+        ts.append({"labels": torch.as_tensor(g["tgt_labels"][sl]).to(dev),
+                   "keypoints": torch.as_tensor(g["tgt_kps"][sl]).to(dev),
+                   "area": torch.as_tensor(g["tgt_area"][sl]).to(dev),
+                   "boxes": torch.as_tensor(g["tgt_boxes"][sl]).to(dev)})
+    return sizes, ts
+
+
+def backbone_feats(g, size="n"):
+    """The golden images' backbone outputs from the pinned oracle (frozen backbone, NCHW f32)."""
+    from oracle.detrpose_cpu import backbone
+    cfg = get_config(size)
+    model, _ = build_model(size)
+    load_synthetic(model, seed=int(g["meta"][1]))
+    sd = {k: v.detach().float() for k, v in model.state_dict().items()}
+    images = synthetic_images(int(g["meta"][0]), seed=int(g["meta"][2]))
+    bc = cfg["backbone"]
+    with torch.no_grad():
+        return backbone(images, sd, bc["name"], bc["return_idx"], bc["use_lab"])
+
+
+def run_step(g, dtype="fp32"):
+    from detrpose_amd.train_engine import TrainEngine
+    dev = torch.device("cuda")
+    feats = backbone_feats(g)
+    model, _ = build_model("n", dtype=dtype)
+    load_synthetic(model, seed=int(g["meta"][1]))
+    eng = TrainEngine(model, dtype, dev, train_encoder=True)
+    B = int(g["meta"][0])
+    shapes = [(f.shape[2], f.shape[3]) for f in feats]
+    ep = eng.encoder_plan(B, shapes)
+    ep.set_inputs([f.to(dev) for f in feats])
+    P = int(g["dn_pad_size"])
+    plan = eng.plan(B, P, shapes, memory=ep.memory, d_memory=ep.d_memory)
+    plan.set_dn(torch.as_tensor(g["dn_label"], dtype=torch.int32, device=dev),
+                torch.sigmoid(torch.as_tensor(g["dn_pose_unsig"], dtype=torch.float32, device=dev)),
+                torch.as_tensor(g["dn_attn_mask"], device=dev).to(torch.uint8))
+    sizes, ts = _targets(g, dev)
+    packed = pack_targets(ts, 17, dev)
+    ep.forward()
+    plan.forward()
+    keys, vals = plan.criterion(packed, sizes, int(g["dn_num_group"]))
+    plan.backward()
+    ep.backward()
+    torch.cuda.synchronize()
+    return eng, ep, plan, dict(zip(keys, vals.cpu().tolist())), feats
+
+
+@pytest.fixture(scope="module")
+def enc_step(golden_dir):
+    g = np.load(os.path.join(golden_dir, "train_dn_enc_n_b2.npz"))
+    return (g,) + run_step(g)
+
+
+def _sampled_err(g, name, flat):
+    idx, val = g[name + "__idx"], g[name + "__val"].astype(np.float64)
+    a = float(g[name + "__abssum"])
+    scale = max(float(np.abs(val).max()), a / flat.size)
+    return float(np.abs(flat[idx] - val).max()) / max(scale, 1e-30), scale, abs(flat.sum() - float(g[name + "__sum"])) / max(a, 1e-30)
+
+
+def test_encoder_outputs_and_losses(enc_step):
+    """The training-mode encoder outputs (BN on batch statistics) and the 27 losses."""
+    g, eng, ep, plan, losses, _ = enc_step
+    for i, lv in enumerate(ep.levels):
+        t = lv.buf.x[:, lv.off:lv.off + lv.c].reshape(lv.B, lv.H, lv.W, lv.c).permute(0, 3, 1, 2)
+        err, scale, _ = _sampled_err(g, f"enc{i}", t.double().cpu().reshape(-1).numpy())
+        print(f"enc{i}: rel err {err:.3g} (scale {scale:.3g})")
+        assert err <= 1e-4, (i, err)
+    ref = dict(zip([str(k) for k in g["loss_keys"]], g["loss_vals"]))
+    assert sorted(losses) == sorted(ref)
+    worst = max(abs(losses[k] - ref[k]) / max(abs(ref[k]), 1.0) for k in ref)
+    print(f"losses: worst rel err {worst:.3g}")
+    assert worst <= 1e-5
+
+
+def test_encoder_step_gradients(enc_step):
+    """Every transformer and encoder parameter gradient (the fixture's sampled entries, and the
+    sum) within 1e-3 of its scale; d loss / d backbone features likewise."""
+    g, eng, ep, plan, _, feats = enc_step
+    names = sorted(k[:-len("__idx")] for k in g.files if k.startswith("grad.") and k.endswith("__idx"))
+    rows = []
+    for n in names:
+        key = n[len("grad."):]
+        key = key if key.startswith("encoder.") else "transformer." + key
+        flat = eng.grads[key].double().cpu().reshape(-1).numpy()
+        err, scale, serr = _sampled_err(g, n, flat)
+        if scale < 1e-5:   # analytically zero (a BN bias followed by another training-mode BN)
+            assert float(np.abs(flat).max()) < 1e-4, (n, float(np.abs(flat).max()))
+            continue
+        rows.append((err, serr, n))
+    for i, f in enumerate(feats):
+        v = ep.feats[i]
+        d = v.buf.g[:, :v.c].reshape(v.B, v.H, v.W, v.c).permute(0, 3, 1, 2)
+        err, scale, serr = _sampled_err(g, f"dfeat{i}", d.double().cpu().reshape(-1).numpy())
+        rows.append((err, serr, f"dfeat{i}"))
+    rows.sort(reverse=True)
+    for r in rows[:12]:
+        print(f"{r[2]}: rel err {r[0]:.3g}, sum rel err {r[1]:.3g}")
+    assert sum(n.startswith("grad.encoder.") for n in names) > 50
+    assert rows[0][0] <= 1e-3, rows[:8]
+    assert max(r[1] for r in rows) <= 1e-3, sorted(rows, key=lambda r: -r[1])[:5]
+
+
+def test_encoder_running_stats(enc_step):
+    """BatchNorm running mean / var after the step's update (momentum 0.1, unbiased variance)."""
+    g, eng, *_ = enc_step
+    keys = [k for k in g.files if k.startswith("bn.")]
+    assert keys
+    for k in keys:
+        np.testing.assert_allclose(eng.running[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+def test_encoder_step_bf16_tracks_fp32(enc_step, golden_dir):
+    """The bf16 encoder + transformer step on the same inputs: losses within 5 % of the
+    reference's and the flat gradient (transformer + encoder) within cosine 0.99 of the fp32 one."""
+    g, eng32, *_ = enc_step
+    eng, ep, plan, losses, _ = run_step(g, "bf16")
+    ref = dict(zip([str(k) for k in g["loss_keys"]], g["loss_vals"]))
+    worst = max(abs(losses[k] - ref[k]) / max(abs(ref[k]), 1.0) for k in ref)
+    a = eng.grad_flat.double().cpu().numpy()
+    b = eng32.grad_flat.double().cpu().numpy()
+    cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+    print(f"bf16 encoder step: worst loss rel err {worst:.3g}, gradient cosine {cos:.6f}")
+    assert worst <= 5e-2 and cos >= 0.99
