@@ -1,0 +1,197 @@
+// Row ops of the HGNetv2 backbone's training step (BASELINE config 5: freeze_at=-1 trains every
+// backbone parameter, freeze_norm=True keeps its norms FrozenBatchNorm2d): the backward of
+// ConvBNAct's epilogue (frozen BN affine, ReLU, LearnableAffineBlock), the input gradient of a
+// strided dense conv as col2im of dz W, and the StemBlock max-pool's backward. The convs run on
+// dp_conv2d / dp_dwconv2d (forward, stride-1 input gradient) and dp_gemm (weight gradients over
+// dp_im2col); see detrpose_amd/backbone_train.py for the tape.
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p) {
+  return to_f32(*p);
+}
+
+// ConvBNAct backward from its stored output y = lab(act(u)), u = s z + b (hgnetv2.py:129-134):
+// dz = dy * a * act'(u) * s[ch]; with LAB (scale a, bias cb) also d a += dy r, d cb += dy where r =
+// relu(u) = (y - cb) / a. relu'(u) is read off y: with LAB, r == 0 stored exactly cb (its dtype
+// rounding), so the unit is on where y differs from that and (y - cb) a > 0.
+template <typename T>
+__global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict__ y, int64_t ldy, const T* __restrict__ dy,
+                                                             int64_t lddy, T* __restrict__ dz, int64_t lddz, int rows,
+                                                             int c, int act, const float* __restrict__ lab_a,
+                                                             const float* __restrict__ lab_b,
+                                                             const float* __restrict__ scale, float* __restrict__ dlab_a,
+                                                             float* __restrict__ dlab_b) {
+  const int64_t total = (int64_t)rows * c;
+  const bool lab = lab_a != nullptr;
+  float a = 1.f, cb = 0.f, yc = 0.f;
+  if (lab) {
+    a = *lab_a;
+    cb = *lab_b;
+    yc = to_f32(from_f32<T>(cb));
+  }
+  float sa = 0.f, sc = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / c;
+    const int ch = (int)(e - r * c);
+    const float g = ldf(dy + r * lddy + ch);
+    float d = g;
+    if (act == DP_ACT_RELU) {
+      const float v = ldf(y + r * ldy + ch);
+      if (lab) {
+        const bool on = v != yc && (v - cb) * a > 0.f;
+        const float rr = on ? (v - cb) / a : 0.f;
+        sa = fmaf(g, rr, sa);
+        sc += g;
+        d = on ? g * a : 0.f;
+      } else {
+        d = v > 0.f ? g : 0.f;
+      }
+    }
+    if (scale) d *= scale[ch];
+    dz[r * lddz + ch] = from_f32<T>(d);
+  }
+  if (!dlab_a) return;
+  __shared__ float red[2][4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sa += __shfl_xor(sa, o);
+    sc += __shfl_xor(sc, o);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wv] = sa;
+    red[1][wv] = sc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(dlab_a, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(dlab_b, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+// dx[b][y][x][ci] (+)= sum over the (ky, kx) whose output (oy, ox) = ((y + pad - ky) / s, ...) is
+// whole and in range of col[(b*oh + oy)*ow + ox][ci*kh*kw + ky*kw + kx]: the input gradient of a
+// stride-s conv from dcol = dz W (the reference weight layout [cout][cin][kh][kw]).
+template <typename T>
+__global__ void col2im_kernel(const T* __restrict__ col, int h, int w, int cin, int kh, int kw, int s, int pad,
+                              int oh, int ow, T* __restrict__ dx, int64_t bs, int ps, int acc, int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int ci = (int)(e % cin);
+  const int64_t p = e / cin;
+  const int x = (int)(p % w);
+  const int64_t t = p / w;
+  const int yy = (int)(t % h), b = (int)(t / h);
+  const int K = cin * kh * kw;
+  float sum = 0.f;
+  for (int ky = 0; ky < kh; ++ky) {
+    const int ny = yy + pad - ky;
+    if (ny < 0 || ny % s) continue;
+    const int oy = ny / s;
+    if (oy >= oh) continue;
+    for (int kx = 0; kx < kw; ++kx) {
+      const int nx = x + pad - kx;
+      if (nx < 0 || nx % s) continue;
+      const int ox = nx / s;
+      if (ox >= ow) continue;
+      sum += ldf(col + (((int64_t)b * oh + oy) * ow + ox) * K + ci * kh * kw + ky * kw + kx);
+    }
+  }
+  T* o = dx + (int64_t)b * bs + ((int64_t)yy * w + x) * ps + ci;
+  *o = from_f32<T>(acc ? ldf(o) + sum : sum);
+}
+
+// F.pad(x, (0,1,0,1)) + MaxPool2d(2, 1, ceil_mode=True) backward (hgnetv2.py:215, 217): each
+// output's gradient goes to its window's first maximum in scan order (max_pool2d's argmax, the
+// pad zeros included: a pad maximum takes the gradient out of the map); gathered per input.
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ x, int64_t xbs, int xps, const T* __restrict__ dout,
+                                   int64_t obs, int ops, int h, int w, int c, T* __restrict__ dx, int64_t dbs, int dps,
+                                   int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int ch = (int)(e % c);
+  const int64_t p = e / c;
+  const int px = (int)(p % w);
+  const int64_t t = p / w;
+  const int py = (int)(t % h), b = (int)(t / h);
+  const T* xb = x + (int64_t)b * xbs + ch;
+  float acc = 0.f;
+  for (int oy = py - 1; oy <= py; ++oy) {
+    if (oy < 0) continue;
+    for (int ox = px - 1; ox <= px; ++ox) {
+      if (ox < 0) continue;
+      float best = -INFINITY;
+      int arg = -1;
+      for (int q = 0; q < 4; ++q) {
+        const int yy = oy + (q >> 1), xx = ox + (q & 1);
+        const float v = (yy < h && xx < w) ? ldf(xb + ((int64_t)yy * w + xx) * xps) : 0.f;
+        if (v > best) {
+          best = v;
+          arg = q;
+        }
+      }
+      if (arg >= 0 && oy + (arg >> 1) == py && ox + (arg & 1) == px)
+        acc += ldf(dout + (int64_t)b * obs + ((int64_t)oy * w + ox) * ops + ch);
+    }
+  }
+  T* o = dx + (int64_t)b * dbs + ((int64_t)py * w + px) * dps + ch;
+  *o = from_f32<T>(ldf(o) + acc);
+}
+
+int grid_of(int64_t total) {
+  int64_t g = (total + 255) / 256;
+  return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+#define DP_DT(CALL)         \
+  do {                      \
+    if (dtype == DP_BF16) { \
+      using T = bf16_t;     \
+      CALL;                 \
+    } else {                \
+      using T = float;      \
+      CALL;                 \
+    }                       \
+  } while (0)
+
+extern "C" int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* dy, int64_t ld_dy, void* dz, int64_t ld_dz,
+                                 int32_t rows, int32_t c, int32_t act, const float* lab_a, const float* lab_b,
+                                 const float* scale, float* dlab_a, float* dlab_b, int32_t dtype, void* stream) {
+  DP_REQUIRE(dy && dz && rows > 0 && c > 0 && (act == DP_ACT_NONE || (act == DP_ACT_RELU && y)) &&
+                 (!lab_a || (lab_b && act == DP_ACT_RELU && dlab_a && dlab_b)),
+             "dp_frozen_act_bwd: bad arguments");
+  DP_DT(hipLaunchKernelGGL(frozen_act_bwd_kernel<T>, dim3(grid_of((int64_t)rows * c)), dim3(256), 0,
+                           as_stream(stream), (const T*)y, ld_y, (const T*)dy, ld_dy, (T*)dz, ld_dz, rows, c, act, lab_a,
+                           lab_b, scale, lab_a ? dlab_a : nullptr, dlab_b));
+  return dp_check_launch("dp_frozen_act_bwd");
+}
+
+extern "C" int dp_col2im(const void* col, int32_t batch, int32_t h, int32_t w, int32_t cin, int32_t kh, int32_t kw,
+                         int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* dx, int64_t dx_bstride,
+                         int32_t dx_pstride, int32_t accumulate, int32_t dtype, void* stream) {
+  DP_REQUIRE(col && dx && batch > 0 && h > 0 && w > 0 && cin > 0 && kh > 0 && kw > 0 && stride > 0 && oh > 0 && ow > 0,
+             "dp_col2im: bad arguments");
+  const int64_t total = (int64_t)batch * h * w * cin;
+  DP_DT(hipLaunchKernelGGL(col2im_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
+                           (const T*)col, h, w, cin, kh, kw, stride, pad, oh, ow, (T*)dx, dx_bstride, dx_pstride,
+                           accumulate, total));
+  return dp_check_launch("dp_col2im");
+}
+
+extern "C" int dp_maxpool2x2_pad_rb_bwd(const void* x, int64_t x_bstride, int32_t x_pstride, const void* dout,
+                                        int64_t dout_bstride, int32_t dout_pstride, int32_t batch, int32_t h,
+                                        int32_t w, int32_t c, void* dx, int64_t dx_bstride, int32_t dx_pstride,
+                                        int32_t dtype, void* stream) {
+  DP_REQUIRE(x && dout && dx && batch > 0 && h > 0 && w > 0 && c > 0, "dp_maxpool2x2_pad_rb_bwd: bad arguments");
+  const int64_t total = (int64_t)batch * h * w * c;
+  DP_DT(hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                           as_stream(stream), (const T*)x, x_bstride, x_pstride, (const T*)dout, dout_bstride,
+                           dout_pstride, h, w, c, (T*)dx, dx_bstride, dx_pstride, total));
+  return dp_check_launch("dp_maxpool2x2_pad_rb_bwd");
+}

@@ -192,9 +192,9 @@ __global__ void bn_act_bwd_apply_kernel(T* __restrict__ dz1, int64_t ld1, T* __r
 // col[row][ci * kh * kw + ky * kw + kx] = x[b][oy * s - pad + ky][ox * s - pad + kx][ci] (0 outside):
 // the [rows][cin][kh][kw] operand whose product with dz^T is the weight gradient in the
 // reference layout [cout][cin][kh][kw]
-template <typename T>
-__global__ void im2col_kernel(const T* __restrict__ x, int64_t bs, int ps, int h, int w, int cin, int kh, int kw,
-                              int stride, int pad, int oh, int ow, T* __restrict__ col, int64_t total) {
+template <typename TI, typename T>
+__global__ void im2col_kernel(const TI* __restrict__ x, int64_t bs, int ps, int64_t cs, int h, int w, int cin, int kh,
+                              int kw, int stride, int pad, int oh, int ow, T* __restrict__ col, int64_t total) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (row, ci)
   if (e >= total) return;
   const int ci = (int)(e % cin);
@@ -207,7 +207,8 @@ __global__ void im2col_kernel(const T* __restrict__ x, int64_t bs, int ps, int h
     for (int kx = 0; kx < kw; ++kx) {
       const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
       const bool ok = (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
-      o[ky * kw + kx] = ok ? x[(int64_t)b * bs + ((int64_t)iy * w + ix) * ps + ci] : from_f32<T>(0.f);
+      o[ky * kw + kx] = ok ? from_f32<T>(to_f32(x[(int64_t)b * bs + ((int64_t)iy * w + ix) * ps + ci * cs]))
+                           : from_f32<T>(0.f);
     }
 }
 
@@ -217,12 +218,18 @@ __global__ void im2col_kernel(const T* __restrict__ x, int64_t bs, int ps, int h
 // real channel count: maps whose channels are padded to a vector multiple), zero in the pads
 template <typename T>
 __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin, int kh, int kw, void* __restrict__ out,
-                                 int kpad, int kc, int mode) {
+                                 int kpad, int kc, int mode, const float* __restrict__ scale) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (mode == 2) {
     if (e >= (int64_t)cout * kh * kw) return;
     const int tap = (int)(e / cout), ch = (int)(e % cout);
-    reinterpret_cast<float*>(out)[e] = w[(int64_t)ch * kh * kw + tap];
+    reinterpret_cast<float*>(out)[e] = w[(int64_t)ch * kh * kw + tap] * (scale ? scale[ch] : 1.f);
+    return;
+  }
+  if (mode == 3) {
+    const int K = cin * kh * kw;
+    if (e >= (int64_t)cout * K) return;
+    reinterpret_cast<float*>(out)[e] = w[e] * (scale ? scale[e / K] : 1.f);
     return;
   }
   const int rows = mode == 0 ? cout : cin;
@@ -233,8 +240,8 @@ __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin,
   const int tap = k / kc, j = k - tap * kc;
   if (tap < kh * kw && j < inner) {
     const int ky = tap / kw, kx = tap - ky * kw;
-    v = mode == 0 ? w[(((int64_t)r * cin + j) * kh + ky) * kw + kx]
-                  : w[(((int64_t)j * cin + r) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)];
+    v = mode == 0 ? w[(((int64_t)r * cin + j) * kh + ky) * kw + kx] * (scale ? scale[r] : 1.f)
+                  : w[(((int64_t)j * cin + r) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)] * (scale ? scale[j] : 1.f);
   }
   reinterpret_cast<T*>(out)[e] = from_f32<T>(v);
 }
@@ -278,7 +285,9 @@ __global__ void dw_bwd_weight_kernel(const T* __restrict__ x, int64_t xbs, int x
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= c) return;
   const int p0 = blockIdx.y * 256, p1 = min(p0 + 256, opix);
-  float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float acc[25];
+#pragma unroll
+  for (int t = 0; t < 25; ++t) acc[t] = 0.f;
   for (int p = p0; p < p1; ++p) {
     const int ox = p % ow, t = p / ow, oy = t % oh, b = t / oh;
     const float g = ld_(dz + (int64_t)b * zbs + ((int64_t)oy * ow + ox) * zps + ch);
@@ -431,26 +440,33 @@ extern "C" int dp_bn_act_bwd_apply(void* dz1, int64_t ld_dz1, void* dz2, int64_t
   return dp_check_launch("dp_bn_act_bwd_apply");
 }
 
-extern "C" int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int32_t batch, int32_t h, int32_t w,
-                         int32_t cin, int32_t kh, int32_t kw, int32_t stride, int32_t pad, int32_t oh, int32_t ow,
-                         void* col, int32_t dtype, void* stream) {
+extern "C" int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int64_t cstride, int32_t batch, int32_t h,
+                         int32_t w, int32_t cin, int32_t kh, int32_t kw, int32_t stride, int32_t pad, int32_t oh,
+                         int32_t ow, void* col, int32_t x_dtype, int32_t dtype, void* stream) {
   DP_REQUIRE(x && col && batch > 0 && cin > 0 && kh > 0 && kw > 0 && stride > 0 && oh > 0 && ow > 0,
              "dp_im2col: bad arguments");
   const int64_t total = (int64_t)batch * oh * ow * cin;
-  DP_DT(hipLaunchKernelGGL(im2col_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
-                           (const T*)x, bstride, pstride, h, w, cin, kh, kw, stride, pad, oh, ow, (T*)col, total));
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (x_dtype == DP_F32)
+    DP_DT(hipLaunchKernelGGL((im2col_kernel<float, T>), grid, dim3(256), 0, as_stream(stream), (const float*)x,
+                             bstride, pstride, cstride, h, w, cin, kh, kw, stride, pad, oh, ow, (T*)col, total));
+  else
+    DP_DT(hipLaunchKernelGGL((im2col_kernel<bf16_t, T>), grid, dim3(256), 0, as_stream(stream), (const bf16_t*)x,
+                             bstride, pstride, cstride, h, w, cin, kh, kw, stride, pad, oh, ow, (T*)col, total));
   return dp_check_launch("dp_im2col");
 }
 
 extern "C" int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out, int32_t kpad,
-                            int32_t kc, int32_t mode, int32_t dtype, void* stream) {
+                            int32_t kc, int32_t mode, const float* scale, int32_t dtype, void* stream) {
   if (kc <= 0) kc = mode == 0 ? cin : cout;
-  DP_REQUIRE(w && out && cout > 0 && cin > 0 && mode >= 0 && mode <= 2 &&
-                 (mode == 2 ? cin == 1 : (kc >= (mode == 0 ? cin : cout) && kpad >= kh * kw * kc)),
+  DP_REQUIRE(w && out && cout > 0 && cin > 0 && mode >= 0 && mode <= 3 &&
+                 (mode == 2 ? cin == 1 : mode == 3 || (kc >= (mode == 0 ? cin : cout) && kpad >= kh * kw * kc)),
              "dp_conv_pack: bad arguments");
-  const int64_t total = mode == 2 ? (int64_t)cout * kh * kw : (int64_t)(mode == 0 ? cout : cin) * kpad;
+  const int64_t total = mode == 2 ? (int64_t)cout * kh * kw
+                        : mode == 3 ? (int64_t)cout * cin * kh * kw
+                                    : (int64_t)(mode == 0 ? cout : cin) * kpad;
   DP_DT(hipLaunchKernelGGL(conv_pack_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
-                           w, cout, cin, kh, kw, out, kpad, kc, mode));
+                           w, cout, cin, kh, kw, out, kpad, kc, mode, scale));
   return dp_check_launch("dp_conv_pack");
 }
 
@@ -458,7 +474,7 @@ extern "C" int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride
                              int32_t z_pstride, const float* wt, int32_t batch, int32_t h, int32_t w, int32_t c,
                              int32_t k, int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* dx,
                              int64_t dx_bstride, int32_t dx_pstride, float* dw, int32_t dtype, void* stream) {
-  DP_REQUIRE(x && dz && wt && batch > 0 && c > 0 && k > 0 && k <= 3 && stride > 0, "dp_dwconv_bwd: bad arguments");
+  DP_REQUIRE(x && dz && wt && batch > 0 && c > 0 && k > 0 && k <= 5 && stride > 0, "dp_dwconv_bwd: bad arguments");
   hipStream_t s = as_stream(stream);
   if (dx) {
     const int64_t total = (int64_t)batch * h * w * c;

@@ -93,18 +93,15 @@ def _host(fn):
     return op
 
 
-class EncoderTrainPlan:
-    """Buffers and tapes of the encoder's training forward / backward for one batch and feature
-    shape set. eng: a TrainEngine built with train_encoder=True (the encoder parameters live in
-    its flat master / gradient buffers)."""
+class TapePlan:
+    """Shared machinery of the conv-network training tapes (encoder_train.EncoderTrainPlan,
+    backbone_train.BackboneTrainPlan): stored NHWC maps with gradient buffers, per-step weight
+    packing from the f32 master, the conv / BatchNorm ops that register their backward."""
 
-    def __init__(self, eng, B: int, feat_shapes):
+    def _setup(self, eng):
         self.eng = eng
-        self.lib = lib = eng.lib
+        self.lib = eng.lib
         self.model = eng.model
-        enc = eng.model.encoder
-        self.enc = enc
-        self.B = B
         self.dt, self.code = eng.tdtype, eng.code
         self.es = self.dt.itemsize
         self.vec = 8 if self.code == DP_BF16 else 4
@@ -115,81 +112,9 @@ class EncoderTrainPlan:
         self.world, self.rank = 1, 0
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             self.world, self.rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
-        Cc, nlev = enc.hidden_dim, enc.n_levels
-        self.Cc = Cc
-        self.c4, self.c4p = enc.c4, pad_to(enc.c4, 8)
-        self.hw = [tuple(s) for s in feat_shapes]
-        self.S = sum(h * w for h, w in self.hw)
-        fw, bw = _lib_tape(lib, self.dev), _lib_tape(lib, self.dev)
-        self.fw, self.bw = fw, bw
-        self.zero_bias = self.f32(max(enc.in_channels + [2 * Cc]))
-        self.zero_bias.zero_()
-        prev = getattr(eng, "cur", None)
-        eng.cur = self
+        self.fw, self.bw = _lib_tape(self.lib, self.dev), _lib_tape(self.lib, self.dev)
         self._packs = {}
         self._col = None
-
-        # ---------------- inputs: backbone features (B*H*W, cin) NHWC rows
-        self.feats = []
-        for (h, w), cin in zip(self.hw, enc.in_channels):
-            self.feats.append(self.view(B, h, w, cin))
-        self.memory = torch.empty(B, self.S, Cc, dtype=self.dt, device=self.dev)
-        self.arena.append(self.memory)
-        self.d_memory = torch.zeros(B, self.S, Cc, dtype=torch.float32, device=self.dev)
-        self.arena.append(self.d_memory)
-
-        # ---------------- forward (hybrid_encoder.py:462-507)
-        hw = self.hw
-        fcat = [self.view(B, *hw[i], 2 * Cc) for i in range(nlev - 1)]       # [up(lateral) | proj]
-        pcat = [self.view(B, *hw[i + 1], 2 * Cc) for i in range(nlev - 1)]   # [down | lateral]
-        proj = []
-        for i, f in enumerate(self.feats):
-            dst = fcat[i].ch(Cc, Cc) if i < nlev - 1 else self.view(B, *hw[i], Cc)
-            p = f"{E_}input_proj.{i}"
-            z = self.conv(f"enc.proj{i}", p + ".conv.weight", [(f, 0, f.c)], Cc)
-            self.bn(f"enc.proj{i}", [(z, p + ".norm")], dst, None)
-            proj.append(dst)
-        for i, ei in enumerate(enc.use_encoder_idx):
-            out = self.view(B, *hw[ei], Cc)
-            self.aifi(i, proj[ei], out)
-            proj[ei] = out
-        high = proj[-1]
-        self.levels = [None] * nlev
-        for idx in range(nlev - 1, 0, -1):
-            j = nlev - 1 - idx
-            lat = pcat[idx - 1].ch(Cc, Cc)
-            p = f"{E_}lateral_convs.{j}"
-            z = self.conv(f"enc.lateral{j}", p + ".conv.weight", [(high, 0, Cc)], Cc)
-            self.bn(f"enc.lateral{j}", [(z, p + ".norm")], lat, enc.act)
-            self.upsample(f"enc.lateral{j}.up", lat, fcat[idx - 1].ch(0, Cc))
-            dst = self.view(B, *hw[idx - 1], Cc)
-            self.elan(f"enc.fpn{j}", f"{E_}fpn_blocks.{j}", fcat[idx - 1], dst)
-            high = dst
-        self.levels[0] = high
-        low = high
-        for idx in range(nlev - 1):
-            p = f"{E_}downsample_convs.{idx}.0"
-            t1 = self.view(B, low.H, low.W, Cc)
-            z = self.conv(f"enc.down{idx}.cv1", p + ".cv1.conv.weight", [(low, 0, Cc)], Cc)
-            self.bn(f"enc.down{idx}.cv1", [(z, p + ".cv1.norm")], t1, None)
-            z2 = self.dwconv(f"enc.down{idx}.cv2", p + ".cv2.conv.weight", t1, 2)
-            self.bn(f"enc.down{idx}.cv2", [(z2, p + ".cv2.norm")], pcat[idx].ch(0, Cc), None)
-            dst = self.view(B, *hw[idx + 1], Cc)
-            self.elan(f"enc.pan{idx}", f"{E_}pan_blocks.{idx}", pcat[idx], dst)
-            self.levels[idx + 1] = dst
-            low = dst
-        # memory (B, S, C): the levels back to back per image (transformer.py:1285-1286)
-        starts = [sum(h * w for h, w in hw[:i]) for i in range(nlev)]
-        self.starts = starts
-        for i, lv in enumerate(self.levels):
-            n = lv.H * lv.W * Cc
-            fw.op(f"enc.memory{i}", lib.dp_convert_rows, lv.xp, self.code, n, _p(self.memory, starts[i] * Cc), self.code,
-                  self.S * Cc, B, n, C.c_float(1.0), 0)
-            self._bwd.append(lambda lv=lv, i=i, n=n: self.bw.op(
-                f"enc.memory{i}.bwd", lib.dp_convert_rows, _p(self.d_memory, starts[i] * Cc), DP_F32, self.S * Cc,
-                lv.gp, self.code, n, B, n, C.c_float(1.0), 1))
-        self._record_backward()
-        eng.cur = prev
 
     # ------------------------------------------------------------------ storage
     def f32(self, *shape):
@@ -222,10 +147,11 @@ class EncoderTrainPlan:
             n = b.x.numel()
             b.g = self.grad_arena[o:o + n].view(b.x.shape)
             o += n
-        self.bw.op("enc.bw.zero", self.lib.dp_zero, _p(self.grad_arena), total * self.es)
+        # zeroed at the end of the forward: a later plan's backward (the encoder's, into the
+        # backbone outputs) may accumulate into these before this plan's backward runs
+        self.fw.op("grads.zero", self.lib.dp_zero, _p(self.grad_arena), total * self.es)
         for fn in reversed(self._bwd):
             fn()
-        self.d_feats = [f.buf.g for f in self.feats]
 
     # ------------------------------------------------------------------ weights
     def wptr(self, key):
@@ -242,15 +168,16 @@ class EncoderTrainPlan:
                        src.numel(), 1, src.numel(), C.c_float(1.0), 0)
         return _p(self._packs[key])
 
-    def packed(self, key, mode, kc, rows_p):
+    def packed(self, key, mode, kc, rows_p, scale=None):
         """dp_conv_pack of the master weight: mode 0 / 1 [rows_p][kpad] of dtype (zero pads),
-        mode 2 f32 depthwise taps."""
-        k2 = (key, mode)
+        mode 2 f32 depthwise taps, mode 3 f32 [cout][cin*kh*kw]; scale: f32 [cout] multiplier
+        (a frozen BatchNorm's scale folded in)."""
+        k2 = (key, mode, scale is not None)
         if k2 not in self._packs:
             w = self.eng.params[key]
             cout, cin, kh, kw = w.shape
-            if mode == 2:
-                t = torch.empty(kh * kw * cout, dtype=torch.float32, device=self.dev)
+            if mode in (2, 3):
+                t = torch.empty(kh * kw * cout * cin, dtype=torch.float32, device=self.dev)
                 kpad = 0
             else:
                 kpad = pad_to(kh * kw * kc, 64)
@@ -258,7 +185,7 @@ class EncoderTrainPlan:
             self.arena.append(t)
             self._packs[k2] = (t, kpad)
             self.fw.op(f"pack.{key}.{mode}", self.lib.dp_conv_pack, _p(w), cout, cin, kh, kw, _p(t), kpad, kc, mode,
-                       self.code if mode != 2 else DP_F32)
+                       _p(scale) if scale is not None else None, self.code if mode < 2 else DP_F32)
         return self._packs[k2]
 
     # ------------------------------------------------------------------ GEMM helper
@@ -307,8 +234,8 @@ class EncoderTrainPlan:
             self._conv2d(self.bw, name + ".dx", z.gp, z.ld, z.cp, x.gp, x.ld, x.cp, wb, kpad2, B, H, W, k, res=x.gp)
             K = cin * k * k
             col = self._colbuf(rows * K)
-            self.bw.op(name + ".im2col", lib.dp_im2col, x.xp, H * W * x.ld, x.ld, B, H, W, cin, k, k, 1, k // 2, H, W,
-                       _p(col), self.code)
+            self.bw.op(name + ".im2col", lib.dp_im2col, x.xp, H * W * x.ld, x.ld, 1, B, H, W, cin, k, k, 1, k // 2, H,
+                       W, _p(col), self.code, self.code)
             self.gemm(self.bw, name + ".dW", z.gp, 1, z.ld, _p(col), K, 1, _p(G), K, cout, K, rows, out_code=DP_F32,
                       beta=1.0)
         self._bwd.append(bwd)
@@ -415,6 +342,112 @@ class EncoderTrainPlan:
                    dst.ld, 0, self.code)
         self._bwd.append(lambda: self.bw.op(name + ".bwd", lib.dp_upsample2x, dst.gp, 4 * h * w * dst.ld, dst.ld, B, h,
                                             w, c, src.gp, h * w * src.ld, src.ld, 1, self.code))
+
+    # ------------------------------------------------------------------ run
+    def set_inputs(self, feats):
+        """feats: backbone outputs, NCHW (B, cin, H, W) or NHWC rows, any float dtype."""
+        for v, f in zip(self.feats, feats):
+            t = f.permute(0, 2, 3, 1) if f.dim() == 4 and f.shape[1] == v.c and f.shape[-1] != v.c else f
+            v.buf.x[:, :v.c].copy_(t.reshape(v.rows, v.c).to(self.dt))
+
+    def forward(self, debug=None):
+        self.fw.run(debug=debug)
+
+    def backward(self, debug=None):
+        self.bw.run(debug=debug)
+
+
+
+
+class EncoderTrainPlan(TapePlan):
+    """Buffers and tapes of the encoder's training forward / backward for one batch and feature
+    shape set. eng: a TrainEngine built with train_encoder=True (the encoder parameters live in
+    its flat master / gradient buffers)."""
+
+    def __init__(self, eng, B: int, feat_shapes, feats=None):
+        """feats: the backbone's output maps (backbone_train.BackboneTrainPlan.outs, their
+        gradients d loss / d feats accumulated by this backward) or None: own input buffers
+        (set_inputs)."""
+        self._setup(eng)
+        lib = self.lib
+        enc = eng.model.encoder
+        self.enc = enc
+        self.B = B
+        Cc, nlev = enc.hidden_dim, enc.n_levels
+        self.Cc = Cc
+        self.c4, self.c4p = enc.c4, pad_to(enc.c4, 8)
+        self.hw = [tuple(s) for s in feat_shapes]
+        self.S = sum(h * w for h, w in self.hw)
+        fw = self.fw
+        self.zero_bias = self.f32(max(enc.in_channels + [2 * Cc]))
+        self.zero_bias.zero_()
+        prev = getattr(eng, "cur", None)
+        eng.cur = self
+
+        # ---------------- inputs: backbone features (B*H*W, cin) NHWC rows
+        if feats is not None:
+            assert [(f.H, f.W, f.c) for f in feats] == [(h, w, c) for (h, w), c in zip(self.hw, enc.in_channels)]
+            self.feats = list(feats)
+        else:
+            self.feats = [self.view(B, h, w, cin) for (h, w), cin in zip(self.hw, enc.in_channels)]
+        self.memory = torch.empty(B, self.S, Cc, dtype=self.dt, device=self.dev)
+        self.arena.append(self.memory)
+        self.d_memory = torch.zeros(B, self.S, Cc, dtype=torch.float32, device=self.dev)
+        self.arena.append(self.d_memory)
+
+        # ---------------- forward (hybrid_encoder.py:462-507)
+        hw = self.hw
+        fcat = [self.view(B, *hw[i], 2 * Cc) for i in range(nlev - 1)]       # [up(lateral) | proj]
+        pcat = [self.view(B, *hw[i + 1], 2 * Cc) for i in range(nlev - 1)]   # [down | lateral]
+        proj = []
+        for i, f in enumerate(self.feats):
+            dst = fcat[i].ch(Cc, Cc) if i < nlev - 1 else self.view(B, *hw[i], Cc)
+            p = f"{E_}input_proj.{i}"
+            z = self.conv(f"enc.proj{i}", p + ".conv.weight", [(f, 0, f.c)], Cc)
+            self.bn(f"enc.proj{i}", [(z, p + ".norm")], dst, None)
+            proj.append(dst)
+        for i, ei in enumerate(enc.use_encoder_idx):
+            out = self.view(B, *hw[ei], Cc)
+            self.aifi(i, proj[ei], out)
+            proj[ei] = out
+        high = proj[-1]
+        self.levels = [None] * nlev
+        for idx in range(nlev - 1, 0, -1):
+            j = nlev - 1 - idx
+            lat = pcat[idx - 1].ch(Cc, Cc)
+            p = f"{E_}lateral_convs.{j}"
+            z = self.conv(f"enc.lateral{j}", p + ".conv.weight", [(high, 0, Cc)], Cc)
+            self.bn(f"enc.lateral{j}", [(z, p + ".norm")], lat, enc.act)
+            self.upsample(f"enc.lateral{j}.up", lat, fcat[idx - 1].ch(0, Cc))
+            dst = self.view(B, *hw[idx - 1], Cc)
+            self.elan(f"enc.fpn{j}", f"{E_}fpn_blocks.{j}", fcat[idx - 1], dst)
+            high = dst
+        self.levels[0] = high
+        low = high
+        for idx in range(nlev - 1):
+            p = f"{E_}downsample_convs.{idx}.0"
+            t1 = self.view(B, low.H, low.W, Cc)
+            z = self.conv(f"enc.down{idx}.cv1", p + ".cv1.conv.weight", [(low, 0, Cc)], Cc)
+            self.bn(f"enc.down{idx}.cv1", [(z, p + ".cv1.norm")], t1, None)
+            z2 = self.dwconv(f"enc.down{idx}.cv2", p + ".cv2.conv.weight", t1, 2)
+            self.bn(f"enc.down{idx}.cv2", [(z2, p + ".cv2.norm")], pcat[idx].ch(0, Cc), None)
+            dst = self.view(B, *hw[idx + 1], Cc)
+            self.elan(f"enc.pan{idx}", f"{E_}pan_blocks.{idx}", pcat[idx], dst)
+            self.levels[idx + 1] = dst
+            low = dst
+        # memory (B, S, C): the levels back to back per image (transformer.py:1285-1286)
+        starts = [sum(h * w for h, w in hw[:i]) for i in range(nlev)]
+        self.starts = starts
+        for i, lv in enumerate(self.levels):
+            n = lv.H * lv.W * Cc
+            fw.op(f"enc.memory{i}", lib.dp_convert_rows, lv.xp, self.code, n, _p(self.memory, starts[i] * Cc), self.code,
+                  self.S * Cc, B, n, C.c_float(1.0), 0)
+            self._bwd.append(lambda lv=lv, i=i, n=n: self.bw.op(
+                f"enc.memory{i}.bwd", lib.dp_convert_rows, _p(self.d_memory, starts[i] * Cc), DP_F32, self.S * Cc,
+                lv.gp, self.code, n, B, n, C.c_float(1.0), 1))
+        self._record_backward()
+        self.d_feats = [f.buf.g for f in self.feats]
+        eng.cur = prev
 
     def csp(self, name, p, x, out):
         """CSPLayer (hybrid_encoder.py:215-240): conv1 -> VGG blocks, + conv2, both SiLU."""
@@ -567,20 +600,6 @@ class EncoderTrainPlan:
             self.gemm(bw, f"aifi{i}.v.dx", dqkv.xp + 2 * Cc * e, 3 * Cc, 1, Wip + 2 * Cc * Cc * e, Cc, 1, src.gp,
                       src.ld, rows, Cc, Cc, beta=1.0)
         self._bwd.append(bwd)
-
-    # ------------------------------------------------------------------ run
-    def set_inputs(self, feats):
-        """feats: backbone outputs, NCHW (B, cin, H, W) or NHWC rows, any float dtype."""
-        for v, f in zip(self.feats, feats):
-            t = f.permute(0, 2, 3, 1) if f.dim() == 4 and f.shape[1] == v.c and f.shape[-1] != v.c else f
-            v.buf.x[:, :v.c].copy_(t.reshape(v.rows, v.c).to(self.dt))
-
-    def forward(self, debug=None):
-        self.fw.run(debug=debug)
-
-    def backward(self, debug=None):
-        self.bw.run(debug=debug)
-
 
 def _lib_tape(lib, dev):
     from .train_engine import Tape

@@ -89,9 +89,10 @@ class TrainEngine:
     dtype 'fp32' (parity mode) or 'bf16' (bf16 activations and activation gradients, f32
     accumulation, f32 LayerNorm statistics, f32 heads and parameter gradients)."""
 
-    def __init__(self, model, dtype="fp32", device="cuda", train_encoder=False):
+    def __init__(self, model, dtype="fp32", device="cuda", train_encoder=False, train_backbone=False):
         self.lib = _lib.load()
-        self.train_encoder = train_encoder
+        self.train_encoder = train_encoder = train_encoder or train_backbone
+        self.train_backbone = train_backbone
         self.model = model
         self.tr = tr = model.transformer
         self.dtype_name = dtype
@@ -114,6 +115,8 @@ class TrainEngine:
         # the transformer's parameters; with train_encoder also the HybridEncoder's
         # (detrpose_amd/encoder_train.py), whose BatchNorm running statistics live in `running`
         pref = (T_, "encoder.") if train_encoder else (T_,)
+        if train_backbone:   # (detrpose_amd/backbone_train.py)
+            pref = pref + ("backbone.",)
         self.pnames = [n for n, p in model.named_parameters() if n.startswith(pref) and p.requires_grad]
         shapes = {n: tuple(p.shape) for n, p in model.named_parameters()}
         # each parameter starts on a 256-byte boundary (16-byte vector loads of any view)
@@ -306,13 +309,23 @@ class TrainEngine:
             self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes], memory, d_memory)
         return self.plans[key]
 
-    def encoder_plan(self, batch: int, feat_shapes):
-        """The HybridEncoder's training forward / backward (encoder_train.EncoderTrainPlan)."""
+    def encoder_plan(self, batch: int, feat_shapes, feats=None):
+        """The HybridEncoder's training forward / backward (encoder_train.EncoderTrainPlan);
+        feats: the backbone plan's output maps (its input), or None (own input buffers)."""
         assert self.train_encoder, "TrainEngine(train_encoder=True) trains the encoder"
         from .encoder_train import EncoderTrainPlan
-        key = (batch, tuple(tuple(s) for s in feat_shapes))
+        key = (batch, tuple(tuple(s) for s in feat_shapes), id(feats[0].buf) if feats else None)
         if key not in self.enc_plans:
-            self.enc_plans[key] = EncoderTrainPlan(self, batch, feat_shapes)
+            self.enc_plans[key] = EncoderTrainPlan(self, batch, feat_shapes, feats)
+        return self.enc_plans[key]
+
+    def backbone_plan(self, batch: int, h: int, w: int):
+        """The HGNetv2 backbone's training forward / backward (backbone_train.BackboneTrainPlan)."""
+        assert self.train_backbone, "TrainEngine(train_backbone=True) trains the backbone"
+        from .backbone_train import BackboneTrainPlan
+        key = ("bb", batch, h, w)
+        if key not in self.enc_plans:
+            self.enc_plans[key] = BackboneTrainPlan(self, batch, h, w)
         return self.enc_plans[key]
 
 

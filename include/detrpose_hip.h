@@ -575,19 +575,23 @@ int dp_bn_act_bwd_apply(void* dz1, int64_t ld_dz1, void* dz2, int64_t ld_dz2, co
                         const void* z2, int64_t ld2, const float* mr2, const float* g2, const float* b2,
                         int32_t rows, int32_t c, int32_t act, const float* sums, float count, int32_t dtype,
                         void* stream);
-/* col [batch*oh*ow][cin*kh*kw] = the conv's input patches, K order (cin, ky, kx): dp_gemm of dz^T
- * with it is the weight gradient in the reference layout [cout][cin][kh][kw]. */
-int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int32_t batch, int32_t h, int32_t w, int32_t cin,
-              int32_t kh, int32_t kw, int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* col, int32_t dtype,
-              void* stream);
+/* col [batch*oh*ow][cin*kh*kw] (of dtype) = the conv's input patches, K order (cin, ky, kx): dp_gemm
+ * of dz^T with it is the weight gradient in the reference layout [cout][cin][kh][kw]. x of x_dtype,
+ * element (b, y, x, c) at b*bstride + (y*w + x)*pstride + c*cstride (NHWC: cstride 1; the f32
+ * NCHW image of stem1: pstride 1, cstride h*w). */
+int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int64_t cstride, int32_t batch, int32_t h, int32_t w,
+              int32_t cin, int32_t kh, int32_t kw, int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* col,
+              int32_t x_dtype, int32_t dtype, void* stream);
 /* f32 master conv weights [cout][cin][kh][kw] -> dp_conv2d's packed layout: mode 0 [cout][kpad]
  * (K = ky, kx, cin; the forward), mode 1 [cin][kpad] (K = ky, kx, cout, taps rotated by 180
  * degrees: the stride-1 input gradient as a conv of dz), mode 2 depthwise taps f32 [kh*kw][cout]
- * (cin = 1, dp_dwconv2d's layout). kc: channel stride of K (the padded channel count of the map
- * the packed conv reads, zero weights in the pads; 0 = unpadded). */
+ * (cin = 1, dp_dwconv2d's layout), mode 3 f32 [cout][cin*kh*kw] (dp_stem_conv's layout). kc:
+ * channel stride of K (the padded channel count of the map the packed conv reads, zero weights
+ * in the pads; 0 = unpadded). scale (f32 [cout], NULL = 1): every output channel's weights
+ * multiplied by it (FrozenBatchNorm2d's scale folded into the conv, hgnetv2.py:51-61). */
 int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out, int32_t kpad,
-                 int32_t kc, int32_t mode, int32_t dtype, void* stream);
-/* Depthwise conv backward (k <= 3, any stride / pad): dx (+=, NULL to skip) and dw f32
+                 int32_t kc, int32_t mode, const float* scale, int32_t dtype, void* stream);
+/* Depthwise conv backward (k <= 5, any stride / pad): dx (+=, NULL to skip) and dw f32
  * [c][k][k] (+=, NULL to skip) from dz. x / dz / dx: NHWC with image and pixel strides. */
 int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride, const void* dz, int64_t z_bstride,
                   int32_t z_pstride, const float* wt, int32_t batch, int32_t h, int32_t w, int32_t c, int32_t k,
@@ -605,6 +609,31 @@ int dp_axpby_rows(void* y, int64_t ld_y, const void* a, int64_t ld_a, float alph
 /* dx = dy * act'(pre) (elementwise; the AIFI FFN's GELU backward). */
 int dp_act_bwd(const void* pre, int64_t ld_pre, const void* dy, int64_t ld_dy, void* dx, int64_t ld_dx, int32_t rows,
                int32_t c, int32_t act, int32_t dtype, void* stream);
+
+
+/* ---- HGNetv2 backbone training step (BASELINE config 5: freeze_at=-1 trains every backbone
+ * parameter, freeze_norm=True keeps FrozenBatchNorm2d; hgnetv2.py:24-61, 82-383). Callers:
+ * detrpose_amd/backbone_train.py. */
+
+/* Backward of ConvBNAct's epilogue y = lab(act(s z + b)) from its stored output (hgnetv2.py:129-134):
+ * dz = dy * a * act'(.) * scale[ch] (scale: the frozen BN scale, NULL = 1; a = *lab_a, or 1 without
+ * LAB); with the LAB scalars (device lab_a / lab_b, NULL = no LAB) *dlab_a += sum dy * relu(.),
+ * *dlab_b += sum dy. act: DP_ACT_NONE (y unused) or DP_ACT_RELU. Rows ld apart, of dtype. */
+int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* dy, int64_t ld_dy, void* dz, int64_t ld_dz,
+                      int32_t rows, int32_t c, int32_t act, const float* lab_a, const float* lab_b, const float* scale,
+                      float* dlab_a, float* dlab_b, int32_t dtype, void* stream);
+/* dx (= or += when accumulate) = col2im(col): col [batch*oh*ow][cin*kh*kw] (K order cin, ky, kx) =
+ * dz W of a stride-s, pad-p conv; each input pixel sums the columns that read it (StemBlock.stem3's
+ * 3x3 stride-2 input gradient). dx NHWC with image / pixel strides. */
+int dp_col2im(const void* col, int32_t batch, int32_t h, int32_t w, int32_t cin, int32_t kh, int32_t kw,
+              int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* dx, int64_t dx_bstride, int32_t dx_pstride,
+              int32_t accumulate, int32_t dtype, void* stream);
+/* Backward of dp_maxpool2x2_pad_rb (F.pad(0,1,0,1) + MaxPool2d(2, 1, ceil_mode=True), hgnetv2.py:215,
+ * 217): dx += each window's output gradient at the window's first maximum in scan order (the pad
+ * zeros take part; a pad maximum drops the gradient). x: the pool's input. */
+int dp_maxpool2x2_pad_rb_bwd(const void* x, int64_t x_bstride, int32_t x_pstride, const void* dout,
+                             int64_t dout_bstride, int32_t dout_pstride, int32_t batch, int32_t h, int32_t w, int32_t c,
+                             void* dx, int64_t dx_bstride, int32_t dx_pstride, int32_t dtype, void* stream);
 
 #ifdef __cplusplus
 }

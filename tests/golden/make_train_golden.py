@@ -241,7 +241,7 @@ def dn_targets(B, K, sizes, seed):
     return out
 
 
-def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_train=False):
+def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_train=False, full_train=False):
     """The reference's full training step with OKS-denoising queries (transformer.py:1265-1385,
     dn_component.py:39-183) on CPU: training-mode forward WITH targets, the Criterion with its
     dn_* losses (criterion.py:385-435), loss.backward(). BatchNorm layers in eval mode (frozen
@@ -269,7 +269,14 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_t
     gradient and its outputs enter the encoder as leaves, so the gradients stored are the
     encoder's and the transformer's parameters' plus d loss / d backbone-output ("dfeat.*"),
     and the encoder outputs ("enc.*") and every encoder BN's running statistics after the
-    step's update ("bn.*") are stored too."""
+    step's update ("bn.*") are stored too.
+
+    full_train=True (the whole of config 5): as enc_train, but the backbone is trained too, as
+    the reference configures it (freeze_at=-1: no stage or stem frozen; freeze_norm=True: its
+    norms are FrozenBatchNorm2d), so every backbone parameter's gradient (conv weights, the
+    LearnableAffineBlock scalars) is stored ("grad.backbone.*") with the backbone outputs
+    ("bb.*") instead of d loss / d backbone-output."""
+    enc_train = enc_train or full_train
     from detrpose_amd.synthetic import load_synthetic, synthetic_images
     import src.models.detrpose.transformer as tmod
     Criterion, HungarianMatcher = _import_criterion()
@@ -283,8 +290,11 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_t
     K = model.transformer.num_body_points
     images = synthetic_images(batch, seed=1)
     targets = dn_targets(batch, K, sizes, tseed)
-    feats_cap, enc_cap = [], []
-    if enc_train:
+    feats_cap, enc_cap, bb_cap = [], [], []
+    if full_train:
+        hk = model.backbone.register_forward_hook(lambda mod, a, out: bb_cap.extend(o.detach() for o in out))
+        he = model.encoder.register_forward_hook(lambda mod, a, out: enc_cap.extend(o.detach() for o in out))
+    elif enc_train:
         model.backbone.eval()
 
         def leaf_feats(mod, a, out):
@@ -384,6 +394,13 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_t
                 ng += 1
         for i, f in enumerate(feats_cap):
             put(f"dfeat{i}", f.grad)
+        if full_train:
+            for n, p in model.backbone.named_parameters():
+                if p.grad is not None:
+                    put("grad.backbone." + n, p.grad)
+                    ng += 1
+            for i, f in enumerate(bb_cap):
+                put(f"bb{i}", f)
         for i, e in enumerate(enc_cap):
             put(f"enc{i}", e)
         for n, m in model.encoder.named_modules():
@@ -399,6 +416,11 @@ def main():
     torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
     Criterion, HungarianMatcher = _import_criterion()
     ref = make_golden._import_reference()
+    if os.environ.get("ONLY_FULL"):
+        st = golden_train_dn(ref, "n", 2, [3, 1], full_train=True)
+        np.savez_compressed(os.path.join(HERE, "train_full_n_b2.npz"), **st)
+        print("wrote train_full_n_b2.npz")
+        return
     if os.environ.get("ONLY_DN_ENC"):
         st = golden_train_dn(ref, "n", 2, [3, 1], enc_train=True)
         np.savez_compressed(os.path.join(HERE, "train_dn_enc_n_b2.npz"), **st)

@@ -140,7 +140,7 @@ def test_conv_pack_forward_dgrad_wgrad(k, cin, cout):
     dyn = dy.permute(0, 2, 3, 1).contiguous()
     kpad = (k * k * cin + 31) // 32 * 32
     wp = torch.empty(cout, kpad, device=DEV)
-    _lib.check(lib.dp_conv_pack(wt.data_ptr(), cout, cin, k, k, wp.data_ptr(), kpad, 0, 0, DP_F32, _s()), "pack")
+    _lib.check(lib.dp_conv_pack(wt.data_ptr(), cout, cin, k, k, wp.data_ptr(), kpad, 0, 0, None, DP_F32, _s()), "pack")
     out = torch.empty(B, h, w, cout, device=DEV)
     d = _conv_desc(xn, wp, kpad, cin, cout, h, w, k, out)
     _lib.check(lib.dp_conv2d(C.byref(d), _s()), "fwd")
@@ -149,7 +149,7 @@ def test_conv_pack_forward_dgrad_wgrad(k, cin, cout):
     # input gradient: conv of dz with the rotated packing, accumulated onto a prior value
     kpad2 = (k * k * cout + 31) // 32 * 32
     wf = torch.empty(cin, kpad2, device=DEV)
-    _lib.check(lib.dp_conv_pack(wt.data_ptr(), cout, cin, k, k, wf.data_ptr(), kpad2, 0, 1, DP_F32, _s()), "flip")
+    _lib.check(lib.dp_conv_pack(wt.data_ptr(), cout, cin, k, k, wf.data_ptr(), kpad2, 0, 1, None, DP_F32, _s()), "flip")
     prior = torch.randn(B, h, w, cin, device=DEV)
     dx = prior.clone()
     d2 = _conv_desc(dyn, wf, kpad2, cout, cin, h, w, k, dx, res=dx)
@@ -159,8 +159,8 @@ def test_conv_pack_forward_dgrad_wgrad(k, cin, cout):
     # weight gradient
     rows, K = B * h * w, cin * k * k
     col = torch.empty(rows, K, device=DEV)
-    _lib.check(lib.dp_im2col(xn.data_ptr(), h * w * cin, cin, B, h, w, cin, k, k, 1, (k - 1) // 2, h, w,
-                             col.data_ptr(), DP_F32, _s()), "im2col")
+    _lib.check(lib.dp_im2col(xn.data_ptr(), h * w * cin, cin, 1, B, h, w, cin, k, k, 1, (k - 1) // 2, h, w,
+                             col.data_ptr(), DP_F32, DP_F32, _s()), "im2col")
     dW = torch.zeros(cout, K, device=DEV)
     g = GemmDesc()
     g.a, g.a_bs, g.a_rs, g.a_ks = dyn.data_ptr(), 0, 1, cout
@@ -188,7 +188,7 @@ def test_depthwise_s2_backward_and_pack():
     y.backward(dy)
     oh, ow = y.shape[2:]
     taps = torch.empty(9, c, device=DEV)
-    _lib.check(lib.dp_conv_pack(wt.data_ptr(), c, 1, 3, 3, taps.data_ptr(), 0, 0, 2, DP_F32, _s()), "pack dw")
+    _lib.check(lib.dp_conv_pack(wt.data_ptr(), c, 1, 3, 3, taps.data_ptr(), 0, 0, 2, None, DP_F32, _s()), "pack dw")
     xn = x.detach().permute(0, 2, 3, 1).contiguous()
     dyn = dy.permute(0, 2, 3, 1).contiguous()
     d = ConvDesc()

@@ -1,0 +1,126 @@
+"""The whole training step of BASELINE config 5 on the HIP kernels: backbone
+(detrpose_amd/backbone_train.py: FrozenBatchNorm2d folded per step, every conv and LAB parameter
+trained, freeze_at=-1), encoder in training mode (encoder_train.py), transformer with
+OKS-denoising queries, criterion and backward (train_engine.py), against the reference's own
+full training step (tests/golden/train_full_n_b2.npz, made by tests/golden/make_train_golden.py,
+oracle pinned in tests/test_train_oracle.py::test_oracle_full_step_matches_reference): backbone
+and encoder outputs, all 27 losses, the gradient of every parameter of the network, the encoder's
+BatchNorm running statistics. fp32 mode, DETRPose-N at batch 2, the reference's DN draws."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from detrpose_amd import build_model
+from detrpose_amd.criterion import pack_targets
+from detrpose_amd.synthetic import load_synthetic, synthetic_images
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from test_gpu_encoder_train_step import _targets  # noqa: E402
+
+
+def run_full(g, dtype="fp32"):
+    from detrpose_amd.train_engine import TrainEngine
+    dev = torch.device("cuda")
+    model, _ = build_model("n", dtype=dtype)
+    load_synthetic(model, seed=int(g["meta"][1]))
+    eng = TrainEngine(model, dtype, dev, train_backbone=True)
+    B = int(g["meta"][0])
+    images = synthetic_images(B, seed=int(g["meta"][2])).to(dev)
+    bb = eng.backbone_plan(B, images.shape[2], images.shape[3])
+    bb.set_image(images)
+    shapes = [(v.H, v.W) for v in bb.outs]
+    ep = eng.encoder_plan(B, shapes, feats=bb.outs)
+    plan = eng.plan(B, int(g["dn_pad_size"]), shapes, memory=ep.memory, d_memory=ep.d_memory)
+    plan.set_dn(torch.as_tensor(g["dn_label"], dtype=torch.int32, device=dev),
+                torch.sigmoid(torch.as_tensor(g["dn_pose_unsig"], dtype=torch.float32, device=dev)),
+                torch.as_tensor(g["dn_attn_mask"], device=dev).to(torch.uint8))
+    sizes, ts = _targets(g, dev)
+    bb.forward()
+    ep.forward()
+    plan.forward()
+    keys, vals = plan.criterion(pack_targets(ts, 17, dev), sizes, int(g["dn_num_group"]))
+    plan.backward()
+    ep.backward()
+    bb.backward()
+    torch.cuda.synchronize()
+    return eng, bb, ep, dict(zip(keys, vals.cpu().tolist()))
+
+
+@pytest.fixture(scope="module")
+def full(golden_dir):
+    g = np.load(os.path.join(golden_dir, "train_full_n_b2.npz"))
+    return (g,) + run_full(g)
+
+
+def _nchw(v, buf):
+    return buf[:, v.off:v.off + v.c].reshape(v.B, v.H, v.W, v.c).permute(0, 3, 1, 2)
+
+
+def test_full_step_outputs_and_losses(full):
+    from test_train_oracle import _sampled
+    g, eng, bb, ep, losses = full
+    for tag, views in (("bb", bb.outs), ("enc", ep.levels)):
+        for i, v in enumerate(views):
+            idx, val, s, a = _sampled(g, f"{tag}{i}")
+            got = _nchw(v, v.buf.x).double().cpu().reshape(-1).numpy()
+            scale = max(float(np.abs(val).max()), a / got.size)
+            err = float(np.abs(got[idx] - val).max()) / scale
+            print(f"{tag}{i}: rel err {err:.3g}")
+            assert err <= 1e-4, (tag, i, err)
+    ref = dict(zip([str(k) for k in g["loss_keys"]], g["loss_vals"]))
+    assert sorted(losses) == sorted(ref)
+    worst = max(abs(losses[k] - ref[k]) / max(abs(ref[k]), 1.0) for k in ref)
+    print(f"losses: worst rel err {worst:.3g}")
+    assert worst <= 1e-5
+
+
+def test_full_step_gradients(full):
+    """Every parameter of backbone + encoder + transformer: sampled entries within 1e-3 of scale
+    (the LAB scalars 1e-2 of theirs, see full_step_scales), sums within 1e-3 of sum |g|."""
+    from test_train_oracle import _sampled, full_step_scales
+    g, eng, bb, ep, _ = full
+    names = sorted(k[:-len("__idx")] for k in g.files if k.startswith("grad.") and k.endswith("__idx"))
+    scales = full_step_scales(g, names)
+    rows = []
+    for n in names:
+        key = n[len("grad."):]
+        key = key if key.startswith(("encoder.", "backbone.")) else "transformer." + key
+        flat = eng.grads[key].double().cpu().reshape(-1).numpy()
+        idx, val, s, a = _sampled(g, n)
+        if scales[n] < 1e-5:
+            assert float(np.abs(flat).max()) < 1e-4, (n, float(np.abs(flat).max()))
+            continue
+        err = float(np.abs(flat[idx] - val).max()) / scales[n]
+        serr = abs(flat.sum() - s) / max(a, 1e-30) if flat.size > 1 else 0.0
+        rows.append((err / (10.0 if flat.size == 1 else 1.0), err, serr, n))
+    rows.sort(reverse=True)
+    for r in rows[:15]:
+        print(f"{r[3]}: rel err {r[1]:.3g}, sum rel err {r[2]:.3g}")
+    assert sum(n.startswith("grad.backbone.") for n in names) > 100
+    assert rows[0][0] <= 1e-3, rows[:8]
+    assert max(r[2] for r in rows) <= 1e-3, sorted(rows, key=lambda r: -r[2])[:5]
+
+
+def test_full_step_running_stats(full):
+    g, eng, *_ = full
+    for k in [k for k in g.files if k.startswith("bn.")]:
+        np.testing.assert_allclose(eng.running[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+def test_full_step_bf16_tracks_fp32(full):
+    """bf16 activations / activation gradients through the whole network: losses within 5 % of
+    the reference's, flat gradient within cosine 0.98 of the fp32 step's."""
+    g, eng32, *_ = full
+    eng, bb, ep, losses = run_full(g, "bf16")
+    ref = dict(zip([str(k) for k in g["loss_keys"]], g["loss_vals"]))
+    worst = max(abs(losses[k] - ref[k]) / max(abs(ref[k]), 1.0) for k in ref)
+    a = eng.grad_flat.double().cpu().numpy()
+    b = eng32.grad_flat.double().cpu().numpy()
+    cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+    print(f"bf16 full step: worst loss rel err {worst:.3g}, gradient cosine {cos:.6f}")
+    assert worst <= 5e-2 and cos >= 0.98

@@ -185,3 +185,87 @@ def test_oracle_encoder_step_gradients_match_reference(enc_case):
             np.testing.assert_allclose(stats[k[3:]].numpy(), g[k], rtol=1e-5, atol=1e-6, err_msg=k)
     worst.sort(reverse=True)
     print("worst relative errors:", worst[:5])
+
+
+def oracle_train_step_full(size, g):
+    """The whole of config 5 on the oracle: backbone (FrozenBatchNorm2d, every conv and LAB
+    parameter trained: freeze_at=-1), encoder in training mode, transformer with the golden DN
+    draws, criterion, backward. Returns (losses, grads keyed like the golden, backbone outputs,
+    encoder outputs, running stats)."""
+    from oracle.detrpose_cpu import backbone
+    from oracle.train_cpu import losses, train_encoder, train_transformer
+    cfg = get_config(size)
+    model, _ = build_model(size)
+    params = {k for k, v in model.named_parameters() if v.requires_grad}
+    load_synthetic(model, seed=int(g["meta"][1]))
+    sd = {k: v.detach().float() for k, v in model.state_dict().items()}
+    B = int(g["meta"][0])
+    images = synthetic_images(B, seed=int(g["meta"][2]))
+    P = {k: (v.clone().requires_grad_(True) if k in params else v) for k, v in sd.items()}
+    stats = {k: v.clone() for k, v in sd.items() if k.startswith("encoder.") and
+             (k.endswith("running_mean") or k.endswith("running_var"))}
+    bc = cfg["backbone"]
+    feats = backbone(images, P, bc["name"], bc["return_idx"], bc["use_lab"])
+    enc = train_encoder(feats, P, cfg["encoder"], stats)
+    res = train_transformer(enc, P, cfg["transformer"], dn=dn_inputs(g))
+    sizes, lab, kps, area = targets_of(g)
+    ld, _, _ = losses(res, sizes, lab, kps, area, cfg["transformer"]["num_body_points"],
+                      cfg["transformer"]["num_classes"])
+    sum(ld.values()).backward()
+    grads = {}
+    for k, v in P.items():
+        if isinstance(v, torch.Tensor) and v.requires_grad and v.grad is not None:
+            grads["grad." + (k[len("transformer."):] if k.startswith("transformer.") else k)] = v.grad
+    return ld, grads, [f.detach() for f in feats], [e.detach() for e in enc], stats
+
+
+@pytest.fixture(scope="module")
+def full_case(golden_dir):
+    g = np.load(os.path.join(golden_dir, "train_full_n_b2.npz"))
+    return g, oracle_train_step_full("n", g)
+
+
+def full_step_scales(g, names):
+    """Per-name error scale for sampled comparisons: max(|sampled values|, mean |entry|); the
+    LearnableAffineBlock scalars (one entry, a sum over a whole feature map that largely
+    cancels) against 1 % of the largest such scalar gradient (a LAB bias ahead of a training-mode
+    BatchNorm is analytically zero: the norm removes the per-channel shift)."""
+    lab = max(abs(float(g[n + "__val"][0])) for n in names if int(np.prod(g[n + "__shape"])) == 1)
+    out = {}
+    for n in names:
+        idx, val, s, a = _sampled(g, n)
+        size = int(np.prod(g[n + "__shape"])) if n + "__shape" in g.files else len(val)
+        out[n] = max(float(np.abs(val).max()), 1e-2 * lab) if size == 1 else max(float(np.abs(val).max()), a / size)
+    return out
+
+
+def test_oracle_full_step_matches_reference(full_case):
+    """Losses, every parameter gradient of backbone + encoder + transformer (sampled entries and
+    sums) within 1e-4 of scale (the LAB scalars 2e-3), backbone / encoder outputs, encoder
+    running statistics."""
+    g, (ld, grads, bb, enc, stats) = full_case
+    np.testing.assert_allclose([float(v) for v in ld.values()], g["loss_vals"], rtol=1e-5, atol=1e-6)
+    names = sorted(k[:-len("__idx")] for k in g.files if k.startswith("grad.") and k.endswith("__idx"))
+    assert names == sorted(grads), set(names) ^ set(grads)
+    assert sum(n.startswith("grad.backbone.") for n in names) > 100
+    checks = [(n, grads[n]) for n in names] + [(f"bb{i}", t) for i, t in enumerate(bb)] + \
+        [(f"enc{i}", t) for i, t in enumerate(enc)]
+    scales = full_step_scales(g, [n for n, _ in checks])
+    worst = []
+    for n, t in checks:
+        idx, val, s, a = _sampled(g, n)
+        got = t.detach().double().reshape(-1).numpy()
+        scale = scales[n]
+        if scale < 1e-5:
+            assert float(np.abs(got).max()) < 1e-5, (n, float(np.abs(got).max()))
+            continue
+        err = float(np.abs(got[idx] - val).max()) / scale
+        worst.append((err, n))
+        assert err <= (2e-3 if got.size == 1 else 1e-4), (n, err)
+        if got.size > 1:
+            assert abs(got.sum() - s) <= 1e-4 * a + 1e-9, (n, got.sum(), s)
+    for k in g.files:
+        if k.startswith("bn."):
+            np.testing.assert_allclose(stats[k[3:]].numpy(), g[k], rtol=1e-5, atol=1e-6, err_msg=k)
+    worst.sort(reverse=True)
+    print("worst relative errors:", worst[:5])
