@@ -256,10 +256,12 @@ def synthetic_targets(batch, K=17, seed=3, dev="cuda"):
 
 
 def train_leg(size, dtype, dev, batch, steps, warmup=3):
-    """BASELINE configs[4] on one GPU, the part that is built: frozen backbone + encoder forward,
-    transformer training forward with OKS-denoising queries, criterion (matching, losses and
-    their gradients), transformer backward, clip_grad_norm_ + AdamW (detrpose_amd.train.Trainer).
-    Per-phase device times from HIP events on the same stream."""
+    """BASELINE configs[4] on one GPU (per-GPU shard of the 8-GPU DDP step): backbone forward
+    (FrozenBatchNorm2d), encoder training forward (BatchNorm batch statistics), transformer
+    training forward with OKS-denoising queries, criterion (matching, losses and their gradients),
+    transformer / encoder / backbone backward, clip_grad_norm_ + AdamW + ModelEMA
+    (detrpose_amd.train.Trainer, scope 'full'). Per-phase device times from HIP events on the
+    same stream."""
     from detrpose_amd import build_model
     from detrpose_amd.synthetic import load_synthetic, synthetic_images
     from detrpose_amd.train import Trainer
@@ -278,35 +280,48 @@ def train_leg(size, dtype, dev, batch, steps, warmup=3):
     ms = (time.perf_counter() - t0) * 1e3 / steps
     # phase split of one more step (HIP events around each phase)
     plan = next(iter(tr.eng.plans.values()))
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    bb, ep = tr.bb, tr.ep
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
     ev[0].record()
-    tr._memory(images)
+    bb.forward()
     ev[1].record()
-    plan.forward()
+    ep.forward()
     ev[2].record()
+    plan.forward()
+    ev[3].record()
     from detrpose_amd.criterion import pack_targets
     from detrpose_amd.train import dn_meta
     packed = pack_targets(ts, 17, dev)
     plan.criterion(packed, packed.sizes, dn_meta(packed.sizes)[1])
-    ev[3].record()
-    plan.backward()
     ev[4].record()
-    tr.eng.optimizer_step(**tr.opt)
+    plan.backward()
     ev[5].record()
+    ep.backward()
+    ev[6].record()
+    bb.backward()
+    ev[7].record()
+    tr.eng.optimizer_step(**tr.opt)
+    tr.eng.ema_update(**tr.ema)
+    ev[8].record()
     torch.cuda.synchronize()
-    names = ["encoder_fwd (frozen)", "transformer_fwd", "criterion", "transformer_bwd", "clip+adamw"]
+    names = ["backbone_fwd", "encoder_fwd", "transformer_fwd", "criterion", "transformer_bwd", "encoder_bwd",
+             "backbone_bwd", "clip+adamw+ema"]
     phases = {n: round(ev[i].elapsed_time(ev[i + 1]), 3) for i, n in enumerate(names)}
-    flops = sum(plan.op_flops.values())
-    t_tr = phases["transformer_fwd"] + phases["transformer_bwd"]
-    return {"workload": f"DETRPose-{size.upper()} training step (BASELINE configs[4] on 1 GPU): frozen backbone + "
-                        f"encoder forward, transformer forward with OKS-denoising queries + criterion (incl. dn_* "
-                        f"losses) + transformer backward + clip_grad_norm_(0.1) + AdamW; {dtype}, batch {batch}, "
+    fl = {"backbone": sum(bb.op_flops.values()), "encoder": sum(ep.op_flops.values()),
+          "transformer": sum(plan.op_flops.values())}
+    t = {"backbone": phases["backbone_fwd"] + phases["backbone_bwd"],
+         "encoder": phases["encoder_fwd"] + phases["encoder_bwd"],
+         "transformer": phases["transformer_fwd"] + phases["transformer_bwd"]}
+    return {"workload": f"DETRPose-{size.upper()} training step (BASELINE configs[4], per-GPU shard on 1 GPU): "
+                        f"backbone (FrozenBN) + encoder (BatchNorm batch statistics) + transformer with "
+                        f"OKS-denoising queries, criterion (incl. dn_* losses), full backward, "
+                        f"clip_grad_norm_(0.1) + AdamW (backbone lr 1e-5) + ModelEMA; {dtype}, batch {batch}, "
                         f"synthetic targets (1-6 persons per image)",
             "ms_per_step": round(ms, 3), "images_per_sec": round(batch / ms * 1e3, 2), "steps": steps,
             "dn_pad": plan.P, "phase_ms": phases,
-            "transformer_gemm_tflops": round(flops / (t_tr * 1e-3) / 1e12, 2) if t_tr > 0 else None,
-            "losses_finite": bool(torch.isfinite(vals).all()),
-            "not_built": "backbone / encoder backward (frozen here), BatchNorm batch statistics"}
+            "tflops_by_part": {k: round(fl[k] / (t[k] * 1e-3) / 1e12, 2) if t[k] > 0 else None for k in fl},
+            "step_tflop": round(sum(fl.values()) / 1e12, 3),
+            "losses_finite": bool(torch.isfinite(vals).all())}
 
 
 def latency_bs1(model, pp, dev, runs, warmup):

@@ -155,7 +155,7 @@ _SIGS = {
                                   vp, f32, i32, vp]),
     "dp_im2col": (i32, [vp, i64, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp]),
     "dp_conv_pack": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, vp, i32, vp]),
-    "dp_frozen_act_bwd": (i32, [vp, i64, vp, i64, vp, i64, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp]),
+    "dp_frozen_act_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp]),
     "dp_col2im": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, i32, i32, i32, vp]),
     "dp_maxpool2x2_pad_rb_bwd": (i32, [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, vp]),
     "dp_dwconv_bwd": (i32, [vp, i64, i32, vp, i64, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, i32,

@@ -106,7 +106,7 @@ class BackboneTrainPlan(TapePlan):
                 x_src = dst
             if si in bb.return_idx:
                 self.outs.append(x_src)
-        self._record_backward()
+        self._record_backward(zero=False)   # zeroed by the encoder's backward, which runs first
         eng.cur = prev
 
     # ------------------------------------------------------------------ frozen BN
@@ -162,11 +162,13 @@ class BackboneTrainPlan(TapePlan):
                       beta=1.0)
         self._bwd.append(bwd)
 
-    def _act_bwd(self, bw, name, out, dz, s, lab, act):
-        """dz = d conv-output from out's gradient through LAB / ReLU / the frozen scale."""
+    def _act_bwd(self, bw, name, out, dz, s, lab, act, res=None):
+        """dz = d conv-output from out's gradient through LAB / ReLU / the frozen scale (res: the
+        residual the stored output includes)."""
         la, lb, gla, glb = lab if lab else (None, None, None, None)
-        bw.op(name + ".act_bwd", self.lib.dp_frozen_act_bwd, out.xp, out.ld, out.gp, out.ld, dz.xp, dz.ld, out.rows,
-              out.c, _lib.DP_ACT_RELU if act else _lib.DP_ACT_NONE, la, lb, _p(s), gla, glb, self.code)
+        bw.op(name + ".act_bwd", self.lib.dp_frozen_act_bwd, out.xp, out.ld, res.xp if res is not None else None,
+              res.ld if res is not None else 0, out.gp, out.ld, dz.xp, dz.ld, out.rows, out.c,
+              _lib.DP_ACT_RELU if act else _lib.DP_ACT_NONE, la, lb, _p(s), gla, glb, self.code)
 
     def cba(self, p, x, out, sd, k=1, stride=1, pad=None, dw=False, act=True, res=None):
         """ConvBNAct (hgnetv2.py:82-134) from x into out (+ res, the HG block's identity)."""
@@ -216,7 +218,7 @@ class BackboneTrainPlan(TapePlan):
             dz = self._dz(out.rows, out.cp)
             if out.cp != cout:   # the rotated-weight dgrad conv reads the pads
                 bw.op(name + ".dz0", lib.dp_zero, dz.xp, out.rows * out.cp * self.es)
-            self._act_bwd(bw, name, out, dz, s, lab, act)
+            self._act_bwd(bw, name, out, dz, s, lab, act, res)
             if dw:
                 taps_raw, _ = self.packed(wkey, 2, 0, 0)
                 bw.op(name + ".dw_bwd", lib.dp_dwconv_bwd, x.xp, H * W_ * x.ld, x.ld, dz.xp, oh * ow * dz.ld, dz.ld,

@@ -13,12 +13,14 @@ __device__ __forceinline__ float ldf(const T* p) {
   return to_f32(*p);
 }
 
-// ConvBNAct backward from its stored output y = lab(act(u)), u = s z + b (hgnetv2.py:129-134):
+// ConvBNAct backward from its stored output y = lab(act(u)) [+ res], u = s z + b (hgnetv2.py:129-134):
 // dz = dy * a * act'(u) * s[ch]; with LAB (scale a, bias cb) also d a += dy r, d cb += dy where r =
-// relu(u) = (y - cb) / a. relu'(u) is read off y: with LAB, r == 0 stored exactly cb (its dtype
-// rounding), so the unit is on where y differs from that and (y - cb) a > 0.
+// relu(u) = (y - res - cb) / a. relu'(u) is read off y: the unit counts as on where a r exceeds
+// the stored output's rounding (exact zero test without LAB and residual).
 template <typename T>
-__global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict__ y, int64_t ldy, const T* __restrict__ dy,
+__global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict__ y, int64_t ldy,
+                                                             const T* __restrict__ res, int64_t ldr,
+                                                             const T* __restrict__ dy,
                                                              int64_t lddy, T* __restrict__ dz, int64_t lddz, int rows,
                                                              int c, int act, const float* __restrict__ lab_a,
                                                              const float* __restrict__ lab_b,
@@ -26,11 +28,13 @@ __global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict
                                                              float* __restrict__ dlab_b) {
   const int64_t total = (int64_t)rows * c;
   const bool lab = lab_a != nullptr;
-  float a = 1.f, cb = 0.f, yc = 0.f;
+  // relative rounding of the stored output (f32: 2^-23, bf16: 2^-8): y = round(a r + cb + res),
+  // so r == 0 is told from r > 0 only up to that
+  const float eps = sizeof(T) == 2 ? 3.90625e-3f : 1.1920929e-7f;
+  float a = 1.f, cb = 0.f;
   if (lab) {
     a = *lab_a;
     cb = *lab_b;
-    yc = to_f32(from_f32<T>(cb));
   }
   float sa = 0.f, sc = 0.f;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -39,15 +43,19 @@ __global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict
     const float g = ldf(dy + r * lddy + ch);
     float d = g;
     if (act == DP_ACT_RELU) {
-      const float v = ldf(y + r * ldy + ch);
+      // the stored output holds lab(act(u)) + res (the HG block's identity, added after the act)
+      const float yv = ldf(y + r * ldy + ch);
+      const float rv = res ? ldf(res + r * ldr + ch) : 0.f;
+      const float v = yv - rv - cb;   // a * relu(u), up to the output's rounding
+      const float tol = (res || lab) ? eps * (fabsf(yv) + fabsf(rv) + fabsf(cb)) : 0.f;
+      const bool on = lab ? (a > 0.f ? v > tol : v < -tol) : v > tol;
       if (lab) {
-        const bool on = v != yc && (v - cb) * a > 0.f;
-        const float rr = on ? (v - cb) / a : 0.f;
+        const float rr = on ? v / a : 0.f;
         sa = fmaf(g, rr, sa);
         sc += g;
         d = on ? g * a : 0.f;
       } else {
-        d = v > 0.f ? g : 0.f;
+        d = on ? g : 0.f;
       }
     }
     if (scale) d *= scale[ch];
@@ -160,14 +168,15 @@ int grid_of(int64_t total) {
     }                       \
   } while (0)
 
-extern "C" int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* dy, int64_t ld_dy, void* dz, int64_t ld_dz,
+extern "C" int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* res, int64_t ld_res, const void* dy,
+                                 int64_t ld_dy, void* dz, int64_t ld_dz,
                                  int32_t rows, int32_t c, int32_t act, const float* lab_a, const float* lab_b,
                                  const float* scale, float* dlab_a, float* dlab_b, int32_t dtype, void* stream) {
   DP_REQUIRE(dy && dz && rows > 0 && c > 0 && (act == DP_ACT_NONE || (act == DP_ACT_RELU && y)) &&
                  (!lab_a || (lab_b && act == DP_ACT_RELU && dlab_a && dlab_b)),
              "dp_frozen_act_bwd: bad arguments");
   DP_DT(hipLaunchKernelGGL(frozen_act_bwd_kernel<T>, dim3(grid_of((int64_t)rows * c)), dim3(256), 0,
-                           as_stream(stream), (const T*)y, ld_y, (const T*)dy, ld_dy, (T*)dz, ld_dz, rows, c, act, lab_a,
+                           as_stream(stream), (const T*)y, ld_y, (const T*)res, ld_res, (const T*)dy, ld_dy, (T*)dz, ld_dz, rows, c, act, lab_a,
                            lab_b, scale, lab_a ? dlab_a : nullptr, dlab_b));
   return dp_check_launch("dp_frozen_act_bwd");
 }

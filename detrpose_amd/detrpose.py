@@ -103,24 +103,23 @@ class DETRPose(nn.Module):
 
         With targets: the full training forward with OKS-denoising queries through the HIP
         training step (detrpose_amd.train.train_forward): the reference's output dict incl.
-        dn_aux_outputs / dn_aux_pre_outputs / dn_meta, differentiable w.r.t. the transformer's
-        parameters, so `criterion(outputs, targets)` then `loss.backward()` fills their .grad
-        (src/solver/engine.py:34-60). The backbone and encoder run frozen (their backward is
-        not built: they receive no gradient).
+        dn_aux_outputs / dn_aux_pre_outputs / dn_meta, differentiable w.r.t. every parameter of
+        the network (the backbone with FrozenBatchNorm2d, the encoder with its BatchNorm2d on
+        batch statistics: SyncBatchNorm across ranks under torch.distributed), so
+        `criterion(outputs, targets)` then `loss.backward()` fills every .grad
+        (src/solver/engine.py:34-60). With the encoder's BatchNorm layers put in eval mode the
+        backbone and encoder run frozen instead and only the transformer is trained.
 
         Without targets: every decoder layer's logits / keypoints / corners (aux_outputs), the
         first layer's pre head and the two-stage selection, values only (the reference's own
-        non-DN training forward stops at transformer.py:1353).
-
-        BatchNorm layers must be in eval mode (frozen BN); train-mode batch statistics /
-        SyncBN are not built."""
+        non-DN training forward stops at transformer.py:1353); BatchNorm in eval mode."""
         bn = [n for n, m in self.named_modules() if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.training]
-        if bn:
-            raise NotImplementedError(f"{len(bn)} BatchNorm layers are in train mode (batch statistics / SyncBN are not "
-                                      f"built, e.g. {bn[0]}): put them in eval mode (frozen-BN training)")
         self._check_input(samples)
         if targets is not None:
-            return self._forward_train_dn(samples, targets)
+            return self._forward_train_dn(samples, targets, "full" if bn else "transformer")
+        if bn:
+            raise NotImplementedError(f"the training forward without targets runs with BatchNorm in eval mode "
+                                      f"({len(bn)} in train mode, e.g. {bn[0]})")
         eng = self.engine(samples.device)
         plan = eng.plan(samples.shape[0], aux=True)
         with torch.cuda.device(samples.device):
@@ -143,12 +142,12 @@ class DETRPose(nn.Module):
             out["aux_pre_outputs"] = {"pred_logits": ao["pre_logits"].clone(), "pred_keypoints": refs.clone()}
         return out
 
-    def _forward_train_dn(self, samples, targets):
+    def _forward_train_dn(self, samples, targets, scope):
         from .train import Trainer, train_forward
         dev = samples.device
         tr = getattr(self, "_trainer", None)
-        if tr is None or tr.device != dev or tr.eng.dtype_name != self.compute_dtype:
-            tr = Trainer(self, dtype=self.compute_dtype, device=dev)
+        if tr is None or tr.device != dev or tr.eng.dtype_name != self.compute_dtype or tr.scope != scope:
+            tr = Trainer(self, dtype=self.compute_dtype, device=dev, scope=scope, ema=False)
             object.__setattr__(self, "_trainer", tr)
         with torch.cuda.device(dev), torch.enable_grad():
             out = train_forward(tr, samples, targets)

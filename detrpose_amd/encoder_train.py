@@ -138,8 +138,10 @@ class TapePlan:
     def cost(self, name, flops):
         self.op_flops[name] = self.op_flops.get(name, 0.0) + flops
 
-    def _record_backward(self):
-        """Gradient buffers for every stored map (one zeroed arena), then the ops in reverse."""
+    def _record_backward(self, zero=True, extra_zero=()):
+        """Gradient buffers for every stored map (one arena), then the ops in reverse. The
+        backward starts by zeroing the arena (zero=False: a later plan's backward zeroes it
+        before accumulating into this plan's outputs: extra_zero = those arenas)."""
         total = sum(b.x.numel() for b in self.bufs)
         self.grad_arena = torch.empty(total, dtype=self.dt, device=self.dev)
         o = 0
@@ -147,9 +149,8 @@ class TapePlan:
             n = b.x.numel()
             b.g = self.grad_arena[o:o + n].view(b.x.shape)
             o += n
-        # zeroed at the end of the forward: a later plan's backward (the encoder's, into the
-        # backbone outputs) may accumulate into these before this plan's backward runs
-        self.fw.op("grads.zero", self.lib.dp_zero, _p(self.grad_arena), total * self.es)
+        for i, t in enumerate(([self.grad_arena] if zero else []) + list(extra_zero)):
+            self.bw.op(f"grads.zero{i}", self.lib.dp_zero, _p(t), t.numel() * t.element_size())
         for fn in reversed(self._bwd):
             fn()
 
@@ -364,10 +365,10 @@ class EncoderTrainPlan(TapePlan):
     shape set. eng: a TrainEngine built with train_encoder=True (the encoder parameters live in
     its flat master / gradient buffers)."""
 
-    def __init__(self, eng, B: int, feat_shapes, feats=None):
+    def __init__(self, eng, B: int, feat_shapes, feats=None, feats_plan=None):
         """feats: the backbone's output maps (backbone_train.BackboneTrainPlan.outs, their
-        gradients d loss / d feats accumulated by this backward) or None: own input buffers
-        (set_inputs)."""
+        gradients d loss / d feats accumulated by this backward; feats_plan: that plan, whose
+        gradient arena this backward zeroes first) or None: own input buffers (set_inputs)."""
         self._setup(eng)
         lib = self.lib
         enc = eng.model.encoder
@@ -445,7 +446,7 @@ class EncoderTrainPlan(TapePlan):
             self._bwd.append(lambda lv=lv, i=i, n=n: self.bw.op(
                 f"enc.memory{i}.bwd", lib.dp_convert_rows, _p(self.d_memory, starts[i] * Cc), DP_F32, self.S * Cc,
                 lv.gp, self.code, n, B, n, C.c_float(1.0), 1))
-        self._record_backward()
+        self._record_backward(extra_zero=[feats_plan.grad_arena] if feats_plan is not None else ())
         self.d_feats = [f.buf.g for f in self.feats]
         eng.cur = prev
 

@@ -1,16 +1,19 @@
-"""One DETRPose training step on the HIP kernels (BASELINE config 5, the transformer half):
+"""One DETRPose training step on the HIP kernels (BASELINE config 5):
 
-    images -> frozen backbone + encoder (the inference plan's launches up to the memory)
+    images -> backbone forward (backbone_train: FrozenBatchNorm2d folded per step)
+           -> encoder training forward (encoder_train: BatchNorm on batch statistics, SyncBN)
            -> OKS-denoising draws (dp_cdn_build)  -> transformer training forward (TrainPlan)
            -> Hungarian matching + losses + their gradients (incl. dn_*)
-           -> transformer backward -> gradient all-reduce over RCCL (DDP, when initialised)
-           -> clip_grad_norm_(0.1) + AdamW (two launches over the flat parameter buffer)
+           -> transformer backward (+ d memory) -> encoder backward -> backbone backward
+           -> gradient all-reduce over RCCL (DDP's mean, when initialised)
+           -> clip_grad_norm_(0.1) + AdamW (backbone lr 1e-5, the rest 1e-4) -> ModelEMA update
 
 Reference: src/solver/engine.py:34-95 (train_one_epoch: model(samples, targets), criterion,
-sum of the loss dict, backward, clip_grad_norm_, optimizer.step), the DN construction of
-src/models/detrpose/dn_component.py:39-183 and DDP's all-reduce (src/misc/dist_utils.py:111-133).
-Scope: the encoder / backbone are frozen here (their backward is not built yet: the encoder
-memory is the transformer's input and receives no gradient); BatchNorm stays in eval mode.
+sum of the loss dict, backward, clip_grad_norm_, optimizer.step, ema.update), the DN construction
+of src/models/detrpose/dn_component.py:39-183, the optimizer / EMA of
+configs/detrpose/detrpose_hgnetv2_*.py, DDP and SyncBN (src/misc/dist_utils.py:111-133).
+scope="transformer" keeps the earlier variant: backbone + encoder frozen (the inference plan's
+launches up to the memory, BatchNorm in eval mode), only the transformer trained.
 """
 from __future__ import annotations
 
@@ -55,13 +58,20 @@ class Trainer:
     values by default (configs/detrpose/detrpose_hgnetv2_*.py, include/detrpose_hgnetv2.py)."""
 
     def __init__(self, model, dtype="bf16", device="cuda", lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4,
-                 max_norm=0.1, dn_number=20, label_noise_ratio=0.5, weights=(2.0, 10.0, 4.0), seed=0):
+                 max_norm=0.1, dn_number=20, label_noise_ratio=0.5, weights=(2.0, 10.0, 4.0), seed=0,
+                 scope="full", backbone_lr=1e-5, ema=True, ema_decay=0.9999, ema_warmups=2000):
+        assert scope in ("full", "transformer"), scope
         self.model = model
         self.device = torch.device(device)
+        self.scope = scope
         model.set_dtype(dtype)
-        self.inf = model.engine(self.device)
-        self.eng = TrainEngine(model, dtype, self.device)
-        self.opt = dict(lr=lr, betas=betas, weight_decay=weight_decay, max_norm=max_norm)
+        if scope == "transformer":
+            self.inf = model.engine(self.device)
+        self.eng = TrainEngine(model, dtype, self.device, train_backbone=scope == "full")
+        self.opt = dict(lr=lr, betas=betas, weight_decay=weight_decay, max_norm=max_norm, backbone_lr=backbone_lr)
+        self.ema = dict(decay=ema_decay, warmups=ema_warmups) if ema else None
+        if ema:
+            self.eng.ema_init()
         self.dn_number, self.label_noise_ratio = dn_number, label_noise_ratio
         self.weights = weights
         self.seed = seed
@@ -71,8 +81,19 @@ class Trainer:
         self.dn_sigmas = torch.tensor(np.concatenate([[0.1], sig]).astype(np.float32), device=self.device)
 
     def _memory(self, images):
-        """The frozen backbone + encoder: the inference plan's launches up to the memory."""
+        """The encoder memory of images and its shapes: scope 'full' runs the backbone and encoder
+        training forwards (their plans kept in self.bb / self.ep for the backward); 'transformer'
+        the frozen inference plan's launches up to the memory."""
         B = images.shape[0]
+        if self.scope == "full":
+            bb = self.eng.backbone_plan(B, images.shape[2], images.shape[3])
+            bb.set_image(images)
+            shapes = [(v.H, v.W) for v in bb.outs]
+            ep = self.eng.encoder_plan(B, shapes, feats=bb.outs, feats_plan=bb)
+            bb.forward()
+            ep.forward()
+            self.bb, self.ep = bb, ep
+            return ep.memory, shapes
         plan = self.inf.plan(B)
         if images.data_ptr() != plan.input.data_ptr():
             plan.input.copy_(images.to(torch.float32))
@@ -115,12 +136,16 @@ class Trainer:
         sizes = packed.sizes
         meta = dn_meta(sizes, self.dn_number)
         pad, groups, single = meta if meta else (0, 1, 1)
-        plan = eng.plan(B, pad, shapes, memory=memory)
+        full = self.scope == "full"
+        plan = eng.plan(B, pad, shapes, memory=memory, d_memory=self.ep.d_memory if full else None)
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         self._draw_dn(plan, packed, images, pad, groups, single)
         plan.forward()
         keys, vals = plan.criterion(packed, sizes, groups, weights=self.weights)
         plan.backward()
+        if full:
+            self.ep.backward()
+            self.bb.backward()
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             world = torch.distributed.get_world_size()
             if world > 1:
@@ -131,6 +156,8 @@ class Trainer:
                            "grad mean")
         if update:
             eng.optimizer_step(**self.opt)
+            if self.ema is not None:
+                eng.ema_update(**self.ema)
         self.steps += 1
         return keys, vals
 
@@ -164,14 +191,19 @@ class _TransformerStep(torch.autograd.Function):
                 else:
                     d.copy_(g.reshape(d.shape))
         plan.backward()
+        if ctx.trainer.scope == "full":
+            ctx.trainer.ep.backward()
+            ctx.trainer.bb.backward()
         return (None, None, *[eng.grads[n].clone() for n in eng.pnames])
 
 
 def train_forward(trainer, images, targets):
     """DETRPose.forward(samples, targets) in training mode (transformer.py:1219-1387): the
     reference's output dict (final head, aux_outputs, aux_pre_outputs, aux_interm_outputs,
-    dn_aux_outputs, dn_aux_pre_outputs, dn_meta), differentiable w.r.t. the transformer's
-    parameters through _TransformerStep."""
+    dn_aux_outputs, dn_aux_pre_outputs, dn_meta), differentiable w.r.t. every trained parameter
+    (scope 'full': backbone + encoder + transformer; 'transformer': the transformer's) through
+    _TransformerStep. The encoder's BatchNorm running statistics are updated in the module, as
+    the reference's train-mode BatchNorm does."""
     eng = trainer.eng
     model = trainer.model
     eng.load_weights()          # the module's current parameter values (the user's optimizer owns them)
@@ -183,8 +215,14 @@ def train_forward(trainer, images, targets):
     packed = pack_targets(targets, K, trainer.device)
     meta = dn_meta(packed.sizes, trainer.dn_number)
     pad, groups, single = meta if meta else (0, 1, 1)
-    plan = eng.plan(B, pad, shapes, memory=memory)
+    full = trainer.scope == "full"
+    plan = eng.plan(B, pad, shapes, memory=memory, d_memory=trainer.ep.d_memory if full else None)
     trainer._draw_dn(plan, packed, images, pad, groups, single)
+    if full:
+        with torch.no_grad():
+            for n, b in model.named_buffers():
+                if n in eng.running:
+                    b.copy_(eng.running[n].to(b.device, b.dtype))
     params = [p for n, p in model.named_parameters() if n in eng.params]
     assert len(params) == len(eng.pnames)
     outs = _TransformerStep.apply(trainer, plan, *params)

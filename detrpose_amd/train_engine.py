@@ -131,11 +131,20 @@ class TrainEngine:
         self.opt_step = 0
         self.grads, self.params = {}, {}
         o = 0
+        self.offsets = {}
         for n, sz in zip(self.pnames, sizes):
             k = int(np.prod(shapes[n]))
             self.grads[n] = self.grad_flat[o:o + k].view(shapes[n])
             self.params[n] = self.master[o:o + k].view(shapes[n])
+            self.offsets[n] = (o, o + sz)
             o += sz
+        # the backbone's parameters are one leading range of the flat buffers (module order):
+        # its own AdamW learning rate (configs/detrpose/detrpose_hgnetv2_*.py: '^(?=.*backbone).*$')
+        bbn = [n for n in self.pnames if n.startswith("backbone.")]
+        self.bb_end = self.offsets[bbn[-1]][1] if bbn else 0
+        assert all(self.offsets[n][1] <= self.bb_end for n in bbn)
+        self.ema = None
+        self.ema_updates = 0
         self.running = {}
         if train_encoder:
             for n, b in model.named_buffers():
@@ -220,20 +229,44 @@ class TrainEngine:
         for p in self.plans.values():
             p.refresh_constants()
 
-    def optimizer_step(self, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4, max_norm=0.1):
-        """clip_grad_norm_(max_norm) + AdamW over every transformer parameter (src/solver/
-        engine.py:78-89, configs: AdamW lr 1e-4, wd 1e-4, clip 0.1) on the flat buffers: two
-        launches, no host synchronisation."""
+    def optimizer_step(self, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4, max_norm=0.1,
+                       backbone_lr=1e-5):
+        """clip_grad_norm_(max_norm) over every trained parameter + AdamW (src/solver/
+        engine.py:78-89, configs: AdamW lr 1e-4 (backbone 1e-5), wd 1e-4, clip 0.1) on the flat
+        buffers: one norm launch, one AdamW launch per learning-rate range, no host
+        synchronisation."""
         lib = self.lib
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         n = self.master.numel()
         self.opt_step += 1
         if max_norm and max_norm > 0:
             _lib.check(lib.dp_grad_sqnorm(_p(self.grad_flat), n, _p(self.sqnorm), s), "dp_grad_sqnorm")
-        _lib.check(lib.dp_adamw(_p(self.master), _p(self.grad_flat), _p(self.exp_avg), _p(self.exp_avg_sq), n, lr,
-                                betas[0], betas[1], eps, weight_decay, self.opt_step,
-                                max_norm if max_norm else 0.0, _p(self.sqnorm), s), "dp_adamw")
+        for o0, o1, lr_ in ((0, self.bb_end, backbone_lr), (self.bb_end, n, lr)):
+            if o1 > o0:
+                _lib.check(lib.dp_adamw(_p(self.master, o0), _p(self.grad_flat, o0), _p(self.exp_avg, o0),
+                                        _p(self.exp_avg_sq, o0), o1 - o0, lr_, betas[0], betas[1], eps, weight_decay,
+                                        self.opt_step, max_norm if max_norm else 0.0, _p(self.sqnorm), s), "dp_adamw")
         self.refresh()
+
+    def ema_init(self):
+        self.ema = self.master.clone()
+        self.ema_running = {k: v.clone() for k, v in self.running.items()}
+        self.ema_updates = 0
+
+    def ema_update(self, decay=0.9999, warmups=2000):
+        """ModelEMA.update (src/nn/optimizer/ema.py:55-70) over the trained parameters and the
+        BatchNorm running statistics: v = d v + (1 - d) p, d = decay (1 - exp(-updates / warmups)),
+        from the copy ema_init() took (ModelEMA deep-copies the model when it is built)."""
+        lib = self.lib
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        if self.ema is None:
+            self.ema_init()
+        self.ema_updates += 1
+        d = decay * (1 - math.exp(-self.ema_updates / warmups)) if warmups else decay
+        pairs = [(self.ema, self.master)] + [(self.ema_running[k], v) for k, v in self.running.items()]
+        for e, p in pairs:
+            _lib.check(lib.dp_axpby_rows(_p(e), e.numel(), _p(e), e.numel(), C.c_float(d), _p(p), p.numel(),
+                                         C.c_float(1.0 - d), 1, e.numel(), 0, DP_F32, s), "ema")
 
     def state_dict_update(self, module=None):
         """Write the master parameters back into the module (reference names)."""
@@ -309,14 +342,14 @@ class TrainEngine:
             self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes], memory, d_memory)
         return self.plans[key]
 
-    def encoder_plan(self, batch: int, feat_shapes, feats=None):
+    def encoder_plan(self, batch: int, feat_shapes, feats=None, feats_plan=None):
         """The HybridEncoder's training forward / backward (encoder_train.EncoderTrainPlan);
         feats: the backbone plan's output maps (its input), or None (own input buffers)."""
         assert self.train_encoder, "TrainEngine(train_encoder=True) trains the encoder"
         from .encoder_train import EncoderTrainPlan
         key = (batch, tuple(tuple(s) for s in feat_shapes), id(feats[0].buf) if feats else None)
         if key not in self.enc_plans:
-            self.enc_plans[key] = EncoderTrainPlan(self, batch, feat_shapes, feats)
+            self.enc_plans[key] = EncoderTrainPlan(self, batch, feat_shapes, feats, feats_plan)
         return self.enc_plans[key]
 
     def backbone_plan(self, batch: int, h: int, w: int):

@@ -615,11 +615,13 @@ int dp_act_bwd(const void* pre, int64_t ld_pre, const void* dy, int64_t ld_dy, v
  * parameter, freeze_norm=True keeps FrozenBatchNorm2d; hgnetv2.py:24-61, 82-383). Callers:
  * detrpose_amd/backbone_train.py. */
 
-/* Backward of ConvBNAct's epilogue y = lab(act(s z + b)) from its stored output (hgnetv2.py:129-134):
- * dz = dy * a * act'(.) * scale[ch] (scale: the frozen BN scale, NULL = 1; a = *lab_a, or 1 without
- * LAB); with the LAB scalars (device lab_a / lab_b, NULL = no LAB) *dlab_a += sum dy * relu(.),
- * *dlab_b += sum dy. act: DP_ACT_NONE (y unused) or DP_ACT_RELU. Rows ld apart, of dtype. */
-int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* dy, int64_t ld_dy, void* dz, int64_t ld_dz,
+/* Backward of ConvBNAct's epilogue y = lab(act(s z + b)) [+ res] from its stored output
+ * (hgnetv2.py:129-134; res: the HG block's identity added after it, hgnetv2.py:326-329, NULL =
+ * none): dz = dy * a * act'(.) * scale[ch] (scale: the frozen BN scale, NULL = 1; a = *lab_a, or 1
+ * without LAB); with the LAB scalars (device lab_a / lab_b, NULL = no LAB) *dlab_a += sum dy *
+ * relu(.), *dlab_b += sum dy. act: DP_ACT_NONE (y unused) or DP_ACT_RELU. Rows ld apart, of dtype. */
+int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* res, int64_t ld_res, const void* dy, int64_t ld_dy,
+                      void* dz, int64_t ld_dz,
                       int32_t rows, int32_t c, int32_t act, const float* lab_a, const float* lab_b, const float* scale,
                       float* dlab_a, float* dlab_b, int32_t dtype, void* stream);
 /* dx (= or += when accumulate) = col2im(col): col [batch*oh*ow][cin*kh*kw] (K order cin, ky, kx) =

@@ -145,3 +145,80 @@ def test_train_forward_with_targets_autograd(golden_dir):
                     float(params[n].grad.abs().max())) for n in names), reverse=True)
     print("autograd vs plan gradient: worst relative differences", rows[:6])
     assert rows[0][0] <= 1e-5
+
+
+def test_train_forward_full_network_autograd(golden_dir):
+    """The reference's training loop with the model in train mode (encoder BatchNorm on batch
+    statistics): model(samples, targets) -> criterion -> loss.backward() gives EVERY trainable
+    parameter (backbone, encoder, transformer) a .grad equal to the training tapes' own gradient
+    replayed on the same forward, and the encoder's BatchNorm running statistics move."""
+    from detrpose_amd.criterion import Criterion, HungarianMatcher, pack_targets
+    model = _model(golden_dir, "n", 0, "fp32").cuda()
+    model.train()
+    rm0 = model.encoder.input_proj[0].norm.running_mean.clone()
+    img = synthetic_images(2, seed=1).cuda()
+    gen = torch.Generator().manual_seed(4)
+    targets = []
+    for n in (3, 2):
+        c = torch.rand(n, 2, generator=gen) * 0.6 + 0.2
+        wh = torch.rand(n, 2, generator=gen) * 0.3 + 0.05
+        kp = torch.cat([torch.rand(n, 34, generator=gen), (torch.rand(n, 17, generator=gen) > 0.3).float()], 1)
+        targets.append({"labels": torch.tensor([i % 2 for i in range(n)]).cuda(), "keypoints": kp.cuda(),
+                        "boxes": torch.cat([c - wh / 2, c + wh / 2], 1).cuda(), "area": (wh.prod(1) * 0.53).cuda()})
+    crit = Criterion(2, HungarianMatcher(2.0, 0.25, 10.0, 4.0), {"loss_vfl": 2.0, "loss_keypoints": 10.0,
+                                                                 "loss_oks": 4.0}, ["vfl", "keypoints"], 17)
+    out = model(img, targets)
+    loss = sum(crit(out, targets).values())
+    assert torch.isfinite(loss)
+    loss.backward()
+    tr = model._trainer
+    assert tr.scope == "full"
+    params = dict(model.named_parameters())
+    names = [n for n, p in params.items() if p.requires_grad]
+    assert all(params[n].grad is not None for n in names), [n for n in names if params[n].grad is None][:5]
+    assert sum(n.startswith("backbone.") for n in names) > 100 and sum(n.startswith("encoder.") for n in names) > 50
+    assert not torch.equal(rm0, model.encoder.input_proj[0].norm.running_mean)
+    # replay: the plan's own criterion + the three backward tapes on the same forward
+    plan = next(p for p in tr.eng.plans.values() if p.P == 36)
+    packed = pack_targets(targets, 17, img.device)
+    plan.criterion(packed, packed.sizes, 6)
+    plan.backward()
+    tr.ep.backward()
+    tr.bb.backward()
+    torch.cuda.synchronize()
+    # relative to each gradient's scale, floored at 1e-4 of the largest (analytically-zero BN
+    # biases ahead of a training-mode BatchNorm carry only atomic-order noise); the LAB scalars
+    # (sums over whole maps that cancel, f32 atomics in another order) to 2.5e-2
+    top = max(float(tr.eng.grads[n].abs().max()) for n in names)
+    rows = sorted(((float((params[n].grad - tr.eng.grads[n]).abs().max()) /
+                    max(float(tr.eng.grads[n].abs().max()), 1e-4 * top) / (50.0 if params[n].numel() == 1 else 1.0),
+                    n) for n in names), reverse=True)
+    print("autograd vs tapes: worst relative differences (scalars / 50)", rows[:6])
+    assert rows[0][0] <= 5e-4
+
+
+def test_trainer_full_steps_reduce_the_loss(golden_dir):
+    """Trainer(scope='full') end to end on N bf16: backbone + encoder (BN batch statistics) +
+    transformer, clip + AdamW (backbone lr 1e-5) + EMA; six steps on one batch lower the loss."""
+    from detrpose_amd.train import Trainer
+    g = np.load(os.path.join(golden_dir, "train_dn_n_b2.npz"))
+    model, _ = build_model("n")
+    from detrpose_amd.synthetic import load_synthetic
+    load_synthetic(model, seed=int(g["meta"][1]))
+    dev = torch.device("cuda")
+    tr = Trainer(model, dtype="bf16", device=dev, lr=2e-4, backbone_lr=2e-5)
+    images = synthetic_images(2, seed=1).to(dev)
+    sizes = [int(v) for v in g["sizes"]]
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    ts = [{"labels": torch.as_tensor(g["tgt_labels"][off[b]:off[b + 1]]).to(dev),
+           "keypoints": torch.as_tensor(g["tgt_kps"][off[b]:off[b + 1]]).to(dev),
+           "area": torch.as_tensor(g["tgt_area"][off[b]:off[b + 1]]).to(dev),
+           "boxes": torch.as_tensor(g["tgt_boxes"][off[b]:off[b + 1]]).to(dev)} for b in range(len(sizes))]
+    totals = []
+    for _ in range(6):
+        keys, vals = tr.step(images, ts)
+        totals.append(float(vals.sum()))
+    print("full-network bf16 total loss per step:", [round(t, 3) for t in totals])
+    assert all(np.isfinite(totals)) and len(keys) == 27
+    assert totals[-1] < totals[0], totals
+    assert tr.eng.ema_updates == 6 and torch.isfinite(tr.eng.ema).all()
