@@ -13,7 +13,7 @@ the f32 master at the start of each step (dp_conv_pack with the per-channel scal
 is the epilogue bias), ReLU and LAB in the epilogue, the HG-block residual as its residual input,
 concats written in place. Backward, per ConvBNAct: dp_frozen_act_bwd (ReLU / LAB read off the
 stored output, LAB scalar gradients, times the frozen scale) gives d conv-output; then
-  1x1            wgrad dp_gemm (dz^T x), dgrad dp_gemm (dz W)
+  1x1            wgrad dp_gemm (dz^T x), dgrad dp_conv2d of dz with the transposed packing
   k x k s1       wgrad dp_im2col + dp_gemm, dgrad dp_conv2d of dz with the rotated weights
                  (stem2a / stem2b read F.pad(0,1,0,1): the rotated conv pads top / left)
   3x3 s2 dense   StemBlock.stem3: dgrad dp_gemm (dz W) + dp_col2im
@@ -227,8 +227,8 @@ class BackboneTrainPlan(TapePlan):
             if k == 1 and stride == 1:
                 self.gemm(bw, name + ".dW", dz.xp, 1, dz.ld, x.xp, x.ld, 1, _p(G), cin, cout, cin, out.rows,
                           out_code=DP_F32, beta=1.0)
-                self.gemm(bw, name + ".dx", dz.xp, dz.ld, 1, self.wptr(wkey), cin, 1, x.gp, x.ld, out.rows, cin, cout,
-                          beta=1.0)
+                wb, kpad2 = self.packed(wkey, 1, dz.cp, x.cp)   # the transposed weights: dx += dz W
+                self._dgrad_conv(bw, name, dz, wb, kpad2, x, 1, 0)
                 return
             K = cin * k * k
             col = self._colbuf(out.rows * K)
@@ -238,22 +238,27 @@ class BackboneTrainPlan(TapePlan):
                       beta=1.0)
             if stride == 1:
                 wb, kpad2 = self.packed(wkey, 1, dz.cp, x.cp)
-                dd = ConvDesc()
-                dd.in_, dd.in_bstride, dd.in_pstride, dd.in_h, dd.in_w, dd.cin = dz.xp, oh * ow * dz.ld, dz.ld, oh, ow, dz.cp
-                dd.weight, dd.kpad, dd.bias = _p(wb), kpad2, None
-                dd.kh, dd.kw, dd.stride, dd.pad_t, dd.pad_l = k, k, 1, k - 1 - pad, k - 1 - pad
-                dd.out, dd.out_bstride, dd.out_pstride, dd.out_h, dd.out_w, dd.cout = x.gp, H * W_ * x.ld, x.ld, H, W_, x.cp
-                dd.res, dd.res_bstride, dd.res_pstride = x.gp, H * W_ * x.ld, x.ld
-                dd.batch, dd.act, dd.dtype = B, _lib.DP_ACT_NONE, self.code
-                bw.keep.append(dd)
-                bw.op(name + ".dx", lib.dp_conv2d, C.byref(dd))
-                self.cost(name + ".dx", 2.0 * x.rows * cin * k * k * cout)
+                self._dgrad_conv(bw, name, dz, wb, kpad2, x, k, k - 1 - pad)
             else:   # strided dense conv (stem3): dcol = dz W, then col2im
                 dcol = self._dcolbuf(out.rows * K)
                 self.gemm(bw, name + ".dcol", dz.xp, dz.ld, 1, self.wptr(wkey), K, 1, _p(dcol), K, out.rows, K, cout)
                 bw.op(name + ".col2im", lib.dp_col2im, _p(dcol), B, H, W_, cin, k, k, stride, pad, oh, ow, x.gp,
                       H * W_ * x.ld, x.ld, 1, self.code)
         self._bwd.append(bwd)
+
+    def _dgrad_conv(self, bw, name, dz, wb, kpad2, x, k, pad):
+        """x.g += the stride-1 conv of dz (of x's spatial size) with the rotated packing wb."""
+        B, H, W_ = x.B, x.H, x.W
+        dd = ConvDesc()
+        dd.in_, dd.in_bstride, dd.in_pstride, dd.in_h, dd.in_w, dd.cin = dz.xp, H * W_ * dz.ld, dz.ld, H, W_, dz.cp
+        dd.weight, dd.kpad, dd.bias = _p(wb), kpad2, None
+        dd.kh, dd.kw, dd.stride, dd.pad_t, dd.pad_l = k, k, 1, pad, pad
+        dd.out, dd.out_bstride, dd.out_pstride, dd.out_h, dd.out_w, dd.cout = x.gp, H * W_ * x.ld, x.ld, H, W_, x.cp
+        dd.res, dd.res_bstride, dd.res_pstride = x.gp, H * W_ * x.ld, x.ld
+        dd.batch, dd.act, dd.dtype = B, _lib.DP_ACT_NONE, self.code
+        bw.keep.append(dd)
+        bw.op(name + ".dx", self.lib.dp_conv2d, C.byref(dd))
+        self.cost(name + ".dx", 2.0 * x.rows * x.c * k * k * dz.c)
 
     def _dz(self, rows, cp):
         """d conv-output of one layer's backward: a view of one shared buffer (the layers'

@@ -13,11 +13,12 @@ reduction sums all-reduced.
 The reference runs this through torch autograd; here the forward records a fixed tape of C-ABI
 launches, each op registering its backward, and the backward tape is those in reverse:
 
-  conv 1x1        dp_gemm forward / dgrad (dz W) / wgrad (dz^T x, split-K f32 atomics), on the
-                  reference weight layout [cout][cin] (segmented inputs: one GEMM per segment)
-  conv 3x3 s1     dp_conv2d on weights packed per step from the f32 master (dp_conv_pack mode 0);
-                  input gradient = dp_conv2d of dz with the 180-degree-rotated packing (mode 1)
-                  accumulated through its residual input; wgrad = dp_im2col + dp_gemm
+  conv k x k s1   dp_conv2d on weights packed per step from the f32 master (dp_conv_pack mode 0);
+                  input gradient = dp_conv2d of dz with the 180-degree-rotated packing (mode 1;
+                  1x1: the transposed weights) accumulated through its residual input; wgrad =
+                  dp_gemm (dz^T x, split-K f32 atomics; 3x3 over dp_im2col)
+  conv 1x1 over   dp_gemm forward / dgrad / wgrad on the reference weight layout [cout][cin],
+  a padded concat one GEMM per segment (DETRPose-N's 21-channel CSP outputs)
   depthwise s2    dp_dwconv2d / dp_dwconv_bwd
   BatchNorm2d     dp_bn_stats (+ all-reduce of the per-rank parts) + dp_bn_finalize, then
   (+ act, + sum)  dp_bn_act_fwd (one or two branches: VGGBlock, the CSP sum fused);
@@ -83,6 +84,17 @@ class V:
 
     def ch(self, c0, c, cp=None):
         return V(self.buf, self.off + c0, self.ld, c, c if cp is None else cp, self.B, self.H, self.W)
+
+
+def all_reduce(t):
+    """Sum over the ranks in place (RCCL on device tensors; host-staged under gloo, whose
+    collectives take host tensors: the one-GPU multi-rank rehearsal and tests)."""
+    if torch.distributed.get_backend() == "gloo" and t.is_cuda:
+        h = t.cpu()
+        torch.distributed.all_reduce(h)
+        t.copy_(h)
+    else:
+        torch.distributed.all_reduce(t)
 
 
 def _host(fn):
@@ -205,7 +217,7 @@ class TapePlan:
         B, H, W = x0.B, x0.H, x0.W
         rows = x0.rows
         G = self.eng.grads[wkey]
-        if k == 1:
+        if k == 1 and len(segs) > 1:   # a padded concat read as segments: one GEMM per segment
             z = self.view(B, H, W, cout)
             Wp = self.wptr(wkey)
             cin_t = self.eng.params[wkey].shape[1]
@@ -231,8 +243,13 @@ class TapePlan:
         cin = x.c
 
         def bwd():
-            # input gradient: conv of dz with the rotated weights, accumulated (residual = itself)
+            # input gradient: conv of dz with the rotated weights (1x1: the transposed weights),
+            # accumulated (residual = itself)
             self._conv2d(self.bw, name + ".dx", z.gp, z.ld, z.cp, x.gp, x.ld, x.cp, wb, kpad2, B, H, W, k, res=x.gp)
+            if k == 1:
+                self.gemm(self.bw, name + ".dW", z.gp, 1, z.ld, x.xp, x.ld, 1, _p(G), cin, cout, cin, rows,
+                          out_code=DP_F32, beta=1.0)
+                return
             K = cin * k * k
             col = self._colbuf(rows * K)
             self.bw.op(name + ".im2col", lib.dp_im2col, x.xp, H * W * x.ld, x.ld, 1, B, H, W, cin, k, k, 1, k // 2, H,
@@ -302,7 +319,7 @@ class TapePlan:
                 fw.op(f"{name}.bn{bi}.zero", lib.dp_zero, _p(parts), parts.numel() * 4)
             fw.op(f"{name}.bn{bi}.stats", lib.dp_bn_stats, z.xp, z.ld, rows, c, _p(parts[self.rank]), code)
             if self.world > 1:
-                fw.op(f"{name}.bn{bi}.sync", _host(lambda t=parts: torch.distributed.all_reduce(t)))
+                fw.op(f"{name}.bn{bi}.sync", _host(lambda t=parts: all_reduce(t)))
             rm, rv = eng.running[p + ".running_mean"], eng.running[p + ".running_var"]
             fw.op(f"{name}.bn{bi}.finalize", lib.dp_bn_finalize, _p(parts), self.world, C.c_float(rows), c,
                   C.c_float(1e-5), C.c_float(0.1), _p(rm), _p(rv), _p(mr))
@@ -328,7 +345,7 @@ class TapePlan:
                   _p(b2) if two else N, rows, c, ACT[act], _p(sums), _p(dg1), _p(db1), _p(dg2) if two else N,
                   _p(db2) if two else N, code)
             if self.world > 1:
-                bw.op(name + ".bn_sync", _host(lambda: torch.distributed.all_reduce(sums)))
+                bw.op(name + ".bn_sync", _host(lambda: all_reduce(sums)))
             bw.op(name + ".bn_apply", lib.dp_bn_act_bwd_apply, z1.gp, z1.ld, z2.gp if two else N, z2.ld if two else 0,
                   out.gp, out.ld, z1.xp, z1.ld, _p(mr1), _p(g1), _p(b1), z2.xp if two else N, z2.ld if two else 0,
                   _p(mr2) if two else N, _p(g2) if two else N, _p(b2) if two else N, rows, c, ACT[act], _p(sums),

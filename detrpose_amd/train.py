@@ -24,6 +24,7 @@ import torch
 
 from . import _lib
 from .criterion import COCO_SIGMAS, CROWDPOSE_SIGMAS, pack_targets
+from .encoder_train import all_reduce
 from .train_engine import TrainEngine, _p
 
 
@@ -150,7 +151,7 @@ class Trainer:
             world = torch.distributed.get_world_size()
             if world > 1:
                 # DDP: mean of the ranks' gradients (one all-reduce of the flat f32 buffer)
-                torch.distributed.all_reduce(eng.grad_flat)
+                all_reduce(eng.grad_flat)
                 _lib.check(lib.dp_convert_rows(_p(eng.grad_flat), 0, eng.grad_flat.numel(), _p(eng.grad_flat), 0,
                                                eng.grad_flat.numel(), 1, eng.grad_flat.numel(), 1.0 / world, 0, s),
                            "grad mean")

@@ -679,8 +679,9 @@ class TrainPlan:
         world = 1
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             # criterion.py:306-323: num_boxes / num_boxes_go summed over the ranks
-            torch.distributed.all_reduce(self.n_boxes)
-            torch.distributed.all_reduce(self.n_go)
+            from .encoder_train import all_reduce
+            all_reduce(self.n_boxes)
+            all_reduce(self.n_go)
             world = torch.distributed.get_world_size()
         heads = (_lib.LossHead * H)()
         for h in range(H):

@@ -1,0 +1,104 @@
+"""SyncBatchNorm of the encoder's training step across ranks (sync_bn: dist_utils.py:122,
+include/detrpose_hgnetv2.py:18): two ranks on the one GPU (gloo, host-staged collectives) each run
+the encoder training forward / backward on one image of a batch of two; every rank's encoder
+outputs, the BatchNorm running statistics and d loss / d backbone features must equal the
+single-process run of the whole batch (BatchNorm statistics over both images), and the ranks'
+parameter gradients summed must equal the single-process ones. The loss is a fixed linear
+functional of the memory (its gradient d memory is given), so the check isolates the encoder."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _step(feats, dmem, seed):
+    """One encoder forward + backward on cuda:0; returns host copies of what is compared."""
+    from detrpose_amd import build_model
+    from detrpose_amd.synthetic import load_synthetic
+    from detrpose_amd.train_engine import TrainEngine
+    model, _ = build_model("n", dtype="fp32")
+    load_synthetic(model, seed=seed)
+    eng = TrainEngine(model, "fp32", torch.device("cuda"), train_encoder=True)
+    B = feats[0].shape[0]
+    ep = eng.encoder_plan(B, [(f.shape[2], f.shape[3]) for f in feats])
+    ep.set_inputs([f.cuda() for f in feats])
+    ep.forward()
+    eng.grad_flat.zero_()
+    ep.d_memory.copy_(dmem.cuda())
+    ep.backward()
+    torch.cuda.synchronize()
+    enc = [n for n in eng.pnames if n.startswith("encoder.")]
+    o0 = eng.offsets[enc[0]][0]
+    o1 = eng.offsets[enc[-1]][1]
+    return {"memory": ep.memory.float().cpu(), "grads": eng.grad_flat[o0:o1].cpu(),
+            "dfeat": [v.buf.g[:, :v.c].float().cpu().reshape(B, v.H, v.W, v.c) for v in ep.feats],
+            "running": {k: v.cpu() for k, v in eng.running.items()}}
+
+
+def _rank_main(rank, port, feats, dmem, seed, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    try:
+        torch.distributed.init_process_group("gloo", rank=rank, world_size=WORLD)
+        torch.cuda.set_device(0)
+        r = _step([f[rank:rank + 1] for f in feats], dmem[rank:rank + 1], seed)
+        from detrpose_amd.encoder_train import all_reduce
+        g = r["grads"].clone()
+        torch.distributed.all_reduce(g)
+        r["grads_sum"] = g
+        q.put((rank, r))
+        torch.distributed.barrier()
+    finally:
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
+
+
+def test_syncbn_two_ranks_equal_one_batch(golden_dir):
+    import sys
+    sys.path.insert(0, HERE)
+    from test_gpu_encoder_train_step import backbone_feats
+    g = np.load(os.path.join(golden_dir, "train_dn_enc_n_b2.npz"))
+    feats = [f.contiguous() for f in backbone_feats(g)]
+    S = sum(f.shape[2] * f.shape[3] for f in feats)
+    dmem = torch.randn(2, S, 128, generator=torch.Generator().manual_seed(3)) * 1e-3
+    seed = int(g["meta"][1])
+    ref = _step(feats, dmem, seed)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, port, feats, dmem, seed, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(WORLD):
+        m = res[r]["memory"]
+        err = float((m - ref["memory"][r:r + 1]).abs().max()) / float(ref["memory"].abs().max())
+        print(f"rank {r}: memory rel err {err:.3g}")
+        assert err <= 1e-5
+        for i, d in enumerate(res[r]["dfeat"]):
+            e = float((d - ref["dfeat"][i][r:r + 1]).abs().max()) / float(ref["dfeat"][i].abs().max())
+            print(f"rank {r}: dfeat{i} rel err {e:.3g}")
+            assert e <= 1e-4
+        for k, v in ref["running"].items():
+            np.testing.assert_allclose(res[r]["running"][k].numpy(), v.numpy(), rtol=1e-4, atol=1e-6, err_msg=k)
+    gs, gr = res[0]["grads_sum"], ref["grads"]
+    e = float((gs - gr).abs().max()) / float(gr.abs().max())
+    print(f"summed rank gradients vs one batch: rel err {e:.3g}")
+    assert e <= 1e-4
