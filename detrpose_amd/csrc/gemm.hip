@@ -248,6 +248,180 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------- 128x128 bf16 tiles
+// The large-shape bf16 path (every decoder / AIFI Linear of the training step at batch 16:
+// M = rows of 10^4-10^5, N and K of 256-1024, and their split-K weight gradients): 128 x 128
+// outputs per 256-thread block, 4 waves of 64 x 64 (4 x 4 MFMA 16x16x32 tiles), K steps of 64,
+// LDS double-buffered (one barrier per K step; the next step's global loads are in registers
+// while the current step's 32 MFMAs run). Operand images in LDS:
+//   k-contiguous operand (mode 0): [128 rows][72] (144-byte rows, 16-byte stores, b128
+//     fragment reads), as the 64 x 64 kernel;
+//   row-contiguous operand (mode 1: the transposed operand of dgrad / wgrad): [64 k][128 rows]
+//     in 256-byte rows with the 16-byte chunk XOR swizzle of cdna_hip_programming.md T10 (b),
+//     written with 16-byte stores and read back with ds_read_b64_tr_b16 (two 4-k reads per
+//     fragment: lane group g takes k = 8g .. 8g+7, the same k slots as the b128 reads).
+constexpr int BT = 128, BKB = 64, P0 = 72;
+constexpr int IMG = BT * P0 > BKB * BT ? BT * P0 : BKB * BT;   // elements per operand image
+
+__device__ __forceinline__ int swz_off(int r, int ch) {   // bytes of chunk ch of k-row r
+  return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+
+struct Tile2Regs {
+  uint4 v[4];
+};
+
+__device__ __forceinline__ void load_tile2(Tile2Regs& t, const Operand& op, int mode, int64_t base, int r0, int k0,
+                                           int K) {
+  const bf16_t* p = reinterpret_cast<const bf16_t*>(op.p) + base;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    int gr, gk;
+    if (mode == 0) {
+      gr = r0 + (c >> 3);
+      gk = k0 + (c & 7) * 8;
+      if (gr < op.rows && gk + 8 <= K) {
+        t.v[i] = *reinterpret_cast<const uint4*>(p + (int64_t)gr * op.rs + gk);
+      } else {
+        bf16_t e8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) e8[e] = (gr < op.rows && gk + e < K) ? p[(int64_t)gr * op.rs + gk + e] : (bf16_t)0.f;
+        t.v[i] = *reinterpret_cast<const uint4*>(e8);
+      }
+    } else {
+      gk = k0 + (c >> 4);
+      gr = r0 + (c & 15) * 8;
+      if (gk < K && gr + 8 <= op.rows) {
+        t.v[i] = *reinterpret_cast<const uint4*>(p + (int64_t)gk * op.ks + gr);
+      } else {
+        bf16_t e8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) e8[e] = (gk < K && gr + e < op.rows) ? p[(int64_t)gk * op.ks + gr + e] : (bf16_t)0.f;
+        t.v[i] = *reinterpret_cast<const uint4*>(e8);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void store_tile2(const Tile2Regs& t, bf16_t* img, int mode) {
+  const int tid = threadIdx.x;
+  char* b = reinterpret_cast<char*>(img);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    if (mode == 0) *reinterpret_cast<uint4*>(img + (c >> 3) * P0 + (c & 7) * 8) = t.v[i];
+    else *reinterpret_cast<uint4*>(b + swz_off(c >> 4, c & 15)) = t.v[i];
+  }
+}
+
+// the 16x16x32 operand fragment of rows r0 .. r0+15 at k = kb + 8 (lane >> 4) .. +7
+__device__ __forceinline__ bf16x8 frag2(const bf16_t* img, int mode, int r0, int kb) {
+  const int lane = threadIdx.x & 63;
+  if (mode == 0) return *reinterpret_cast<const bf16x8*>(img + (r0 + (lane & 15)) * P0 + kb + 8 * (lane >> 4));
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const int q = (lane & 15) >> 2, pp = lane & 3, g = lane >> 4;
+  const char* b = reinterpret_cast<const char*>(img);
+  const int ch = (r0 >> 3) + (pp >> 1);
+  const int k0 = kb + 8 * g + q;
+  const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4*)(b + swz_off(k0, ch) + 8 * (pp & 1)));
+  const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4*)(b + swz_off(k0 + 4, ch) + 8 * (pp & 1)));
+  short t8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return *reinterpret_cast<const bf16x8*>(t8);
+}
+
+__global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem128[];   // [buffer][A | B][IMG]
+  bf16_t(*sm)[2][IMG] = reinterpret_cast<bf16_t(*)[2][IMG]>(smem128);
+  const int tile = blockIdx.x;
+  const int tm = tile / g.tiles_n, tn = tile - tm * g.tiles_n;
+  const int zb = blockIdx.y;
+  const int bidx = zb / g.splits, split = zb - bidx * g.splits;
+  const int m0 = tm * BT, n0 = tn * BT;
+  const int kb = split * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const Operand A = g.A, B = g.B;
+  const int64_t aoff = (int64_t)bidx * A.bs + (int64_t)kb * A.ks, boff = (int64_t)bidx * B.bs + (int64_t)kb * B.ks;
+  const int KC = ke - kb;
+  Tile2Regs ra, rb;
+  if (KC > 0) {
+    load_tile2(ra, A, g.modeA, aoff, m0, 0, KC);
+    load_tile2(rb, B, g.modeB, boff, n0, 0, KC);
+    store_tile2(ra, sm[0][0], g.modeA);
+    store_tile2(rb, sm[0][1], g.modeB);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < KC; k0 += BKB) {
+    const bool more = k0 + BKB < KC;
+    if (more) {
+      load_tile2(ra, A, g.modeA, aoff, m0, k0 + BKB, KC);
+      load_tile2(rb, B, g.modeB, boff, n0, k0 + BKB, KC);
+    }
+    const bf16_t* Ai = sm[cur][0];
+    const bf16_t* Bi = sm[cur][1];
+#pragma unroll
+    for (int ks = 0; ks < BKB / 32; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag2(Ai, g.modeA, wm + 16 * i, 32 * ks);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag2(Bi, g.modeB, wn + 16 * j, 32 * ks);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {   // the other buffer's readers passed the previous iteration's barrier
+      store_tile2(ra, sm[cur ^ 1][0], g.modeA);
+      store_tile2(rb, sm[cur ^ 1][1], g.modeB);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const int64_t cbo = (int64_t)bidx * g.c_bs;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn + 16 * j + (lane & 15);
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+        if (m >= g.M) continue;
+        const int64_t o = cbo + (int64_t)m * g.c_rs + n;
+        float v = g.alpha * acc[i][j][r];
+        if (g.splits > 1) {
+          unsafeAtomicAdd(g.cf + o, v);
+          continue;
+        }
+        if (g.bias) v += g.bias[n];
+        if (g.beta != 0.f) v += g.beta * (g.cf ? g.cf[o] : (float)g.cb[o]);
+        if (g.act == DP_ACT_RELU) v = fmaxf(v, 0.f);
+        else if (g.act == DP_ACT_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+        if (g.gate) {
+          const int64_t go = (int64_t)bidx * g.g_bs + (int64_t)m * g.g_rs + n;
+          const float gv = g.gate_bf16 ? (float)reinterpret_cast<const bf16_t*>(g.gate)[go]
+                                       : reinterpret_cast<const float*>(g.gate)[go];
+          if (!(gv > 0.f)) v = 0.f;
+        }
+        if (g.cf) g.cf[o] = v;
+        else g.cb[o] = (bf16_t)v;
+      }
+    }
+}
+
 int operand_mode(const Operand& op, int vec, int64_t align_bytes_ok) {
   if (op.ks == 1 && op.rs % vec == 0 && align_bytes_ok) return 0;
   if (op.rs == 1 && op.ks % vec == 0 && align_bytes_ok) return 1;
@@ -290,7 +464,15 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
   g.g_bs = d.gate_bs;
   g.g_rs = d.gate_rs;
   g.gate_bf16 = d.gate_dtype == DP_BF16;
-  const int tm = (d.m + TM - 1) / TM, tn = (d.n + TN - 1) / TN;
+  // 128 x 128 tiles for large bf16 shapes whose operands load as 16-byte rows or columns
+  // (DETRPOSE_GEMM64=1: the 64 x 64 kernel everywhere, for A/B)
+  static const bool force64 = getenv("DETRPOSE_GEMM64") != nullptr;
+  const bool splittable = d.out_dtype == DP_F32 && !d.bias && d.act == DP_ACT_NONE && !d.gate && d.beta == 1.f &&
+                          d.k >= 8 * 64;
+  const bool big = !force64 && d.in_dtype == DP_BF16 && g.modeA < 2 && g.modeB < 2 && d.m >= 128 && d.n >= 96 &&
+                   ((int64_t)d.m * d.n >= (int64_t)128 * 128 * 64 || (splittable && d.split_k == 0));
+  const int TMs = big ? BT : TM, TNs = big ? BT : TN;
+  const int tm = (d.m + TMs - 1) / TMs, tn = (d.n + TNs - 1) / TNs;
   g.tiles_n = tn;
   // split-K when the output grid cannot fill the chip and K is long (f32 C, plain epilogue)
   int splits = 1;
@@ -312,7 +494,15 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
   DP_REQUIRE(tiles * 1 < (1ll << 31) && (int64_t)d.batch * splits < 65536, "dp_gemm: grid too large");
   dim3 grid((unsigned)(tm * tn), (unsigned)(d.batch * splits)), block(256);
   hipStream_t s = as_stream(stream);
-  if (d.in_dtype == DP_BF16)
+  if (big) {
+    constexpr size_t lds = sizeof(bf16_t) * 4 * IMG;   // 72 KB: two buffers of both operands
+    static const bool attr_ok =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm128_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) == hipSuccess;
+    DP_REQUIRE(attr_ok, "dp_gemm: cannot set the 128x128 kernel's LDS size");
+    hipLaunchKernelGGL(gemm128_kernel, grid, block, lds, s, g);
+  }
+  else if (d.in_dtype == DP_BF16)
     hipLaunchKernelGGL(gemm_kernel<bf16_t>, grid, block, 0, s, g);
   else
     hipLaunchKernelGGL(gemm_kernel<float>, grid, block, 0, s, g);

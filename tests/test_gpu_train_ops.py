@@ -37,9 +37,12 @@ def gemm(a, a_st, b, b_st, c, c_rs, m, n, k, bias=None, alpha=1.0, beta=0.0, act
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("m,n,k", [(300, 72, 256), (64, 64, 64), (1000, 288, 130), (7, 2, 256)])
+@pytest.mark.parametrize("m,n,k", [(300, 72, 256), (64, 64, 64), (1000, 288, 130), (7, 2, 256), (4100, 288, 520),
+                                   (2056, 1032, 264)])
 def test_gemm_linear_dgrad_wgrad(dt, m, n, k):
-    """y = x W^T + b (+relu), dx = dy W (relu gate), dW += dy^T x (split-K atomics)."""
+    """y = x W^T + b (+relu), dx = dy W (relu gate), dW += dy^T x (split-K atomics). The last two
+    shapes take the bf16 128 x 128 path (k-strided operands through transposed LDS reads),
+    with ragged M / N / K edges."""
     torch.manual_seed(0)
     x = torch.randn(m, k, device=DEV).to(dt)
     W = torch.randn(n, k, device=DEV).to(dt)
