@@ -4,6 +4,8 @@
 // strided dense conv as col2im of dz W, and the StemBlock max-pool's backward. The convs run on
 // dp_conv2d / dp_dwconv2d (forward, stride-1 input gradient) and dp_gemm (weight gradients over
 // dp_im2col); see detrpose_amd/backbone_train.py for the tape.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -20,13 +22,16 @@ __device__ __forceinline__ float ldf(const T* p) {
 template <typename T>
 __global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict__ y, int64_t ldy,
                                                              const T* __restrict__ res, int64_t ldr,
-                                                             const T* __restrict__ dy,
-                                                             int64_t lddy, T* __restrict__ dz, int64_t lddz, int rows,
-                                                             int c, int act, const float* __restrict__ lab_a,
+                                                             const T* __restrict__ dy, int64_t lddy, T* __restrict__ dz,
+                                                             int64_t lddz, int rows, int c, int act,
+                                                             const float* __restrict__ lab_a,
                                                              const float* __restrict__ lab_b,
                                                              const float* __restrict__ scale, float* __restrict__ dlab_a,
                                                              float* __restrict__ dlab_b) {
-  const int64_t total = (int64_t)rows * c;
+  // a thread owns one channel and walks the rows blockIdx.x, + gridDim.x, ... (no per-element
+  // division); grid = (row slices, channel blocks)
+  const int ch = blockIdx.y * blockDim.x + threadIdx.x;
+  const bool active = ch < c;
   const bool lab = lab_a != nullptr;
   // relative rounding of the stored output (f32: 2^-23, bf16: 2^-8): y = round(a r + cb + res),
   // so r == 0 is told from r > 0 only up to that
@@ -36,30 +41,30 @@ __global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict
     a = *lab_a;
     cb = *lab_b;
   }
+  const float sc_ch = (scale && active) ? scale[ch] : 1.f;
   float sa = 0.f, sc = 0.f;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / c;
-    const int ch = (int)(e - r * c);
-    const float g = ldf(dy + r * lddy + ch);
-    float d = g;
-    if (act == DP_ACT_RELU) {
-      // the stored output holds lab(act(u)) + res (the HG block's identity, added after the act)
-      const float yv = ldf(y + r * ldy + ch);
-      const float rv = res ? ldf(res + r * ldr + ch) : 0.f;
-      const float v = yv - rv - cb;   // a * relu(u), up to the output's rounding
-      const float tol = (res || lab) ? eps * (fabsf(yv) + fabsf(rv) + fabsf(cb)) : 0.f;
-      const bool on = lab ? (a > 0.f ? v > tol : v < -tol) : v > tol;
-      if (lab) {
-        const float rr = on ? v / a : 0.f;
-        sa = fmaf(g, rr, sa);
-        sc += g;
-        d = on ? g * a : 0.f;
-      } else {
-        d = on ? g : 0.f;
+  if (active) {
+    for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+      const float g = ldf(dy + (int64_t)r * lddy + ch);
+      float d = g;
+      if (act == DP_ACT_RELU) {
+        // the stored output holds lab(act(u)) + res (the HG block's identity, added after the act)
+        const float yv = ldf(y + (int64_t)r * ldy + ch);
+        const float rv = res ? ldf(res + (int64_t)r * ldr + ch) : 0.f;
+        const float v = yv - rv - cb;   // a * relu(u), up to the output's rounding
+        const float tol = (res || lab) ? eps * (fabsf(yv) + fabsf(rv) + fabsf(cb)) : 0.f;
+        const bool on = lab ? (a > 0.f ? v > tol : v < -tol) : v > tol;
+        if (lab) {
+          const float rr = on ? v / a : 0.f;
+          sa = fmaf(g, rr, sa);
+          sc += g;
+          d = on ? g * a : 0.f;
+        } else {
+          d = on ? g : 0.f;
+        }
       }
+      dz[(int64_t)r * lddz + ch] = from_f32<T>(d * sc_ch);
     }
-    if (scale) d *= scale[ch];
-    dz[r * lddz + ch] = from_f32<T>(d);
   }
   if (!dlab_a) return;
   __shared__ float red[2][4];
@@ -68,15 +73,20 @@ __global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict
     sa += __shfl_xor(sa, o);
     sc += __shfl_xor(sc, o);
   }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (lane == 0) {
     red[0][wv] = sa;
     red[1][wv] = sc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(dlab_a, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    atomicAdd(dlab_b, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    float ta = 0.f, tc = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      ta += red[0][w];
+      tc += red[1][w];
+    }
+    atomicAdd(dlab_a, ta);
+    atomicAdd(dlab_b, tc);
   }
 }
 
@@ -175,8 +185,9 @@ extern "C" int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* res, i
   DP_REQUIRE(dy && dz && rows > 0 && c > 0 && (act == DP_ACT_NONE || (act == DP_ACT_RELU && y)) &&
                  (!lab_a || (lab_b && act == DP_ACT_RELU && dlab_a && dlab_b)),
              "dp_frozen_act_bwd: bad arguments");
-  DP_DT(hipLaunchKernelGGL(frozen_act_bwd_kernel<T>, dim3(grid_of((int64_t)rows * c)), dim3(256), 0,
-                           as_stream(stream), (const T*)y, ld_y, (const T*)res, ld_res, (const T*)dy, ld_dy, (T*)dz, ld_dz, rows, c, act, lab_a,
+  const int bx = c >= 256 ? 256 : (c + 63) / 64 * 64, gy = (c + bx - 1) / bx;
+  const int gx = std::max(1, std::min(rows, (1 << 16) / (bx * gy)));
+  DP_DT(hipLaunchKernelGGL(frozen_act_bwd_kernel<T>, dim3(gx, gy), dim3(bx), 0, as_stream(stream), (const T*)y, ld_y, (const T*)res, ld_res, (const T*)dy, ld_dy, (T*)dz, ld_dz, rows, c, act, lab_a,
                            lab_b, scale, lab_a ? dlab_a : nullptr, dlab_b));
   return dp_check_launch("dp_frozen_act_bwd");
 }

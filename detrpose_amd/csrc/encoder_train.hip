@@ -108,20 +108,29 @@ __device__ __forceinline__ float bn_of(const BnBranch& p, int64_t r, int ch, int
   return fmaf(p.g[ch], h, p.b[ch]);
 }
 
+// Row kernels: a thread owns one channel (its per-channel parameters in registers) and walks
+// the rows blockIdx.x, + gridDim.x, ...; consecutive threads take consecutive channels of a row.
+// grid = (row slices, channel blocks of blockDim.x): see rc_grid.
+
 // y = act(bn1(z1) [+ bn2(z2)]) (+ res when res != NULL)
 template <typename T>
-__global__ void bn_act_fwd_kernel(T* __restrict__ y, int64_t ldy, BnBranch p1, BnBranch p2, const T* __restrict__ res,
-                                  int64_t ldr, int rows, int c, int act) {
-  const int64_t total = (int64_t)rows * c;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / c;
-    const int ch = (int)(e - r * c);
-    float h;
-    float v = bn_of<T>(p1, r, ch, c, &h);
-    if (p2.z) v += bn_of<T>(p2, r, ch, c, &h);
+__global__ __launch_bounds__(256) void bn_act_fwd_kernel(T* __restrict__ y, int64_t ldy, BnBranch p1, BnBranch p2,
+                                                         const T* __restrict__ res, int64_t ldr, int rows, int c,
+                                                         int act) {
+  const int ch = blockIdx.y * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  const float m1 = p1.mr[ch], s1 = p1.mr[c + ch], g1 = p1.g[ch], b1 = p1.b[ch];
+  const bool two = p2.z != nullptr;
+  const float m2 = two ? p2.mr[ch] : 0.f, s2 = two ? p2.mr[c + ch] : 0.f, g2 = two ? p2.g[ch] : 0.f,
+              b2 = two ? p2.b[ch] : 0.f;
+  const T* z1 = reinterpret_cast<const T*>(p1.z) + ch;
+  const T* z2 = two ? reinterpret_cast<const T*>(p2.z) + ch : nullptr;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+    float v = fmaf(g1, (ld_(z1 + (int64_t)r * p1.ld) - m1) * s1, b1);
+    if (two) v += fmaf(g2, (ld_(z2 + (int64_t)r * p2.ld) - m2) * s2, b2);
     v = act_f(v, act);
-    if (res) v += ld_(res + r * ldr + ch);
-    y[r * ldy + ch] = from_f32<T>(v);
+    if (res) v += ld_(res + (int64_t)r * ldr + ch);
+    y[(int64_t)r * ldy + ch] = from_f32<T>(v);
   }
 }
 
@@ -171,20 +180,30 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restr
 // dz_k = g_k rstd_k (dp - sum dp / N - xh_k sum (dp xh_k) / N) (torch batch_norm_backward with
 // the synced sums)
 template <typename T>
-__global__ void bn_act_bwd_apply_kernel(T* __restrict__ dz1, int64_t ld1, T* __restrict__ dz2, int64_t ld2,
-                                        const T* __restrict__ dy, int64_t ldy, BnBranch p1, BnBranch p2, int rows,
-                                        int c, int act, const float* __restrict__ sums, float inv_n) {
-  const int64_t total = (int64_t)rows * c;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / c;
-    const int ch = (int)(e - r * c);
-    float h1, h2 = 0.f;
-    float pre = bn_of<T>(p1, r, ch, c, &h1);
-    if (p2.z) pre += bn_of<T>(p2, r, ch, c, &h2);
-    const float dp = ld_(dy + r * ldy + ch) * act_d(pre, act);
-    const float m0 = sums[ch] * inv_n;
-    dz1[r * ld1 + ch] = from_f32<T>(p1.g[ch] * p1.mr[c + ch] * (dp - m0 - h1 * sums[c + ch] * inv_n));
-    if (dz2) dz2[r * ld2 + ch] = from_f32<T>(p2.g[ch] * p2.mr[c + ch] * (dp - m0 - h2 * sums[2 * c + ch] * inv_n));
+__global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(T* __restrict__ dz1, int64_t ld1, T* __restrict__ dz2,
+                                                               int64_t ld2, const T* __restrict__ dy, int64_t ldy,
+                                                               BnBranch p1, BnBranch p2, int rows, int c, int act,
+                                                               const float* __restrict__ sums, float inv_n) {
+  const int ch = blockIdx.y * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  const float m1 = p1.mr[ch], s1 = p1.mr[c + ch], g1 = p1.g[ch], b1 = p1.b[ch];
+  const bool two = p2.z != nullptr;
+  const float m2 = two ? p2.mr[ch] : 0.f, s2 = two ? p2.mr[c + ch] : 0.f, g2 = two ? p2.g[ch] : 0.f,
+              b2 = two ? p2.b[ch] : 0.f;
+  const float m0 = sums[ch] * inv_n, c1 = sums[c + ch] * inv_n, c2 = sums[2 * c + ch] * inv_n;
+  const float k1 = g1 * s1, k2 = g2 * s2;
+  const T* z1 = reinterpret_cast<const T*>(p1.z) + ch;
+  const T* z2 = two ? reinterpret_cast<const T*>(p2.z) + ch : nullptr;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+    const float h1 = (ld_(z1 + (int64_t)r * p1.ld) - m1) * s1;
+    float pre = fmaf(g1, h1, b1), h2 = 0.f;
+    if (two) {
+      h2 = (ld_(z2 + (int64_t)r * p2.ld) - m2) * s2;
+      pre += fmaf(g2, h2, b2);
+    }
+    const float dp = ld_(dy + (int64_t)r * ldy + ch) * act_d(pre, act);
+    dz1[(int64_t)r * ld1 + ch] = from_f32<T>(k1 * (dp - m0 - h1 * c1));
+    if (dz2) dz2[(int64_t)r * ld2 + ch] = from_f32<T>(k2 * (dp - m0 - h2 * c2));
   }
 }
 
@@ -329,29 +348,43 @@ __global__ void up2_kernel(const T* __restrict__ src, int64_t sbs, int sps, int 
 
 // y (=|+=) alpha a [+ beta b]: residual adds and their backward (gradient fan-out)
 template <typename T>
-__global__ void axpby_kernel(T* __restrict__ y, int64_t ldy, const T* __restrict__ a, int64_t lda, float alpha,
-                             const T* __restrict__ b, int64_t ldb, float beta, int rows, int c, int acc) {
-  const int64_t total = (int64_t)rows * c;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / c;
-    const int ch = (int)(e - r * c);
-    float v = alpha * ld_(a + r * lda + ch);
-    if (b) v = fmaf(beta, ld_(b + r * ldb + ch), v);
-    T* o = y + r * ldy + ch;
+__global__ __launch_bounds__(256) void axpby_kernel(T* __restrict__ y, int64_t ldy, const T* __restrict__ a, int64_t lda,
+                                                    float alpha, const T* __restrict__ b, int64_t ldb, float beta,
+                                                    int rows, int c, int acc) {
+  const int ch = blockIdx.y * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+    float v = alpha * ld_(a + (int64_t)r * lda + ch);
+    if (b) v = fmaf(beta, ld_(b + (int64_t)r * ldb + ch), v);
+    T* o = y + (int64_t)r * ldy + ch;
     *o = from_f32<T>(acc ? ld_(o) + v : v);
   }
 }
 
 // dx = dy * act'(pre) (the AIFI FFN's GELU, hybrid_encoder.py:292)
 template <typename T>
-__global__ void act_bwd_kernel(const T* __restrict__ pre, int64_t ldp, const T* __restrict__ dy, int64_t ldy,
-                               T* __restrict__ dx, int64_t ldx, int rows, int c, int act) {
-  const int64_t total = (int64_t)rows * c;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / c;
-    const int ch = (int)(e - r * c);
-    dx[r * ldx + ch] = from_f32<T>(ld_(dy + r * ldy + ch) * act_d(ld_(pre + r * ldp + ch), act));
-  }
+__global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ pre, int64_t ldp, const T* __restrict__ dy,
+                                                      int64_t ldy, T* __restrict__ dx, int64_t ldx, int rows, int c,
+                                                      int act) {
+  const int ch = blockIdx.y * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x)
+    dx[(int64_t)r * ldx + ch] =
+        from_f32<T>(ld_(dy + (int64_t)r * ldy + ch) * act_d(ld_(pre + (int64_t)r * ldp + ch), act));
+}
+
+// (row slices, channel blocks) of a row kernel: blockDim.x = the channels rounded to a wave (at
+// most 256), about 64 K threads in flight per launch
+struct RC {
+  dim3 grid, block;
+};
+RC rc_grid(int rows, int c) {
+  const int bx = c >= 256 ? 256 : (c + 63) / 64 * 64;
+  const int gy = (c + bx - 1) / bx;
+  int gx = (1 << 16) / (bx * gy);
+  if (gx > rows) gx = rows;
+  if (gx < 1) gx = 1;
+  return {dim3((unsigned)gx, (unsigned)gy), dim3((unsigned)bx)};
 }
 
 int grid_for(int64_t total) {
@@ -401,8 +434,9 @@ extern "C" int dp_bn_act_fwd(void* y, int64_t ld_y, const void* z1, int64_t ld1,
   DP_REQUIRE(y && z1 && mr1 && g1 && b1 && rows > 0 && c > 0 && (!z2 || (mr2 && g2 && b2)),
              "dp_bn_act_fwd: bad arguments");
   const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
-  DP_DT(hipLaunchKernelGGL(bn_act_fwd_kernel<T>, dim3(grid_for((int64_t)rows * c)), dim3(256), 0, as_stream(stream),
-                           (T*)y, ld_y, p1, p2, (const T*)res, ld_res, rows, c, act));
+  const RC g = rc_grid(rows, c);
+  DP_DT(hipLaunchKernelGGL(bn_act_fwd_kernel<T>, g.grid, g.block, 0, as_stream(stream), (T*)y, ld_y, p1, p2,
+                           (const T*)res, ld_res, rows, c, act));
   return dp_check_launch("dp_bn_act_fwd");
 }
 
@@ -434,9 +468,10 @@ extern "C" int dp_bn_act_bwd_apply(void* dz1, int64_t ld_dz1, void* dz2, int64_t
                  (!z2 || (mr2 && g2 && b2 && dz2)),
              "dp_bn_act_bwd_apply: bad arguments");
   const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
-  DP_DT(hipLaunchKernelGGL(bn_act_bwd_apply_kernel<T>, dim3(grid_for((int64_t)rows * c)), dim3(256), 0,
-                           as_stream(stream), (T*)dz1, ld_dz1, (T*)(z2 ? dz2 : nullptr), ld_dz2, (const T*)dy, ld_dy,
-                           p1, p2, rows, c, act, sums, 1.f / count));
+  const RC g = rc_grid(rows, c);
+  DP_DT(hipLaunchKernelGGL(bn_act_bwd_apply_kernel<T>, g.grid, g.block, 0, as_stream(stream), (T*)dz1, ld_dz1,
+                           (T*)(z2 ? dz2 : nullptr), ld_dz2, (const T*)dy, ld_dy, p1, p2, rows, c, act, sums,
+                           1.f / count));
   return dp_check_launch("dp_bn_act_bwd_apply");
 }
 
@@ -506,15 +541,25 @@ extern "C" int dp_axpby_rows(void* y, int64_t ld_y, const void* a, int64_t ld_a,
                              int64_t ld_b, float beta, int32_t rows, int32_t c, int32_t accumulate, int32_t dtype,
                              void* stream) {
   DP_REQUIRE(y && a && rows > 0 && c > 0, "dp_axpby_rows: bad arguments");
-  DP_DT(hipLaunchKernelGGL(axpby_kernel<T>, dim3(grid_for((int64_t)rows * c)), dim3(256), 0, as_stream(stream), (T*)y,
-                           ld_y, (const T*)a, ld_a, alpha, (const T*)b, ld_b, beta, rows, c, accumulate));
+  if (rows == 1 && c > 65536) {   // one long row (the EMA over the flat parameters): 1024-wide rows
+    const int main = c / 1024 * 1024, es = dtype == DP_BF16 ? 2 : 4;
+    int rc = dp_axpby_rows(y, 1024, a, 1024, alpha, b, 1024, beta, main / 1024, 1024, accumulate, dtype, stream);
+    if (rc || main == c) return rc;
+    return dp_axpby_rows((char*)y + (int64_t)main * es, c - main, (const char*)a + (int64_t)main * es, c - main, alpha,
+                         b ? (const char*)b + (int64_t)main * es : nullptr, c - main, beta, 1, c - main, accumulate,
+                         dtype, stream);
+  }
+  const RC g = rc_grid(rows, c);
+  DP_DT(hipLaunchKernelGGL(axpby_kernel<T>, g.grid, g.block, 0, as_stream(stream), (T*)y, ld_y, (const T*)a, ld_a, alpha,
+                           (const T*)b, ld_b, beta, rows, c, accumulate));
   return dp_check_launch("dp_axpby_rows");
 }
 
 extern "C" int dp_act_bwd(const void* pre, int64_t ld_pre, const void* dy, int64_t ld_dy, void* dx, int64_t ld_dx,
                           int32_t rows, int32_t c, int32_t act, int32_t dtype, void* stream) {
   DP_REQUIRE(pre && dy && dx && rows > 0 && c > 0, "dp_act_bwd: bad arguments");
-  DP_DT(hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(grid_for((int64_t)rows * c)), dim3(256), 0, as_stream(stream),
-                           (const T*)pre, ld_pre, (const T*)dy, ld_dy, (T*)dx, ld_dx, rows, c, act));
+  const RC g = rc_grid(rows, c);
+  DP_DT(hipLaunchKernelGGL(act_bwd_kernel<T>, g.grid, g.block, 0, as_stream(stream), (const T*)pre, ld_pre,
+                           (const T*)dy, ld_dy, (T*)dx, ld_dx, rows, c, act));
   return dp_check_launch("dp_act_bwd");
 }
