@@ -296,28 +296,30 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, i
 }
 
 // ---------------------------------------------------------------- Gate
+// (row slices x channel blocks: a thread owns channel j and walks rows, no per-element division)
 template <typename T>
 __global__ void gate_fwd_kernel(const T* __restrict__ G, const T* __restrict__ xcat, T* __restrict__ gs,
                                 T* __restrict__ z, int rows, int c) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)rows * c) return;
-  const int64_t r = e / c;
-  const int j = (int)(e - r * c);
-  const int64_t b2 = r * 2 * c;
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  if (j >= c) return;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+  const int64_t e = (int64_t)r * c + j;
+  const int64_t b2 = (int64_t)r * 2 * c;
   const float g1 = sigmoidf_(to_f32(G[b2 + j])), g2 = sigmoidf_(to_f32(G[b2 + c + j]));
   gs[b2 + j] = from_f32<T>(g1);
   gs[b2 + c + j] = from_f32<T>(g2);
   z[e] = from_f32<T>(g1 * to_f32(xcat[b2 + j]) + g2 * to_f32(xcat[b2 + c + j]));
+  }
 }
 
 template <typename T>
 __global__ void gate_bwd_kernel(const T* __restrict__ dz, const T* __restrict__ gs, const T* __restrict__ xcat,
                                 T* __restrict__ dG, T* __restrict__ dx, int rows, int c) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)rows * c) return;
-  const int64_t r = e / c;
-  const int j = (int)(e - r * c);
-  const int64_t b2 = r * 2 * c;
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  if (j >= c) return;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+  const int64_t e = (int64_t)r * c + j;
+  const int64_t b2 = (int64_t)r * 2 * c;
   const float d = to_f32(dz[e]);
   const float g1 = to_f32(gs[b2 + j]), g2 = to_f32(gs[b2 + c + j]);
   const float x1 = to_f32(xcat[b2 + j]), x2 = to_f32(xcat[b2 + c + j]);
@@ -325,6 +327,16 @@ __global__ void gate_bwd_kernel(const T* __restrict__ dz, const T* __restrict__ 
   dG[b2 + c + j] = from_f32<T>(d * x2 * g2 * (1.f - g2));
   dx[b2 + j] = from_f32<T>(d * g1);
   dx[b2 + c + j] = from_f32<T>(d * g2);
+  }
+}
+
+dim3 rows_grid(int rows, int c, dim3* block) {
+  const int bx = c >= 256 ? 256 : (c + 63) / 64 * 64, gy = (c + bx - 1) / bx;
+  int gx = (1 << 16) / (bx * gy);
+  if (gx > rows) gx = rows;
+  if (gx < 1) gx = 1;
+  *block = dim3((unsigned)bx);
+  return dim3((unsigned)gx, (unsigned)gy);
 }
 
 // ---------------------------------------------------------------- query construction
@@ -553,8 +565,18 @@ __global__ void convert_kernel(const TS* __restrict__ src, int64_t lds, TD* __re
                                int n, float scale, int acc) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)rows * n) return;
-  const int64_t r = e / n;
-  const int j = (int)(e - r * n);
+  // 32-bit division when the index fits (every launch of the step), 64-bit otherwise
+  int64_t r;
+  int j;
+  if (e < 0x7fffffff) {
+    const unsigned ue = (unsigned)e, un = (unsigned)n;
+    const unsigned ur = ue / un;
+    r = ur;
+    j = (int)(ue - ur * un);
+  } else {
+    r = e / n;
+    j = (int)(e - r * n);
+  }
   float v = to_f32(src[r * lds + j]) * scale;
   TD* p = dst + r * ldd + j;
   if (acc) v += to_f32(*p);
@@ -788,28 +810,30 @@ extern "C" int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const voi
 extern "C" int dp_gate_fwd(const void* G, const void* xcat, void* g, void* z, int32_t rows, int32_t c, int32_t dtype,
                            void* stream) {
   DP_REQUIRE(G && xcat && g && z && rows > 0 && c > 0, "dp_gate_fwd: bad arguments");
-  const int64_t n = (int64_t)rows * c;
   hipStream_t s = as_stream(stream);
+  dim3 block;
+  const dim3 grid = rows_grid(rows, c, &block);
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(gate_fwd_kernel<bf16_t>, dim3(nblk(n, 256)), dim3(256), 0, s, (const bf16_t*)G,
-                       (const bf16_t*)xcat, (bf16_t*)g, (bf16_t*)z, rows, c);
+    hipLaunchKernelGGL(gate_fwd_kernel<bf16_t>, grid, block, 0, s, (const bf16_t*)G, (const bf16_t*)xcat, (bf16_t*)g,
+                       (bf16_t*)z, rows, c);
   else
-    hipLaunchKernelGGL(gate_fwd_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, s, (const float*)G, (const float*)xcat,
-                       (float*)g, (float*)z, rows, c);
+    hipLaunchKernelGGL(gate_fwd_kernel<float>, grid, block, 0, s, (const float*)G, (const float*)xcat, (float*)g,
+                       (float*)z, rows, c);
   return dp_check_launch("dp_gate_fwd");
 }
 
 extern "C" int dp_gate_bwd(const void* dz, const void* g, const void* xcat, void* dG, void* dxcat, int32_t rows,
                            int32_t c, int32_t dtype, void* stream) {
   DP_REQUIRE(dz && g && xcat && dG && dxcat && rows > 0 && c > 0, "dp_gate_bwd: bad arguments");
-  const int64_t n = (int64_t)rows * c;
   hipStream_t s = as_stream(stream);
+  dim3 block;
+  const dim3 grid = rows_grid(rows, c, &block);
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, dim3(nblk(n, 256)), dim3(256), 0, s, (const bf16_t*)dz,
-                       (const bf16_t*)g, (const bf16_t*)xcat, (bf16_t*)dG, (bf16_t*)dxcat, rows, c);
+    hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, grid, block, 0, s, (const bf16_t*)dz, (const bf16_t*)g,
+                       (const bf16_t*)xcat, (bf16_t*)dG, (bf16_t*)dxcat, rows, c);
   else
-    hipLaunchKernelGGL(gate_bwd_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, s, (const float*)dz, (const float*)g,
-                       (const float*)xcat, (float*)dG, (float*)dxcat, rows, c);
+    hipLaunchKernelGGL(gate_bwd_kernel<float>, grid, block, 0, s, (const float*)dz, (const float*)g, (const float*)xcat,
+                       (float*)dG, (float*)dxcat, rows, c);
   return dp_check_launch("dp_gate_bwd");
 }
 
