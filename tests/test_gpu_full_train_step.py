@@ -87,12 +87,12 @@ LOCATION = ("cross_attn.sampling_offsets", "lqe_embed.")
 
 
 def test_full_step_gradients(full):
-    """Every parameter of backbone + encoder + transformer: sampled entries within 5e-3 of scale
+    """Every parameter of backbone + encoder + transformer: sampled entries within 6e-3 of scale
     (the LAB scalars 6e-2 of theirs, see full_step_scales; location-derivative gradients see
     LOCATION: relative L2 <= 0.1, measured 1.6e-2), relative L2 error of the other sampled
     non-scalar entries within 5e-3, sums within 3e-3
-    of sum |g|. Measured on MI355X: worst 3.9e-3 (stem2a's conv weight, the deepest backward
-    chain), L2 <= 3.2e-3, LAB scalars <= 4.7e-2 of |g| (a sum over a whole map that cancels),
+    of sum |g|. Measured on MI355X: worst 3.9e-3 / 4.0e-3 / 4.0e-3 on three runs (stem2a's conv
+    weight, the deepest backward chain), L2 <= 3.2e-3, LAB scalars <= 4.7e-2 of |g| (a sum over a whole map that cancels),
     transformer parameters <= 2.8e-3."""
     from test_train_oracle import _sampled, full_step_scales
     g, eng, bb, ep, _ = full
@@ -111,7 +111,7 @@ def test_full_step_gradients(full):
         err = float(np.abs(d).max()) / scales[n]
         l2 = float(np.linalg.norm(d) / max(np.linalg.norm(val), 1e-30))
         serr = abs(flat.sum() - s) / max(a, 1e-30) if flat.size > 1 else 0.0
-        lim = 6e-2 if flat.size == 1 else (1e9 if any(t in n for t in LOCATION) else 5e-3)
+        lim = 6e-2 if flat.size == 1 else (1e9 if any(t in n for t in LOCATION) else 6e-3)
         rows.append((err / lim, err, l2, serr, n))
     rows.sort(reverse=True)
     for r in rows[:12]:
