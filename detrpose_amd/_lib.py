@@ -129,7 +129,7 @@ _SIGS = {
     "dp_ln_bwd": (i32, [vp, vp, i32, vp, vp, vp, i32, i32, vp, vp, i32, i32, vp]),
     "dp_colsum": (i32, [vp, i64, i32, i32, vp, i32, i32, vp]),
     "dp_attn_fwd": (i32, [vp, i32, vp, vp, i32, vp, i32, vp, vp, i32, i32, i64, i64, i64, i32, i32, i32, i32, vp]),
-    "dp_attn_bwd": (i32, [vp, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, i64, i64, i64, i32, i32,
+    "dp_attn_bwd": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, i64, i64, i64, i32, i32,
                           i32, i32, vp]),
     "dp_gate_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "dp_gate_bwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, vp]),

@@ -231,6 +231,102 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(const T* __restrict
   }
 }
 
+// The same backward with one channel per lane (dh lanes per (token, head), dh a power of two
+// <= 64), used when the value gradient is wanted: each of its float-atomic wave instructions
+// then adds 64/dh contiguous dh*4-byte row segments (two 128-byte rows at dh 32), the shape
+// the memory-side atomic units take at full rate (MI355X_MICROARCH.md § Global float atomics),
+// where the 16-byte-per-lane mapping above issued 16 scattered 4-byte adds per instruction
+// (9.3 -> see DESIGN.md per L b16 layer). The per-point dot products are xor-shuffle sums over
+// the pair's dh lanes.
+template <typename T>
+__global__ __launch_bounds__(256) void msda_fused_bwd_cl_kernel(const T* __restrict__ value, int S, TLevels lv, int L,
+                                                                int P, const float* __restrict__ oa,
+                                                                const float* __restrict__ ref,
+                                                                const T* __restrict__ gout, int ldg,
+                                                                float* __restrict__ gvalue, float* __restrict__ goa,
+                                                                float* __restrict__ gref, int lq, int pairs, int nh,
+                                                                int dh) {
+  const int ppw = 64 / dh;
+  const int lane = threadIdx.x & 63;
+  const int slot = lane / dh, c = lane - slot * dh;
+  const int pair0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw;
+  if (pair0 >= pairs) return;                    // whole waves leave together
+  const int pair = min(pair0 + slot, pairs - 1);  // a ragged last wave repeats its last pair...
+  const bool live = pair0 + slot < pairs;         // ...without storing or adding anything
+  const int r = pair / nh, h = pair - r * nh;
+  const int b = r / lq;
+  const int C = nh * dh;
+  const int LP = L * P;
+  const int ncol = nh * LP * 3;
+  const int ch = h * dh + c;
+  const T* vb = value + (int64_t)b * S * C + ch;
+  const float* orow = oa + (int64_t)r * ncol;
+  float* grow = goa + (int64_t)r * ncol;
+  const float* lg = orow + nh * LP * 2 + h * LP;
+  const float go = to_f32(gout[(int64_t)r * ldg + ch]);
+  float mx = -INFINITY;
+  for (int j = 0; j < LP; ++j) mx = fmaxf(mx, lg[j]);
+  float den = 0.f;
+  for (int j = 0; j < LP; ++j) den += expf(lg[j] - mx);
+  const float inv = 1.f / den;
+  const float rx = ref[2 * r], ry = ref[2 * r + 1];
+  float dot = 0.f, grx = 0.f, gry = 0.f;
+  float* gvb = gvalue + (int64_t)b * S * C + ch;
+  for (int j = 0; j < LP; ++j) {
+    const int l = j / P;
+    const int H = lv.h[l], W = lv.w[l];
+    const float ox = orow[(h * LP + j) * 2], oy = orow[(h * LP + j) * 2 + 1];
+    const float x = (rx + ox / W) * W - 0.5f, y = (ry + oy / H) * H - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float fx = x - fx0, fy = y - fy0;
+    const float a = expf(lg[j] - mx) * inv;
+    const float wk[4] = {(1.f - fx) * (1.f - fy), fx * (1.f - fy), (1.f - fx) * fy, fx * fy};
+    float v[4];
+    int row[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int xi = x0 + (k & 1), yi = y0 + (k >> 1);
+      const bool ok = xi >= 0 && xi < W && yi >= 0 && yi < H;
+      row[k] = ok ? lv.start[l] + yi * W + xi : -1;
+      v[k] = ok ? to_f32(vb[(int64_t)row[k] * C]) : 0.f;
+    }
+    const float sv = wk[0] * v[0] + wk[1] * v[1] + wk[2] * v[2] + wk[3] * v[3];
+    float ga = go * sv;
+    float gx = go * ((v[1] - v[0]) * (1.f - fy) + (v[3] - v[2]) * fy);
+    float gy = go * ((v[2] - v[0]) * (1.f - fx) + (v[3] - v[1]) * fx);
+    for (int o = dh >> 1; o > 0; o >>= 1) {
+      ga += __shfl_xor(ga, o, 64);
+      gx += __shfl_xor(gx, o, 64);
+      gy += __shfl_xor(gy, o, 64);
+    }
+    dot += a * ga;
+    if (c == 0 && live) {
+      grow[(h * LP + j) * 2] = a * gx;
+      grow[(h * LP + j) * 2 + 1] = a * gy;
+      grow[nh * LP * 2 + h * LP + j] = ga;
+      grx += a * gx * W;
+      gry += a * gy * H;
+    }
+    if (live) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (row[k] >= 0) unsafeAtomicAdd(gvb + (int64_t)row[k] * C, a * wk[k] * go);
+    }
+  }
+  if (c == 0 && live) {
+    float* gl = grow + nh * LP * 2 + h * LP;
+    for (int j = 0; j < LP; ++j) {
+      const float a = expf(lg[j] - mx) * inv;
+      gl[j] = a * (gl[j] - dot);
+    }
+    if (gref) {
+      unsafeAtomicAdd(gref + 2 * r, grx);
+      unsafeAtomicAdd(gref + 2 * r + 1, gry);
+    }
+  }
+}
+
 template <typename T, bool BWD>
 int launch_core(const void* value, int batch, int S, const TLevels& lv, int L, int P, const float* loc,
                 const float* attn, const void* gout, void* out, float* gvalue, float* gloc, float* gattn, int lq, int nh,
@@ -324,8 +420,21 @@ extern "C" int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const in
        hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess) ||
       (grad_ref && hipMemsetAsync(grad_ref, 0, (size_t)batch * lq * 2 * sizeof(float), s) != hipSuccess))
     return dp_check_launch("dp_msda_bwd(memset)");
-  const int ppw = 64 / (dh / VEC);
   const int pairs = batch * lq * nhead;
+  if (grad_value && dh <= 64 && (dh & (dh - 1)) == 0 && !getenv("DETRPOSE_MSDA_BWD_VEC")) {
+    const int ppw = 64 / dh;
+    const int grid = ((pairs + ppw - 1) / ppw + 3) / 4;
+    if (dtype == DP_BF16)
+      hipLaunchKernelGGL(msda_fused_bwd_cl_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)value, S, lv,
+                         nlevels, npoints, offattn, ref, (const bf16_t*)grad_out, ld_grad_out, grad_value,
+                         grad_offattn, grad_ref, lq, pairs, nhead, dh);
+    else
+      hipLaunchKernelGGL(msda_fused_bwd_cl_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)value, S, lv,
+                         nlevels, npoints, offattn, ref, (const float*)grad_out, ld_grad_out, grad_value, grad_offattn,
+                         grad_ref, lq, pairs, nhead, dh);
+    return dp_check_launch("dp_msda_bwd");
+  }
+  const int ppw = 64 / (dh / VEC);
   const int grid = ((pairs + ppw - 1) / ppw + 3) / 4;
   if (dtype == DP_BF16)
     hipLaunchKernelGGL(msda_fused_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)value, S, lv,

@@ -136,162 +136,227 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
 }
 
 // ---------------------------------------------------------------- attention core
-// One wave per (sequence, head). K and V of the sequence's head in LDS (f32); lane i owns
-// query rows i, i + 64, ... P is saved as [key j][query i] so the writes are coalesced.
-constexpr int ATT_DH = 64;
+// One wave per (sequence, head, 64-row block): lane = a query (forward, dQ) or a key (dK, dV) of
+// the block, so every sequence length keeps the chip busy (the AIFI layer's 400 tokens give 7
+// blocks per (image, head)). The other side's rows stream through LDS in 64-row chunks (f32, row
+// pitch 64: the lanes' uniform reads are broadcasts and vectorise). P is saved as [key j][query i]
+// (coalesced over the query lanes) and only read by the backward, so a backward can be replayed;
+// the backward's D_i = sum_j P_ij dO_i . V_j is dO_i . O_i, from the forward's output O.
+constexpr int ATT_DH = 64, ACH = 64, MPT = ACH + 4;
 
-template <typename T>
+template <int DH, typename T>
+__device__ __forceinline__ void stage_rows(float* dst, const T* src, int64_t ld, int64_t row0, int64_t st, int j0,
+                                           int L, int col0, int dh) {
+  // rows j0 .. j0+63 of the sequence (zero past L), columns col0 .. col0+dh-1, into dst[ACH][DH]
+  for (int e = threadIdx.x; e < ACH * dh; e += 64) {
+    const int t = e / dh, dd = e - t * dh;
+    const int j = j0 + t;
+    dst[t * DH + dd] = j < L ? to_f32(src[(row0 + (int64_t)j * st) * ld + col0 + dd]) : 0.f;
+  }
+}
+
+template <typename T, int DH>
 __global__ __launch_bounds__(64) void attn_fwd_kernel(const T* __restrict__ q, int ldq, const T* __restrict__ k,
                                                       const T* __restrict__ v, int ldkv, T* __restrict__ out, int ldo,
                                                       float* __restrict__ psave, const uint8_t* __restrict__ mask,
                                                       int n_inner, int64_t so, int64_t si, int64_t st, int L,
                                                       int nhead, int dh, float scale) {
-  extern __shared__ float sm[];
-  float* Ks = sm;
-  float* Vs = sm + L * dh;
+  __shared__ float Ks[ACH * DH], Vs[ACH * DH];
+  __shared__ uint8_t Ms[ACH * MPT];   // [query a][key c], pitch 68 B: lane rows hit distinct banks
   const int lane = threadIdx.x;
   const int h = blockIdx.x % nhead;
   const int seq = blockIdx.x / nhead;
   const int o = seq / n_inner, ii = seq - o * n_inner;
   const int64_t row0 = o * so + ii * si;
-  for (int e = lane; e < L * dh; e += 64) {
-    const int t = e / dh, dd = e - t * dh;
-    const int64_t rr = row0 + t * st;
-    Ks[e] = to_f32(k[rr * ldkv + h * dh + dd]);
-    Vs[e] = to_f32(v[rr * ldkv + h * dh + dd]);
-  }
-  __syncthreads();
-  float* P = psave + (int64_t)blockIdx.x * L * L;
-  for (int i = lane; i < L; i += 64) {
-    const int64_t ri = row0 + i * st;
-    float qi[ATT_DH];
+  const int ib = blockIdx.y * ACH;
+  const int i = ib + lane;
+  const bool live = i < L;
+  const int64_t ri = row0 + (int64_t)(live ? i : L - 1) * st;
+  float qi[DH];
 #pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd) qi[dd] = dd < dh ? to_f32(q[ri * ldq + h * dh + dd]) * scale : 0.f;
-    float m = -INFINITY, l = 0.f;
-    for (int j = 0; j < L; ++j) {
-      if (mask && mask[i * L + j]) continue;
+  for (int dd = 0; dd < DH; ++dd) qi[dd] = dd < dh ? to_f32(q[ri * ldq + h * dh + dd]) * scale : 0.f;
+  float* P = psave + (int64_t)blockIdx.x * L * L;
+  auto stage_mask = [&](int j0) {
+    for (int e = lane; e < ACH * ACH; e += 64) {
+      const int qa = e / ACH, kc = e - qa * ACH;
+      Ms[qa * MPT + kc] = (ib + qa < L && j0 + kc < L) ? mask[(int64_t)(ib + qa) * L + j0 + kc] : 1;
+    }
+  };
+  // pass 1: row max and sum (online)
+  float m = -INFINITY, l = 0.f;
+  for (int j0 = 0; j0 < L; j0 += ACH) {
+    __syncthreads();
+    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * dh, dh);
+    if (mask) stage_mask(j0);
+    __syncthreads();
+    const int nj = min(ACH, L - j0);
+    for (int t = 0; t < nj; ++t) {
+      if (mask && Ms[lane * MPT + t]) continue;
       float sc = 0.f;
 #pragma unroll
-      for (int dd = 0; dd < ATT_DH; ++dd)
-        if (dd < dh) sc = fmaf(qi[dd], Ks[j * dh + dd], sc);
+      for (int dd = 0; dd < DH; ++dd)
+        if (dd < dh) sc = fmaf(qi[dd], Ks[t * DH + dd], sc);
       const float mn = fmaxf(m, sc);
       l = l * __expf(m - mn) + __expf(sc - mn);
       m = mn;
     }
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    float acc[ATT_DH];
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  float acc[DH];
 #pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
-    for (int j = 0; j < L; ++j) {
+  for (int dd = 0; dd < DH; ++dd) acc[dd] = 0.f;
+  // pass 2: P (saved) and P V
+  for (int j0 = 0; j0 < L; j0 += ACH) {
+    __syncthreads();
+    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * dh, dh);
+    stage_rows<DH>(Vs, v, ldkv, row0, st, j0, L, h * dh, dh);
+    if (mask) stage_mask(j0);
+    __syncthreads();
+    const int nj = min(ACH, L - j0);
+    for (int t = 0; t < nj; ++t) {
       float p = 0.f;
-      if (!(mask && mask[i * L + j])) {
+      if (!(mask && Ms[lane * MPT + t])) {
         float sc = 0.f;
 #pragma unroll
-        for (int dd = 0; dd < ATT_DH; ++dd)
-          if (dd < dh) sc = fmaf(qi[dd], Ks[j * dh + dd], sc);
+        for (int dd = 0; dd < DH; ++dd)
+          if (dd < dh) sc = fmaf(qi[dd], Ks[t * DH + dd], sc);
         p = __expf(sc - m) * inv;
       }
-      P[(int64_t)j * L + i] = p;
+      if (live) P[(int64_t)(j0 + t) * L + i] = p;
 #pragma unroll
-      for (int dd = 0; dd < ATT_DH; ++dd)
-        if (dd < dh) acc[dd] = fmaf(p, Vs[j * dh + dd], acc[dd]);
+      for (int dd = 0; dd < DH; ++dd)
+        if (dd < dh) acc[dd] = fmaf(p, Vs[t * DH + dd], acc[dd]);
     }
+  }
+  if (live) {
 #pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd)
+    for (int dd = 0; dd < DH; ++dd)
       if (dd < dh) out[ri * ldo + h * dh + dd] = from_f32<T>(acc[dd]);
   }
 }
 
-// Backward: dV_j = sum_i P_ij dO_i; dS_ij = P_ij (dO_i . V_j - D_i), D_i = sum_j P_ij dO_i . V_j;
-// dQ_i = scale sum_j dS_ij K_j; dK_j = scale sum_i dS_ij Q_i. P is only read (the step's backward
-// can be replayed); dS is recomputed where it is needed, D_i kept in LDS.
-template <typename T>
-__global__ __launch_bounds__(64) void attn_bwd_kernel(const T* __restrict__ q, int ldq, const T* __restrict__ k,
-                                                      const T* __restrict__ v, int ldkv, const float* __restrict__ psave,
-                                                      const T* __restrict__ dout, int ldo, T* __restrict__ dq, int lddq,
-                                                      T* __restrict__ dk, T* __restrict__ dv, int lddkv, int n_inner,
-                                                      int64_t so, int64_t si, int64_t st, int L, int nhead, int dh,
-                                                      float scale) {
-  // Q is read from global memory in the dK phase (every lane the same row: broadcast loads),
-  // which keeps a 400-token sequence (the AIFI layer, dh 32) within 160 KB of LDS
-  extern __shared__ float sm[];
-  float* Ks = sm;
-  float* Vs = sm + L * dh;
-  float* Ds = sm + 2 * L * dh;   // dO
-  float* Dr = sm + 3 * L * dh;   // D_i = sum_j P_ij dP_ij
+// Backward, query side (lane = query i): dS_ij = P_ij (dO_i . V_j - D_i), dQ_i = scale sum_j dS_ij K_j.
+template <typename T, int DH>
+__global__ __launch_bounds__(64) void attn_bwd_q_kernel(const T* __restrict__ k, const T* __restrict__ v, int ldkv,
+                                                        const float* __restrict__ psave, const T* __restrict__ dout,
+                                                        const T* __restrict__ out, int ldo, T* __restrict__ dq,
+                                                        int lddq, int n_inner, int64_t so, int64_t si, int64_t st,
+                                                        int L, int nhead, int dh, float scale) {
+  __shared__ float Ks[ACH * DH], Vs[ACH * DH];
   const int lane = threadIdx.x;
   const int h = blockIdx.x % nhead;
   const int seq = blockIdx.x / nhead;
   const int o = seq / n_inner, ii = seq - o * n_inner;
   const int64_t row0 = o * so + ii * si;
-  for (int e = lane; e < L * dh; e += 64) {
-    const int t = e / dh, dd = e - t * dh;
-    const int64_t rr = row0 + t * st;
-    Ks[e] = to_f32(k[rr * ldkv + h * dh + dd]);
-    Vs[e] = to_f32(v[rr * ldkv + h * dh + dd]);
-    Ds[e] = to_f32(dout[rr * ldo + h * dh + dd]);
+  const int i = blockIdx.y * ACH + lane;
+  const bool live = i < L;
+  const int iq = live ? i : L - 1;
+  const int64_t ri = row0 + (int64_t)iq * st;
+  float dOi[DH], acc[DH];
+  float Di = 0.f;
+#pragma unroll
+  for (int dd = 0; dd < DH; ++dd) {
+    dOi[dd] = dd < dh ? to_f32(dout[ri * ldo + h * dh + dd]) : 0.f;
+    if (dd < dh) Di = fmaf(dOi[dd], to_f32(out[ri * ldo + h * dh + dd]), Di);
+    acc[dd] = 0.f;
   }
-  __syncthreads();
   const float* P = psave + (int64_t)blockIdx.x * L * L;
-  auto dpv = [&](int i, int j) {   // dP_ij = dO_i . V_j
-    float dp = 0.f;
+  for (int j0 = 0; j0 < L; j0 += ACH) {
+    __syncthreads();
+    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * dh, dh);
+    stage_rows<DH>(Vs, v, ldkv, row0, st, j0, L, h * dh, dh);
+    __syncthreads();
+    const int nj = min(ACH, L - j0);
+    for (int t = 0; t < nj; ++t) {
+      const float p = P[(int64_t)(j0 + t) * L + iq];
+      float dp = 0.f;
 #pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd)
-      if (dd < dh) dp = fmaf(Ds[i * dh + dd], Vs[j * dh + dd], dp);
-    return dp;
-  };
-  // dV (lane = key j)
-  for (int j = lane; j < L; j += 64) {
-    float acc[ATT_DH];
+      for (int dd = 0; dd < DH; ++dd)
+        if (dd < dh) dp = fmaf(dOi[dd], Vs[t * DH + dd], dp);
+      const float ds = p * (dp - Di);
 #pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
-    for (int i = 0; i < L; ++i) {
-      const float p = P[(int64_t)j * L + i];
-#pragma unroll
-      for (int dd = 0; dd < ATT_DH; ++dd)
-        if (dd < dh) acc[dd] = fmaf(p, Ds[i * dh + dd], acc[dd]);
+      for (int dd = 0; dd < DH; ++dd)
+        if (dd < dh) acc[dd] = fmaf(ds, Ks[t * DH + dd], acc[dd]);
     }
-    const int64_t rj = row0 + j * st;
-#pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd)
-      if (dd < dh) dv[rj * lddkv + h * dh + dd] = from_f32<T>(acc[dd]);
   }
-  // D and dQ (lane = query i)
-  for (int i = lane; i < L; i += 64) {
-    float di = 0.f;
-    for (int j = 0; j < L; ++j) di = fmaf(P[(int64_t)j * L + i], dpv(i, j), di);
-    Dr[i] = di;
-    float acc[ATT_DH];
+  if (live) {
 #pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
-    for (int j = 0; j < L; ++j) {
-      const float ds = P[(int64_t)j * L + i] * (dpv(i, j) - di);
-#pragma unroll
-      for (int dd = 0; dd < ATT_DH; ++dd)
-        if (dd < dh) acc[dd] = fmaf(ds, Ks[j * dh + dd], acc[dd]);
-    }
-    const int64_t ri = row0 + i * st;
-#pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd)
+    for (int dd = 0; dd < DH; ++dd)
       if (dd < dh) dq[ri * lddq + h * dh + dd] = from_f32<T>(acc[dd] * scale);
   }
-  __syncthreads();
-  // dK (lane = key j)
-  for (int j = lane; j < L; j += 64) {
-    float acc[ATT_DH];
+}
+
+// Backward, key side (lane = key j): dV_j = sum_i P_ij dO_i, dK_j = scale sum_i dS_ij Q_i. The
+// 64 x 64 block of P (this block's keys x a chunk of queries) is staged through LDS with coalesced
+// row reads (row j of P is contiguous in i), pitch 65.
+template <typename T, int DH>
+__global__ __launch_bounds__(64) void attn_bwd_k_kernel(const T* __restrict__ q, int ldq, const T* __restrict__ v,
+                                                        int ldkv, const float* __restrict__ psave,
+                                                        const T* __restrict__ dout, const T* __restrict__ out, int ldo,
+                                                        T* __restrict__ dk, T* __restrict__ dv, int lddkv, int n_inner,
+                                                        int64_t so, int64_t si, int64_t st, int L, int nhead, int dh,
+                                                        float scale) {
+  __shared__ float Qs[ACH * DH], Gs[ACH * DH], Ps[ACH * (ACH + 1)], Dr[ACH];
+  const int lane = threadIdx.x;
+  const int h = blockIdx.x % nhead;
+  const int seq = blockIdx.x / nhead;
+  const int o = seq / n_inner, ii = seq - o * n_inner;
+  const int64_t row0 = o * so + ii * si;
+  const int jb = blockIdx.y * ACH;
+  const int j = jb + lane;
+  const bool live = j < L;
+  const int64_t rj = row0 + (int64_t)(live ? j : L - 1) * st;
+  float Vj[DH], dvacc[DH], dkacc[DH];
 #pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd) acc[dd] = 0.f;
-    for (int i = 0; i < L; ++i) {
-      const float ds = P[(int64_t)j * L + i] * (dpv(i, j) - Dr[i]);
-      const T* qi = q + (row0 + i * st) * ldq + h * dh;
-#pragma unroll
-      for (int dd = 0; dd < ATT_DH; ++dd)
-        if (dd < dh) acc[dd] = fmaf(ds, to_f32(qi[dd]), acc[dd]);
+  for (int dd = 0; dd < DH; ++dd) {
+    Vj[dd] = dd < dh ? to_f32(v[rj * ldkv + h * dh + dd]) : 0.f;
+    dvacc[dd] = 0.f;
+    dkacc[dd] = 0.f;
+  }
+  const float* P = psave + (int64_t)blockIdx.x * L * L;
+  const int nkb = min(ACH, L - jb);
+  for (int i0 = 0; i0 < L; i0 += ACH) {
+    __syncthreads();
+    stage_rows<DH>(Qs, q, ldq, row0, st, i0, L, h * dh, dh);
+    stage_rows<DH>(Gs, dout, ldo, row0, st, i0, L, h * dh, dh);
+    {   // D of the chunk's queries (lane = query)
+      const int iq = i0 + lane;
+      float d = 0.f;
+      if (iq < L) {
+        const int64_t ri = row0 + (int64_t)iq * st;
+        for (int dd = 0; dd < dh; ++dd)
+          d = fmaf(to_f32(dout[ri * ldo + h * dh + dd]), to_f32(out[ri * ldo + h * dh + dd]), d);
+      }
+      Dr[lane] = d;
     }
-    const int64_t rj = row0 + j * st;
+    const int ni = min(ACH, L - i0);
+    for (int e = lane; e < nkb * ACH; e += 64) {
+      const int t = e / ACH, c = e - t * ACH;
+      Ps[t * (ACH + 1) + c] = c < ni ? P[(int64_t)(jb + t) * L + i0 + c] : 0.f;
+    }
+    __syncthreads();
+    for (int c = 0; c < ni; ++c) {
+      const float p = Ps[lane * (ACH + 1) + c];
+      float dp = 0.f;
 #pragma unroll
-    for (int dd = 0; dd < ATT_DH; ++dd)
-      if (dd < dh) dk[rj * lddkv + h * dh + dd] = from_f32<T>(acc[dd] * scale);
+      for (int dd = 0; dd < DH; ++dd)
+        if (dd < dh) dp = fmaf(Gs[c * DH + dd], Vj[dd], dp);
+      const float ds = p * (dp - Dr[c]);
+#pragma unroll
+      for (int dd = 0; dd < DH; ++dd)
+        if (dd < dh) {
+          dvacc[dd] = fmaf(p, Gs[c * DH + dd], dvacc[dd]);
+          dkacc[dd] = fmaf(ds, Qs[c * DH + dd], dkacc[dd]);
+        }
+    }
+  }
+  if (live) {
+#pragma unroll
+    for (int dd = 0; dd < DH; ++dd)
+      if (dd < dh) {
+        dv[rj * lddkv + h * dh + dd] = from_f32<T>(dvacc[dd]);
+        dk[rj * lddkv + h * dh + dd] = from_f32<T>(dkacc[dd] * scale);
+      }
   }
 }
 
@@ -693,17 +758,6 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
 
 inline unsigned nblk(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
-// dynamic LDS above 64 KB needs the per-kernel attribute (once per instantiation)
-template <typename K>
-void allow_lds(K kern) {
-  static bool done = [&] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    return true;
-  }();
-  (void)done;
-}
-
 }  // namespace
 
 // ================================================================== C ABI
@@ -758,52 +812,61 @@ extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, flo
   return dp_check_launch("dp_colsum");
 }
 
+// the head dim picks the instantiation (the decoder's and the AIFI layer's heads are 32 wide)
+#define ATT_LAUNCH(KERN, T, GRID, BLOCK, LDS, STREAM, ...)                    \
+  do {                                                                        \
+    if (dh <= 32)                                                             \
+      hipLaunchKernelGGL((KERN<T, 32>), GRID, BLOCK, LDS, STREAM, __VA_ARGS__); \
+    else                                                                      \
+      hipLaunchKernelGGL((KERN<T, 64>), GRID, BLOCK, LDS, STREAM, __VA_ARGS__); \
+  } while (0)
+
 extern "C" int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out,
                            int32_t ld_o, float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner,
                            int64_t so, int64_t si, int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype,
                            void* stream) {
   DP_REQUIRE(q && k && v && out && p_save, "dp_attn_fwd: null pointer");
-  DP_REQUIRE(seqlen > 0 && seqlen <= 1024 && dh > 0 && dh <= ATT_DH && (size_t)2 * seqlen * dh * 4 <= 160 * 1024,
-             "dp_attn_fwd: seqlen %d x dh %d (<= 1024, <= 64, K and V in 160 KB of LDS)", seqlen, dh);
+  DP_REQUIRE(seqlen > 0 && dh > 0 && dh <= ATT_DH, "dp_attn_fwd: seqlen %d x dh %d (dh <= 64)", seqlen, dh);
   DP_REQUIRE((int64_t)n_outer * n_inner * nhead < (1ll << 31), "dp_attn_fwd: too many sequences");
-  const size_t lds = (size_t)2 * seqlen * dh * 4;
   const float scale = 1.f / sqrtf((float)dh);
-  dim3 grid((unsigned)(n_outer * n_inner * nhead));
+  dim3 grid((unsigned)(n_outer * n_inner * nhead), (unsigned)((seqlen + ACH - 1) / ACH));
   hipStream_t s = as_stream(stream);
-  if (lds > 64 * 1024) dtype == DP_BF16 ? allow_lds(attn_fwd_kernel<bf16_t>) : allow_lds(attn_fwd_kernel<float>);
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, dim3(64), lds, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
+    ATT_LAUNCH(attn_fwd_kernel, bf16_t, grid, dim3(64), 0, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
                        (const bf16_t*)v, ld_kv, (bf16_t*)out, ld_o, p_save, mask, n_inner, so, si, st, seqlen, nhead,
                        dh, scale);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(64), lds, s, (const float*)q, ld_q, (const float*)k,
+    ATT_LAUNCH(attn_fwd_kernel, float, grid, dim3(64), 0, s, (const float*)q, ld_q, (const float*)k,
                        (const float*)v, ld_kv, (float*)out, ld_o, p_save, mask, n_inner, so, si, st, seqlen, nhead, dh,
                        scale);
   return dp_check_launch("dp_attn_fwd");
 }
 
 extern "C" int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv,
-                           const float* p_save, const void* dout, int32_t ld_o, void* dq, int32_t ld_dq, void* dk,
-                           void* dv, int32_t ld_dkv, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
-                           int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype, void* stream) {
-  DP_REQUIRE(q && k && v && p_save && dout && dq && dk && dv, "dp_attn_bwd: null pointer");
-  DP_REQUIRE(seqlen > 0 && seqlen <= 1024 && dh > 0 && dh <= ATT_DH &&
-                 (size_t)(3 * seqlen * dh + seqlen) * 4 <= 160 * 1024,
-             "dp_attn_bwd: seqlen %d x dh %d (<= 1024, <= 64, K, V, dO in 160 KB of LDS)", seqlen, dh);
-  const size_t lds = (size_t)(3 * seqlen * dh + seqlen) * 4;
+                           const float* p_save, const void* dout, const void* out, int32_t ld_o, void* dq,
+                           int32_t ld_dq, void* dk, void* dv, int32_t ld_dkv, int32_t n_outer, int32_t n_inner,
+                           int64_t so, int64_t si, int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype,
+                           void* stream) {
+  DP_REQUIRE(q && k && v && p_save && dout && out && dq && dk && dv, "dp_attn_bwd: null pointer");
+  DP_REQUIRE(seqlen > 0 && dh > 0 && dh <= ATT_DH, "dp_attn_bwd: seqlen %d x dh %d (dh <= 64)", seqlen, dh);
   const float scale = 1.f / sqrtf((float)dh);
-  dim3 grid((unsigned)(n_outer * n_inner * nhead));
+  dim3 grid((unsigned)(n_outer * n_inner * nhead), (unsigned)((seqlen + ACH - 1) / ACH));
   hipStream_t s = as_stream(stream);
-  const float* P = p_save;
-  if (lds > 64 * 1024) dtype == DP_BF16 ? allow_lds(attn_bwd_kernel<bf16_t>) : allow_lds(attn_bwd_kernel<float>);
-  if (dtype == DP_BF16)
-    hipLaunchKernelGGL(attn_bwd_kernel<bf16_t>, grid, dim3(64), lds, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
-                       (const bf16_t*)v, ld_kv, P, (const bf16_t*)dout, ld_o, (bf16_t*)dq, ld_dq, (bf16_t*)dk,
-                       (bf16_t*)dv, ld_dkv, n_inner, so, si, st, seqlen, nhead, dh, scale);
-  else
-    hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(64), lds, s, (const float*)q, ld_q, (const float*)k,
-                       (const float*)v, ld_kv, P, (const float*)dout, ld_o, (float*)dq, ld_dq, (float*)dk, (float*)dv,
-                       ld_dkv, n_inner, so, si, st, seqlen, nhead, dh, scale);
+  if (dtype == DP_BF16) {
+    ATT_LAUNCH(attn_bwd_q_kernel, bf16_t, grid, dim3(64), 0, s, (const bf16_t*)k, (const bf16_t*)v, ld_kv,
+                       p_save, (const bf16_t*)dout, (const bf16_t*)out, ld_o, (bf16_t*)dq, ld_dq, n_inner, so, si, st,
+                       seqlen, nhead, dh, scale);
+    ATT_LAUNCH(attn_bwd_k_kernel, bf16_t, grid, dim3(64), 0, s, (const bf16_t*)q, ld_q, (const bf16_t*)v,
+                       ld_kv, p_save, (const bf16_t*)dout, (const bf16_t*)out, ld_o, (bf16_t*)dk, (bf16_t*)dv, ld_dkv,
+                       n_inner, so, si, st, seqlen, nhead, dh, scale);
+  } else {
+    ATT_LAUNCH(attn_bwd_q_kernel, float, grid, dim3(64), 0, s, (const float*)k, (const float*)v, ld_kv, p_save,
+                       (const float*)dout, (const float*)out, ld_o, (float*)dq, ld_dq, n_inner, so, si, st, seqlen,
+                       nhead, dh, scale);
+    ATT_LAUNCH(attn_bwd_k_kernel, float, grid, dim3(64), 0, s, (const float*)q, ld_q, (const float*)v, ld_kv,
+                       p_save, (const float*)dout, (const float*)out, ld_o, (float*)dk, (float*)dv, ld_dkv, n_inner,
+                       so, si, st, seqlen, nhead, dh, scale);
+  }
   return dp_check_launch("dp_attn_bwd");
 }
 

@@ -602,8 +602,8 @@ class EncoderTrainPlan(TapePlan):
                   code)
             self.gemm(bw, f"aifi{i}.out.dx", dsum1.xp, Cc, 1, self.wptr(Wo), Cc, 1, datt.xp, Cc, rows, Cc, Cc)
             bw.op(f"aifi{i}.attn.bwd", lib.dp_attn_bwd, qkv.xp, 3 * Cc, qkv.xp + Cc * e, qkv.xp + 2 * Cc * e, 3 * Cc,
-                  _p(Pm), datt.xp, Cc, dqkv.xp, 3 * Cc, dqkv.xp + Cc * e, dqkv.xp + 2 * Cc * e, 3 * Cc, B, 1, n, 0, 1, n,
-                  nh, dh, code)
+                  _p(Pm), datt.xp, att.xp, Cc, dqkv.xp, 3 * Cc, dqkv.xp + Cc * e, dqkv.xp + 2 * Cc * e, 3 * Cc,
+                  B, 1, n, 0, 1, n, nh, dh, code)
             GW = G[Wi]
             self.gemm(bw, f"aifi{i}.qk.dW", dqkv.xp, 1, 3 * Cc, q.xp, Cc, 1, _p(GW), Cc, 2 * Cc, Cc, rows,
                       out_code=DP_F32, beta=1.0)

@@ -981,7 +981,7 @@ class TrainPlan:
         eng.dgrad(bw, n + ".out.dx", _p(dsum), Cc, rows, ap + "out_proj.weight", _p(datt), Cc)
         dqkv = self._scratch(("dqkv", rows, 3 * Cc), rows, 3 * Cc)
         bw.op(n + ".attn_bwd", lib.dp_attn_bwd, _p(qkv), 3 * Cc, _p(qkv, Cc), _p(qkv, 2 * Cc), 3 * Cc, _p(Pbuf),
-              _p(datt), Cc, _p(dqkv), 3 * Cc, _p(dqkv, Cc), _p(dqkv, 2 * Cc), 3 * Cc, n_outer, n_inner, so, si, st, L,
+              _p(datt), _p(att), Cc, _p(dqkv), 3 * Cc, _p(dqkv, Cc), _p(dqkv, 2 * Cc), 3 * Cc, n_outer, n_inner, so, si, st, L,
               nh, Cc // nh, code)
         eng.wgrad(bw, n + ".in", _p(dqkv), 3 * Cc, rows, ap + "in_proj_weight", _p(xin), Cc)
         eng.dgrad(bw, n + ".in.dx", _p(dqkv), 3 * Cc, rows, ap + "in_proj_weight", _p(dsum), Cc, beta=1.0)

@@ -449,16 +449,16 @@ int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, float* out, in
  * != 0: query i may not see key j; nn.MultiheadAttention attn_mask semantics). Sequences and
  * rows addressed as dp_attention (row o*so + i*si + t*st; q / k / v columns h*dh of rows ld_q /
  * ld_kv apart, out ld_o). Saves P f32 [seq][head][key][query] (softmax probabilities) for the
- * backward. seqlen <= 1024, dh <= 64, K and V of a sequence within 160 KB of LDS (the decoder's
- * 18 / 60 + DN tokens, the AIFI layer's 400: hybrid_encoder.py:276-279). */
+ * backward. dh <= 64; one wave per (sequence, head, 64 queries), keys streamed through LDS in
+ * 64-row chunks (the decoder's 18 / 60 + DN tokens, the AIFI layer's 400: hybrid_encoder.py:276-279). */
 int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out, int32_t ld_o,
                 float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
                 int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype, void* stream);
-/* Its backward: dq / dk / dv (same addressing as q / k / v, ld_dq / ld_dkv) from dout (ld_o);
- * p_save is only read (the backward can be replayed on the same forward). K, V, dout of a
- * sequence within 160 KB of LDS. */
+/* Its backward: dq / dk / dv (same addressing as q / k / v, ld_dq / ld_dkv) from dout and the
+ * forward's output out (both ld_o; D_i = dout_i . out_i); p_save is only read (the backward can be
+ * replayed on the same forward). */
 int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, const float* p_save,
-                const void* dout, int32_t ld_o, void* dq, int32_t ld_dq, void* dk, void* dv, int32_t ld_dkv,
+                const void* dout, const void* out, int32_t ld_o, void* dq, int32_t ld_dq, void* dk, void* dv, int32_t ld_dkv,
                 int32_t n_outer, int32_t n_inner, int64_t so, int64_t si, int64_t st, int32_t seqlen,
                 int32_t nhead, int32_t dh, int32_t dtype, void* stream);
 

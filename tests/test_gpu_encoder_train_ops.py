@@ -268,7 +268,8 @@ def test_attention_400_tokens(C_, nh):
                                B, 1, L, 0, 1, L, nh, dh, DP_F32, _s()), "attn fwd")
     d = torch.zeros(B, L, 3 * C_, device=DEV)
     db = d.data_ptr()
-    _lib.check(lib.dp_attn_bwd(base, 3 * C_, base + 4 * C_, base + 8 * C_, 3 * C_, P.data_ptr(), do.data_ptr(), C_, db,
+    _lib.check(lib.dp_attn_bwd(base, 3 * C_, base + 4 * C_, base + 8 * C_, 3 * C_, P.data_ptr(), do.data_ptr(),
+                               out.data_ptr(), C_, db,
                                3 * C_, db + 4 * C_, db + 8 * C_, 3 * C_, B, 1, L, 0, 1, L, nh, dh, DP_F32, _s()),
                "attn bwd")
     torch.cuda.synchronize()

@@ -102,7 +102,7 @@ def test_layernorm_fwd_bwd():
     assert torch.allclose(dg, gg.grad, atol=1e-3) and torch.allclose(db, bb.grad, atol=1e-3)
 
 
-@pytest.mark.parametrize("L,dh,masked", [(18, 16, False), (96, 32, True), (150, 48, True)])
+@pytest.mark.parametrize("L,dh,masked", [(18, 16, False), (64, 32, True), (65, 32, False), (96, 32, True), (150, 48, True), (200, 64, True)])
 def test_attention_fwd_bwd(L, dh, masked):
     """Across-attention addressing (rows o*so + i*si + t*st) with an attn_mask."""
     lib = _lib.load()
@@ -131,7 +131,7 @@ def test_attention_fwd_bwd(L, dh, masked):
     ref.backward(dout)
     dqkv = torch.empty(rows, 3 * Cc, device=DEV)
     _lib.check(lib.dp_attn_bwd(qkv.data_ptr(), 3 * Cc, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), 3 * Cc,
-                               P.data_ptr(), dout.data_ptr(), Cc, dqkv.data_ptr(), 3 * Cc, dqkv[:, Cc:].data_ptr(),
+                               P.data_ptr(), dout.data_ptr(), out.data_ptr(), Cc, dqkv.data_ptr(), 3 * Cc, dqkv[:, Cc:].data_ptr(),
                                dqkv[:, 2 * Cc:].data_ptr(), 3 * Cc, *args, _s()), "attn_bwd")
     assert torch.allclose(dqkv, q.grad, atol=1e-4), (dqkv - q.grad).abs().max()
 
