@@ -7,6 +7,8 @@
 //
 // Layout: NHWC activations as [rows][c] with a row stride (channel slices of concat buffers),
 // rows = batch * h * w. f32 statistics. Activations / activation gradients of dtype.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -265,59 +267,139 @@ __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin,
   reinterpret_cast<T*>(out)[e] = from_f32<T>(v);
 }
 
-// depthwise conv backward (SCDown's 3x3 s2, hybrid_encoder.py:156-170): dx (+=) by gathering the
-// output positions each input pixel feeds, dw [c][kh][kw] (+=, f32 atomics) by column sums over
-// the output pixels of a 256-pixel chunk
-template <typename T>
-__global__ void dw_bwd_data_kernel(const T* __restrict__ dz, int64_t zbs, int zps, const float* __restrict__ wt,
-                                   int h, int w, int c, int k, int s, int pad, int oh, int ow, T* __restrict__ dx,
-                                   int64_t xbs, int xps, int64_t total) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= total) return;
-  const int ch = (int)(e % c);
-  const int64_t p = e / c;
-  const int x = (int)(p % w);
-  const int64_t t = p / w;
-  const int y = (int)(t % h), b = (int)(t / h);
-  float acc = 0.f;
-  for (int ky = 0; ky < k; ++ky) {
-    const int ny = y + pad - ky;
-    if (ny < 0 || ny % s) continue;
-    const int oy = ny / s;
-    if (oy >= oh) continue;
-    for (int kx = 0; kx < k; ++kx) {
-      const int nx = x + pad - kx;
-      if (nx < 0 || nx % s) continue;
-      const int ox = nx / s;
-      if (ox >= ow) continue;
-      acc = fmaf(ld_(dz + (int64_t)b * zbs + ((int64_t)oy * ow + ox) * zps + ch), wt[(ky * k + kx) * c + ch], acc);
+// depthwise conv backward (SCDown's 3x3 s2, hybrid_encoder.py:156-170; HGNetv2's 3x3 s2
+// downsample and 5x5 / 3x3 LightConvBNAct, hgnetv2.py:144-163). A wave = 64 channels (lanes) of one
+// row tile of TW pixels; K, S compile-time so the taps, the tile and the accumulators live in
+// registers. dx (+=): stride 1 slides a register window of the dz row over the tile; dw (+=): a
+// thread sums its channel's K*K taps over the tiles it walks, the block's 64 channels x K*K sums
+// are transposed through LDS so the f32 atomics hit contiguous addresses of the [c][K][K] gradient.
+constexpr int DW_TW = 8;
+
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void dw_bwd_data_kernel(const T* __restrict__ dz, int64_t zbs, int zps,
+                                                          const float* __restrict__ wt, int h, int w, int c, int pad,
+                                                          int oh, int ow, T* __restrict__ dx, int64_t xbs, int xps,
+                                                          int ntiles) {
+  const int ch = blockIdx.x * 64 + threadIdx.x;
+  if (ch >= c) return;
+  float wk[K * K];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) wk[t] = wt[t * c + ch];
+  const int ntx = (w + DW_TW - 1) / DW_TW;
+  for (int tt = blockIdx.y * 4 + threadIdx.y; tt < ntiles; tt += gridDim.y * 4) {
+    const int x0 = (tt % ntx) * DW_TW, t2 = tt / ntx;
+    const int y = t2 % h, b = t2 / h;
+    const T* zb = dz + (int64_t)b * zbs + ch;
+    float acc[DW_TW];
+#pragma unroll
+    for (int i = 0; i < DW_TW; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int ny = y + pad - ky;
+      if (ny < 0 || ny % S) continue;
+      const int oy = ny / S;
+      if (oy >= oh) continue;
+      const T* zr = zb + (int64_t)oy * ow * zps;
+      if (S == 1) {
+        // output x0 + i takes dz[ox = x0 + i + pad - kx]: window j = i + K - 1 - kx
+        float zw[DW_TW + K - 1];
+#pragma unroll
+        for (int j = 0; j < DW_TW + K - 1; ++j) {
+          const int ox = x0 + pad - (K - 1) + j;
+          zw[j] = (ox >= 0 && ox < ow) ? to_f32(zr[(int64_t)ox * zps]) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < DW_TW; ++i)
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx) acc[i] = fmaf(zw[i + K - 1 - kx], wk[ky * K + kx], acc[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < DW_TW; ++i)
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx) {
+            const int nx = x0 + i + pad - kx;
+            if (nx < 0 || nx % S) continue;
+            const int ox = nx / S;
+            if (ox < ow) acc[i] = fmaf(to_f32(zr[(int64_t)ox * zps]), wk[ky * K + kx], acc[i]);
+          }
+      }
     }
+    T* o = dx + (int64_t)b * xbs + ((int64_t)y * w + x0) * xps + ch;
+#pragma unroll
+    for (int i = 0; i < DW_TW; ++i)
+      if (x0 + i < w) o[(int64_t)i * xps] = from_f32<T>(to_f32(o[(int64_t)i * xps]) + acc[i]);
   }
-  T* o = dx + (int64_t)b * xbs + ((int64_t)y * w + x) * xps + ch;
-  *o = from_f32<T>(ld_(o) + acc);
 }
 
-template <typename T>
-__global__ void dw_bwd_weight_kernel(const T* __restrict__ x, int64_t xbs, int xps, const T* __restrict__ dz,
-                                     int64_t zbs, int zps, int h, int w, int c, int k, int s, int pad, int oh, int ow,
-                                     int opix, float* __restrict__ dw) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  const int p0 = blockIdx.y * 256, p1 = min(p0 + 256, opix);
-  float acc[25];
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void dw_bwd_weight_kernel(const T* __restrict__ x, int64_t xbs, int xps,
+                                                            const T* __restrict__ dz, int64_t zbs, int zps, int h,
+                                                            int w, int c, int pad, int oh, int ow, int ntiles,
+                                                            float* __restrict__ dw) {
+  constexpr int XW = (DW_TW - 1) * S + K;
+  __shared__ float red[4][64 * K * K];
+  const int ch = blockIdx.x * 64 + threadIdx.x;
+  const bool active = ch < c;
+  float acc[K * K];
 #pragma unroll
-  for (int t = 0; t < 25; ++t) acc[t] = 0.f;
-  for (int p = p0; p < p1; ++p) {
-    const int ox = p % ow, t = p / ow, oy = t % oh, b = t / oh;
-    const float g = ld_(dz + (int64_t)b * zbs + ((int64_t)oy * ow + ox) * zps + ch);
-    for (int ky = 0; ky < k; ++ky)
-      for (int kx = 0; kx < k; ++kx) {
-        const int iy = oy * s - pad + ky, ix = ox * s - pad + kx;
-        if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w)
-          acc[ky * k + kx] = fmaf(g, ld_(x + (int64_t)b * xbs + ((int64_t)iy * w + ix) * xps + ch), acc[ky * k + kx]);
+  for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
+  const int ntx = (ow + DW_TW - 1) / DW_TW;
+  if (active) {
+    for (int tt = blockIdx.y * 4 + threadIdx.y; tt < ntiles; tt += gridDim.y * 4) {
+      const int ox0 = (tt % ntx) * DW_TW, t2 = tt / ntx;
+      const int oy = t2 % oh, b = t2 / oh;
+      float g[DW_TW];
+      const T* zr = dz + (int64_t)b * zbs + (int64_t)oy * ow * zps + ch;
+#pragma unroll
+      for (int i = 0; i < DW_TW; ++i) g[i] = ox0 + i < ow ? to_f32(zr[(int64_t)(ox0 + i) * zps]) : 0.f;
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky) {
+        const int iy = oy * S - pad + ky;
+        if (iy < 0 || iy >= h) continue;
+        const T* xr = x + (int64_t)b * xbs + (int64_t)iy * w * xps + ch;
+        float xw[XW];
+#pragma unroll
+        for (int j = 0; j < XW; ++j) {
+          const int ix = ox0 * S - pad + j;
+          xw[j] = (ix >= 0 && ix < w) ? to_f32(xr[(int64_t)ix * xps]) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < DW_TW; ++i)
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx) acc[ky * K + kx] = fmaf(g[i], xw[i * S + kx], acc[ky * K + kx]);
       }
+    }
   }
-  for (int t = 0; t < k * k; ++t) atomicAdd(dw + (int64_t)ch * k * k + t, acc[t]);
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) red[threadIdx.y][threadIdx.x * K * K + t] = acc[t];
+  __syncthreads();
+  // the block's channels ch0 .. ch0+63 own dw[ch0*K*K ..] contiguously
+  const int ch0 = blockIdx.x * 64;
+  const int n = min(64, c - ch0) * K * K;
+  for (int e = threadIdx.y * 64 + threadIdx.x; e < n; e += 256) {
+    const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+    atomicAdd(dw + (int64_t)ch0 * K * K + e, v);
+  }
+}
+
+template <typename T, int K, int S>
+void dw_bwd_launch(const void* x, int64_t xbs, int xps, const void* dz, int64_t zbs, int zps, const float* wt,
+                   int batch, int h, int w, int c, int pad, int oh, int ow, void* dx, int64_t dxbs, int dxps,
+                   float* dw, hipStream_t s) {
+  const unsigned gx = (unsigned)((c + 63) / 64);
+  if (dx) {
+    const int ntiles = batch * h * ((w + DW_TW - 1) / DW_TW);
+    const unsigned gy = (unsigned)std::min((ntiles + 3) / 4, 65535);
+    hipLaunchKernelGGL((dw_bwd_data_kernel<T, K, S>), dim3(gx, gy), dim3(64, 4), 0, s, (const T*)dz, zbs, zps, wt, h,
+                       w, c, pad, oh, ow, (T*)dx, dxbs, dxps, ntiles);
+  }
+  if (dw) {
+    const int ntiles = batch * oh * ((ow + DW_TW - 1) / DW_TW);
+    // about 16 tiles per thread: the atomics stay a small fraction of the work
+    const unsigned gy = (unsigned)std::max(1, std::min((ntiles + 63) / 64, 65535));
+    hipLaunchKernelGGL((dw_bwd_weight_kernel<T, K, S>), dim3(gx, gy), dim3(64, 4), 0, s, (const T*)x, xbs, xps,
+                       (const T*)dz, zbs, zps, h, w, c, pad, oh, ow, ntiles, dw);
+  }
 }
 
 // ---------------------------------------------------------------- rows
@@ -509,20 +591,18 @@ extern "C" int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride
                              int32_t z_pstride, const float* wt, int32_t batch, int32_t h, int32_t w, int32_t c,
                              int32_t k, int32_t stride, int32_t pad, int32_t oh, int32_t ow, void* dx,
                              int64_t dx_bstride, int32_t dx_pstride, float* dw, int32_t dtype, void* stream) {
-  DP_REQUIRE(x && dz && wt && batch > 0 && c > 0 && k > 0 && k <= 5 && stride > 0, "dp_dwconv_bwd: bad arguments");
+  DP_REQUIRE(x && dz && wt && batch > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0,
+             "dp_dwconv_bwd: bad arguments");
+  DP_REQUIRE((k == 3 || k == 5) && (stride == 1 || stride == 2), "dp_dwconv_bwd: k %d stride %d (3 / 5, 1 / 2)", k,
+             stride);
   hipStream_t s = as_stream(stream);
-  if (dx) {
-    const int64_t total = (int64_t)batch * h * w * c;
-    DP_DT(hipLaunchKernelGGL(dw_bwd_data_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                             (const T*)dz, z_bstride, z_pstride, wt, h, w, c, k, stride, pad, oh, ow, (T*)dx,
-                             dx_bstride, dx_pstride, total));
+#define DW_CASE(KK, SS)                                                                                          \
+  if (k == KK && stride == SS) {                                                                                 \
+    DP_DT((dw_bwd_launch<T, KK, SS>(x, x_bstride, x_pstride, dz, z_bstride, z_pstride, wt, batch, h, w, c, pad, oh, \
+                                    ow, dx, dx_bstride, dx_pstride, dw, s)));                                   \
   }
-  if (dw) {
-    const int opix = batch * oh * ow;
-    dim3 grid((c + 63) / 64, (opix + 255) / 256);
-    DP_DT(hipLaunchKernelGGL(dw_bwd_weight_kernel<T>, grid, dim3(64), 0, s, (const T*)x, x_bstride, x_pstride,
-                             (const T*)dz, z_bstride, z_pstride, h, w, c, k, stride, pad, oh, ow, opix, dw));
-  }
+  DW_CASE(3, 1) else DW_CASE(3, 2) else DW_CASE(5, 1) else DW_CASE(5, 2)
+#undef DW_CASE
   return dp_check_launch("dp_dwconv_bwd");
 }
 

@@ -174,39 +174,42 @@ def test_conv_pack_forward_dgrad_wgrad(k, cin, cout):
     _close(dW.view(cout, cin, k, k), wr.grad, f"conv{k} wgrad")
 
 
-def test_depthwise_s2_backward_and_pack():
+@pytest.mark.parametrize("k,st,c", [(3, 2, 64), (5, 1, 96), (3, 1, 40), (5, 2, 68)])
+def test_depthwise_s2_backward_and_pack(k, st, c):
     """SCDown's depthwise 3x3 stride-2 conv (hybrid_encoder.py:156-170): dp_conv_pack mode 2 +
-    dp_dwconv2d forward, dp_dwconv_bwd input and weight gradients vs autograd."""
+    dp_dwconv2d forward, dp_dwconv_bwd input and weight gradients vs autograd; also HGNetv2's 5x5 /
+    3x3 stride-1 LightConvBNAct depthwise convs (hgnetv2.py:144-163), ragged channel blocks."""
     lib = _lib.load()
     torch.manual_seed(9)
-    B, c, h, w = 2, 64, 17, 12
-    wt = torch.randn(c, 1, 3, 3, device=DEV)
+    B, h, w = 2, 17, 12
+    p = (k - 1) // 2
+    wt = torch.randn(c, 1, k, k, device=DEV)
     x = torch.randn(B, c, h, w, device=DEV).requires_grad_(True)
     wr = wt.clone().requires_grad_(True)
-    y = F.conv2d(x, wr, None, 2, 1, 1, c)
+    y = F.conv2d(x, wr, None, st, p, 1, c)
     dy = torch.randn_like(y)
     y.backward(dy)
     oh, ow = y.shape[2:]
-    taps = torch.empty(9, c, device=DEV)
-    _lib.check(lib.dp_conv_pack(wt.data_ptr(), c, 1, 3, 3, taps.data_ptr(), 0, 0, 2, None, DP_F32, _s()), "pack dw")
+    taps = torch.empty(k * k, c, device=DEV)
+    _lib.check(lib.dp_conv_pack(wt.data_ptr(), c, 1, k, k, taps.data_ptr(), 0, 0, 2, None, DP_F32, _s()), "pack dw")
     xn = x.detach().permute(0, 2, 3, 1).contiguous()
     dyn = dy.permute(0, 2, 3, 1).contiguous()
     d = ConvDesc()
     out = torch.empty(B, oh, ow, c, device=DEV)
     d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = xn.data_ptr(), h * w * c, c, h, w, c
     d.weight, d.kpad, d.bias = taps.data_ptr(), 0, None
-    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = 3, 3, 2, 1, 1
+    d.kh, d.kw, d.stride, d.pad_t, d.pad_l = k, k, st, p, p
     d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out.data_ptr(), oh * ow * c, c, oh, ow, c
     d.batch, d.act, d.dtype = B, 0, DP_F32
     _lib.check(lib.dp_dwconv2d(C.byref(d), _s()), "dw fwd")
     dx = torch.zeros(B, h, w, c, device=DEV)
-    dw = torch.zeros(c, 3, 3, device=DEV)
+    dw = torch.zeros(c, k, k, device=DEV)
     _lib.check(lib.dp_dwconv_bwd(xn.data_ptr(), h * w * c, c, dyn.data_ptr(), oh * ow * c, c, taps.data_ptr(), B, h, w,
-                                 c, 3, 2, 1, oh, ow, dx.data_ptr(), h * w * c, c, dw.data_ptr(), DP_F32, _s()), "dw bwd")
+                                 c, k, st, p, oh, ow, dx.data_ptr(), h * w * c, c, dw.data_ptr(), DP_F32, _s()), "dw bwd")
     torch.cuda.synchronize()
     _close(out, y.detach().permute(0, 2, 3, 1), "dw fwd")
     _close(dx, x.grad.permute(0, 2, 3, 1), "dw dx")
-    _close(dw, wr.grad.view(c, 3, 3), "dw dw")
+    _close(dw, wr.grad.view(c, k, k), "dw dw")
 
 
 def test_upsample_axpby_gelu_backward():
