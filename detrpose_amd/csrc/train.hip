@@ -139,19 +139,43 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
 // One wave per (sequence, head, 64-row block): lane = a query (forward, dQ) or a key (dK, dV) of
 // the block, so every sequence length keeps the chip busy (the AIFI layer's 400 tokens give 7
 // blocks per (image, head)). The other side's rows stream through LDS in 64-row chunks (f32, row
-// pitch 64: the lanes' uniform reads are broadcasts and vectorise). P is saved as [key j][query i]
+// pitch DH: the lanes' uniform reads are broadcasts and vectorise). P is saved as [key j][query i]
 // (coalesced over the query lanes) and only read by the backward, so a backward can be replayed;
 // the backward's D_i = sum_j P_ij dO_i . V_j is dO_i . O_i, from the forward's output O.
-constexpr int ATT_DH = 64, ACH = 64, MPT = ACH + 4;
+// The head dim is a template constant and every load is unconditional (row indices clamped,
+// out-of-range values selected away): a guarded load compiles to a branch around it, and the
+// loads then issue one at a time.
+constexpr int ACH = 64, MPT = ACH + 4;
 
+// one row's DH values (f32) of a head
+template <int DH, typename T>
+__device__ __forceinline__ void load_head(float (&x)[DH], const T* p, float mul) {
+#pragma unroll
+  for (int dd = 0; dd < DH; ++dd) x[dd] = to_f32(p[dd]) * mul;
+}
+
+// rows j0 .. j0+63 of the sequence (zero past L), head columns col0 .., into dst[ACH][DH]
 template <int DH, typename T>
 __device__ __forceinline__ void stage_rows(float* dst, const T* src, int64_t ld, int64_t row0, int64_t st, int j0,
-                                           int L, int col0, int dh) {
-  // rows j0 .. j0+63 of the sequence (zero past L), columns col0 .. col0+dh-1, into dst[ACH][DH]
-  for (int e = threadIdx.x; e < ACH * dh; e += 64) {
-    const int t = e / dh, dd = e - t * dh;
+                                           int L, int col0) {
+#pragma unroll 8
+  for (int r = 0; r < DH; ++r) {
+    const int e = r * 64 + threadIdx.x;
+    const int t = e / DH, dd = e % DH;
     const int j = j0 + t;
-    dst[t * DH + dd] = j < L ? to_f32(src[(row0 + (int64_t)j * st) * ld + col0 + dd]) : 0.f;
+    const float v = to_f32(src[(row0 + (int64_t)min(j, L - 1) * st) * ld + col0 + dd]);
+    dst[e] = j < L ? v : 0.f;
+  }
+}
+
+// P[j0 .. j0+63][i0 .. i0+63] of one (sequence, head) into dst[64][65] (zero past L)
+__device__ __forceinline__ void stage_p(float* dst, const float* P, int L, int j0, int i0) {
+  const int c = threadIdx.x;
+  const int ic = min(i0 + c, L - 1);
+#pragma unroll 8
+  for (int t = 0; t < ACH; ++t) {
+    const float v = P[(int64_t)min(j0 + t, L - 1) * L + ic];
+    dst[t * (ACH + 1) + c] = (j0 + t < L && i0 + c < L) ? v : 0.f;
   }
 }
 
@@ -160,7 +184,7 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const T* __restrict__ q, i
                                                       const T* __restrict__ v, int ldkv, T* __restrict__ out, int ldo,
                                                       float* __restrict__ psave, const uint8_t* __restrict__ mask,
                                                       int n_inner, int64_t so, int64_t si, int64_t st, int L,
-                                                      int nhead, int dh, float scale) {
+                                                      int nhead, float scale) {
   __shared__ float Ks[ACH * DH], Vs[ACH * DH];
   __shared__ uint8_t Ms[ACH * MPT];   // [query a][key c], pitch 68 B: lane rows hit distinct banks
   const int lane = threadIdx.x;
@@ -171,31 +195,31 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const T* __restrict__ q, i
   const int ib = blockIdx.y * ACH;
   const int i = ib + lane;
   const bool live = i < L;
-  const int64_t ri = row0 + (int64_t)(live ? i : L - 1) * st;
+  const int64_t ri = row0 + (int64_t)min(i, L - 1) * st;
   float qi[DH];
-#pragma unroll
-  for (int dd = 0; dd < DH; ++dd) qi[dd] = dd < dh ? to_f32(q[ri * ldq + h * dh + dd]) * scale : 0.f;
+  load_head<DH>(qi, q + ri * ldq + h * DH, scale);
   float* P = psave + (int64_t)blockIdx.x * L * L;
-  auto stage_mask = [&](int j0) {
-    for (int e = lane; e < ACH * ACH; e += 64) {
-      const int qa = e / ACH, kc = e - qa * ACH;
-      Ms[qa * MPT + kc] = (ib + qa < L && j0 + kc < L) ? mask[(int64_t)(ib + qa) * L + j0 + kc] : 1;
+  auto stage_mask = [&](int j0) {   // lane = key column
+    const int kc = min(j0 + lane, L - 1);
+#pragma unroll 8
+    for (int qa = 0; qa < ACH; ++qa) {
+      const uint8_t mv = mask[(int64_t)min(ib + qa, L - 1) * L + kc];
+      Ms[qa * MPT + lane] = j0 + lane < L ? mv : (uint8_t)1;
     }
   };
   // pass 1: row max and sum (online)
   float m = -INFINITY, l = 0.f;
   for (int j0 = 0; j0 < L; j0 += ACH) {
     __syncthreads();
-    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * dh, dh);
+    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * DH);
     if (mask) stage_mask(j0);
     __syncthreads();
     const int nj = min(ACH, L - j0);
     for (int t = 0; t < nj; ++t) {
-      if (mask && Ms[lane * MPT + t]) continue;
       float sc = 0.f;
 #pragma unroll
-      for (int dd = 0; dd < DH; ++dd)
-        if (dd < dh) sc = fmaf(qi[dd], Ks[t * DH + dd], sc);
+      for (int dd = 0; dd < DH; ++dd) sc = fmaf(qi[dd], Ks[t * DH + dd], sc);
+      if (mask && Ms[lane * MPT + t]) continue;
       const float mn = fmaxf(m, sc);
       l = l * __expf(m - mn) + __expf(sc - mn);
       m = mn;
@@ -208,30 +232,25 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const T* __restrict__ q, i
   // pass 2: P (saved) and P V
   for (int j0 = 0; j0 < L; j0 += ACH) {
     __syncthreads();
-    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * dh, dh);
-    stage_rows<DH>(Vs, v, ldkv, row0, st, j0, L, h * dh, dh);
+    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * DH);
+    stage_rows<DH>(Vs, v, ldkv, row0, st, j0, L, h * DH);
     if (mask) stage_mask(j0);
     __syncthreads();
     const int nj = min(ACH, L - j0);
     for (int t = 0; t < nj; ++t) {
-      float p = 0.f;
-      if (!(mask && Ms[lane * MPT + t])) {
-        float sc = 0.f;
+      float sc = 0.f;
 #pragma unroll
-        for (int dd = 0; dd < DH; ++dd)
-          if (dd < dh) sc = fmaf(qi[dd], Ks[t * DH + dd], sc);
-        p = __expf(sc - m) * inv;
-      }
+      for (int dd = 0; dd < DH; ++dd) sc = fmaf(qi[dd], Ks[t * DH + dd], sc);
+      float p = __expf(sc - m) * inv;
+      if (mask && Ms[lane * MPT + t]) p = 0.f;
       if (live) P[(int64_t)(j0 + t) * L + i] = p;
 #pragma unroll
-      for (int dd = 0; dd < DH; ++dd)
-        if (dd < dh) acc[dd] = fmaf(p, Vs[t * DH + dd], acc[dd]);
+      for (int dd = 0; dd < DH; ++dd) acc[dd] = fmaf(p, Vs[t * DH + dd], acc[dd]);
     }
   }
   if (live) {
 #pragma unroll
-    for (int dd = 0; dd < DH; ++dd)
-      if (dd < dh) out[ri * ldo + h * dh + dd] = from_f32<T>(acc[dd]);
+    for (int dd = 0; dd < DH; ++dd) out[ri * ldo + h * DH + dd] = from_f32<T>(acc[dd]);
   }
 }
 
@@ -241,8 +260,8 @@ __global__ __launch_bounds__(64) void attn_bwd_q_kernel(const T* __restrict__ k,
                                                         const float* __restrict__ psave, const T* __restrict__ dout,
                                                         const T* __restrict__ out, int ldo, T* __restrict__ dq,
                                                         int lddq, int n_inner, int64_t so, int64_t si, int64_t st,
-                                                        int L, int nhead, int dh, float scale) {
-  __shared__ float Ks[ACH * DH], Vs[ACH * DH];
+                                                        int L, int nhead, float scale) {
+  __shared__ float Ks[ACH * DH], Vs[ACH * DH], Ps[ACH * (ACH + 1)];
   const int lane = threadIdx.x;
   const int h = blockIdx.x % nhead;
   const int seq = blockIdx.x / nhead;
@@ -250,39 +269,37 @@ __global__ __launch_bounds__(64) void attn_bwd_q_kernel(const T* __restrict__ k,
   const int64_t row0 = o * so + ii * si;
   const int i = blockIdx.y * ACH + lane;
   const bool live = i < L;
-  const int iq = live ? i : L - 1;
-  const int64_t ri = row0 + (int64_t)iq * st;
-  float dOi[DH], acc[DH];
+  const int64_t ri = row0 + (int64_t)min(i, L - 1) * st;
+  float dOi[DH], oi[DH], acc[DH];
+  load_head<DH>(dOi, dout + ri * ldo + h * DH, 1.f);
+  load_head<DH>(oi, out + ri * ldo + h * DH, 1.f);
   float Di = 0.f;
 #pragma unroll
   for (int dd = 0; dd < DH; ++dd) {
-    dOi[dd] = dd < dh ? to_f32(dout[ri * ldo + h * dh + dd]) : 0.f;
-    if (dd < dh) Di = fmaf(dOi[dd], to_f32(out[ri * ldo + h * dh + dd]), Di);
+    Di = fmaf(dOi[dd], oi[dd], Di);
     acc[dd] = 0.f;
   }
   const float* P = psave + (int64_t)blockIdx.x * L * L;
   for (int j0 = 0; j0 < L; j0 += ACH) {
     __syncthreads();
-    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * dh, dh);
-    stage_rows<DH>(Vs, v, ldkv, row0, st, j0, L, h * dh, dh);
+    stage_rows<DH>(Ks, k, ldkv, row0, st, j0, L, h * DH);
+    stage_rows<DH>(Vs, v, ldkv, row0, st, j0, L, h * DH);
+    stage_p(Ps, P, L, j0, blockIdx.y * ACH);
     __syncthreads();
     const int nj = min(ACH, L - j0);
     for (int t = 0; t < nj; ++t) {
-      const float p = P[(int64_t)(j0 + t) * L + iq];
+      const float p = Ps[t * (ACH + 1) + lane];
       float dp = 0.f;
 #pragma unroll
-      for (int dd = 0; dd < DH; ++dd)
-        if (dd < dh) dp = fmaf(dOi[dd], Vs[t * DH + dd], dp);
+      for (int dd = 0; dd < DH; ++dd) dp = fmaf(dOi[dd], Vs[t * DH + dd], dp);
       const float ds = p * (dp - Di);
 #pragma unroll
-      for (int dd = 0; dd < DH; ++dd)
-        if (dd < dh) acc[dd] = fmaf(ds, Ks[t * DH + dd], acc[dd]);
+      for (int dd = 0; dd < DH; ++dd) acc[dd] = fmaf(ds, Ks[t * DH + dd], acc[dd]);
     }
   }
   if (live) {
 #pragma unroll
-    for (int dd = 0; dd < DH; ++dd)
-      if (dd < dh) dq[ri * lddq + h * dh + dd] = from_f32<T>(acc[dd] * scale);
+    for (int dd = 0; dd < DH; ++dd) dq[ri * lddq + h * DH + dd] = from_f32<T>(acc[dd] * scale);
   }
 }
 
@@ -294,7 +311,7 @@ __global__ __launch_bounds__(64) void attn_bwd_k_kernel(const T* __restrict__ q,
                                                         int ldkv, const float* __restrict__ psave,
                                                         const T* __restrict__ dout, const T* __restrict__ out, int ldo,
                                                         T* __restrict__ dk, T* __restrict__ dv, int lddkv, int n_inner,
-                                                        int64_t so, int64_t si, int64_t st, int L, int nhead, int dh,
+                                                        int64_t so, int64_t si, int64_t st, int L, int nhead,
                                                         float scale) {
   __shared__ float Qs[ACH * DH], Gs[ACH * DH], Ps[ACH * (ACH + 1)], Dr[ACH];
   const int lane = threadIdx.x;
@@ -305,58 +322,51 @@ __global__ __launch_bounds__(64) void attn_bwd_k_kernel(const T* __restrict__ q,
   const int jb = blockIdx.y * ACH;
   const int j = jb + lane;
   const bool live = j < L;
-  const int64_t rj = row0 + (int64_t)(live ? j : L - 1) * st;
+  const int64_t rj = row0 + (int64_t)min(j, L - 1) * st;
   float Vj[DH], dvacc[DH], dkacc[DH];
+  load_head<DH>(Vj, v + rj * ldkv + h * DH, 1.f);
 #pragma unroll
   for (int dd = 0; dd < DH; ++dd) {
-    Vj[dd] = dd < dh ? to_f32(v[rj * ldkv + h * dh + dd]) : 0.f;
     dvacc[dd] = 0.f;
     dkacc[dd] = 0.f;
   }
   const float* P = psave + (int64_t)blockIdx.x * L * L;
-  const int nkb = min(ACH, L - jb);
   for (int i0 = 0; i0 < L; i0 += ACH) {
     __syncthreads();
-    stage_rows<DH>(Qs, q, ldq, row0, st, i0, L, h * dh, dh);
-    stage_rows<DH>(Gs, dout, ldo, row0, st, i0, L, h * dh, dh);
-    {   // D of the chunk's queries (lane = query)
-      const int iq = i0 + lane;
+    stage_rows<DH>(Qs, q, ldq, row0, st, i0, L, h * DH);
+    stage_rows<DH>(Gs, dout, ldo, row0, st, i0, L, h * DH);
+    stage_p(Ps, P, L, jb, i0);
+    __syncthreads();
+    {   // D of the chunk's queries (lane = query): its dO row is staged, its O row read here
+      const int64_t ri = row0 + (int64_t)min(i0 + lane, L - 1) * st;
+      float oi[DH];
+      load_head<DH>(oi, out + ri * ldo + h * DH, 1.f);
       float d = 0.f;
-      if (iq < L) {
-        const int64_t ri = row0 + (int64_t)iq * st;
-        for (int dd = 0; dd < dh; ++dd)
-          d = fmaf(to_f32(dout[ri * ldo + h * dh + dd]), to_f32(out[ri * ldo + h * dh + dd]), d);
-      }
+#pragma unroll
+      for (int dd = 0; dd < DH; ++dd) d = fmaf(Gs[lane * DH + dd], oi[dd], d);
       Dr[lane] = d;
     }
-    const int ni = min(ACH, L - i0);
-    for (int e = lane; e < nkb * ACH; e += 64) {
-      const int t = e / ACH, c = e - t * ACH;
-      Ps[t * (ACH + 1) + c] = c < ni ? P[(int64_t)(jb + t) * L + i0 + c] : 0.f;
-    }
     __syncthreads();
+    const int ni = min(ACH, L - i0);
     for (int c = 0; c < ni; ++c) {
       const float p = Ps[lane * (ACH + 1) + c];
       float dp = 0.f;
 #pragma unroll
-      for (int dd = 0; dd < DH; ++dd)
-        if (dd < dh) dp = fmaf(Gs[c * DH + dd], Vj[dd], dp);
+      for (int dd = 0; dd < DH; ++dd) dp = fmaf(Gs[c * DH + dd], Vj[dd], dp);
       const float ds = p * (dp - Dr[c]);
 #pragma unroll
-      for (int dd = 0; dd < DH; ++dd)
-        if (dd < dh) {
-          dvacc[dd] = fmaf(p, Gs[c * DH + dd], dvacc[dd]);
-          dkacc[dd] = fmaf(ds, Qs[c * DH + dd], dkacc[dd]);
-        }
+      for (int dd = 0; dd < DH; ++dd) {
+        dvacc[dd] = fmaf(p, Gs[c * DH + dd], dvacc[dd]);
+        dkacc[dd] = fmaf(ds, Qs[c * DH + dd], dkacc[dd]);
+      }
     }
   }
   if (live) {
 #pragma unroll
-    for (int dd = 0; dd < DH; ++dd)
-      if (dd < dh) {
-        dv[rj * lddkv + h * dh + dd] = from_f32<T>(dvacc[dd]);
-        dk[rj * lddkv + h * dh + dd] = from_f32<T>(dkacc[dd] * scale);
-      }
+    for (int dd = 0; dd < DH; ++dd) {
+      dv[rj * lddkv + h * DH + dd] = from_f32<T>(dvacc[dd]);
+      dk[rj * lddkv + h * DH + dd] = from_f32<T>(dkacc[dd] * scale);
+    }
   }
 }
 
@@ -813,12 +823,14 @@ extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, flo
 }
 
 // the head dim picks the instantiation (the decoder's and the AIFI layer's heads are 32 wide)
-#define ATT_LAUNCH(KERN, T, GRID, BLOCK, LDS, STREAM, ...)                    \
-  do {                                                                        \
-    if (dh <= 32)                                                             \
-      hipLaunchKernelGGL((KERN<T, 32>), GRID, BLOCK, LDS, STREAM, __VA_ARGS__); \
-    else                                                                      \
-      hipLaunchKernelGGL((KERN<T, 64>), GRID, BLOCK, LDS, STREAM, __VA_ARGS__); \
+#define ATT_LAUNCH(KERN, T, GRID, BLOCK, LDS, STREAM, ...)                                                \
+  do {                                                                                                    \
+    switch (dh) {                                                                                         \
+      case 16: hipLaunchKernelGGL((KERN<T, 16>), GRID, BLOCK, LDS, STREAM, __VA_ARGS__); break;           \
+      case 32: hipLaunchKernelGGL((KERN<T, 32>), GRID, BLOCK, LDS, STREAM, __VA_ARGS__); break;           \
+      case 48: hipLaunchKernelGGL((KERN<T, 48>), GRID, BLOCK, LDS, STREAM, __VA_ARGS__); break;           \
+      default: hipLaunchKernelGGL((KERN<T, 64>), GRID, BLOCK, LDS, STREAM, __VA_ARGS__); break;           \
+    }                                                                                                     \
   } while (0)
 
 extern "C" int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out,
@@ -826,7 +838,8 @@ extern "C" int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const voi
                            int64_t so, int64_t si, int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype,
                            void* stream) {
   DP_REQUIRE(q && k && v && out && p_save, "dp_attn_fwd: null pointer");
-  DP_REQUIRE(seqlen > 0 && dh > 0 && dh <= ATT_DH, "dp_attn_fwd: seqlen %d x dh %d (dh <= 64)", seqlen, dh);
+  DP_REQUIRE(seqlen > 0 && (dh == 16 || dh == 32 || dh == 48 || dh == 64),
+             "dp_attn_fwd: seqlen %d x dh %d (dh 16 / 32 / 48 / 64)", seqlen, dh);
   DP_REQUIRE((int64_t)n_outer * n_inner * nhead < (1ll << 31), "dp_attn_fwd: too many sequences");
   const float scale = 1.f / sqrtf((float)dh);
   dim3 grid((unsigned)(n_outer * n_inner * nhead), (unsigned)((seqlen + ACH - 1) / ACH));
@@ -834,10 +847,10 @@ extern "C" int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const voi
   if (dtype == DP_BF16)
     ATT_LAUNCH(attn_fwd_kernel, bf16_t, grid, dim3(64), 0, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
                        (const bf16_t*)v, ld_kv, (bf16_t*)out, ld_o, p_save, mask, n_inner, so, si, st, seqlen, nhead,
-                       dh, scale);
+                       scale);
   else
     ATT_LAUNCH(attn_fwd_kernel, float, grid, dim3(64), 0, s, (const float*)q, ld_q, (const float*)k,
-                       (const float*)v, ld_kv, (float*)out, ld_o, p_save, mask, n_inner, so, si, st, seqlen, nhead, dh,
+                       (const float*)v, ld_kv, (float*)out, ld_o, p_save, mask, n_inner, so, si, st, seqlen, nhead,
                        scale);
   return dp_check_launch("dp_attn_fwd");
 }
@@ -848,24 +861,25 @@ extern "C" int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const voi
                            int64_t so, int64_t si, int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype,
                            void* stream) {
   DP_REQUIRE(q && k && v && p_save && dout && out && dq && dk && dv, "dp_attn_bwd: null pointer");
-  DP_REQUIRE(seqlen > 0 && dh > 0 && dh <= ATT_DH, "dp_attn_bwd: seqlen %d x dh %d (dh <= 64)", seqlen, dh);
+  DP_REQUIRE(seqlen > 0 && (dh == 16 || dh == 32 || dh == 48 || dh == 64),
+             "dp_attn_bwd: seqlen %d x dh %d (dh 16 / 32 / 48 / 64)", seqlen, dh);
   const float scale = 1.f / sqrtf((float)dh);
   dim3 grid((unsigned)(n_outer * n_inner * nhead), (unsigned)((seqlen + ACH - 1) / ACH));
   hipStream_t s = as_stream(stream);
   if (dtype == DP_BF16) {
     ATT_LAUNCH(attn_bwd_q_kernel, bf16_t, grid, dim3(64), 0, s, (const bf16_t*)k, (const bf16_t*)v, ld_kv,
                        p_save, (const bf16_t*)dout, (const bf16_t*)out, ld_o, (bf16_t*)dq, ld_dq, n_inner, so, si, st,
-                       seqlen, nhead, dh, scale);
+                       seqlen, nhead, scale);
     ATT_LAUNCH(attn_bwd_k_kernel, bf16_t, grid, dim3(64), 0, s, (const bf16_t*)q, ld_q, (const bf16_t*)v,
                        ld_kv, p_save, (const bf16_t*)dout, (const bf16_t*)out, ld_o, (bf16_t*)dk, (bf16_t*)dv, ld_dkv,
-                       n_inner, so, si, st, seqlen, nhead, dh, scale);
+                       n_inner, so, si, st, seqlen, nhead, scale);
   } else {
     ATT_LAUNCH(attn_bwd_q_kernel, float, grid, dim3(64), 0, s, (const float*)k, (const float*)v, ld_kv, p_save,
                        (const float*)dout, (const float*)out, ld_o, (float*)dq, ld_dq, n_inner, so, si, st, seqlen,
-                       nhead, dh, scale);
+                       nhead, scale);
     ATT_LAUNCH(attn_bwd_k_kernel, float, grid, dim3(64), 0, s, (const float*)q, ld_q, (const float*)v, ld_kv,
                        p_save, (const float*)dout, (const float*)out, ld_o, (float*)dk, (float*)dv, ld_dkv, n_inner,
-                       so, si, st, seqlen, nhead, dh, scale);
+                       so, si, st, seqlen, nhead, scale);
   }
   return dp_check_launch("dp_attn_bwd");
 }

@@ -449,7 +449,7 @@ int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, float* out, in
  * != 0: query i may not see key j; nn.MultiheadAttention attn_mask semantics). Sequences and
  * rows addressed as dp_attention (row o*so + i*si + t*st; q / k / v columns h*dh of rows ld_q /
  * ld_kv apart, out ld_o). Saves P f32 [seq][head][key][query] (softmax probabilities) for the
- * backward. dh <= 64; one wave per (sequence, head, 64 queries), keys streamed through LDS in
+ * backward. dh 16 / 32 / 48 / 64; one wave per (sequence, head, 64 queries), keys streamed through LDS in
  * 64-row chunks (the decoder's 18 / 60 + DN tokens, the AIFI layer's 400: hybrid_encoder.py:276-279). */
 int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out, int32_t ld_o,
                 float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
