@@ -19,74 +19,82 @@ __device__ __forceinline__ float ldf(const T* p) {
 // dz = dy * a * act'(u) * s[ch]; with LAB (scale a, bias cb) also d a += dy r, d cb += dy where r =
 // relu(u) = (y - res - cb) / a. relu'(u) is read off y: the unit counts as on where a r exceeds
 // the stored output's rounding (exact zero test without LAB and residual).
-template <typename T>
+// A block = 256 threads = (256 / cw) rows x cw channels (cw = c rounded up to a power of two, at
+// most 256), so narrow maps (the stem's 16 / 32 channels) fill the lanes; each thread does RU rows
+// per step with all their loads issued first. RELU / RES / LAB are template flags: no branch
+// around a load.
+template <typename T, bool RELU, bool RES, bool LAB>
 __global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict__ y, int64_t ldy,
                                                              const T* __restrict__ res, int64_t ldr,
                                                              const T* __restrict__ dy, int64_t lddy, T* __restrict__ dz,
-                                                             int64_t lddz, int rows, int c, int act,
+                                                             int64_t lddz, int rows, int c, int cw_log2,
                                                              const float* __restrict__ lab_a,
                                                              const float* __restrict__ lab_b,
                                                              const float* __restrict__ scale, float* __restrict__ dlab_a,
                                                              float* __restrict__ dlab_b) {
-  // a thread owns one channel and walks the rows blockIdx.x, + gridDim.x, ... (no per-element
-  // division); grid = (row slices, channel blocks)
-  const int ch = blockIdx.y * blockDim.x + threadIdx.x;
+  constexpr int RU = 4;
+  const int cw = 1 << cw_log2, rpb = 256 >> cw_log2;
+  const int ch = blockIdx.y * cw + (threadIdx.x & (cw - 1));
+  const int rsub = threadIdx.x >> cw_log2;
   const bool active = ch < c;
-  const bool lab = lab_a != nullptr;
+  const int chc = active ? ch : c - 1;
   // relative rounding of the stored output (f32: 2^-23, bf16: 2^-8): y = round(a r + cb + res),
   // so r == 0 is told from r > 0 only up to that
   const float eps = sizeof(T) == 2 ? 3.90625e-3f : 1.1920929e-7f;
   float a = 1.f, cb = 0.f;
-  if (lab) {
+  if (LAB) {
     a = *lab_a;
     cb = *lab_b;
   }
-  const float sc_ch = (scale && active) ? scale[ch] : 1.f;
+  const float sc_ch = scale ? scale[chc] : 1.f;
   float sa = 0.f, sc = 0.f;
-  if (active) {
-    for (int r = blockIdx.x; r < rows; r += gridDim.x) {
-      const float g = ldf(dy + (int64_t)r * lddy + ch);
-      float d = g;
-      if (act == DP_ACT_RELU) {
+  const int step = gridDim.x * rpb * RU;
+  for (int r0 = blockIdx.x * rpb * RU + rsub; r0 < rows; r0 += step) {
+    float g[RU], yv[RU], rv[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t r = min(r0 + u * rpb, rows - 1);
+      g[u] = ldf(dy + r * lddy + chc);
+      yv[u] = RELU ? ldf(y + r * ldy + chc) : 0.f;
+      rv[u] = RES ? ldf(res + r * ldr + chc) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const bool ok = active && r0 + u * rpb < rows;
+      float d = g[u];
+      if (RELU) {
         // the stored output holds lab(act(u)) + res (the HG block's identity, added after the act)
-        const float yv = ldf(y + (int64_t)r * ldy + ch);
-        const float rv = res ? ldf(res + (int64_t)r * ldr + ch) : 0.f;
-        const float v = yv - rv - cb;   // a * relu(u), up to the output's rounding
-        const float tol = (res || lab) ? eps * (fabsf(yv) + fabsf(rv) + fabsf(cb)) : 0.f;
-        const bool on = lab ? (a > 0.f ? v > tol : v < -tol) : v > tol;
-        if (lab) {
+        const float v = yv[u] - rv[u] - cb;   // a * relu(u), up to the output's rounding
+        const float tol = (RES || LAB) ? eps * (fabsf(yv[u]) + fabsf(rv[u]) + fabsf(cb)) : 0.f;
+        const bool on = LAB ? (a > 0.f ? v > tol : v < -tol) : v > tol;
+        if (LAB) {
           const float rr = on ? v / a : 0.f;
-          sa = fmaf(g, rr, sa);
-          sc += g;
-          d = on ? g * a : 0.f;
+          sa = fmaf(ok ? g[u] : 0.f, rr, sa);
+          sc += ok ? g[u] : 0.f;
+          d = on ? g[u] * a : 0.f;
         } else {
-          d = on ? g : 0.f;
+          d = on ? g[u] : 0.f;
         }
       }
-      dz[(int64_t)r * lddz + ch] = from_f32<T>(d * sc_ch);
+      if (ok) dz[(int64_t)(r0 + u * rpb) * lddz + ch] = from_f32<T>(d * sc_ch);
     }
   }
-  if (!dlab_a) return;
+  if (!LAB) return;
   __shared__ float red[2][4];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     sa += __shfl_xor(sa, o);
     sc += __shfl_xor(sc, o);
   }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) {
     red[0][wv] = sa;
     red[1][wv] = sc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float ta = 0.f, tc = 0.f;
-    for (int w = 0; w < nw; ++w) {
-      ta += red[0][w];
-      tc += red[1][w];
-    }
-    atomicAdd(dlab_a, ta);
-    atomicAdd(dlab_b, tc);
+    atomicAdd(dlab_a, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(dlab_b, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
   }
 }
 
@@ -185,10 +193,29 @@ extern "C" int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* res, i
   DP_REQUIRE(dy && dz && rows > 0 && c > 0 && (act == DP_ACT_NONE || (act == DP_ACT_RELU && y)) &&
                  (!lab_a || (lab_b && act == DP_ACT_RELU && dlab_a && dlab_b)),
              "dp_frozen_act_bwd: bad arguments");
-  const int bx = c >= 256 ? 256 : (c + 63) / 64 * 64, gy = (c + bx - 1) / bx;
-  const int gx = std::max(1, std::min(rows, (1 << 16) / (bx * gy)));
-  DP_DT(hipLaunchKernelGGL(frozen_act_bwd_kernel<T>, dim3(gx, gy), dim3(bx), 0, as_stream(stream), (const T*)y, ld_y, (const T*)res, ld_res, (const T*)dy, ld_dy, (T*)dz, ld_dz, rows, c, act, lab_a,
-                           lab_b, scale, lab_a ? dlab_a : nullptr, dlab_b));
+  int lg = 0;
+  while ((1 << lg) < c && lg < 8) ++lg;
+  const int cw = 1 << lg, rpb = 256 / cw, gy = (c + cw - 1) / cw;
+  const int gx = std::max(1, std::min((rows + rpb * 4 - 1) / (rpb * 4), std::max(1, 4096 / gy)));
+  const bool relu = act == DP_ACT_RELU, hres = relu && res, lab = lab_a != nullptr;
+  hipStream_t s = as_stream(stream);
+#define FAB(T_, R_, S_, L_)                                                                                      \
+  hipLaunchKernelGGL((frozen_act_bwd_kernel<T_, R_, S_, L_>), dim3(gx, gy), dim3(256), 0, s, (const T_*)y, ld_y, \
+                     (const T_*)res, ld_res, (const T_*)dy, ld_dy, (T_*)dz, ld_dz, rows, c, lg, lab_a, lab_b, scale, \
+                     dlab_a, dlab_b)
+#define FAB_T(T_)                                      \
+  if (!relu) FAB(T_, false, false, false);             \
+  else if (!hres && !lab) FAB(T_, true, false, false); \
+  else if (!hres) FAB(T_, true, false, true);          \
+  else if (!lab) FAB(T_, true, true, false);           \
+  else FAB(T_, true, true, true)
+  if (dtype == DP_BF16) {
+    FAB_T(bf16_t);
+  } else {
+    FAB_T(float);
+  }
+#undef FAB_T
+#undef FAB
   return dp_check_launch("dp_frozen_act_bwd");
 }
 

@@ -306,7 +306,8 @@ __global__ __launch_bounds__(256) void dw_bwd_data_kernel(const T* __restrict__ 
 #pragma unroll
         for (int j = 0; j < DW_TW + K - 1; ++j) {
           const int ox = x0 + pad - (K - 1) + j;
-          zw[j] = (ox >= 0 && ox < ow) ? to_f32(zr[(int64_t)ox * zps]) : 0.f;
+          const float zv = to_f32(zr[(int64_t)min(max(ox, 0), ow - 1) * zps]);
+          zw[j] = (ox >= 0 && ox < ow) ? zv : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < DW_TW; ++i)
@@ -318,16 +319,19 @@ __global__ __launch_bounds__(256) void dw_bwd_data_kernel(const T* __restrict__ 
 #pragma unroll
           for (int kx = 0; kx < K; ++kx) {
             const int nx = x0 + i + pad - kx;
-            if (nx < 0 || nx % S) continue;
             const int ox = nx / S;
-            if (ox < ow) acc[i] = fmaf(to_f32(zr[(int64_t)ox * zps]), wk[ky * K + kx], acc[i]);
+            const float zv = to_f32(zr[(int64_t)min(max(ox, 0), ow - 1) * zps]);
+            acc[i] = fmaf((nx >= 0 && nx % S == 0 && ox < ow) ? zv : 0.f, wk[ky * K + kx], acc[i]);
           }
       }
     }
-    T* o = dx + (int64_t)b * xbs + ((int64_t)y * w + x0) * xps + ch;
+    T* o = dx + (int64_t)b * xbs + (int64_t)y * w * xps + ch;
+    float prev[DW_TW];
+#pragma unroll
+    for (int i = 0; i < DW_TW; ++i) prev[i] = to_f32(o[(int64_t)min(x0 + i, w - 1) * xps]);
 #pragma unroll
     for (int i = 0; i < DW_TW; ++i)
-      if (x0 + i < w) o[(int64_t)i * xps] = from_f32<T>(to_f32(o[(int64_t)i * xps]) + acc[i]);
+      if (x0 + i < w) o[(int64_t)(x0 + i) * xps] = from_f32<T>(prev[i] + acc[i]);
   }
 }
 
@@ -351,7 +355,10 @@ __global__ __launch_bounds__(256) void dw_bwd_weight_kernel(const T* __restrict_
       float g[DW_TW];
       const T* zr = dz + (int64_t)b * zbs + (int64_t)oy * ow * zps + ch;
 #pragma unroll
-      for (int i = 0; i < DW_TW; ++i) g[i] = ox0 + i < ow ? to_f32(zr[(int64_t)(ox0 + i) * zps]) : 0.f;
+      for (int i = 0; i < DW_TW; ++i) {
+        const float gv = to_f32(zr[(int64_t)min(ox0 + i, ow - 1) * zps]);
+        g[i] = ox0 + i < ow ? gv : 0.f;
+      }
 #pragma unroll
       for (int ky = 0; ky < K; ++ky) {
         const int iy = oy * S - pad + ky;
@@ -361,7 +368,8 @@ __global__ __launch_bounds__(256) void dw_bwd_weight_kernel(const T* __restrict_
 #pragma unroll
         for (int j = 0; j < XW; ++j) {
           const int ix = ox0 * S - pad + j;
-          xw[j] = (ix >= 0 && ix < w) ? to_f32(xr[(int64_t)ix * xps]) : 0.f;
+          const float xv = to_f32(xr[(int64_t)min(max(ix, 0), w - 1) * xps]);
+          xw[j] = (ix >= 0 && ix < w) ? xv : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < DW_TW; ++i)
@@ -395,8 +403,8 @@ void dw_bwd_launch(const void* x, int64_t xbs, int xps, const void* dz, int64_t 
   }
   if (dw) {
     const int ntiles = batch * oh * ((ow + DW_TW - 1) / DW_TW);
-    // about 16 tiles per thread: the atomics stay a small fraction of the work
-    const unsigned gy = (unsigned)std::max(1, std::min((ntiles + 63) / 64, 65535));
+    // about 4 tiles per thread: enough waves to fill the chip, the atomics a small fraction
+    const unsigned gy = (unsigned)std::max(1, std::min((ntiles + 15) / 16, 65535));
     hipLaunchKernelGGL((dw_bwd_weight_kernel<T, K, S>), dim3(gx, gy), dim3(64, 4), 0, s, (const T*)x, xbs, xps,
                        (const T*)dz, zbs, zps, h, w, c, pad, oh, ow, ntiles, dw);
   }
