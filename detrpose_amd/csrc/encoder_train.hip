@@ -46,18 +46,23 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
   __shared__ float red[2][4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + lane;
+  const int chc = min(ch, c - 1);
   const int r0 = blockIdx.y * 256;
   float s1 = 0.f, s2 = 0.f;
-  if (ch < c) {
-    const float k = ld_(x + ch);
-    const int r1 = min(r0 + 256, rows);
-    for (int r = r0 + wv; r < r1; r += 4) {
-      const float d = ld_(x + (int64_t)r * ld + ch) - k;
-      s1 += d;
-      s2 = fmaf(d, d, s2);
-    }
-    if (blockIdx.y == 0 && wv == 0) out[ch] = k;
+  const float k = ld_(x + chc);
+  const int r1 = min(r0 + 256, rows);
+  for (int r = r0 + wv; r < r1; r += 32) {   // 8 rows per step, loads issued together
+    float d[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) d[u] = ld_(x + (int64_t)min(r + 4 * u, r1 - 1) * ld + chc) - k;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (r + 4 * u < r1) {
+        s1 += d[u];
+        s2 = fmaf(d[u], d[u], s2);
+      }
   }
+  if (blockIdx.y == 0 && wv == 0 && ch < c) out[ch] = k;
   red[0][wv][lane] = s1;
   red[1][wv][lane] = s2;
   __syncthreads();
@@ -102,43 +107,47 @@ struct BnBranch {
   const float* b;
 };
 
-template <typename T>
-__device__ __forceinline__ float bn_of(const BnBranch& p, int64_t r, int ch, int c, float* xh) {
-  const float x = ld_(reinterpret_cast<const T*>(p.z) + r * p.ld + ch);
-  const float h = (x - p.mr[ch]) * p.mr[c + ch];
-  *xh = h;
-  return fmaf(p.g[ch], h, p.b[ch]);
-}
-
 // Row kernels: a thread owns one channel (its per-channel parameters in registers) and walks
-// the rows blockIdx.x, + gridDim.x, ...; consecutive threads take consecutive channels of a row.
-// grid = (row slices, channel blocks of blockDim.x): see rc_grid.
+// the rows blockIdx.x + u gridDim.x (u = 0 .. RU-1), + RU gridDim.x, ...; consecutive threads take
+// consecutive channels of a row. The RU rows' loads are issued together (row indices clamped,
+// out-of-range rows not stored). grid = (row slices, channel blocks of blockDim.x): see rc_grid.
+constexpr int RU = 4;
 
 // y = act(bn1(z1) [+ bn2(z2)]) (+ res when res != NULL)
-template <typename T>
+template <typename T, bool TWO, bool RES>
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(T* __restrict__ y, int64_t ldy, BnBranch p1, BnBranch p2,
                                                          const T* __restrict__ res, int64_t ldr, int rows, int c,
                                                          int act) {
   const int ch = blockIdx.y * blockDim.x + threadIdx.x;
   if (ch >= c) return;
   const float m1 = p1.mr[ch], s1 = p1.mr[c + ch], g1 = p1.g[ch], b1 = p1.b[ch];
-  const bool two = p2.z != nullptr;
-  const float m2 = two ? p2.mr[ch] : 0.f, s2 = two ? p2.mr[c + ch] : 0.f, g2 = two ? p2.g[ch] : 0.f,
-              b2 = two ? p2.b[ch] : 0.f;
+  const float m2 = TWO ? p2.mr[ch] : 0.f, s2 = TWO ? p2.mr[c + ch] : 0.f, g2 = TWO ? p2.g[ch] : 0.f,
+              b2 = TWO ? p2.b[ch] : 0.f;
   const T* z1 = reinterpret_cast<const T*>(p1.z) + ch;
-  const T* z2 = two ? reinterpret_cast<const T*>(p2.z) + ch : nullptr;
-  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
-    float v = fmaf(g1, (ld_(z1 + (int64_t)r * p1.ld) - m1) * s1, b1);
-    if (two) v += fmaf(g2, (ld_(z2 + (int64_t)r * p2.ld) - m2) * s2, b2);
-    v = act_f(v, act);
-    if (res) v += ld_(res + (int64_t)r * ldr + ch);
-    y[(int64_t)r * ldy + ch] = from_f32<T>(v);
+  const T* z2 = reinterpret_cast<const T*>(p2.z) + ch;
+  for (int r0 = blockIdx.x; r0 < rows; r0 += RU * gridDim.x) {
+    float x1[RU], x2[RU], rv[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t r = min(r0 + u * (int)gridDim.x, rows - 1);
+      x1[u] = ld_(z1 + r * p1.ld);
+      x2[u] = TWO ? ld_(z2 + r * p2.ld) : 0.f;
+      rv[u] = RES ? ld_(res + r * ldr + ch) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int r = r0 + u * gridDim.x;
+      float v = fmaf(g1, (x1[u] - m1) * s1, b1);
+      if (TWO) v += fmaf(g2, (x2[u] - m2) * s2, b2);
+      v = act_f(v, act) + rv[u];
+      if (r < rows) y[(int64_t)r * ldy + ch] = from_f32<T>(v);
+    }
   }
 }
 
 // dp = dy * act'(pre): column sums sums[0] += sum dp, sums[1] += sum dp xh1, sums[2] += sum dp
 // xh2, and the parameter gradients dg1 += sum dp xh1, db1 += sum dp (dg2 / db2 likewise)
-template <typename T>
+template <typename T, bool TWO>
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restrict__ dy, int64_t ldy, BnBranch p1,
                                                                 BnBranch p2, int rows, int c, int act,
                                                                 float* __restrict__ sums, float* __restrict__ dg1,
@@ -147,15 +156,30 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restr
   __shared__ float red[3][4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + lane;
+  const int chc = min(ch, c - 1);
   const int r0 = blockIdx.y * 256;
+  const float m1 = p1.mr[chc], s1 = p1.mr[c + chc], g1 = p1.g[chc], b1 = p1.b[chc];
+  const float m2 = TWO ? p2.mr[chc] : 0.f, s2 = TWO ? p2.mr[c + chc] : 0.f, g2 = TWO ? p2.g[chc] : 0.f,
+              b2 = TWO ? p2.b[chc] : 0.f;
+  const T* z1 = reinterpret_cast<const T*>(p1.z) + chc;
+  const T* z2 = reinterpret_cast<const T*>(p2.z) + chc;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-  if (ch < c) {
-    const int r1 = min(r0 + 256, rows);
-    for (int r = r0 + wv; r < r1; r += 4) {
-      float h1, h2 = 0.f;
-      float pre = bn_of<T>(p1, r, ch, c, &h1);
-      if (p2.z) pre += bn_of<T>(p2, r, ch, c, &h2);
-      const float dp = ld_(dy + (int64_t)r * ldy + ch) * act_d(pre, act);
+  const int r1 = min(r0 + 256, rows);
+  for (int r = r0 + wv; r < r1; r += 4 * RU) {
+    float x1[RU], x2[RU], g[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t rr = min(r + 4 * u, r1 - 1);
+      x1[u] = ld_(z1 + rr * p1.ld);
+      x2[u] = TWO ? ld_(z2 + rr * p2.ld) : 0.f;
+      g[u] = ld_(dy + rr * ldy + chc);
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const float h1 = (x1[u] - m1) * s1, h2 = TWO ? (x2[u] - m2) * s2 : 0.f;
+      float pre = fmaf(g1, h1, b1);
+      if (TWO) pre += fmaf(g2, h2, b2);
+      const float dp = r + 4 * u < r1 ? g[u] * act_d(pre, act) : 0.f;
       a0 += dp;
       a1 = fmaf(dp, h1, a1);
       a2 = fmaf(dp, h2, a2);
@@ -166,22 +190,22 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restr
   red[2][wv][lane] = a2;
   __syncthreads();
   if (wv == 0 && ch < c) {
-    const float s0 = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
-    const float s1 = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
-    const float s2 = red[2][0][lane] + red[2][1][lane] + red[2][2][lane] + red[2][3][lane];
-    atomicAdd(sums + ch, s0);
-    atomicAdd(sums + c + ch, s1);
-    atomicAdd(sums + 2 * c + ch, s2);
-    if (dg1) atomicAdd(dg1 + ch, s1);
-    if (db1) atomicAdd(db1 + ch, s0);
-    if (dg2) atomicAdd(dg2 + ch, s2);
-    if (db2) atomicAdd(db2 + ch, s0);
+    const float t0 = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+    const float t1 = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+    const float t2 = red[2][0][lane] + red[2][1][lane] + red[2][2][lane] + red[2][3][lane];
+    atomicAdd(sums + ch, t0);
+    atomicAdd(sums + c + ch, t1);
+    atomicAdd(sums + 2 * c + ch, t2);
+    if (dg1) atomicAdd(dg1 + ch, t1);
+    if (db1) atomicAdd(db1 + ch, t0);
+    if (dg2) atomicAdd(dg2 + ch, t2);
+    if (db2) atomicAdd(db2 + ch, t0);
   }
 }
 
 // dz_k = g_k rstd_k (dp - sum dp / N - xh_k sum (dp xh_k) / N) (torch batch_norm_backward with
 // the synced sums)
-template <typename T>
+template <typename T, bool TWO>
 __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(T* __restrict__ dz1, int64_t ld1, T* __restrict__ dz2,
                                                                int64_t ld2, const T* __restrict__ dy, int64_t ldy,
                                                                BnBranch p1, BnBranch p2, int rows, int c, int act,
@@ -189,23 +213,33 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(T* __restrict__ d
   const int ch = blockIdx.y * blockDim.x + threadIdx.x;
   if (ch >= c) return;
   const float m1 = p1.mr[ch], s1 = p1.mr[c + ch], g1 = p1.g[ch], b1 = p1.b[ch];
-  const bool two = p2.z != nullptr;
-  const float m2 = two ? p2.mr[ch] : 0.f, s2 = two ? p2.mr[c + ch] : 0.f, g2 = two ? p2.g[ch] : 0.f,
-              b2 = two ? p2.b[ch] : 0.f;
+  const float m2 = TWO ? p2.mr[ch] : 0.f, s2 = TWO ? p2.mr[c + ch] : 0.f, g2 = TWO ? p2.g[ch] : 0.f,
+              b2 = TWO ? p2.b[ch] : 0.f;
   const float m0 = sums[ch] * inv_n, c1 = sums[c + ch] * inv_n, c2 = sums[2 * c + ch] * inv_n;
   const float k1 = g1 * s1, k2 = g2 * s2;
   const T* z1 = reinterpret_cast<const T*>(p1.z) + ch;
-  const T* z2 = two ? reinterpret_cast<const T*>(p2.z) + ch : nullptr;
-  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
-    const float h1 = (ld_(z1 + (int64_t)r * p1.ld) - m1) * s1;
-    float pre = fmaf(g1, h1, b1), h2 = 0.f;
-    if (two) {
-      h2 = (ld_(z2 + (int64_t)r * p2.ld) - m2) * s2;
-      pre += fmaf(g2, h2, b2);
+  const T* z2 = reinterpret_cast<const T*>(p2.z) + ch;
+  for (int r0 = blockIdx.x; r0 < rows; r0 += RU * gridDim.x) {
+    float x1[RU], x2[RU], g[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t r = min(r0 + u * (int)gridDim.x, rows - 1);
+      x1[u] = ld_(z1 + r * p1.ld);
+      x2[u] = TWO ? ld_(z2 + r * p2.ld) : 0.f;
+      g[u] = ld_(dy + r * ldy + ch);
     }
-    const float dp = ld_(dy + (int64_t)r * ldy + ch) * act_d(pre, act);
-    dz1[(int64_t)r * ld1 + ch] = from_f32<T>(k1 * (dp - m0 - h1 * c1));
-    if (dz2) dz2[(int64_t)r * ld2 + ch] = from_f32<T>(k2 * (dp - m0 - h2 * c2));
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int r = r0 + u * gridDim.x;
+      const float h1 = (x1[u] - m1) * s1, h2 = TWO ? (x2[u] - m2) * s2 : 0.f;
+      float pre = fmaf(g1, h1, b1);
+      if (TWO) pre += fmaf(g2, h2, b2);
+      const float dp = g[u] * act_d(pre, act);
+      if (r < rows) {
+        dz1[(int64_t)r * ld1 + ch] = from_f32<T>(k1 * (dp - m0 - h1 * c1));
+        if (TWO) dz2[(int64_t)r * ld2 + ch] = from_f32<T>(k2 * (dp - m0 - h2 * c2));
+      }
+    }
   }
 }
 
@@ -437,17 +471,28 @@ __global__ void up2_kernel(const T* __restrict__ src, int64_t sbs, int sps, int 
 }
 
 // y (=|+=) alpha a [+ beta b]: residual adds and their backward (gradient fan-out)
-template <typename T>
+template <typename T, bool HB, bool ACC>
 __global__ __launch_bounds__(256) void axpby_kernel(T* __restrict__ y, int64_t ldy, const T* __restrict__ a, int64_t lda,
                                                     float alpha, const T* __restrict__ b, int64_t ldb, float beta,
-                                                    int rows, int c, int acc) {
+                                                    int rows, int c) {
   const int ch = blockIdx.y * blockDim.x + threadIdx.x;
   if (ch >= c) return;
-  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
-    float v = alpha * ld_(a + (int64_t)r * lda + ch);
-    if (b) v = fmaf(beta, ld_(b + (int64_t)r * ldb + ch), v);
-    T* o = y + (int64_t)r * ldy + ch;
-    *o = from_f32<T>(acc ? ld_(o) + v : v);
+  for (int r0 = blockIdx.x; r0 < rows; r0 += RU * gridDim.x) {
+    float va[RU], vb[RU], vy[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t r = min(r0 + u * (int)gridDim.x, rows - 1);
+      va[u] = ld_(a + r * lda + ch);
+      vb[u] = HB ? ld_(b + r * ldb + ch) : 0.f;
+      vy[u] = ACC ? ld_(y + r * ldy + ch) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int r = r0 + u * gridDim.x;
+      float v = alpha * va[u];
+      if (HB) v = fmaf(beta, vb[u], v);
+      if (r < rows) y[(int64_t)r * ldy + ch] = from_f32<T>(ACC ? vy[u] + v : v);
+    }
   }
 }
 
@@ -458,21 +503,32 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ pre,
                                                       int act) {
   const int ch = blockIdx.y * blockDim.x + threadIdx.x;
   if (ch >= c) return;
-  for (int r = blockIdx.x; r < rows; r += gridDim.x)
-    dx[(int64_t)r * ldx + ch] =
-        from_f32<T>(ld_(dy + (int64_t)r * ldy + ch) * act_d(ld_(pre + (int64_t)r * ldp + ch), act));
+  for (int r0 = blockIdx.x; r0 < rows; r0 += RU * gridDim.x) {
+    float vp[RU], vg[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t r = min(r0 + u * (int)gridDim.x, rows - 1);
+      vp[u] = ld_(pre + r * ldp + ch);
+      vg[u] = ld_(dy + r * ldy + ch);
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int r = r0 + u * gridDim.x;
+      if (r < rows) dx[(int64_t)r * ldx + ch] = from_f32<T>(vg[u] * act_d(vp[u], act));
+    }
+  }
 }
 
 // (row slices, channel blocks) of a row kernel: blockDim.x = the channels rounded to a wave (at
-// most 256), about 64 K threads in flight per launch
+// most 256), about 512 K threads per launch (8 waves per SIMD), each at least RU rows
 struct RC {
   dim3 grid, block;
 };
 RC rc_grid(int rows, int c) {
   const int bx = c >= 256 ? 256 : (c + 63) / 64 * 64;
   const int gy = (c + bx - 1) / bx;
-  int gx = (1 << 16) / (bx * gy);
-  if (gx > rows) gx = rows;
+  int gx = (1 << 19) / (bx * gy);
+  if (gx > (rows + RU - 1) / RU) gx = (rows + RU - 1) / RU;
   if (gx < 1) gx = 1;
   return {dim3((unsigned)gx, (unsigned)gy), dim3((unsigned)bx)};
 }
@@ -525,8 +581,15 @@ extern "C" int dp_bn_act_fwd(void* y, int64_t ld_y, const void* z1, int64_t ld1,
              "dp_bn_act_fwd: bad arguments");
   const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
   const RC g = rc_grid(rows, c);
-  DP_DT(hipLaunchKernelGGL(bn_act_fwd_kernel<T>, g.grid, g.block, 0, as_stream(stream), (T*)y, ld_y, p1, p2,
-                           (const T*)res, ld_res, rows, c, act));
+#define BNF(TW_, RS_)                                                                                           \
+  DP_DT(hipLaunchKernelGGL((bn_act_fwd_kernel<T, TW_, RS_>), g.grid, g.block, 0, as_stream(stream), (T*)y, ld_y, p1, \
+                           p2, (const T*)res, ld_res, rows, c, act))
+  if (z2) {
+    if (res) BNF(true, true); else BNF(true, false);
+  } else {
+    if (res) BNF(false, true); else BNF(false, false);
+  }
+#undef BNF
   return dp_check_launch("dp_bn_act_fwd");
 }
 
@@ -544,8 +607,12 @@ extern "C" int dp_bn_act_bwd_reduce(const void* dy, int64_t ld_dy, const void* z
   }
   const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
   dim3 grid((c + 63) / 64, (rows + 255) / 256);
-  DP_DT(hipLaunchKernelGGL(bn_act_bwd_reduce_kernel<T>, grid, dim3(256), 0, s, (const T*)dy, ld_dy, p1, p2, rows, c,
-                           act, sums, dg1, db1, dg2, db2));
+  if (z2)
+    DP_DT(hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, s, (const T*)dy, ld_dy, p1, p2,
+                             rows, c, act, sums, dg1, db1, dg2, db2));
+  else
+    DP_DT(hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, s, (const T*)dy, ld_dy, p1, p2,
+                             rows, c, act, sums, dg1, db1, dg2, db2));
   return dp_check_launch("dp_bn_act_bwd_reduce");
 }
 
@@ -559,9 +626,13 @@ extern "C" int dp_bn_act_bwd_apply(void* dz1, int64_t ld_dz1, void* dz2, int64_t
              "dp_bn_act_bwd_apply: bad arguments");
   const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
   const RC g = rc_grid(rows, c);
-  DP_DT(hipLaunchKernelGGL(bn_act_bwd_apply_kernel<T>, g.grid, g.block, 0, as_stream(stream), (T*)dz1, ld_dz1,
-                           (T*)(z2 ? dz2 : nullptr), ld_dz2, (const T*)dy, ld_dy, p1, p2, rows, c, act, sums,
-                           1.f / count));
+  if (z2)
+    DP_DT(hipLaunchKernelGGL((bn_act_bwd_apply_kernel<T, true>), g.grid, g.block, 0, as_stream(stream), (T*)dz1,
+                             ld_dz1, (T*)dz2, ld_dz2, (const T*)dy, ld_dy, p1, p2, rows, c, act, sums, 1.f / count));
+  else
+    DP_DT(hipLaunchKernelGGL((bn_act_bwd_apply_kernel<T, false>), g.grid, g.block, 0, as_stream(stream), (T*)dz1,
+                             ld_dz1, (T*)nullptr, ld_dz2, (const T*)dy, ld_dy, p1, p2, rows, c, act, sums,
+                             1.f / count));
   return dp_check_launch("dp_bn_act_bwd_apply");
 }
 
@@ -638,8 +709,15 @@ extern "C" int dp_axpby_rows(void* y, int64_t ld_y, const void* a, int64_t ld_a,
                          dtype, stream);
   }
   const RC g = rc_grid(rows, c);
-  DP_DT(hipLaunchKernelGGL(axpby_kernel<T>, g.grid, g.block, 0, as_stream(stream), (T*)y, ld_y, (const T*)a, ld_a, alpha,
-                           (const T*)b, ld_b, beta, rows, c, accumulate));
+#define AXP(HB_, AC_)                                                                                            \
+  DP_DT(hipLaunchKernelGGL((axpby_kernel<T, HB_, AC_>), g.grid, g.block, 0, as_stream(stream), (T*)y, ld_y,          \
+                           (const T*)a, ld_a, alpha, (const T*)b, ld_b, beta, rows, c))
+  if (b) {
+    if (accumulate) AXP(true, true); else AXP(true, false);
+  } else {
+    if (accumulate) AXP(false, true); else AXP(false, false);
+  }
+#undef AXP
   return dp_check_launch("dp_axpby_rows");
 }
 

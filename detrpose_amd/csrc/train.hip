@@ -378,12 +378,12 @@ __global__ void gate_fwd_kernel(const T* __restrict__ G, const T* __restrict__ x
   const int j = blockIdx.y * blockDim.x + threadIdx.x;
   if (j >= c) return;
   for (int r = blockIdx.x; r < rows; r += gridDim.x) {
-  const int64_t e = (int64_t)r * c + j;
-  const int64_t b2 = (int64_t)r * 2 * c;
-  const float g1 = sigmoidf_(to_f32(G[b2 + j])), g2 = sigmoidf_(to_f32(G[b2 + c + j]));
-  gs[b2 + j] = from_f32<T>(g1);
-  gs[b2 + c + j] = from_f32<T>(g2);
-  z[e] = from_f32<T>(g1 * to_f32(xcat[b2 + j]) + g2 * to_f32(xcat[b2 + c + j]));
+    const int64_t e = (int64_t)r * c + j;
+    const int64_t b2 = (int64_t)r * 2 * c;
+    const float g1 = sigmoidf_(to_f32(G[b2 + j])), g2 = sigmoidf_(to_f32(G[b2 + c + j]));
+    gs[b2 + j] = from_f32<T>(g1);
+    gs[b2 + c + j] = from_f32<T>(g2);
+    z[e] = from_f32<T>(g1 * to_f32(xcat[b2 + j]) + g2 * to_f32(xcat[b2 + c + j]));
   }
 }
 
@@ -393,21 +393,23 @@ __global__ void gate_bwd_kernel(const T* __restrict__ dz, const T* __restrict__ 
   const int j = blockIdx.y * blockDim.x + threadIdx.x;
   if (j >= c) return;
   for (int r = blockIdx.x; r < rows; r += gridDim.x) {
-  const int64_t e = (int64_t)r * c + j;
-  const int64_t b2 = (int64_t)r * 2 * c;
-  const float d = to_f32(dz[e]);
-  const float g1 = to_f32(gs[b2 + j]), g2 = to_f32(gs[b2 + c + j]);
-  const float x1 = to_f32(xcat[b2 + j]), x2 = to_f32(xcat[b2 + c + j]);
-  dG[b2 + j] = from_f32<T>(d * x1 * g1 * (1.f - g1));
-  dG[b2 + c + j] = from_f32<T>(d * x2 * g2 * (1.f - g2));
-  dx[b2 + j] = from_f32<T>(d * g1);
-  dx[b2 + c + j] = from_f32<T>(d * g2);
+    const int64_t e = (int64_t)r * c + j;
+    const int64_t b2 = (int64_t)r * 2 * c;
+    const float d = to_f32(dz[e]);
+    const float g1 = to_f32(gs[b2 + j]), g2 = to_f32(gs[b2 + c + j]);
+    const float x1 = to_f32(xcat[b2 + j]), x2 = to_f32(xcat[b2 + c + j]);
+    dG[b2 + j] = from_f32<T>(d * x1 * g1 * (1.f - g1));
+    dG[b2 + c + j] = from_f32<T>(d * x2 * g2 * (1.f - g2));
+    dx[b2 + j] = from_f32<T>(d * g1);
+    dx[b2 + c + j] = from_f32<T>(d * g2);
   }
 }
 
+// (row slices, channel blocks): about 512 K threads (8 waves per SIMD), so the per-thread row walk
+// stays short
 dim3 rows_grid(int rows, int c, dim3* block) {
   const int bx = c >= 256 ? 256 : (c + 63) / 64 * 64, gy = (c + bx - 1) / bx;
-  int gx = (1 << 16) / (bx * gy);
+  int gx = (1 << 19) / (bx * gy);
   if (gx > rows) gx = rows;
   if (gx < 1) gx = 1;
   *block = dim3((unsigned)bx);
