@@ -58,7 +58,24 @@ __device__ __forceinline__ void load_tile(TileRegs<TI>& t, const Operand& op, in
   constexpr int BK = GemmTraits<TI>::BK, VEC = GemmTraits<TI>::VEC;
   const TI* p = reinterpret_cast<const TI*>(op.p) + base;
   const int tid = threadIdx.x;
-  if (mode == 0) {
+  // a tile wholly inside the operand (block-uniform test): both chunks load unguarded, back to
+  // back (a per-lane guard makes a branch around each load, and the loads issue one at a time)
+  const bool interior = mode < 2 && r0 + TM <= op.rows && k0 + BK <= K;
+  if (interior && mode == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / (BK / VEC), kc = (c % (BK / VEC)) * VEC;
+      *reinterpret_cast<uint4*>(&t.v[i * VEC]) = *reinterpret_cast<const uint4*>(p + (int64_t)(r0 + r) * op.rs + k0 + kc);
+    }
+  } else if (interior) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int kk = c / (TM / VEC), rc = (c % (TM / VEC)) * VEC;
+      *reinterpret_cast<uint4*>(&t.v[i * VEC]) = *reinterpret_cast<const uint4*>(p + (int64_t)(k0 + kk) * op.ks + r0 + rc);
+    }
+  } else if (mode == 0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + 256 * i;
@@ -275,6 +292,15 @@ __device__ __forceinline__ void load_tile2(Tile2Regs& t, const Operand& op, int 
                                            int K) {
   const bf16_t* p = reinterpret_cast<const bf16_t*>(op.p) + base;
   const int tid = threadIdx.x;
+  if (r0 + BT <= op.rows && k0 + BKB <= K) {   // interior tile (block-uniform): unguarded loads
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      t.v[i] = mode == 0 ? *reinterpret_cast<const uint4*>(p + (int64_t)(r0 + (c >> 3)) * op.rs + k0 + (c & 7) * 8)
+                         : *reinterpret_cast<const uint4*>(p + (int64_t)(k0 + (c >> 4)) * op.ks + r0 + (c & 15) * 8);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i;
@@ -333,6 +359,8 @@ __device__ __forceinline__ bf16x8 frag2(const bf16_t* img, int mode, int r0, int
   return *reinterpret_cast<const bf16x8*>(t8);
 }
 
+// MA / MB: the operands' modes as compile-time constants (no branch in the fragment reads)
+template <int MA, int MB>
 __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem128[];   // [buffer][A | B][IMG]
   bf16_t(*sm)[2][IMG] = reinterpret_cast<bf16_t(*)[2][IMG]>(smem128);
@@ -355,18 +383,18 @@ __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
   const int KC = ke - kb;
   Tile2Regs ra, rb;
   if (KC > 0) {
-    load_tile2(ra, A, g.modeA, aoff, m0, 0, KC);
-    load_tile2(rb, B, g.modeB, boff, n0, 0, KC);
-    store_tile2(ra, sm[0][0], g.modeA);
-    store_tile2(rb, sm[0][1], g.modeB);
+    load_tile2(ra, A, MA, aoff, m0, 0, KC);
+    load_tile2(rb, B, MB, boff, n0, 0, KC);
+    store_tile2(ra, sm[0][0], MA);
+    store_tile2(rb, sm[0][1], MB);
   }
   __syncthreads();
   int cur = 0;
   for (int k0 = 0; k0 < KC; k0 += BKB) {
     const bool more = k0 + BKB < KC;
     if (more) {
-      load_tile2(ra, A, g.modeA, aoff, m0, k0 + BKB, KC);
-      load_tile2(rb, B, g.modeB, boff, n0, k0 + BKB, KC);
+      load_tile2(ra, A, MA, aoff, m0, k0 + BKB, KC);
+      load_tile2(rb, B, MB, boff, n0, k0 + BKB, KC);
     }
     const bf16_t* Ai = sm[cur][0];
     const bf16_t* Bi = sm[cur][1];
@@ -374,17 +402,17 @@ __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
     for (int ks = 0; ks < BKB / 32; ++ks) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag2(Ai, g.modeA, wm + 16 * i, 32 * ks);
+      for (int i = 0; i < 4; ++i) af[i] = frag2(Ai, MA, wm + 16 * i, 32 * ks);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag2(Bi, g.modeB, wn + 16 * j, 32 * ks);
+      for (int j = 0; j < 4; ++j) bfr[j] = frag2(Bi, MB, wn + 16 * j, 32 * ks);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (more) {   // the other buffer's readers passed the previous iteration's barrier
-      store_tile2(ra, sm[cur ^ 1][0], g.modeA);
-      store_tile2(rb, sm[cur ^ 1][1], g.modeB);
+      store_tile2(ra, sm[cur ^ 1][0], MA);
+      store_tile2(rb, sm[cur ^ 1][1], MB);
     }
     __syncthreads();
     cur ^= 1;
@@ -482,8 +510,12 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
     splits = d.split_k;
   } else if (tiles < 512 && ksteps >= 8 && d.out_dtype == DP_F32 && !d.bias && d.act == DP_ACT_NONE && !d.gate &&
              d.beta == 1.f) {
-    splits = (int)((512 + tiles - 1) / tiles);
-    if (splits > ksteps / 4) splits = ksteps / 4;
+    // 128 x 128 tiles: ~512 blocks (more splits only add atomics); 64 x 64 tiles (small M, the
+    // stage-0/1 convs' weight gradients): ~4096 blocks, measured 535 -> 400 us (M 48, K 409600)
+    // and 463 -> 312 us (M 96, K 102400) over the 512 target (scripts/gemm_bench.py)
+    const int target = big ? 512 : 4096, kmin = big ? 4 : 8;
+    splits = (int)((target + tiles - 1) / tiles);
+    if (splits > ksteps / kmin) splits = ksteps / kmin;
     if (splits < 1) splits = 1;
   }
   if (splits > ksteps) splits = ksteps;
@@ -496,11 +528,20 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
   hipStream_t s = as_stream(stream);
   if (big) {
     constexpr size_t lds = sizeof(bf16_t) * 4 * IMG;   // 72 KB: two buffers of both operands
-    static const bool attr_ok =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm128_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) == hipSuccess;
+    static const bool attr_ok = [] {
+      bool ok = true;
+      for (const void* k : {reinterpret_cast<const void*>(&gemm128_kernel<0, 0>),
+                            reinterpret_cast<const void*>(&gemm128_kernel<0, 1>),
+                            reinterpret_cast<const void*>(&gemm128_kernel<1, 0>),
+                            reinterpret_cast<const void*>(&gemm128_kernel<1, 1>)})
+        ok = ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+      return ok;
+    }();
     DP_REQUIRE(attr_ok, "dp_gemm: cannot set the 128x128 kernel's LDS size");
-    hipLaunchKernelGGL(gemm128_kernel, grid, block, lds, s, g);
+    if (g.modeA == 0 && g.modeB == 0) hipLaunchKernelGGL((gemm128_kernel<0, 0>), grid, block, lds, s, g);
+    else if (g.modeA == 0) hipLaunchKernelGGL((gemm128_kernel<0, 1>), grid, block, lds, s, g);
+    else if (g.modeB == 0) hipLaunchKernelGGL((gemm128_kernel<1, 0>), grid, block, lds, s, g);
+    else hipLaunchKernelGGL((gemm128_kernel<1, 1>), grid, block, lds, s, g);
   }
   else if (d.in_dtype == DP_BF16)
     hipLaunchKernelGGL(gemm_kernel<bf16_t>, grid, block, 0, s, g);

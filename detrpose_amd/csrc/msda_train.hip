@@ -272,6 +272,10 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_cl_kernel(const T* __restr
   const float rx = ref[2 * r], ry = ref[2 * r + 1];
   float dot = 0.f, grx = 0.f, gry = 0.f;
   float* gvb = gvalue + (int64_t)b * S * C + ch;
+  // unrolled, with every corner load unconditional (index clamped into the map, value selected
+  // away outside it): a guarded load compiles to a branch around it, and the points' loads then
+  // issue one at a time
+#pragma unroll 4
   for (int j = 0; j < LP; ++j) {
     const int l = j / P;
     const int H = lv.h[l], W = lv.w[l];
@@ -288,8 +292,10 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_cl_kernel(const T* __restr
     for (int k = 0; k < 4; ++k) {
       const int xi = x0 + (k & 1), yi = y0 + (k >> 1);
       const bool ok = xi >= 0 && xi < W && yi >= 0 && yi < H;
-      row[k] = ok ? lv.start[l] + yi * W + xi : -1;
-      v[k] = ok ? to_f32(vb[(int64_t)row[k] * C]) : 0.f;
+      const int rc = lv.start[l] + min(max(yi, 0), H - 1) * W + min(max(xi, 0), W - 1);
+      const float vv = to_f32(vb[(int64_t)rc * C]);
+      row[k] = ok ? rc : -1;
+      v[k] = ok ? vv : 0.f;
     }
     const float sv = wk[0] * v[0] + wk[1] * v[1] + wk[2] * v[2] + wk[3] * v[3];
     float ga = go * sv;
