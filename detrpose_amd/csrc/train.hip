@@ -3,6 +3,8 @@
 // OKS-denoising queries. The Linear layers are dp_gemm (gemm.hip); the MSDA module is
 // dp_msda / dp_msda_bwd (msda.hip, msda_train.hip). Reference lines on each entry point in
 // include/detrpose_hip.h. f32 math everywhere; activations / activation gradients of dtype.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -124,15 +126,33 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(T* __restrict__ dx, const T
 }
 
 // ---------------------------------------------------------------- column sums (bias grads)
+// A block = (256 / cw) row phases x cw columns (cw = n rounded up to a power of two, at most 256):
+// narrow outputs (the pose heads' 34 / 4 columns) keep the lanes busy; 8 rows per step with the
+// loads issued together; the block's phases are summed through LDS, one atomic per column.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, int64_t ld, int rows, int n,
-                                                     float* __restrict__ out, int rows_per) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= n) return;
+                                                     float* __restrict__ out, int rows_per, int cw_log2) {
+  __shared__ float red[256];
+  const int cw = 1 << cw_log2, nph = 256 >> cw_log2;
+  const int jl = threadIdx.x & (cw - 1), ph = threadIdx.x >> cw_log2;
+  const int j = blockIdx.x * cw + jl;
+  const int jc = min(j, n - 1);
   const int r0 = blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
   float acc = 0.f;
-  for (int r = r0; r < r1; ++r) acc += to_f32(x[(int64_t)r * ld + j]);
-  unsafeAtomicAdd(out + j, acc);
+  for (int r = r0 + ph; r < r1; r += 8 * nph) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = to_f32(x[(int64_t)min(r + u * nph, r1 - 1) * ld + jc]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += r + u * nph < r1 ? v[u] : 0.f;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (ph == 0 && j < n) {
+    float t = 0.f;
+    for (int q = 0; q < nph; ++q) t += red[q * cw + jl];
+    unsafeAtomicAdd(out + j, t);
+  }
 }
 
 // ---------------------------------------------------------------- attention core
@@ -814,13 +834,19 @@ extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, flo
   DP_REQUIRE(x && out && rows > 0 && n > 0 && ld >= n, "dp_colsum: bad arguments");
   hipStream_t st = as_stream(stream);
   if (!accumulate && hipMemsetAsync(out, 0, (size_t)n * 4, st) != hipSuccess) return dp_check_launch("dp_colsum");
-  const int chunks = rows < 256 ? 1 : (rows + 255) / 256 > 512 ? 512 : (rows + 255) / 256;
+  int lg = 0;
+  while ((1 << lg) < n && lg < 8) ++lg;
+  const int cw = 1 << lg, gx = (n + cw - 1) / cw;
+  // about 1024 blocks, each at least 8 row steps of its phases
+  const int nph = 256 / cw;
+  int chunks = std::max(1, std::min((rows + 8 * nph - 1) / (8 * nph), std::max(1, 1024 / gx)));
   const int per = (rows + chunks - 1) / chunks;
-  dim3 grid(nblk(n, 256), (unsigned)chunks);
+  chunks = (rows + per - 1) / per;
+  dim3 grid((unsigned)gx, (unsigned)chunks);
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, ld, rows, n, out, per);
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, ld, rows, n, out, per, lg);
   else
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)x, ld, rows, n, out, per);
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)x, ld, rows, n, out, per, lg);
   return dp_check_launch("dp_colsum");
 }
 

@@ -38,7 +38,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import DP_BF16, DP_F32, GemmDesc, contiguous_rows, rowmap
+from ._lib import DP_BF16, DP_F32, ConvDesc, GemmDesc, contiguous_rows, rowmap
 from .criterion import COCO_SIGMAS, CROWDPOSE_SIGMAS, pack_targets
 from .transformer import weighting_function
 
@@ -298,6 +298,44 @@ class TrainEngine:
         tape.op(name, self.lib.dp_gemm, C.byref(d))
         self.cur.cost(name, 2.0 * batch * m * n * k)
 
+    @staticmethod
+    def _rows_ok(ptr, ld):
+        """A bf16 row operand the 1x1 conv kernel takes: 16-byte aligned rows."""
+        return ptr % 16 == 0 and ld % 8 == 0
+
+    def _conv1x1(self, tape, name, x, ldx, rows, w, kpad, cin, cout, out, ldo, bias, act, res=False):
+        """out = act(x W^T + bias) [+ out] on the 1x1 conv kernel (conv_stream: weight-stationary
+        MFMA tiles streaming the rows), W packed [cout][kpad] bf16; the rows are one image of
+        1 x rows pixels. ~10x dp_gemm's rate on the decoder's linears (scripts/gemm_bench.py)."""
+        d = ConvDesc()
+        d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = x, rows * ldx, ldx, 1, rows, cin
+        d.weight, d.kpad, d.bias = w, kpad, bias
+        d.kh, d.kw, d.stride, d.pad_t, d.pad_l = 1, 1, 1, 0, 0
+        d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = out, rows * ldo, ldo, 1, rows, cout
+        if res:   # out += ...: the residual read and the store are the same element of the same thread
+            d.res, d.res_bstride, d.res_pstride = out, rows * ldo, ldo
+        d.batch, d.act, d.dtype = 1, act, DP_BF16
+        tape.keep.append(d)
+        tape.op(name, self.lib.dp_conv2d, C.byref(d))
+        self.cur.cost(name, 2.0 * rows * cin * cout)
+
+    def _wt_pack(self, wkey):
+        """W^T of a linear's weight packed [K][pad64(N)] bf16 (dp_conv_pack mode 1 of the f32
+        master): the input-gradient conv's weights, re-packed by an op at the end of the current
+        plan's forward tape (after every update the next forward refreshes it)."""
+        if not hasattr(self, "_wts"):
+            self._wts, self._wt_ops = {}, set()
+        N, K = self.sd32[wkey].shape
+        if wkey not in self._wts:
+            kpad = (N + 63) // 64 * 64
+            self._wts[wkey] = (torch.zeros(K, kpad, dtype=torch.bfloat16, device=self.device), kpad)
+        t, kpad = self._wts[wkey]
+        if (id(self.cur), wkey) not in self._wt_ops:
+            self._wt_ops.add((id(self.cur), wkey))
+            self.cur.fw.op(f"pack.{wkey}.T", self.lib.dp_conv_pack, _p(self.sd32[wkey]), N, K, 1, 1, _p(t), kpad, N, 1,
+                           None, DP_BF16)
+        return t, kpad
+
     def lin(self, tape, name, x, ldx, rows, wkey, out, ldo, act=0, out_code=None, bias=True, beta=0.0, wt=None,
             in_code=None):
         """out = act(x W^T + b): nn.Linear forward."""
@@ -305,6 +343,13 @@ class TrainEngine:
         N, K = W.shape
         bk = wkey[:-len("weight")] + "bias"
         b = self.sd32.get(bk) if bias else None
+        ic = self.code if in_code is None else in_code
+        oc = self.code if out_code is None else out_code
+        if (ic == oc == DP_BF16 and K % 64 == 0 and W.is_contiguous() and self._rows_ok(x, ldx) and
+                self._rows_ok(out, ldo) and act in (0, 1) and (beta == 0.0 or (beta == 1.0 and act == 0))):
+            self._conv1x1(tape, name, x, ldx, rows, _p(W), K, K, N, out, ldo,
+                          _p(b) if b is not None else None, act, res=beta == 1.0)
+            return
         self._gemm(tape, name, x, ldx, 1, _p(W), 1, K, out, ldo, rows, N, K, self.code if in_code is None else in_code,
                    self.code if out_code is None else out_code, bias=_p(b) if b is not None else None, beta=beta,
                    act=act)
@@ -315,6 +360,14 @@ class TrainEngine:
         W = self.w[wkey] if wt is None else wt
         N, K = W.shape
         code = self.code if in_code is None else in_code
+        gc = self.code if gate_code is None else gate_code
+        if (code == DP_BF16 and wt is None and wkey in self.sd32 and N % 8 == 0 and self._rows_ok(dy, ldy) and self._rows_ok(dx, ldx) and
+                (beta == 0.0 or (beta == 1.0 and gate is None)) and (gate is None or gc == DP_BF16)):
+            Wt, kpad = self._wt_pack(wkey)
+            self._conv1x1(tape, name, dy, ldy, rows, _p(Wt), kpad, N, K, dx, ldx, None, 0, res=beta == 1.0)
+            if gate is not None:   # relu'(gate): the mask applied in place
+                tape.op(name + ".mask", self.lib.dp_act_bwd, gate, ld_gate, dx, ldx, dx, ldx, rows, K, 1, code)
+            return
         self._gemm(tape, name, dy, ldy, 1, _p(W), K, 1, dx, ldx, rows, K, N, code, code, beta=beta, gate=gate,
                    gate_rs=ld_gate, gate_code=gate_code)
 
