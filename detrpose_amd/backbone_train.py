@@ -241,7 +241,7 @@ class BackboneTrainPlan(TapePlan):
                 self._dgrad_conv(bw, name, dz, wb, kpad2, x, k, k - 1 - pad)
             else:   # strided dense conv (stem3): dcol = dz W, then col2im
                 dcol = self._dcolbuf(out.rows * K)
-                self.gemm(bw, name + ".dcol", dz.xp, dz.ld, 1, self.wptr(wkey), K, 1, _p(dcol), K, out.rows, K, cout)
+                self._dcol_conv(bw, name, dz, cout, wkey, dcol, K, out.rows)
                 bw.op(name + ".col2im", lib.dp_col2im, _p(dcol), B, H, W_, cin, k, k, stride, pad, oh, ow, x.gp,
                       H * W_ * x.ld, x.ld, 1, self.code)
         self._bwd.append(bwd)
@@ -259,6 +259,29 @@ class BackboneTrainPlan(TapePlan):
         bw.keep.append(dd)
         bw.op(name + ".dx", self.lib.dp_conv2d, C.byref(dd))
         self.cost(name + ".dx", 2.0 * x.rows * x.c * k * k * dz.c)
+
+    def _dcol_conv(self, bw, name, dz, cout, wkey, dcol, K, rows):
+        """dcol = dz W ([rows][cout] x [cout][cin*kh*kw]) on the 1x1 conv kernel: W^T packed
+        [K][pad64(cout)] (dp_conv_pack mode 1 of the weight read as a (cout, K, 1, 1) linear)."""
+        key = (wkey, "T")
+        if key not in self._packs:
+            w = self.eng.params[wkey]
+            kpad = pad_to(cout, 64)
+            t = torch.zeros(K, kpad, dtype=self.dt, device=self.dev)
+            self.arena.append(t)
+            self._packs[key] = (t, kpad)
+            self.fw.op(f"pack.{wkey}.T", self.lib.dp_conv_pack, _p(w), cout, K, 1, 1, _p(t), kpad, cout, 1, None,
+                       self.code)
+        t, kpad = self._packs[key]
+        d = ConvDesc()
+        d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = dz.xp, rows * dz.ld, dz.ld, 1, rows, cout
+        d.weight, d.kpad, d.bias = _p(t), kpad, None
+        d.kh, d.kw, d.stride, d.pad_t, d.pad_l = 1, 1, 1, 0, 0
+        d.out, d.out_bstride, d.out_pstride, d.out_h, d.out_w, d.cout = _p(dcol), rows * K, K, 1, rows, K
+        d.batch, d.act, d.dtype = 1, _lib.DP_ACT_NONE, self.code
+        bw.keep.append(d)
+        bw.op(name + ".dcol", self.lib.dp_conv2d, C.byref(d))
+        self.cost(name + ".dcol", 2.0 * rows * cout * K)
 
     def _dz(self, rows, cp):
         """d conv-output of one layer's backward: a view of one shared buffer (the layers'
