@@ -127,6 +127,8 @@ _SIGS = {
     "dp_gemm": (i32, [C.POINTER(GemmDesc), vp]),
     "dp_ln_fwd": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp, i32, i32, i32, vp]),
     "dp_ln_bwd": (i32, [vp, vp, i32, vp, vp, vp, i32, i32, vp, vp, i32, i32, vp]),
+    "dp_conv_wgrad": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                            i32, vp]),
     "dp_colsum": (i32, [vp, i64, i32, i32, vp, i32, i32, vp]),
     "dp_attn_fwd": (i32, [vp, i32, vp, vp, i32, vp, i32, vp, vp, i32, i32, i64, i64, i64, i32, i32, i32, i32, vp]),
     "dp_attn_bwd": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, i64, i64, i64, i32, i32,

@@ -231,11 +231,7 @@ class BackboneTrainPlan(TapePlan):
                 self._dgrad_conv(bw, name, dz, wb, kpad2, x, 1, 0)
                 return
             K = cin * k * k
-            col = self._colbuf(out.rows * K)
-            bw.op(name + ".im2col", lib.dp_im2col, x.xp, H * W_ * x.ld, x.ld, 1, B, H, W_, cin, k, k, stride, pad, oh,
-                  ow, _p(col), self.code, self.code)
-            self.gemm(bw, name + ".dW", dz.xp, 1, dz.ld, _p(col), K, 1, _p(G), K, cout, K, out.rows, out_code=DP_F32,
-                      beta=1.0)
+            self.wgrad_kxk(bw, name, x.xp, x.ld, B, H, W_, cin, dz.xp, dz.ld, oh, ow, cout, k, stride, pad, G)
             if stride == 1:
                 wb, kpad2 = self.packed(wkey, 1, dz.cp, x.cp)
                 self._dgrad_conv(bw, name, dz, wb, kpad2, x, k, k - 1 - pad)

@@ -156,6 +156,11 @@ struct GemmArgs {
   int gate_bf16;
   int modeA, modeB;
   int tiles_n;
+  // B operand mode 3 (dp_conv_wgrad): B(k = output pixel p, n = tap * cin + ci) = x at the
+  // tap's input pixel of p (zero outside the map) -- im2col on the fly
+  const bf16_t* ix;
+  int64_t ix_bs;
+  int ix_ps, ih, iw, icin, ioh, iow, ikw, istride, ipad;
 };
 
 template <typename TI>
@@ -331,6 +336,29 @@ __device__ __forceinline__ void load_tile2(Tile2Regs& t, const Operand& op, int 
   }
 }
 
+// B tile of mode 3: k rows kabs .. kabs+63 (output pixels), n columns n0 .. n0+127 (tap-major:
+// n = tap * cin + ci; cin % 8 == 0 so a 16-byte chunk is 8 channels of one tap). Every load is
+// issued (address clamped into the map), the chunk zeroed where the tap falls outside it.
+__device__ __forceinline__ void load_tile_im(Tile2Regs& t, const GemmArgs& g, int kabs, int n0, int kend) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    const int p = kabs + (c >> 4), n = n0 + (c & 15) * 8;
+    const int pc = min(p, kend - 1);
+    const int ox = pc % g.iow, t2 = pc / g.iow;
+    const int oy = t2 % g.ioh, b = t2 / g.ioh;
+    const int tap = n / g.icin, ci = n - tap * g.icin;
+    const int ky = tap / g.ikw, kx = tap - ky * g.ikw;
+    const int y = oy * g.istride - g.ipad + ky, x = ox * g.istride - g.ipad + kx;
+    const bool ok = p < kend && n < g.N && (unsigned)y < (unsigned)g.ih && (unsigned)x < (unsigned)g.iw;
+    const int yc = min(max(y, 0), g.ih - 1), xc = min(max(x, 0), g.iw - 1);
+    const int cic = n < g.N ? ci : 0;
+    const uint4 v = *reinterpret_cast<const uint4*>(g.ix + (int64_t)b * g.ix_bs + ((int64_t)yc * g.iw + xc) * g.ix_ps + cic);
+    t.v[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
+  }
+}
+
 __device__ __forceinline__ void store_tile2(const Tile2Regs& t, bf16_t* img, int mode) {
   const int tid = threadIdx.x;
   char* b = reinterpret_cast<char*>(img);
@@ -384,9 +412,10 @@ __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
   Tile2Regs ra, rb;
   if (KC > 0) {
     load_tile2(ra, A, MA, aoff, m0, 0, KC);
-    load_tile2(rb, B, MB, boff, n0, 0, KC);
+    if constexpr (MB == 3) load_tile_im(rb, g, kb, n0, ke);
+    else load_tile2(rb, B, MB, boff, n0, 0, KC);
     store_tile2(ra, sm[0][0], MA);
-    store_tile2(rb, sm[0][1], MB);
+    store_tile2(rb, sm[0][1], MB == 3 ? 1 : MB);
   }
   __syncthreads();
   int cur = 0;
@@ -394,7 +423,8 @@ __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
     const bool more = k0 + BKB < KC;
     if (more) {
       load_tile2(ra, A, MA, aoff, m0, k0 + BKB, KC);
-      load_tile2(rb, B, MB, boff, n0, k0 + BKB, KC);
+      if constexpr (MB == 3) load_tile_im(rb, g, kb + k0 + BKB, n0, ke);
+      else load_tile2(rb, B, MB, boff, n0, k0 + BKB, KC);
     }
     const bf16_t* Ai = sm[cur][0];
     const bf16_t* Bi = sm[cur][1];
@@ -404,7 +434,7 @@ __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = frag2(Ai, MA, wm + 16 * i, 32 * ks);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag2(Bi, MB, wn + 16 * j, 32 * ks);
+      for (int j = 0; j < 4; ++j) bfr[j] = frag2(Bi, MB == 3 ? 1 : MB, wn + 16 * j, 32 * ks);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -412,7 +442,7 @@ __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
     }
     if (more) {   // the other buffer's readers passed the previous iteration's barrier
       store_tile2(ra, sm[cur ^ 1][0], MA);
-      store_tile2(rb, sm[cur ^ 1][1], MB);
+      store_tile2(rb, sm[cur ^ 1][1], MB == 3 ? 1 : MB);
     }
     __syncthreads();
     cur ^= 1;
@@ -454,6 +484,18 @@ int operand_mode(const Operand& op, int vec, int64_t align_bytes_ok) {
   if (op.ks == 1 && op.rs % vec == 0 && align_bytes_ok) return 0;
   if (op.rs == 1 && op.ks % vec == 0 && align_bytes_ok) return 1;
   return 2;
+}
+
+
+// dw[co][ci][tap] += s[co][tap][ci] (the reference's [cout][cin][kh][kw] from the tap-major sums)
+__global__ void wgrad_permute_kernel(const float* __restrict__ s, float* __restrict__ dw, int cout, int cin, int taps) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over dw
+  const int64_t total = (int64_t)cout * cin * taps;
+  if (e >= total) return;
+  const int tap = (int)(e % taps);
+  const int64_t r = e / taps;
+  const int ci = (int)(r % cin), co = (int)(r / cin);
+  dw[e] += s[((int64_t)co * taps + tap) * cin + ci];
 }
 
 }  // namespace
@@ -548,4 +590,59 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
   else
     hipLaunchKernelGGL(gemm_kernel<float>, grid, block, 0, s, g);
   return dp_check_launch("dp_gemm");
+}
+
+extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride, int32_t batch, int32_t h,
+                             int32_t w, int32_t cin, const void* dz, int64_t dz_ld, int32_t oh, int32_t ow,
+                             int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad, float* scratch,
+                             float* dw, int32_t dtype, void* stream) {
+  DP_REQUIRE(x && dz && scratch && dw && batch > 0 && h > 0 && w > 0 && oh > 0 && ow > 0 && cout > 0 && kh > 0 &&
+                 kw > 0 && stride > 0 && pad >= 0,
+             "dp_conv_wgrad: bad arguments");
+  DP_REQUIRE(dtype == DP_BF16 && cin % 8 == 0 && x_pstride % 8 == 0 && x_bstride % 8 == 0 && dz_ld % 8 == 0 &&
+                 (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(dz) & 15) == 0,
+             "dp_conv_wgrad: bf16, cin %% 8 == 0, 16-byte aligned pixels (cin %d, pstride %d, ld %lld)", cin,
+             x_pstride, (long long)dz_ld);
+  const int64_t K = (int64_t)batch * oh * ow;
+  DP_REQUIRE(K < (1ll << 31), "dp_conv_wgrad: too many pixels");
+  hipStream_t s = as_stream(stream);
+  const int taps = kh * kw, N = taps * cin;
+  if (hipMemsetAsync(scratch, 0, (size_t)cout * N * sizeof(float), s) != hipSuccess) {
+    dp_set_error("dp_conv_wgrad: memset failed");
+    return DP_EINVAL;
+  }
+  GemmArgs g{};
+  g.A = Operand{dz, 0, 1, dz_ld, cout};   // A(m = co, k = p) = dz[p][co]: rows contiguous (mode 1)
+  g.B = Operand{x, 0, 0, 0, N};
+  g.modeA = 1;
+  g.modeB = 3;
+  g.cf = scratch;
+  g.cb = nullptr;
+  g.c_bs = 0;
+  g.c_rs = N;
+  g.M = cout, g.N = N, g.K = (int)K, g.batch = 1;
+  g.alpha = 1.f;
+  g.beta = 1.f;
+  g.act = DP_ACT_NONE;
+  g.ix = reinterpret_cast<const bf16_t*>(x);
+  g.ix_bs = x_bstride;
+  g.ix_ps = x_pstride;
+  g.ih = h, g.iw = w, g.icin = cin, g.ioh = oh, g.iow = ow, g.ikw = kw, g.istride = stride, g.ipad = pad;
+  const int tm = (cout + BT - 1) / BT, tn = (N + BT - 1) / BT;
+  g.tiles_n = tn;
+  const int ksteps = (int)((K + BKB - 1) / BKB);
+  int splits = (512 + tm * tn - 1) / (tm * tn);
+  if (splits > ksteps / 4) splits = ksteps / 4;
+  if (splits < 1) splits = 1;
+  g.splits = splits;
+  g.kchunk = ((ksteps + splits - 1) / splits) * BKB;
+  constexpr size_t lds = sizeof(bf16_t) * 4 * IMG;
+  static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm128_kernel<1, 3>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+  DP_REQUIRE(attr_ok, "dp_conv_wgrad: cannot set the kernel's LDS size");
+  hipLaunchKernelGGL((gemm128_kernel<1, 3>), dim3((unsigned)(tm * tn), (unsigned)splits), dim3(256), lds, s, g);
+  const int64_t total = (int64_t)cout * N;
+  hipLaunchKernelGGL(wgrad_permute_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, scratch, dw, cout,
+                     cin, taps);
+  return dp_check_launch("dp_conv_wgrad");
 }

@@ -250,14 +250,26 @@ class TapePlan:
                 self.gemm(self.bw, name + ".dW", z.gp, 1, z.ld, x.xp, x.ld, 1, _p(G), cin, cout, cin, rows,
                           out_code=DP_F32, beta=1.0)
                 return
-            K = cin * k * k
-            col = self._colbuf(rows * K)
-            self.bw.op(name + ".im2col", lib.dp_im2col, x.xp, H * W * x.ld, x.ld, 1, B, H, W, cin, k, k, 1, k // 2, H,
-                       W, _p(col), self.code, self.code)
-            self.gemm(self.bw, name + ".dW", z.gp, 1, z.ld, _p(col), K, 1, _p(G), K, cout, K, rows, out_code=DP_F32,
-                      beta=1.0)
+            self.wgrad_kxk(self.bw, name, x.xp, x.ld, B, H, W, cin, z.gp, z.ld, H, W, cout, k, 1, k // 2, G)
         self._bwd.append(bwd)
         return z
+
+    def wgrad_kxk(self, bw, name, xp, x_ld, B, H, W, cin, dzp, dz_ld, oh, ow, cout, k, stride, pad, G):
+        """dW += the k x k conv's weight gradient: bf16 with 8-channel pixels on dp_conv_wgrad
+        (implicit GEMM, no im2col columns), else dp_im2col + dp_gemm (dz^T col)."""
+        lib = self.lib
+        if self.code == DP_BF16 and cin % 8 == 0 and x_ld % 8 == 0 and dz_ld % 8 == 0:
+            scratch = self.f32(cout * cin * k * k)
+            bw.op(name + ".dW", lib.dp_conv_wgrad, xp, H * W * x_ld, x_ld, B, H, W, cin, dzp, dz_ld, oh, ow, cout, k, k,
+                  stride, pad, _p(scratch), _p(G), self.code)
+            self.cost(name + ".dW", 2.0 * B * oh * ow * cout * cin * k * k)
+            return
+        K = cin * k * k
+        rows = B * oh * ow
+        col = self._colbuf(rows * K)
+        bw.op(name + ".im2col", lib.dp_im2col, xp, H * W * x_ld, x_ld, 1, B, H, W, cin, k, k, stride, pad, oh, ow,
+              _p(col), self.code, self.code)
+        self.gemm(bw, name + ".dW", dzp, 1, dz_ld, _p(col), K, 1, _p(G), K, cout, K, rows, out_code=DP_F32, beta=1.0)
 
     def _colbuf(self, n):
         if self._col is None or self._col.numel() < n:

@@ -427,6 +427,18 @@ typedef struct dp_gemm_desc {
 } dp_gemm_desc;
 int dp_gemm(const dp_gemm_desc* d, void* stream);
 
+/* Weight gradient of a dense k x k conv without im2col columns (the training step's 3x3 convs:
+ * ConvNormLayer / VGGBlock, hybrid_encoder.py:56-127; HG_Block's ConvBNAct, hgnetv2.py:82-134):
+ * dw[cout][cin][kh][kw] += sum over output pixels p of dz[p][co] * x[tap's input pixel of p][ci]
+ * (the reference weight layout). The 128 x 128 MFMA GEMM with its B tile gathered from NHWC x per
+ * (pixel, tap, 8 channels) on the fly (zero outside the map), split-K f32 sums into scratch
+ * [cout][kh*kw*cin] (zeroed here), then permuted into dw. x: batch images of h x w pixels
+ * x_pstride apart (x_bstride per image), cin % 8 == 0; dz: batch*oh*ow rows dz_ld apart
+ * (cout used). bf16 only. */
+int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride, int32_t batch, int32_t h, int32_t w,
+                  int32_t cin, const void* dz, int64_t dz_ld, int32_t oh, int32_t ow, int32_t cout, int32_t kh,
+                  int32_t kw, int32_t stride, int32_t pad, float* scratch, float* dw, int32_t dtype, void* stream);
+
 /* y = LayerNorm(x [+ res]) over contiguous rows of c (nn.LayerNorm, eps): writes y, the pre-norm
  * sum s = x + res (if s != NULL; the backward's input) and stats f32 [rows][2] = (mean, rstd);
  * x / res / s rows contiguous, y rows ld_y apart.

@@ -11,7 +11,7 @@ import torch
 import torch.nn.functional as F
 
 from detrpose_amd import _lib
-from detrpose_amd._lib import DP_F32, ConvDesc, GemmDesc
+from detrpose_amd._lib import DP_BF16, DP_F32, ConvDesc, GemmDesc
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -278,3 +278,34 @@ def test_attention_400_tokens(C_, nh):
     torch.cuda.synchronize()
     _close(out, o.detach(), "attn400 fwd")
     _close(d, t.grad, "attn400 bwd")
+
+
+@pytest.mark.parametrize("B,h,w,cin,cout,k,st,pad,xpad", [(2, 17, 12, 48, 48, 3, 1, 1, 0), (2, 20, 20, 64, 130, 3, 2, 1, 8),
+                                                         (3, 9, 13, 96, 96, 3, 1, 1, 16), (2, 10, 11, 16, 24, 2, 1, 0, 0)])
+def test_conv_wgrad_implicit(B, h, w, cin, cout, k, st, pad, xpad):
+    """dp_conv_wgrad (implicit-GEMM weight gradient, the training step's 3x3 / 2x2 convs) vs the
+    fp32 autograd weight gradient on the same bf16-rounded x and dz; padded pixel strides, an
+    M tile past cout, a stride-2 map, StemBlock's right/bottom-padded 2x2 (pad 0, output = input size)."""
+    lib = _lib.load()
+    torch.manual_seed(5)
+    if k == 2:   # F.pad(x, (0, 1, 0, 1)) then a 2x2 valid conv: output h x w
+        oh, ow = h, w
+    else:
+        oh, ow = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
+    ps = cin + xpad
+    x = torch.randn(B, h, w, ps, device=DEV).bfloat16()
+    dz = torch.randn(B * oh * ow, cout + 8, device=DEV).bfloat16()
+    xr = x[..., :cin].float().permute(0, 3, 1, 2).contiguous()
+    wr = torch.zeros(cout, cin, k, k, device=DEV, requires_grad=True)
+    xin = F.pad(xr, (0, 1, 0, 1)) if k == 2 else xr
+    y = F.conv2d(xin, wr, None, st, 0 if k == 2 else pad)
+    assert y.shape[2:] == (oh, ow)
+    y.backward(dz[:, :cout].float().view(B, oh, ow, cout).permute(0, 3, 1, 2))
+    dw = torch.full((cout, cin, k, k), 0.5, device=DEV)   # accumulates
+    scratch = torch.empty(cout * cin * k * k, device=DEV)
+    _lib.check(lib.dp_conv_wgrad(x.data_ptr(), h * w * ps, ps, B, h, w, cin, dz.data_ptr(), cout + 8, oh, ow, cout, k,
+                                 k, st, pad, scratch.data_ptr(), dw.data_ptr(), DP_BF16, _s()), "conv_wgrad")
+    torch.cuda.synchronize()
+    ref = wr.grad + 0.5
+    err = (dw - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-3, err
