@@ -137,6 +137,8 @@ template <typename T>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ x, int64_t xbs, int xps, const T* __restrict__ dout,
                                    int64_t obs, int ops, int h, int w, int c, T* __restrict__ dx, int64_t dbs, int dps,
                                    int64_t total) {
+  // every load unconditional (clamped address, value selected away): the 3x3 neighbourhood of
+  // x and the 2x2 of dout are in flight together
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int ch = (int)(e % c);
@@ -145,25 +147,36 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ x, int64_t xbs, int xps
   const int64_t t = p / w;
   const int py = (int)(t % h), b = (int)(t / h);
   const T* xb = x + (int64_t)b * xbs + ch;
+  float xv[3][3];   // x at rows py-1 .. py+1, columns px-1 .. px+1 (0 past the right / bottom edge)
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dxx = 0; dxx < 3; ++dxx) {
+      const int yy = py - 1 + dy, xx = px - 1 + dxx;
+      const float v = ldf(xb + ((int64_t)min(max(yy, 0), h - 1) * w + min(max(xx, 0), w - 1)) * xps);
+      xv[dy][dxx] = (yy < h && xx < w) ? v : 0.f;   // yy, xx >= 0 wherever a window reads them
+    }
   float acc = 0.f;
-  for (int oy = py - 1; oy <= py; ++oy) {
-    if (oy < 0) continue;
-    for (int ox = px - 1; ox <= px; ++ox) {
-      if (ox < 0) continue;
+#pragma unroll
+  for (int oy = 0; oy < 2; ++oy)
+#pragma unroll
+    for (int ox = 0; ox < 2; ++ox) {
+      // output (py - 1 + oy, px - 1 + ox): window rows oy .. oy+1, columns ox .. ox+1 of xv
+      const int qy = py - 1 + oy, qx = px - 1 + ox;
+      const float g = ldf(dout + (int64_t)b * obs + ((int64_t)max(qy, 0) * w + max(qx, 0)) * ops + ch);
       float best = -INFINITY;
-      int arg = -1;
+      int arg = 0;
+#pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int yy = oy + (q >> 1), xx = ox + (q & 1);
-        const float v = (yy < h && xx < w) ? ldf(xb + ((int64_t)yy * w + xx) * xps) : 0.f;
+        const float v = xv[oy + (q >> 1)][ox + (q & 1)];
         if (v > best) {
           best = v;
           arg = q;
         }
       }
-      if (arg >= 0 && oy + (arg >> 1) == py && ox + (arg & 1) == px)
-        acc += ldf(dout + (int64_t)b * obs + ((int64_t)oy * w + ox) * ops + ch);
+      // this pixel is the window's (1 - oy, 1 - ox) element
+      if (qy >= 0 && qx >= 0 && arg == ((1 - oy) << 1 | (1 - ox))) acc += g;
     }
-  }
   T* o = dx + (int64_t)b * dbs + ((int64_t)py * w + px) * dps + ch;
   *o = from_f32<T>(ldf(o) + acc);
 }
