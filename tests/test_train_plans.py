@@ -53,3 +53,24 @@ def test_every_parameter_gets_a_gradient(size, B):
     assert ep.d_memory.data_ptr() in _pointers(plan.bw)
     assert all(v.buf.g is not None for v in bb.outs)
     assert len(bb.fw.ops) > 100 and len(ep.bw.ops) > 100
+
+
+def test_bf16_tapes_route_to_the_fast_kernels():
+    """bf16 L tapes: the k x k weight gradients run as implicit GEMMs (dp_conv_wgrad; only stem1,
+    over the f32 image, keeps im2col columns), the transformer's linears and their input
+    gradients on the 1x1 conv kernel (dp_gemm keeps the weight gradients)."""
+    from detrpose_amd.train_engine import TrainEngine
+    model, _ = build_model("l", dtype="bf16")
+    eng = TrainEngine(model, "bf16", "cpu", train_backbone=True)
+    bb = eng.backbone_plan(1, 640, 640)
+    shapes = [(v.H, v.W) for v in bb.outs]
+    ep = eng.encoder_plan(1, shapes, feats=bb.outs, feats_plan=bb)
+    plan = eng.plan(1, 36, shapes, memory=ep.memory, d_memory=ep.d_memory)
+    lib = eng.lib
+    names = lambda t, fn: [n for n, f, _ in t.ops if f is fn]   # noqa: E731
+    im2col = names(bb.bw, lib.dp_im2col) + names(ep.bw, lib.dp_im2col)
+    assert im2col == ["stem1.im2col"], im2col
+    assert len(names(bb.bw, lib.dp_conv_wgrad)) >= 15 and len(names(ep.bw, lib.dp_conv_wgrad)) > 10
+    fw_conv = names(plan.fw, lib.dp_conv2d)
+    assert any(n.endswith(".ffn1") for n in fw_conv) and any(n.endswith(".ffn2") for n in fw_conv), fw_conv[:8]
+    assert any(n.endswith(".ffn2.dx") for n in names(plan.bw, lib.dp_conv2d))
