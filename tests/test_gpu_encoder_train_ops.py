@@ -294,7 +294,8 @@ def test_conv_wgrad_implicit(B, h, w, cin, cout, k, st, pad, xpad):
         oh, ow = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
     ps = cin + xpad
     x = torch.randn(B, h, w, ps, device=DEV).bfloat16()
-    dz = torch.randn(B * oh * ow, cout + 8, device=DEV).bfloat16()
+    ldz = (cout + 7) // 8 * 8 + 8   # padded rows (16-byte aligned)
+    dz = torch.randn(B * oh * ow, ldz, device=DEV).bfloat16()
     xr = x[..., :cin].float().permute(0, 3, 1, 2).contiguous()
     wr = torch.zeros(cout, cin, k, k, device=DEV, requires_grad=True)
     xin = F.pad(xr, (0, 1, 0, 1)) if k == 2 else xr
@@ -303,7 +304,7 @@ def test_conv_wgrad_implicit(B, h, w, cin, cout, k, st, pad, xpad):
     y.backward(dz[:, :cout].float().view(B, oh, ow, cout).permute(0, 3, 1, 2))
     dw = torch.full((cout, cin, k, k), 0.5, device=DEV)   # accumulates
     scratch = torch.empty(cout * cin * k * k, device=DEV)
-    _lib.check(lib.dp_conv_wgrad(x.data_ptr(), h * w * ps, ps, B, h, w, cin, dz.data_ptr(), cout + 8, oh, ow, cout, k,
+    _lib.check(lib.dp_conv_wgrad(x.data_ptr(), h * w * ps, ps, B, h, w, cin, dz.data_ptr(), ldz, oh, ow, cout, k,
                                  k, st, pad, scratch.data_ptr(), dw.data_ptr(), DP_BF16, _s()), "conv_wgrad")
     torch.cuda.synchronize()
     ref = wr.grad + 0.5
