@@ -91,7 +91,9 @@ def test_syncbn_two_ranks_equal_one_batch(golden_dir):
         m = res[r]["memory"]
         err = float(np.abs(m - ref["memory"][r:r + 1]).max()) / float(np.abs(ref["memory"]).max())
         print(f"rank {r}: memory rel err {err:.3g}")
-        assert err <= 1e-5
+        # fp32; the batch statistics are f32 atomic sums over row blocks whose order differs
+        # between the two-rank split and the one-process batch (measured 0.3-1.01e-5)
+        assert err <= 3e-5
         for i, d in enumerate(res[r]["dfeat"]):
             e = float(np.abs(d - ref["dfeat"][i][r:r + 1]).max()) / float(np.abs(ref["dfeat"][i]).max())
             print(f"rank {r}: dfeat{i} rel err {e:.3g}")
