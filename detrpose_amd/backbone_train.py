@@ -16,7 +16,7 @@ stored output, LAB scalar gradients, times the frozen scale) gives d conv-output
   1x1            wgrad dp_gemm (dz^T x), dgrad dp_conv2d of dz with the transposed packing
   k x k s1       wgrad dp_im2col + dp_gemm, dgrad dp_conv2d of dz with the rotated weights
                  (stem2a / stem2b read F.pad(0,1,0,1): the rotated conv pads top / left)
-  3x3 s2 dense   StemBlock.stem3: dgrad dp_gemm (dz W) + dp_col2im
+  3x3 s2 dense   StemBlock.stem3: dgrad dz W on the 1x1 conv kernel (columns tap-major) + dp_col2im
   depthwise      dp_dwconv_bwd (3x3 s2 downsample, 5x5 / 3x3 LightConv)
   stem1          wgrad only (the image takes no gradient): dp_im2col over the f32 NCHW image
   max-pool       dp_maxpool2x2_pad_rb_bwd
@@ -237,7 +237,7 @@ class BackboneTrainPlan(TapePlan):
                 self._dgrad_conv(bw, name, dz, wb, kpad2, x, k, k - 1 - pad)
             else:   # strided dense conv (stem3): dcol = dz W, then col2im
                 dcol = self._dcolbuf(out.rows * K)
-                self._dcol_conv(bw, name, dz, cout, wkey, dcol, K, out.rows)
+                self._dcol_conv(bw, name, dz, cout, cin, k, wkey, dcol, out.rows)
                 bw.op(name + ".col2im", lib.dp_col2im, _p(dcol), B, H, W_, cin, k, k, stride, pad, oh, ow, x.gp,
                       H * W_ * x.ld, x.ld, 1, self.code)
         self._bwd.append(bwd)
@@ -256,9 +256,11 @@ class BackboneTrainPlan(TapePlan):
         bw.op(name + ".dx", self.lib.dp_conv2d, C.byref(dd))
         self.cost(name + ".dx", 2.0 * x.rows * x.c * k * k * dz.c)
 
-    def _dcol_conv(self, bw, name, dz, cout, wkey, dcol, K, rows):
-        """dcol = dz W ([rows][cout] x [cout][cin*kh*kw]) on the 1x1 conv kernel: W^T packed
-        [K][pad64(cout)] (dp_conv_pack mode 1 of the weight read as a (cout, K, 1, 1) linear)."""
+    def _dcol_conv(self, bw, name, dz, cout, cin, k, wkey, dcol, rows):
+        """dcol = dz W ([rows][cout] x [cout][k*k*cin], columns tap-major (ky, kx, ci): the order
+        dp_col2im reads, so its lanes load consecutive entries) on the 1x1 conv kernel: W^T packed
+        [K][pad64(cout)] by dp_conv_pack mode 4."""
+        K = cin * k * k
         key = (wkey, "T")
         if key not in self._packs:
             w = self.eng.params[wkey]
@@ -266,7 +268,7 @@ class BackboneTrainPlan(TapePlan):
             t = torch.zeros(K, kpad, dtype=self.dt, device=self.dev)
             self.arena.append(t)
             self._packs[key] = (t, kpad)
-            self.fw.op(f"pack.{wkey}.T", self.lib.dp_conv_pack, _p(w), cout, K, 1, 1, _p(t), kpad, cout, 1, None,
+            self.fw.op(f"pack.{wkey}.T", self.lib.dp_conv_pack, _p(w), cout, cin, k, k, _p(t), kpad, 0, 4, None,
                        self.code)
         t, kpad = self._packs[key]
         d = ConvDesc()

@@ -99,8 +99,10 @@ __global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict
 }
 
 // dx[b][y][x][ci] (+)= sum over the (ky, kx) whose output (oy, ox) = ((y + pad - ky) / s, ...) is
-// whole and in range of col[(b*oh + oy)*ow + ox][ci*kh*kw + ky*kw + kx]: the input gradient of a
-// stride-s conv from dcol = dz W (the reference weight layout [cout][cin][kh][kw]).
+// whole and in range of col[(b*oh + oy)*ow + ox][(ky*kw + kx)*cin + ci]: the input gradient of a
+// stride-s conv from dcol = dz W (W^T packed tap-major, dp_conv_pack mode 4), so the lanes of a
+// wave (consecutive ci) read consecutive column entries. The (ky, oy) / (kx, ox) pairs of a pixel
+// are enumerated directly (ky = (y + pad) mod s + s*i) instead of testing every tap.
 template <typename T>
 __global__ void col2im_kernel(const T* __restrict__ col, int h, int w, int cin, int kh, int kw, int s, int pad,
                               int oh, int ow, T* __restrict__ dx, int64_t bs, int ps, int acc, int64_t total) {
@@ -111,19 +113,20 @@ __global__ void col2im_kernel(const T* __restrict__ col, int h, int w, int cin, 
   const int x = (int)(p % w);
   const int64_t t = p / w;
   const int yy = (int)(t % h), b = (int)(t / h);
-  const int K = cin * kh * kw;
+  const int64_t K = (int64_t)cin * kh * kw;
   float sum = 0.f;
-  for (int ky = 0; ky < kh; ++ky) {
+  for (int ky = (yy + pad) % s; ky < kh; ky += s) {
     const int ny = yy + pad - ky;
-    if (ny < 0 || ny % s) continue;
+    if (ny < 0) break;
     const int oy = ny / s;
     if (oy >= oh) continue;
-    for (int kx = 0; kx < kw; ++kx) {
+    const T* crow = col + ((int64_t)b * oh + oy) * ow * K + (int64_t)ky * kw * cin + ci;
+    for (int kx = (x + pad) % s; kx < kw; kx += s) {
       const int nx = x + pad - kx;
-      if (nx < 0 || nx % s) continue;
+      if (nx < 0) break;
       const int ox = nx / s;
       if (ox >= ow) continue;
-      sum += ldf(col + (((int64_t)b * oh + oy) * ow + ox) * K + ci * kh * kw + ky * kw + kx);
+      sum += ldf(crow + ox * K + kx * cin);
     }
   }
   T* o = dx + (int64_t)b * bs + ((int64_t)yy * w + x) * ps + ci;

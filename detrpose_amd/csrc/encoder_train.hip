@@ -269,8 +269,10 @@ __global__ void im2col_kernel(const TI* __restrict__ x, int64_t bs, int ps, int6
 
 // f32 master weights [cout][cin][kh][kw] -> the conv kernels' packed [rows][kpad] (K = ky, kx, ci):
 // mode 0 forward (rows = cout), mode 1 input gradient (rows = cin, K over cout, taps flipped),
-// mode 2 depthwise taps [kh*kw][c] f32 (cin = 1). kc: the K dimension's channel stride (>= the
-// real channel count: maps whose channels are padded to a vector multiple), zero in the pads
+// mode 2 depthwise taps [kh*kw][c] f32 (cin = 1), mode 4 W^T of a strided conv's column GEMM
+// (rows = kh*kw*cin in tap-major order (ky, kx, ci), K over cout, taps not flipped: dcol = dz W
+// in the order dp_col2im reads). kc: the K dimension's channel stride (>= the real channel count:
+// maps whose channels are padded to a vector multiple), zero in the pads
 template <typename T>
 __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin, int kh, int kw, void* __restrict__ out,
                                  int kpad, int kc, int mode, const float* __restrict__ scale) {
@@ -285,6 +287,14 @@ __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin,
     const int K = cin * kh * kw;
     if (e >= (int64_t)cout * K) return;
     reinterpret_cast<float*>(out)[e] = w[e] * (scale ? scale[e / K] : 1.f);
+    return;
+  }
+  if (mode == 4) {
+    if (e >= (int64_t)kh * kw * cin * kpad) return;
+    const int r = (int)(e / kpad), j = (int)(e % kpad);
+    const int tap = r / cin, ci = r - tap * cin;
+    const float v = j < cout ? w[((int64_t)j * cin + ci) * kh * kw + tap] * (scale ? scale[j] : 1.f) : 0.f;
+    reinterpret_cast<T*>(out)[e] = from_f32<T>(v);
     return;
   }
   const int rows = mode == 0 ? cout : cin;
@@ -655,11 +665,13 @@ extern "C" int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int64_
 extern "C" int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out, int32_t kpad,
                             int32_t kc, int32_t mode, const float* scale, int32_t dtype, void* stream) {
   if (kc <= 0) kc = mode == 0 ? cin : cout;
-  DP_REQUIRE(w && out && cout > 0 && cin > 0 && mode >= 0 && mode <= 3 &&
-                 (mode == 2 ? cin == 1 : mode == 3 || (kc >= (mode == 0 ? cin : cout) && kpad >= kh * kw * kc)),
+  DP_REQUIRE(w && out && cout > 0 && cin > 0 && mode >= 0 && mode <= 4 &&
+                 (mode == 2 ? cin == 1 : mode == 3 || (mode == 4 ? kpad >= cout : kc >= (mode == 0 ? cin : cout) &&
+                                                                                    kpad >= kh * kw * kc)),
              "dp_conv_pack: bad arguments");
   const int64_t total = mode == 2 ? (int64_t)cout * kh * kw
                         : mode == 3 ? (int64_t)cout * cin * kh * kw
+                        : mode == 4 ? (int64_t)kh * kw * cin * kpad
                                     : (int64_t)(mode == 0 ? cout : cin) * kpad;
   DP_DT(hipLaunchKernelGGL(conv_pack_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
                            w, cout, cin, kh, kw, out, kpad, kc, mode, scale));

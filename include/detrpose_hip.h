@@ -597,7 +597,9 @@ int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int64_t cstride, 
 /* f32 master conv weights [cout][cin][kh][kw] -> dp_conv2d's packed layout: mode 0 [cout][kpad]
  * (K = ky, kx, cin; the forward), mode 1 [cin][kpad] (K = ky, kx, cout, taps rotated by 180
  * degrees: the stride-1 input gradient as a conv of dz), mode 2 depthwise taps f32 [kh*kw][cout]
- * (cin = 1, dp_dwconv2d's layout), mode 3 f32 [cout][cin*kh*kw] (dp_stem_conv's layout). kc:
+ * (cin = 1, dp_dwconv2d's layout), mode 3 f32 [cout][cin*kh*kw] (dp_stem_conv's layout), mode 4
+ * [kh*kw*cin][kpad >= cout] (rows tap-major ky, kx, ci; K over cout: W^T for the column GEMM
+ * dcol = dz W that dp_col2im reads). kc:
  * channel stride of K (the padded channel count of the map the packed conv reads, zero weights
  * in the pads; 0 = unpadded). scale (f32 [cout], NULL = 1): every output channel's weights
  * multiplied by it (FrozenBatchNorm2d's scale folded into the conv, hgnetv2.py:51-61). */
@@ -636,7 +638,7 @@ int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* res, int64_t ld_r
                       void* dz, int64_t ld_dz,
                       int32_t rows, int32_t c, int32_t act, const float* lab_a, const float* lab_b, const float* scale,
                       float* dlab_a, float* dlab_b, int32_t dtype, void* stream);
-/* dx (= or += when accumulate) = col2im(col): col [batch*oh*ow][cin*kh*kw] (K order cin, ky, kx) =
+/* dx (= or += when accumulate) = col2im(col): col [batch*oh*ow][kh*kw*cin] (K order ky, kx, cin) =
  * dz W of a stride-s, pad-p conv; each input pixel sums the columns that read it (StemBlock.stem3's
  * 3x3 stride-2 input gradient). dx NHWC with image / pixel strides. */
 int dp_col2im(const void* col, int32_t batch, int32_t h, int32_t w, int32_t cin, int32_t kh, int32_t kw,

@@ -83,12 +83,22 @@ def test_col2im_strided_dgrad():
     dy = torch.randn_like(y)
     y.backward(dy)
     oh, ow = y.shape[2:]
-    dcol = dy.permute(0, 2, 3, 1).reshape(-1, cout) @ wt.reshape(cout, -1)
+    # columns tap-major (ky, kx, ci), the order dp_conv_pack mode 4 packs W^T in
+    dcol = dy.permute(0, 2, 3, 1).reshape(-1, cout) @ wt.permute(0, 2, 3, 1).reshape(cout, -1)
     dx = torch.ones(B, h, w, cin, device=DEV)
     _lib.check(lib.dp_col2im(dcol.contiguous().data_ptr(), B, h, w, cin, 3, 3, 2, 1, oh, ow, dx.data_ptr(), h * w * cin,
                              cin, 1, DP_F32, _s()), "col2im")
     torch.cuda.synchronize()
     _close(dx, 1 + x.grad.permute(0, 2, 3, 1), "col2im dx")
+    # the W^T that produces these columns on the 1x1 conv kernel: dp_conv_pack mode 4
+    kpad = 64
+    wp = torch.full((9 * cin, kpad), 7.0, device=DEV)
+    _lib.check(lib.dp_conv_pack(C.c_void_p(wt.data_ptr()), cout, cin, 3, 3, C.c_void_p(wp.data_ptr()), kpad, 0, 4,
+                                None, DP_F32, _s()), "conv_pack mode 4")
+    torch.cuda.synchronize()
+    ref = torch.zeros(9 * cin, kpad, device=DEV)
+    ref[:, :cout] = wt.permute(0, 2, 3, 1).reshape(cout, -1).t()
+    assert torch.equal(wp, ref)
 
 
 @pytest.mark.parametrize("dtype", [DP_F32, DP_BF16])
