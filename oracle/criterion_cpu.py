@@ -118,10 +118,17 @@ def loss_keypoints(kps, go, sizes, tgt_kps, tgt_area, K, num_boxes_go):
     return pose.sum() / num_boxes_go, oks_loss.sum() / num_boxes_go
 
 
-def criterion(heads, sizes, tgt_labels, tgt_kps, tgt_area, K, ncls, n_aux, weights=(2.0, 10.0, 4.0)):
+def criterion(heads, sizes, tgt_labels, tgt_kps, tgt_area, K, ncls, n_aux, weights=(2.0, 10.0, 4.0),
+              force_match=None):
     """heads: [(logits, kps)] in the reference's order (final, aux 0..n_aux-1, pre, interm).
+    force_match: (H, B, Q) matchings to use instead of the matcher's (a run whose near-tied costs
+    another summation order resolves differently is compared on the same assignment).
     Returns (loss dict, matches (H, B, Q), go (B, Q))."""
-    matches = np.stack([match(lg.detach(), kp.detach(), sizes, tgt_labels, tgt_kps, tgt_area, K) for lg, kp in heads])
+    if force_match is not None:
+        matches = np.asarray(force_match, np.int64)
+    else:
+        matches = np.stack([match(lg.detach(), kp.detach(), sizes, tgt_labels, tgt_kps, tgt_area, K)
+                            for lg, kp in heads])
     go = union(matches)
     num_boxes = max(float(sum(sizes)), 1.0)
     num_go = max(float((go >= 0).sum()), 1.0)

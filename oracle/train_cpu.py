@@ -148,7 +148,7 @@ def train_transformer(feats, P, cfg, dn=None, force_topk=None):
         ref = torch.cat([dref, ref], 1)
         mask = torch.as_tensor(dn["attn_mask"])
     Qt = tgt.shape[1]
-    project = weighting_function(reg_max, 0.5, reg_scale)
+    project = weighting_function(reg_max, 0.5, reg_scale).to(memory.dtype)   # float64 checker runs too
     dim_t = P[T_ + "decoder.dim_t"]
     feat0 = feats[0].permute(0, 2, 3, 1)
     out = tgt
@@ -216,13 +216,15 @@ def dn_match(sizes, pad_size, num_group):
     return m
 
 
-def losses(res, sizes, tgt_labels, tgt_kps, tgt_area, K, ncls, weights=(2.0, 10.0, 4.0)):
-    """Criterion.forward (criterion.py:285-435) incl. the dn_* losses."""
+def losses(res, sizes, tgt_labels, tgt_kps, tgt_area, K, ncls, weights=(2.0, 10.0, 4.0), force_match=None):
+    """Criterion.forward (criterion.py:285-435) incl. the dn_* losses; force_match: the (H, B, Q)
+    per-head matchings to use (criterion_cpu.criterion)."""
     heads = [(res["final"]["pred_logits"], res["final"]["pred_keypoints"])]
     heads += [(h["pred_logits"], h["pred_keypoints"]) for h in res["aux"]]
     heads += [(res["pre"]["pred_logits"], res["pre"]["pred_keypoints"]),
               (res["interm"]["pred_logits"], res["interm"]["pred_keypoints"])]
-    out, matches, go = crit.criterion(heads, sizes, tgt_labels, tgt_kps, tgt_area, K, ncls, len(res["aux"]), weights)
+    out, matches, go = crit.criterion(heads, sizes, tgt_labels, tgt_kps, tgt_area, K, ncls, len(res["aux"]), weights,
+                                      force_match)
     if "dn" in res:
         meta = res["dn_meta"]
         m = dn_match(sizes, meta["pad_size"], meta["num_dn_group"])
@@ -248,7 +250,15 @@ def _bn_train(x, P, p, stats=None):
     rm = rv = None
     if stats is not None:
         rm, rv = stats[p + ".running_mean"], stats[p + ".running_var"]
-    return F.batch_norm(x, rm, rv, P[p + ".weight"], P[p + ".bias"], True, 0.1, 1e-5)
+    y = F.batch_norm(x, rm, rv, P[p + ".weight"], P[p + ".bias"], True, 0.1, 1e-5)
+    if y.requires_grad:
+        # torch 2.10's CPU batch-norm backward (training mode) returns wrong input / weight
+        # gradients when the incoming gradient is channels-last strided while x is NCHW
+        # contiguous — the layout the memory's flatten(2).permute(0, 2, 1) backward hands the
+        # encoder outputs (finite-difference check in DESIGN.md, "Training parity at
+        # DETRPose-L"): hand it a contiguous gradient
+        y.register_hook(lambda g: g.contiguous())
+    return y
 
 
 def _act(x, name):

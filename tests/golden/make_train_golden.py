@@ -45,6 +45,37 @@ CASES = {
 }
 
 
+class _bn_contiguous_grad:
+    """While active, every F.batch_norm output hands its backward a contiguous gradient.
+
+    torch 2.10's CPU batch-norm backward in training mode returns wrong input / weight / bias
+    gradients when the incoming gradient is channels-last strided while the input is NCHW
+    contiguous (checked against central finite differences; DESIGN.md, "Training parity at
+    DETRPose-L"). The reference's HybridEncoder hands exactly that layout to the BatchNorm in
+    front of the AIFI layer (src_flatten = proj.flatten(2).permute(0, 2, 1),
+    hybrid_encoder.py:476; its backward is a permuted view), so on this CPU build its own
+    gradients of input_proj[use_encoder_idx] and of the backbone below it are wrong. Making the
+    gradient contiguous changes no value of the reference's arithmetic, only the memory layout
+    the backward kernel sees (the GPU kernels the reference trains on are not affected)."""
+
+    def __enter__(self):
+        import torch.nn.functional as F
+        self.F, self.orig = F, F.batch_norm
+
+        def bn(*a, **k):
+            y = self.orig(*a, **k)
+            if y.requires_grad:
+                y.register_hook(lambda g: g.contiguous())
+            return y
+
+        F.batch_norm = bn
+        return self
+
+    def __exit__(self, *exc):
+        self.F.batch_norm = self.orig
+        return False
+
+
 def _import_criterion():
     make_golden._import_reference()
     ref = make_golden.REF
@@ -241,7 +272,8 @@ def dn_targets(B, K, sizes, seed):
     return out
 
 
-def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_train=False, full_train=False):
+def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_train=False, full_train=False,
+                    accum=1):
     """The reference's full training step with OKS-denoising queries (transformer.py:1265-1385,
     dn_component.py:39-183) on CPU: training-mode forward WITH targets, the Criterion with its
     dn_* losses (criterion.py:385-435), loss.backward(). BatchNorm layers in eval mode (frozen
@@ -254,6 +286,8 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_t
       - prepare_for_cdn is wrapped to record the DN inputs it draws (noised labels, noised
         keypoints, attention mask, dn_meta), so the build can be fed the same ones;
       - torch.argsort is the stable sort inside the criterion (see the module docstring);
+      - every BatchNorm output hands its backward a contiguous gradient (_bn_contiguous_grad:
+        a torch CPU bug, not the reference's arithmetic);
       - each class_embed[l] gets a copy of its input (a forward pre-hook returning x.clone()).
         Its input output[:, :, 0] is a view of the decoder output that the next layer's
         in-place with_pos_embed (transformer.py:369) bumps the version of, so in fp32 autograd
@@ -275,7 +309,22 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_t
     the reference configures it (freeze_at=-1: no stage or stem frozen; freeze_norm=True: its
     norms are FrozenBatchNorm2d), so every backbone parameter's gradient (conv weights, the
     LearnableAffineBlock scalars) is stored ("grad.backbone.*") with the backbone outputs
-    ("bb.*") instead of d loss / d backbone-output."""
+    ("bb.*") instead of d loss / d backbone-output.
+
+    accum > 1 (train_one_epoch's gradient accumulation, src/solver/engine.py:28, 43-59; the L
+    config inherits grad_accum_steps=2 from configs/detrpose/include/detrpose_hgnetv2.py:15):
+    the batch is split into `accum` consecutive sub-batches, each runs its own forward (its own
+    DN draws, BatchNorm batch statistics and running-statistics update), criterion (its own
+    matching and num_boxes) and backward into the same .grad, exactly the loop of engine.py:43-59.
+    Per sub-batch j the DN draws, losses, the matcher's per-head assignments, backbone / encoder
+    outputs and the full d loss / d memory the transformer hands the encoder ("s{j}.dmem", f32
+    (B/accum, sum HW, C)) are stored under "s{j}." (heads are not stored); the gradients are the
+    accumulated sums, the running statistics those after the last sub-batch. d memory is stored
+    whole because the backbone / encoder gradients are a badly conditioned function of it at L
+    ("Training parity at DETRPose-L"): a checker drives its encoder / backbone backward
+    with the reference's own d memory."""
+    if accum > 1:
+        return _golden_train_accum(ref, size, batch, sizes, wseed, tseed, dn_seed, accum)
     enc_train = enc_train or full_train
     from detrpose_amd.synthetic import load_synthetic, synthetic_images
     import src.models.detrpose.transformer as tmod
@@ -324,6 +373,7 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_t
                      losses=["vfl", "keypoints"], num_body_points=K, focal_alpha=0.25)
     tmod.prepare_for_cdn = cdn_spy
     torch.Tensor.cuda = lambda self, *a, **k: self
+    bnfix = _bn_contiguous_grad().__enter__()
     try:
         torch.manual_seed(dn_seed)
         out = model(images, targets)
@@ -334,6 +384,7 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_t
         total = sum(losses.values())
         total.backward()
     finally:
+        bnfix.__exit__()
         tmod.prepare_for_cdn = orig_cdn
         torch.Tensor.cuda = orig_cuda
         torch.argsort = orig_argsort
@@ -412,10 +463,166 @@ def golden_train_dn(ref, size, batch, sizes, wseed=0, tseed=21, dn_seed=5, enc_t
     return st
 
 
+def _dn_label_slots(model, label):
+    """Which label_enc row each DN slot embeds (-1: padding), matched back from the rows."""
+    le = model.transformer.label_enc.weight.detach()
+    lab = label[:, :, 0].detach()   # (B, pad, C)
+    d = ((lab[:, :, None, :] - le[None, None]) ** 2).sum(-1)
+    slot = d.argmin(-1)
+    pad_zero = lab.abs().sum(-1) == 0
+    assert float(d.min(-1)[0][~pad_zero].max()) == 0.0
+    return torch.where(pad_zero, torch.full_like(slot, -1), slot).numpy()
+
+
+def _golden_train_accum(ref, size, batch, sizes, wseed, tseed, dn_seed, accum):
+    """golden_train_dn(full_train=True, accum>1): the whole network trained, engine.py:43-59's
+    sub-batch loop (see golden_train_dn's docstring for the deliberate changes and the keys)."""
+    from detrpose_amd.synthetic import load_synthetic, synthetic_images
+    import src.models.detrpose.transformer as tmod
+    Criterion, HungarianMatcher = _import_criterion()
+    assert batch % accum == 0
+    sub = batch // accum
+    torch.manual_seed(0)
+    model, _ = make_golden.build_reference(ref, size)
+    load_synthetic(model, seed=wseed)
+    model.train()
+    for m in model.backbone.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.eval()
+    K = model.transformer.num_body_points
+    images = synthetic_images(batch, seed=1)
+    targets = dn_targets(batch, K, sizes, tseed)
+    bb_cap, enc_cap = [], []
+    hk = model.backbone.register_forward_hook(lambda mod, a, out: bb_cap.extend(o.detach() for o in out))
+    he = model.encoder.register_forward_hook(lambda mod, a, out: enc_cap.extend(o.detach() for o in out))
+    hcls = [m.register_forward_pre_hook(lambda mod, a: (a[0].clone(),) + tuple(a[1:]))
+            for m in model.transformer.class_embed]
+    cdn = []
+    orig_cdn = tmod.prepare_for_cdn
+
+    def cdn_spy(*a, **kw):
+        r = orig_cdn(*a, **kw)
+        cdn.append(r)
+        return r
+
+    orig_cuda = torch.Tensor.cuda
+    orig_argsort = torch.argsort
+    matcher = HungarianMatcher(cost_class=2.0, cost_keypoints=10.0, cost_oks=4.0, focal_alpha=0.25,
+                               num_body_points=K)
+    crit = Criterion(num_classes=2, matcher=matcher, weight_dict={"loss_vfl": 2.0, "loss_keypoints": 10.0,
+                                                                 "loss_oks": 4.0},
+                     losses=["vfl", "keypoints"], num_body_points=K, focal_alpha=0.25)
+    # the matcher's assignments per call (Criterion.forward's order: final, aux 0..L-2, pre,
+    # interm; criterion.py:289-303), recorded so a checker can run on the same assignment
+    calls = []
+    orig_fwd = matcher.forward
+
+    def match_spy(outputs, targets_):
+        r = orig_fwd(outputs, targets_)
+        calls.append(r)
+        return r
+
+    matcher.forward = match_spy
+    # d loss / d (the transformer's input feats) of each sub-batch: the gradient the transformer
+    # alone hands the encoder (a view of each feat, consumed only by the transformer, with a
+    # grad hook), in the layout of its memory (B, sum HW, C)
+    dmem = []
+
+    def tr_pre(mod, args):
+        feats = [f.view_as(f) for f in args[0]]
+        parts = [None] * len(feats)
+
+        def keep(i):
+            def hook(gr):
+                parts[i] = gr.detach().flatten(2).permute(0, 2, 1)
+                if all(p_ is not None for p_ in parts):
+                    dmem.append(torch.cat(parts, 1).contiguous())
+            return hook
+
+        for i, f in enumerate(feats):
+            f.register_hook(keep(i))
+        return (feats,) + tuple(args[1:])
+
+    htr = model.transformer.register_forward_pre_hook(tr_pre)
+    st = {"meta": np.array([batch, wseed, 1, tseed, dn_seed, accum], np.int64), "sizes": np.array(sizes, np.int64)}
+    st["tgt_labels"] = torch.cat([t["labels"] for t in targets]).numpy()
+    st["tgt_boxes"] = torch.cat([t["boxes"] for t in targets]).numpy()
+    st["tgt_kps"] = torch.cat([t["keypoints"] for t in targets]).numpy()
+    st["tgt_area"] = torch.cat([t["area"] for t in targets]).numpy()
+    tmod.prepare_for_cdn = cdn_spy
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    totals = []
+    bnfix = _bn_contiguous_grad().__enter__()
+    try:
+        torch.manual_seed(dn_seed)
+        for j in range(accum):          # engine.py:43-59
+            sl = slice(j * sub, (j + 1) * sub)
+            out = model(images[sl], targets[sl])
+            torch.argsort = lambda x, dim=-1, descending=False, **kw: torch.sort(
+                x, dim=dim, descending=descending, stable=True)[1]
+            losses = crit(out, targets[sl])
+            torch.argsort = orig_argsort
+            total = sum(losses.values())
+            total.backward()
+            totals.append(float(total))
+            label, pose, mask, meta = cdn[-1]
+            p = f"s{j}."
+            st[p + "dn_label"] = _dn_label_slots(model, label)
+            st[p + "dn_pose_unsig"] = pose.detach().numpy()
+            st[p + "dn_attn_mask"] = mask.numpy()
+            st[p + "dn_pad_size"] = np.array(meta["pad_size"])
+            st[p + "dn_num_group"] = np.array(meta["num_dn_group"])
+            keys = sorted(losses)
+            st[p + "loss_keys"] = np.array(keys)
+            st[p + "loss_vals"] = np.array([float(losses[k]) for k in keys], np.float64)
+            nq = out["pred_logits"].shape[1]
+            match = np.full((len(calls), sub, nq), -1, np.int64)
+            for h, r in enumerate(calls):
+                for b, (I, J) in enumerate(r):
+                    match[h, b, I.numpy()] = J.numpy()
+            st[p + "match"] = match
+            calls.clear()
+            st[p + "dmem"] = dmem[-1].numpy().astype(np.float32)
+    finally:
+        bnfix.__exit__()
+        tmod.prepare_for_cdn = orig_cdn
+        torch.Tensor.cuda = orig_cuda
+        torch.argsort = orig_argsort
+        hk.remove()
+        he.remove()
+        htr.remove()
+        for h in hcls:
+            h.remove()
+    nb, ne = len(bb_cap) // accum, len(enc_cap) // accum
+    for j in range(accum):
+        for i in range(nb):
+            make_golden._sample(st, f"s{j}.bb{i}", bb_cap[j * nb + i])
+        for i in range(ne):
+            make_golden._sample(st, f"s{j}.enc{i}", enc_cap[j * ne + i])
+    ng = 0
+    for prefix, mod in (("", model.transformer), ("encoder.", model.encoder), ("backbone.", model.backbone)):
+        for n, p in mod.named_parameters():
+            if p.grad is not None:
+                make_golden._sample(st, "grad." + prefix + n, p.grad)
+                ng += 1
+    for n, m in model.encoder.named_modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            st[f"bn.encoder.{n}.running_mean"] = m.running_mean.numpy()
+            st[f"bn.encoder.{n}.running_var"] = m.running_var.numpy()
+    print(f"  [{size}] DN train step b{batch} = {accum} x b{sub}, targets {sizes}: pads "
+          f"{[int(st[f's{j}.dn_pad_size']) for j in range(accum)]}, totals {totals}, {ng} parameter gradients")
+    return st
+
+
 def main():
     torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
     Criterion, HungarianMatcher = _import_criterion()
     ref = make_golden._import_reference()
+    if os.environ.get("ONLY_FULL_L"):
+        st = golden_train_dn(ref, "l", 2, [3, 1], full_train=True, accum=2)
+        np.savez_compressed(os.path.join(HERE, "train_full_l_b2a2.npz"), **st)
+        print("wrote train_full_l_b2a2.npz")
+        return
     if os.environ.get("ONLY_FULL"):
         st = golden_train_dn(ref, "n", 2, [3, 1], full_train=True)
         np.savez_compressed(os.path.join(HERE, "train_full_n_b2.npz"), **st)
