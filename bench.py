@@ -255,32 +255,60 @@ def synthetic_targets(batch, K=17, seed=3, dev="cuda"):
     return ts
 
 
-def train_leg(size, dtype, dev, batch, steps, warmup=3):
-    """BASELINE configs[4] on one GPU (per-GPU shard of the 8-GPU DDP step): backbone forward
-    (FrozenBatchNorm2d), encoder training forward (BatchNorm batch statistics), transformer
-    training forward with OKS-denoising queries, criterion (matching, losses and their gradients),
-    transformer / encoder / backbone backward, clip_grad_norm_ + AdamW + ModelEMA
-    (detrpose_amd.train.Trainer, scope 'full'). Per-phase device times from HIP events on the
-    same stream."""
-    from detrpose_amd import build_model
+def train_leg(size, dtype, dev, batch, steps, warmup=3, rank=0, world=1):
+    """BASELINE configs[4]: the training step of detrpose_amd.train.Trainer (scope 'full') on this
+    rank's shard of `batch` images: backbone forward (FrozenBatchNorm2d), encoder training forward
+    (BatchNorm batch statistics, SyncBN across ranks), transformer training forward with
+    OKS-denoising queries, criterion (matching, losses and their gradients; num_boxes all-reduced),
+    transformer / encoder / backbone backward — per sub-batch of the config's grad_accum_steps —,
+    DDP's gradient mean (one all-reduce of the flat f32 gradient), clip_grad_norm_ + AdamW +
+    ModelEMA. Timed like the inference line: barrier + synchronize around `steps` steps, the
+    slowest rank's time. Then one instrumented step times every collective (synchronised: a
+    separate number, not part of ms_per_step) and HIP events split one sub-batch into phases."""
+    from detrpose_amd import build_model, encoder_train
     from detrpose_amd.synthetic import load_synthetic, synthetic_images
     from detrpose_amd.train import Trainer
+    from detrpose_amd import dist as dp
     model, _ = build_model(size, dtype=dtype)
     load_synthetic(model, 0)
     tr = Trainer(model, dtype=dtype, device=dev)
-    images = synthetic_images(batch, seed=11).to(dev)
-    ts = synthetic_targets(batch, dev=dev)
+    images = synthetic_images(batch, seed=11 + rank).to(dev)
+    ts = synthetic_targets(batch, seed=3 + rank, dev=dev)
     for _ in range(warmup):
         tr.step(images, ts)
+    torch.cuda.synchronize()
+    if world > 1:
+        dp.dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         keys, vals = tr.step(images, ts)
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / steps
-    # phase split of one more step (HIP events around each phase)
-    plan = next(iter(tr.eng.plans.values()))
+    if world > 1:
+        dp.dist.barrier()
+    torch.cuda.synchronize()
+    own = time.perf_counter() - t0
+    el = dp.max_over_ranks(own, world, dev)
+    ms = el * 1e3 / steps
+    comm = None
+    if world > 1:   # one instrumented step: every collective synchronised and timed
+        encoder_train.COMM_LOG = []
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        tr.step(images, ts)
+        torch.cuda.synchronize()
+        inst = time.perf_counter() - t1
+        log, encoder_train.COMM_LOG = encoder_train.COMM_LOG, None
+        big = max(log, key=lambda x: x[0])
+        comm = {"collectives_per_step": len(log), "ms_in_collectives": round(sum(x[1] for x in log) * 1e3, 3),
+                "instrumented_step_ms": round(inst * 1e3, 3),
+                "grad_allreduce_bytes": big[0], "grad_allreduce_ms": round(big[1] * 1e3, 3),
+                "backend": dp.dist.get_backend()}
+    # phase split of one more sub-batch (HIP events around each phase; on every rank, whose
+    # SyncBN collectives pair up)
+    plan = tr.plan
     bb, ep = tr.bb, tr.ep
+    sub = batch // tr.grad_accum_steps
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
     ev[0].record()
     bb.forward()
@@ -291,7 +319,7 @@ def train_leg(size, dtype, dev, batch, steps, warmup=3):
     ev[3].record()
     from detrpose_amd.criterion import pack_targets
     from detrpose_amd.train import dn_meta
-    packed = pack_targets(ts, 17, dev)
+    packed = pack_targets(ts[batch - sub:], 17, dev)
     plan.criterion(packed, packed.sizes, dn_meta(packed.sizes)[1])
     ev[4].record()
     plan.backward()
@@ -312,16 +340,23 @@ def train_leg(size, dtype, dev, batch, steps, warmup=3):
     t = {"backbone": phases["backbone_fwd"] + phases["backbone_bwd"],
          "encoder": phases["encoder_fwd"] + phases["encoder_bwd"],
          "transformer": phases["transformer_fwd"] + phases["transformer_bwd"]}
-    return {"workload": f"DETRPose-{size.upper()} training step (BASELINE configs[4], per-GPU shard on 1 GPU): "
-                        f"backbone (FrozenBN) + encoder (BatchNorm batch statistics) + transformer with "
-                        f"OKS-denoising queries, criterion (incl. dn_* losses), full backward, "
-                        f"clip_grad_norm_(0.1) + AdamW (backbone lr 1e-5) + ModelEMA; {dtype}, batch {batch}, "
-                        f"synthetic targets (1-6 persons per image)",
-            "ms_per_step": round(ms, 3), "images_per_sec": round(batch / ms * 1e3, 2), "steps": steps,
-            "dn_pad": plan.P, "phase_ms": phases,
-            "tflops_by_part": {k: round(fl[k] / (t[k] * 1e-3) / 1e12, 2) if t[k] > 0 else None for k in fl},
-            "step_tflop": round(sum(fl.values()) / 1e12, 3),
-            "losses_finite": bool(torch.isfinite(vals).all())}
+    cfg = tr.opt
+    out = {"workload": f"DETRPose-{size.upper()} training step (BASELINE configs[4]) on {world} GPU(s), {batch} "
+                       f"images per GPU in grad_accum_steps={tr.grad_accum_steps} sub-batches of {sub}: backbone "
+                       f"(FrozenBN) + encoder (BatchNorm batch statistics{', SyncBN' if world > 1 else ''}) + "
+                       f"transformer with OKS-denoising queries, criterion (incl. dn_* losses), full backward, "
+                       f"{'DDP gradient mean, ' if world > 1 else ''}clip_grad_norm_({cfg['max_norm']}) + AdamW "
+                       f"(backbone lr {cfg['backbone_lr']:g}) + ModelEMA; {dtype}, synthetic targets (1-6 persons "
+                       f"per image)",
+           "n_gpus": world, "ms_per_step": round(ms, 3), "images_per_sec": round(batch * world / ms * 1e3, 2),
+           "images_per_sec_per_gpu": round(batch / ms * 1e3, 2), "steps": steps, "grad_accum_steps": tr.grad_accum_steps,
+           "dn_pad_last_sub_batch": plan.P, "phase_ms_one_sub_batch": phases,
+           "tflops_by_part": {k: round(fl[k] / (t[k] * 1e-3) / 1e12, 2) if t[k] > 0 else None for k in fl},
+           "sub_batch_tflop": round(sum(fl.values()) / 1e12, 3),
+           "losses_finite": bool(torch.isfinite(vals).all()), "update_skipped": tr.eng.step_skipped()}
+    if comm is not None:
+        out["collectives"] = comm
+    return out
 
 
 def latency_bs1(model, pp, dev, runs, warmup):
@@ -521,11 +556,17 @@ def main():
                                          "value": round(v, 2), "unit": "images/sec", "outputs_finite": fin})
                 del ms
                 torch.cuda.empty_cache()
-        if world == 1 and not a.no_train:
-            out["train_step"] = train_leg(a.size, a.dtype, dev, a.train_batch, a.train_steps)
-            torch.cuda.empty_cache()
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.size, a.cpu_baseline_seconds)
+    if not a.no_train:
+        # every rank runs the training leg (its collectives pair up across ranks); rank 0 reports
+        del g
+        torch.cuda.empty_cache()
+        ts = train_leg(a.size, a.dtype, dev, a.train_batch, a.train_steps, rank=rank, world=world)
+        torch.cuda.empty_cache()
+    if rank == 0:
+        if not a.no_train:
+            out["train_step"] = ts
         if not finite:
             out["error"] = "non-finite outputs"
         print(json.dumps(out), flush=True)

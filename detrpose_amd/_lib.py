@@ -146,7 +146,9 @@ _SIGS = {
     "dp_zero": (i32, [vp, i64, vp]),
     "dp_cdn_build": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, i32, f32, f32, C.c_uint64, vp, vp, vp]),
     "dp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
-    "dp_adamw": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp]),
+    "dp_adamw": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp, vp]),
+    "dp_finite_guard": (i32, [vp, i64, vp, vp]),
+    "dp_ema": (i32, [vp, vp, i64, f32, vp, vp]),
     # HybridEncoder training (csrc/encoder_train.hip)
     "dp_bn_stats": (i32, [vp, i64, i32, i32, vp, i32, vp]),
     "dp_bn_finalize": (i32, [vp, i32, f32, i32, f32, f32, vp, vp, vp, vp]),

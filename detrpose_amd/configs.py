@@ -106,6 +106,24 @@ def get_config(size: str) -> dict:
     raise ValueError(f"unknown DETRPose size {size!r} (expected n, l or x)")
 
 
+# The training loop's hyper-parameters (configs/detrpose/include/detrpose_hgnetv2.py:13-21
+# training_params: clip 0.1, grad_accum_steps 2 unless a size file overrides it; the size files'
+# AdamW (lr 1e-4, betas (0.9, 0.999), weight_decay 1e-4) with the backbone parameter group's lr,
+# ModelEMA(0.9999, warmups 2000)): detrpose_hgnetv2_n.py:13, 26; detrpose_hgnetv2_l.py:25 (no
+# grad_accum override); detrpose_hgnetv2_x.py:13, 26.
+TRAINING = {
+    "n": dict(grad_accum_steps=1, backbone_lr=1e-4),
+    "l": dict(grad_accum_steps=2, backbone_lr=1e-5),
+    "x": dict(grad_accum_steps=1, backbone_lr=5e-5),
+}
+TRAINING_COMMON = dict(lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4, max_norm=0.1, ema_decay=0.9999,
+                       ema_warmups=2000)
+
+
+def training_params(size: str) -> dict:
+    return {**TRAINING_COMMON, **TRAINING[size.lower()]}
+
+
 # Algorithmic forward FLOPs per 640x640 image (2 FLOP / MAC), measured with
 # torch.utils.flop_counter on the reference in the survey.
 GFLOP_PER_IMAGE = {"n": 8.91, "l": 103.86, "x": 232.04}

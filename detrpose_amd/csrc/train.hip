@@ -771,13 +771,22 @@ __global__ void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* __r
 
 // torch.optim.AdamW step (decoupled weight decay, bias corrections) after
 // clip_grad_norm_(max_norm): g *= min(max_norm / (||g|| + 1e-6), 1) with ||g||^2 from sqnorm
+// skip (device flag, NULL = never): a non-zero value leaves parameters and moments unchanged
+// (dp_finite_guard set it: a non-finite loss or gradient norm). A non-finite norm skips too:
+// fminf(max_norm / NaN, 1) would otherwise be 1, silently turning the clipping off.
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
-                             float bc1, float bc2, float max_norm, const float* __restrict__ sq) {
+                             float bc1, float bc2, float max_norm, const float* __restrict__ sq,
+                             const float* __restrict__ skip) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (skip && *skip != 0.f) return;
   float scale = 1.f;
-  if (max_norm > 0.f) scale = fminf(max_norm / (sqrtf(*sq) + 1e-6f), 1.f);
+  if (max_norm > 0.f) {
+    const float nrm = sqrtf(*sq);
+    if (!isfinite(nrm)) return;
+    scale = fminf(max_norm / (nrm + 1e-6f), 1.f);
+  }
   const float gi = g[i] * scale;
   float pi = p[i] * (1.f - lr * wd);
   const float mi = b1 * m[i] + (1.f - b1) * gi;
@@ -786,6 +795,21 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   v[i] = vi;
   pi -= (lr / bc1) * mi / (sqrtf(vi) / sqrtf(bc2) + eps);
   p[i] = pi;
+}
+
+// bad[0] = 1 when any of v[0..n) is not finite (left unchanged otherwise): one block
+__global__ void finite_guard_kernel(const float* __restrict__ v, int64_t n, float* __restrict__ bad) {
+  int nonfinite = 0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) nonfinite |= !isfinite(v[i]);
+  if (__syncthreads_or(nonfinite) && threadIdx.x == 0) bad[0] = 1.f;
+}
+
+// ModelEMA: e = d e + (1 - d) p, unless *skip != 0
+__global__ void ema_kernel(float* __restrict__ e, const float* __restrict__ p, int64_t n, float d,
+                           const float* __restrict__ skip) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (skip && *skip != 0.f)) return;
+  e[i] = d * e[i] + (1.f - d) * p[i];
 }
 
 inline unsigned nblk(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
@@ -1099,13 +1123,25 @@ extern "C" int dp_grad_sqnorm(const float* g, int64_t n, float* out, void* strea
 
 extern "C" int dp_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
                         float beta1, float beta2, float eps, float weight_decay, int32_t step, float max_norm,
-                        const float* grad_sqnorm, void* stream) {
+                        const float* grad_sqnorm, const float* skip, void* stream) {
   DP_REQUIRE(param && grad && exp_avg && exp_avg_sq && n > 0 && step > 0, "dp_adamw: bad arguments");
   DP_REQUIRE(max_norm <= 0.f || grad_sqnorm, "dp_adamw: clipping needs the gradient's squared norm");
   const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
   hipLaunchKernelGGL(adamw_kernel, dim3(nblk(n, 256)), dim3(256), 0, as_stream(stream), param, grad, exp_avg,
-                     exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, bc1, bc2, max_norm, grad_sqnorm);
+                     exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, bc1, bc2, max_norm, grad_sqnorm, skip);
   return dp_check_launch("dp_adamw");
+}
+
+extern "C" int dp_finite_guard(const float* v, int64_t n, float* bad, void* stream) {
+  DP_REQUIRE(v && bad && n > 0, "dp_finite_guard: bad arguments");
+  hipLaunchKernelGGL(finite_guard_kernel, dim3(1), dim3(256), 0, as_stream(stream), v, n, bad);
+  return dp_check_launch("dp_finite_guard");
+}
+
+extern "C" int dp_ema(float* ema, const float* p, int64_t n, float decay, const float* skip, void* stream) {
+  DP_REQUIRE(ema && p && n > 0, "dp_ema: bad arguments");
+  hipLaunchKernelGGL(ema_kernel, dim3(nblk(n, 256)), dim3(256), 0, as_stream(stream), ema, p, n, decay, skip);
+  return dp_check_launch("dp_ema");
 }
 
 extern "C" int dp_zero(void* p, int64_t bytes, void* stream) {

@@ -86,9 +86,24 @@ class V:
         return V(self.buf, self.off + c0, self.ld, c, c if cp is None else cp, self.B, self.H, self.W)
 
 
+COMM_LOG = None   # when a list: every all_reduce is synchronised and timed into it (bench.py's train leg)
+
+
 def all_reduce(t):
     """Sum over the ranks in place (RCCL on device tensors; host-staged under gloo, whose
     collectives take host tensors: the one-GPU multi-rank rehearsal and tests)."""
+    if COMM_LOG is not None:
+        import time
+        torch.cuda.synchronize(t.device) if t.is_cuda else None
+        t0 = time.perf_counter()
+        _all_reduce(t)
+        torch.cuda.synchronize(t.device) if t.is_cuda else None
+        COMM_LOG.append((t.numel() * t.element_size(), time.perf_counter() - t0))
+        return
+    _all_reduce(t)
+
+
+def _all_reduce(t):
     if torch.distributed.get_backend() == "gloo" and t.is_cuda:
         h = t.cpu()
         torch.distributed.all_reduce(h)

@@ -53,15 +53,32 @@ def dn_attn_mask(pad, groups, single, nq):
     return m
 
 
+_SIZE_OF_BACKBONE = {"B0": "n", "B4": "l", "B5": "x"}
+
+
+def model_size(model):
+    """'n' | 'l' | 'x' from the backbone arch (configs: B0 / B4 / B5), or None."""
+    return _SIZE_OF_BACKBONE.get(getattr(model.backbone, "name", None))
+
+
 class Trainer:
     """The training step for a DETRPose module (reference parameter names), dtype 'bf16' or
-    'fp32'. Optimizer: AdamW(lr, betas, weight_decay) + clip_grad_norm_(max_norm), the configs'
-    values by default (configs/detrpose/detrpose_hgnetv2_*.py, include/detrpose_hgnetv2.py)."""
+    'fp32'. Optimizer: AdamW(lr, betas, weight_decay) + clip_grad_norm_(max_norm), the backbone's
+    own learning rate, ModelEMA and the gradient accumulation of train_one_epoch: each argument
+    left None takes the model size's config value (detrpose_amd.configs.training_params:
+    configs/detrpose/detrpose_hgnetv2_*.py, include/detrpose_hgnetv2.py)."""
 
-    def __init__(self, model, dtype="bf16", device="cuda", lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4,
-                 max_norm=0.1, dn_number=20, label_noise_ratio=0.5, weights=(2.0, 10.0, 4.0), seed=0,
-                 scope="full", backbone_lr=1e-5, ema=True, ema_decay=0.9999, ema_warmups=2000):
+    def __init__(self, model, dtype="bf16", device="cuda", lr=None, betas=None, weight_decay=None,
+                 max_norm=None, dn_number=20, label_noise_ratio=0.5, weights=(2.0, 10.0, 4.0), seed=0,
+                 scope="full", backbone_lr=None, ema=True, ema_decay=None, ema_warmups=None, grad_accum_steps=None):
+        from .configs import training_params
         assert scope in ("full", "transformer"), scope
+        size = model_size(model)
+        cfg = training_params(size) if size else training_params("l")
+
+        def pick(v, k):
+            return cfg[k] if v is None else v
+
         self.model = model
         self.device = torch.device(device)
         self.scope = scope
@@ -69,14 +86,18 @@ class Trainer:
         if scope == "transformer":
             self.inf = model.engine(self.device)
         self.eng = TrainEngine(model, dtype, self.device, train_backbone=scope == "full")
-        self.opt = dict(lr=lr, betas=betas, weight_decay=weight_decay, max_norm=max_norm, backbone_lr=backbone_lr)
-        self.ema = dict(decay=ema_decay, warmups=ema_warmups) if ema else None
+        self.opt = dict(lr=pick(lr, "lr"), betas=tuple(pick(betas, "betas")),
+                        weight_decay=pick(weight_decay, "weight_decay"), max_norm=pick(max_norm, "max_norm"),
+                        backbone_lr=pick(backbone_lr, "backbone_lr"))
+        self.ema = dict(decay=pick(ema_decay, "ema_decay"), warmups=pick(ema_warmups, "ema_warmups")) if ema else None
         if ema:
             self.eng.ema_init()
+        self.grad_accum_steps = int(pick(grad_accum_steps, "grad_accum_steps"))
         self.dn_number, self.label_noise_ratio = dn_number, label_noise_ratio
         self.weights = weights
         self.seed = seed
         self.steps = 0
+        self.draws = 0
         K = self.eng.K
         sig = COCO_SIGMAS if K == 17 else CROWDPOSE_SIGMAS
         self.dn_sigmas = torch.tensor(np.concatenate([[0.1], sig]).astype(np.float32), device=self.device)
@@ -121,25 +142,26 @@ class Trainer:
         _lib.check(lib.dp_cdn_build(_p(packed.off), _p(packed.label), _p(packed.kps), _p(packed.area),
                                     _p(packed.boxes), _p(self.dn_sigmas), images.shape[0], pad, single, eng.K,
                                     self.label_noise_ratio, 80, float(h), float(w),
-                                    (self.seed * 1000003 + self.steps) & 0xFFFFFFFFFFFF, _p(plan.dn_label),
+                                    (self.seed * 1000003 + self.draws) & 0xFFFFFFFFFFFF, _p(plan.dn_label),
                                     _p(plan.dn_ref), s), "dp_cdn_build")
+        self.draws += 1
         if getattr(plan, "_mask_key", None) != (pad, groups, single):
             plan.mask.copy_(torch.from_numpy(dn_attn_mask(pad, groups, single, eng.nq).astype(np.uint8)))
             plan._mask_key = (pad, groups, single)
 
-    def step(self, images, targets, update=True):
-        """One step; returns (loss names, device tensor of the losses) (sum = the backward's loss)."""
-        eng, lib = self.eng, self.eng.lib
+    def sub_step(self, images, targets):
+        """Forward + criterion + backward of one sub-batch (engine.py:44-59): the gradients of
+        its summed losses in eng.grad_flat (overwritten). Returns (loss names, device losses)."""
+        eng = self.eng
         B = images.shape[0]
-        K, nq = eng.K, eng.nq
         memory, shapes = self._memory(images)
-        packed = pack_targets(targets, K, self.device)
+        packed = pack_targets(targets, eng.K, self.device)
         sizes = packed.sizes
         meta = dn_meta(sizes, self.dn_number)
         pad, groups, single = meta if meta else (0, 1, 1)
         full = self.scope == "full"
         plan = eng.plan(B, pad, shapes, memory=memory, d_memory=self.ep.d_memory if full else None)
-        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        self.plan = plan
         self._draw_dn(plan, packed, images, pad, groups, single)
         plan.forward()
         keys, vals = plan.criterion(packed, sizes, groups, weights=self.weights)
@@ -147,6 +169,28 @@ class Trainer:
         if full:
             self.ep.backward()
             self.bb.backward()
+        return keys, vals
+
+    def step(self, images, targets, update=True):
+        """One step of train_one_epoch (src/solver/engine.py:41-89): the batch split into
+        grad_accum_steps consecutive sub-batches, each with its own forward (DN draws, BatchNorm
+        batch statistics), criterion (matching, num_boxes) and backward, the gradients summed;
+        then DDP's gradient mean, clip_grad_norm_ + AdamW and the EMA update — skipped on the
+        device when the summed losses or the gradient norm are not finite (the reference stops
+        before optimizer.step on a non-finite loss, engine.py:62-66). Returns (loss names, device
+        tensor of the last sub-batch's losses), like the loss_dict the reference logs."""
+        eng, lib = self.eng, self.eng.lib
+        B = images.shape[0]
+        n = self.grad_accum_steps
+        if B % n:
+            raise ValueError(f"batch {B} is not divisible by grad_accum_steps {n}")
+        sub = B // n
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        eng.step_ok_reset()
+        for j in range(n):
+            keys, vals = self.sub_step(images[j * sub:(j + 1) * sub], targets[j * sub:(j + 1) * sub])
+            eng.check_finite(vals)
+            eng.accumulate_grads(first=j == 0, last=j == n - 1)
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             world = torch.distributed.get_world_size()
             if world > 1:

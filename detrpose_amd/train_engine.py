@@ -128,6 +128,8 @@ class TrainEngine:
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
         self.sqnorm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.bad = torch.zeros(1, dtype=torch.float32, device=dev)   # step guard (dp_finite_guard)
+        self.grad_acc = None   # gradient-accumulation buffer (accumulate_grads)
         self.opt_step = 0
         self.grads, self.params = {}, {}
         o = 0
@@ -142,7 +144,10 @@ class TrainEngine:
         # its own AdamW learning rate (configs/detrpose/detrpose_hgnetv2_*.py: '^(?=.*backbone).*$')
         bbn = [n for n in self.pnames if n.startswith("backbone.")]
         self.bb_end = self.offsets[bbn[-1]][1] if bbn else 0
-        assert all(self.offsets[n][1] <= self.bb_end for n in bbn)
+        nbb = len(bbn)
+        assert self.pnames[:nbb] == bbn, "backbone parameters must lead the flat buffer"
+        assert all(self.offsets[n][0] >= self.bb_end for n in self.pnames[nbb:]), \
+            "a non-backbone parameter inside the backbone learning-rate range"
         self.ema = None
         self.ema_updates = 0
         self.running = {}
@@ -151,7 +156,8 @@ class TrainEngine:
                 if n.startswith("encoder.") and (n.endswith(".running_mean") or n.endswith(".running_var")):
                     self.running[n] = b.detach().to(dev, torch.float32).clone()
         self.load_weights()
-        self.plans = {}
+        self.plans = {}          # TrainPlan per (batch, DN pad, shapes, ...), LRU order
+        self.max_plans = 6
         self.enc_plans = {}
 
     # ------------------------------------------------------------------ weights
@@ -241,12 +247,43 @@ class TrainEngine:
         self.opt_step += 1
         if max_norm and max_norm > 0:
             _lib.check(lib.dp_grad_sqnorm(_p(self.grad_flat), n, _p(self.sqnorm), s), "dp_grad_sqnorm")
+            _lib.check(lib.dp_finite_guard(_p(self.sqnorm), 1, _p(self.bad), s), "dp_finite_guard")
         for o0, o1, lr_ in ((0, self.bb_end, backbone_lr), (self.bb_end, n, lr)):
             if o1 > o0:
                 _lib.check(lib.dp_adamw(_p(self.master, o0), _p(self.grad_flat, o0), _p(self.exp_avg, o0),
                                         _p(self.exp_avg_sq, o0), o1 - o0, lr_, betas[0], betas[1], eps, weight_decay,
-                                        self.opt_step, max_norm if max_norm else 0.0, _p(self.sqnorm), s), "dp_adamw")
+                                        self.opt_step, max_norm if max_norm else 0.0, _p(self.sqnorm), _p(self.bad),
+                                        s), "dp_adamw")
         self.refresh()
+
+    def step_ok_reset(self):
+        """Clear the step guard (dp_finite_guard sets it; dp_adamw / dp_ema skip while set)."""
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(self.lib.dp_zero(_p(self.bad), 4, s), "guard reset")
+
+    def check_finite(self, vals):
+        """Set the step guard when any of the device losses `vals` is not finite."""
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(self.lib.dp_finite_guard(_p(vals), vals.numel(), _p(self.bad), s), "dp_finite_guard")
+
+    def step_skipped(self) -> bool:
+        """Whether the last optimizer step was skipped by the guard (synchronises)."""
+        return float(self.bad) != 0.0
+
+    def accumulate_grads(self, first: bool, last: bool):
+        """Gradient accumulation over sub-batches (engine.py:43-59: .grad sums over the loop's
+        backward calls): every backward overwrites grad_flat, so sub-batch j's gradient is added
+        into grad_acc, and the last one's grad_flat receives the sum (2 passes over the flat
+        buffer per step for 2 sub-batches)."""
+        if first and last:
+            return
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        n = self.grad_flat.numel()
+        if self.grad_acc is None:
+            self.grad_acc = torch.empty_like(self.grad_flat)
+        src, dst, acc = (self.grad_acc, self.grad_flat, 1) if last else (self.grad_flat, self.grad_acc, 0 if first else 1)
+        _lib.check(self.lib.dp_convert_rows(_p(src), DP_F32, n, _p(dst), DP_F32, n, 1, n, C.c_float(1.0), acc, s),
+                   "grad accumulate")
 
     def ema_init(self):
         self.ema = self.master.clone()
@@ -265,8 +302,7 @@ class TrainEngine:
         d = decay * (1 - math.exp(-self.ema_updates / warmups)) if warmups else decay
         pairs = [(self.ema, self.master)] + [(self.ema_running[k], v) for k, v in self.running.items()]
         for e, p in pairs:
-            _lib.check(lib.dp_axpby_rows(_p(e), e.numel(), _p(e), e.numel(), C.c_float(d), _p(p), p.numel(),
-                                         C.c_float(1.0 - d), 1, e.numel(), 0, DP_F32, s), "ema")
+            _lib.check(lib.dp_ema(_p(e), _p(p), e.numel(), C.c_float(d), _p(self.bad), s), "dp_ema")
 
     def state_dict_update(self, module=None):
         """Write the master parameters back into the module (reference names)."""
@@ -385,14 +421,30 @@ class TrainEngine:
             self.cur.cost(name + ".db", 4.0 * rows * N)
 
     # ------------------------------------------------------------------ plan
-    def plan(self, batch: int, pad: int, shapes, memory=None, d_memory=None) -> "TrainPlan":
+    def plan(self, batch: int, pad: int, shapes, memory=None, d_memory=None, cut_location_grads=False) -> "TrainPlan":
         """memory: an existing (B, S, C) device buffer of dtype the plan reads the encoder memory
         from (e.g. the inference plan's), instead of its own input buffer. d_memory: a (B, S, C)
-        f32 buffer the backward writes d loss / d memory into (the encoder's training step)."""
+        f32 buffer the backward writes d loss / d memory into (the encoder's training step).
+        cut_location_grads: a parity-analysis variant whose backward drops the gradient through
+        the bilinear sampling locations (MSDA's sampling offsets, the LQE's keypoints) — the
+        function's discontinuous part, so precision can be compared per parameter; never for
+        training (tests/test_gpu_full_train_step_l.py)."""
         key = (batch, pad, tuple(tuple(s) for s in shapes), memory.data_ptr() if memory is not None else None,
-               d_memory.data_ptr() if d_memory is not None else None)
-        if key not in self.plans:
-            self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes], memory, d_memory)
+               d_memory.data_ptr() if d_memory is not None else None, bool(cut_location_grads))
+        if key in self.plans:
+            self.plans[key] = self.plans.pop(key)   # most recently used last
+            return self.plans[key]
+        # the DN pad (2 x the batch's largest person count x groups) varies from batch to batch on
+        # real data: keep the max_plans most recently used plans, drop the rest (their arenas
+        # return to the caching allocator)
+        while len(self.plans) >= self.max_plans:
+            old_key = next(iter(self.plans))
+            old = self.plans.pop(old_key)
+            if hasattr(self, "_wt_ops"):
+                self._wt_ops = {k for k in self._wt_ops if k[0] != id(old)}
+            old.arena.clear()
+        self.plans[key] = TrainPlan(self, batch, pad, [tuple(s) for s in shapes], memory, d_memory,
+                                    cut_location_grads)
         return self.plans[key]
 
     def encoder_plan(self, batch: int, feat_shapes, feats=None, feats_plan=None):
@@ -418,9 +470,10 @@ class TrainEngine:
 class TrainPlan:
     """Buffers and tapes for one (batch, DN pad size, feature shapes)."""
 
-    def __init__(self, eng: TrainEngine, B: int, P: int, shapes, memory=None, d_memory=None):
+    def __init__(self, eng: TrainEngine, B: int, P: int, shapes, memory=None, d_memory=None, cut_location_grads=False):
         self.eng = eng
         self.d_memory = d_memory
+        self.cut_loc = cut_location_grads
         eng.cur = self
         self.B, self.P, self.shapes = B, P, shapes
         self.op_flops = {}
@@ -878,8 +931,11 @@ class TrainPlan:
             dst = f32(qrows, K * 5)
             eng.dgrad(bw, n + ".lqe0.dx", _p(dhq), nhid, qrows, qe + "0.weight", _p(dst), K * 5, wt=sd[qe + "0.weight"],
                       in_code=DP_F32)
+            dkps_lqe = self.d_kps[l]
+            if self.cut_loc:   # parity-analysis variant: no gradient through the sampling keypoints
+                dkps_lqe = f32(B * Qt * K * 2)
             bw.op(n + ".lqe_stats_bwd", lib.dp_lqe_stats_bwd, _p(self.memory), self.S * Cc, lv0[0], lv0[1], Cc,
-                  _p(self.kps[l]), _p(dst), B, Qt, K, _p(self.d_kps[l]), _p(dm) if dm is not None else None,
+                  _p(self.kps[l]), _p(dst), B, Qt, K, _p(dkps_lqe), _p(dm) if dm is not None else None,
                   self.S * Cc, code)
             # class head on the instance token: score = class_embed[l](output[:, :, 0])
             ck = f"{T_}class_embed.{l}.weight"
@@ -938,6 +994,10 @@ class TrainPlan:
             bw.op(n + ".msda_bwd", lib.dp_msda_bwd, _p(self.memory), B, self.S, self.lvl_hw, len(self.shapes),
                   _p(S_["oa"]), _p(self.refs[l]), _p(dx, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt,
                   _p(dm) if dm is not None else None, 1, _p(doa), None, code)
+            if self.cut_loc:   # parity-analysis variant: d sampling offsets = 0 (the location columns)
+                nof = eng.nh * eng.nlev * eng.npnt * 2
+                bw.op(n + ".cut_loc", lib.dp_convert_rows, _p(doa), DP_F32, ncol, _p(doa), DP_F32, ncol, rows, nof,
+                      C.c_float(0.0), 0)
             doa_dt, ldo = to_dt(n + ".doa", doa, rows, ncol)
             ok = lp + "cross_attn.offattn.weight"
             self._wgrad_offattn(bw, n, doa_dt, ldo, doa, rows, ok, S_["xcat"], lp)

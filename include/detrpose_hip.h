@@ -542,10 +542,18 @@ int dp_cdn_build(const int32_t* tgt_off, const int32_t* tgt_label, const float* 
 int dp_grad_sqnorm(const float* g, int64_t n, float* out, void* stream);
 /* torch.optim.AdamW step over a flat f32 parameter buffer (decoupled weight decay, bias
  * correction for `step`), after clip_grad_norm_(max_norm) (src/solver/engine.py:78-89) read
- * from grad_sqnorm on the device (max_norm <= 0: no clipping). */
+ * from grad_sqnorm on the device (max_norm <= 0: no clipping). Parameters and moments are left
+ * unchanged when *skip != 0 (skip may be NULL) or the norm is not finite: the reference stops
+ * before optimizer.step on a non-finite loss (engine.py:62-66). */
 int dp_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
              float beta2, float eps, float weight_decay, int32_t step, float max_norm, const float* grad_sqnorm,
-             void* stream);
+             const float* skip, void* stream);
+/* *bad = 1 when any of v[0..n) is not finite (unchanged otherwise): the step guard dp_adamw /
+ * dp_ema read (engine.py:62-66's math.isfinite(loss) check, on the device). */
+int dp_finite_guard(const float* v, int64_t n, float* bad, void* stream);
+/* ModelEMA.update over a flat f32 buffer (src/nn/optimizer/ema.py:55-70): ema = decay ema +
+ * (1 - decay) p, skipped when *skip != 0 (skip may be NULL). */
+int dp_ema(float* ema, const float* p, int64_t n, float decay, const float* skip, void* stream);
 /* hipMemsetAsync(p, 0, bytes) on the stream (gradient buffers at the start of a step). */
 int dp_zero(void* p, int64_t bytes, void* stream);
 /* Element conversion / copy between f32 and dtype rows (the head outputs' f32 views, gradient

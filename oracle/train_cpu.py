@@ -69,7 +69,7 @@ def _mha(x, P, p, nhead, mask=None):
     return F.linear(o, P[p + ".out_proj.weight"], P[p + ".out_proj.bias"])
 
 
-def decoder_layer(tgt, pos, ref, memory, shapes, P, p, nhead, n_levels, n_points, mask):
+def decoder_layer(tgt, pos, ref, memory, shapes, P, p, nhead, n_levels, n_points, mask, cut_loc=False):
     """DeformableTransformerDecoderLayer.forward (transformer.py:387-442), training mode.
     tgt (B, Q, 1+K, C) already carries the in-place pos of transformer.py:369 (the caller adds
     it, because the addition is visible to the previous layer's output_pose_detach)."""
@@ -87,6 +87,8 @@ def decoder_layer(tgt, pos, ref, memory, shapes, P, p, nhead, n_levels, n_points
     aw = torch.softmax(aw, -1).reshape(B, Lq, nhead, n_levels, n_points)
     norm = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32).reshape(1, 1, 1, n_levels, 1, 2)
     loc = ref.reshape(B, Lq, 1, 1, 1, 2) + off / norm
+    if cut_loc:   # parity-analysis variant (train_transformer): no gradient through the locations
+        loc = loc.detach()
     m = msda_core(memory, shapes, loc, aw).reshape(B, Q, T, C)
     g = torch.sigmoid(_lin(torch.cat([t, m], -1), P, p + ".gateway.gate"))
     g1, g2 = g.chunk(2, -1)
@@ -116,10 +118,13 @@ def dn_queries(P, dn, B, K, C):
     return tgt, ref
 
 
-def train_transformer(feats, P, cfg, dn=None, force_topk=None):
+def train_transformer(feats, P, cfg, dn=None, force_topk=None, cut_loc=False):
     """Transformer.forward in training mode (targets given => dn draws given), returning the
     reference's output dict (transformer.py:1348-1385). feats: encoder outputs (detached);
-    P: name -> tensor (reference keys, parameters as autograd leaves)."""
+    P: name -> tensor (reference keys, parameters as autograd leaves). cut_loc: the values are
+    the same, but no gradient flows through the bilinear sampling locations (MSDA's sampling
+    offsets, the LQE's keypoints) — the comparison variant detrpose_amd's TrainPlan
+    (cut_location_grads) mirrors, for per-parameter precision checks."""
     C, nhead, nq, K = cfg["hidden_dim"], cfg["nhead"], cfg["num_queries"], cfg["num_body_points"]
     nlayers, reg_max = cfg["num_decoder_layers"], cfg["reg_max"]
     reg_scale = float(cfg["reg_scale"])
@@ -163,7 +168,7 @@ def train_transformer(feats, P, cfg, dn=None, force_topk=None):
         if prev_pose_detach is not None:
             prev_pose_detach = x0[:, :, 1:].detach()   # the aliased view sees the pos add
         out = decoder_layer(x0, pos, ref, memory, shapes, P, f"{T_}decoder.layers.{l}", nhead,
-                            cfg["num_feature_levels"], cfg["dec_n_points"], mask)
+                            cfg["num_feature_levels"], cfg["dec_n_points"], mask, cut_loc)
         pose, inst = out[:, :, 1:], out[:, :, 0]
         if l == 0:
             pre_poses = torch.sigmoid(_mlp(pose, P, T_ + "pre_pose_embed", 3) + inverse_sigmoid(ref_kp))
@@ -177,7 +182,7 @@ def train_transformer(feats, P, cfg, dn=None, force_topk=None):
         d = F.linear(prob, project[None]).reshape(B, Qt, K, 2)
         kps = ref_init + d / abs(reg_scale)
         score = _lin(inst, P, f"{T_}class_embed.{l}")
-        logit = lqe(score, kps, feat0, P, f"{T_}lqe_embed.{l}")
+        logit = lqe(score, kps.detach() if cut_loc else kps, feat0, P, f"{T_}lqe_embed.{l}")
         poses.append(kps)
         logits.append(logit)
         corners_l.append(corners)

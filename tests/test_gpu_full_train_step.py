@@ -132,20 +132,21 @@ def test_full_step_running_stats(full):
         np.testing.assert_allclose(eng.running[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
 
 
-def test_full_step_bf16_tracks_fp32(full):
-    """bf16 activations / activation gradients through the whole network: losses within 5 % of
-    the reference's on average and 25 % at worst (the encoder-step test's rule: bf16 changes which
-    queries the two-stage top-k selects, SURVEY.md §0 note 5, so single losses move; measured
-    worst 0.017 (r4m) and 0.065 (r4n) on different boxes), flat gradient within cosine 0.98 of
-    the fp32 step's."""
-    g, eng32, *_ = full
-    eng, bb, ep, losses = run_full(g, "bf16")
-    ref = dict(zip([str(k) for k in g["loss_keys"]], g["loss_vals"]))
-    errs = {k: abs(losses[k] - ref[k]) / max(abs(ref[k]), 1.0) for k in ref}
-    worst, mean = max(errs.values()), sum(errs.values()) / len(errs)
-    a = eng.grad_flat.double().cpu().numpy()
-    b = eng32.grad_flat.double().cpu().numpy()
-    cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
-    print(f"bf16 full step: loss rel err mean {mean:.3g} worst {worst:.3g}, gradient cosine {cos:.6f}")
-    print(sorted(((round(v, 4), k) for k, v in errs.items()), reverse=True)[:6])
-    assert mean <= 5e-2 and worst <= 0.25 and cos >= 0.98
+def test_full_step_bf16_per_parameter_forced_selection(golden_dir):
+    """bf16 activations / activation gradients through the whole N network against the fp32
+    oracle run on the bf16 step's own two-stage selection and per-head matchings, the location
+    gradients cut on both sides (tests/test_gpu_full_train_step_l.py: the sampling-location
+    derivative jumps at pixel boundaries, so a bf16-sized change of the forward scrambles it;
+    its kernels are pinned by their own bf16 tests): every loss within 3 % (measured 1.4 %) and EACH parameter's
+    gradient within its family's relative L2 bound (BF16_BOUNDS; the flat-gradient cosine this
+    replaces let a 127 %-off tgt_embed gradient through)."""
+    from test_gpu_full_train_step_l import check_bf16_families, forced_per_parameter, loss_errors, \
+        per_parameter_table, run_full_accum
+    g = np.load(os.path.join(golden_dir, "train_full_n_b2.npz"))
+    r = run_full_accum(g, "n", dtype="bf16", split=False, cut=True)
+    lds, rel = forced_per_parameter(g, "n", r)
+    worst = loss_errors(g, r, lds)
+    print("bf16 (cut) vs forced fp32 oracle, worst losses:", worst[:5])
+    fam = per_parameter_table(rel, "N bf16 cut")
+    assert worst[0][0] <= 3e-2, worst[:5]
+    check_bf16_families(fam, "n")

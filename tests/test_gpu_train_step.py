@@ -190,8 +190,50 @@ def test_adamw_clip_matches_torch():
         opt.step()
         _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), s), "sq")
         _lib.check(lib.dp_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8,
-                                1e-4, step, 0.1, sq.data_ptr(), s), "adamw")
+                                1e-4, step, 0.1, sq.data_ptr(), None, s), "adamw")
     assert torch.allclose(p, ref.detach(), atol=1e-6, rtol=1e-5), (p - ref).abs().max()
+
+
+def test_step_guard_skips_non_finite_updates():
+    """dp_finite_guard + dp_adamw / dp_ema: a NaN among the losses (or a non-finite gradient
+    norm) leaves parameters, moments and the EMA unchanged (engine.py:62-66 stops before
+    optimizer.step); finite values update as usual."""
+    import ctypes as C
+    from detrpose_amd import _lib
+    lib = _lib.load()
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    n = 1000
+    p = torch.randn(n, device="cuda")
+    m, v, e = torch.zeros_like(p), torch.zeros_like(p), p.clone()
+    g = torch.randn(n, device="cuda")
+    sq, bad = torch.zeros(1, device="cuda"), torch.zeros(1, device="cuda")
+    losses = torch.tensor([1.0, float("nan"), 2.0], device="cuda")
+    p0 = p.clone()
+    _lib.check(lib.dp_finite_guard(losses.data_ptr(), 3, bad.data_ptr(), s), "guard")
+    _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), s), "sq")
+    _lib.check(lib.dp_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1,
+                            0.1, sq.data_ptr(), bad.data_ptr(), s), "adamw")
+    _lib.check(lib.dp_ema(e.data_ptr(), g.data_ptr(), n, 0.5, bad.data_ptr(), s), "ema")
+    torch.cuda.synchronize()
+    assert float(bad) == 1.0 and torch.equal(p, p0) and torch.equal(e, p0) and not m.any() and not v.any()
+    # a NaN gradient: the norm is NaN, the update is skipped even without the flag
+    g2 = g.clone()
+    g2[7] = float("nan")
+    _lib.check(lib.dp_grad_sqnorm(g2.data_ptr(), n, sq.data_ptr(), s), "sq")
+    _lib.check(lib.dp_adamw(p.data_ptr(), g2.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1,
+                            0.1, sq.data_ptr(), None, s), "adamw")
+    torch.cuda.synchronize()
+    assert torch.equal(p, p0) and not m.any()
+    bad.zero_()
+    ok = torch.tensor([1.0, 2.0], device="cuda")
+    _lib.check(lib.dp_finite_guard(ok.data_ptr(), 2, bad.data_ptr(), s), "guard")
+    _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), s), "sq")
+    _lib.check(lib.dp_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1,
+                            0.1, sq.data_ptr(), bad.data_ptr(), s), "adamw")
+    _lib.check(lib.dp_ema(e.data_ptr(), g.data_ptr(), n, 0.5, bad.data_ptr(), s), "ema")
+    torch.cuda.synchronize()
+    assert float(bad) == 0.0 and not torch.equal(p, p0)
+    torch.testing.assert_close(e, 0.5 * p0 + 0.5 * g)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

@@ -1,0 +1,133 @@
+"""Trainer.step at world size 2 (DDP, src/misc/dist_utils.py:111-133; the engine loop
+src/solver/engine.py:41-89): two ranks on the one GPU (gloo, host-staged collectives) each train
+on one image of a two-image batch; one process trains on both. With equal person counts per image
+(so both ranks build the same DN pad and groups as the one-process batch, dn_component.py:54-63)
+and the same DN draws, DDP's semantics make the runs equal:
+
+  * each rank's losses are its own terms over num_boxes / num_boxes_go all-reduced and divided
+    by the world size (criterion.py:306-323), so the ranks' mean loss is the one-process loss;
+  * the all-reduced mean of the ranks' gradients is the one-process gradient;
+  * SyncBatchNorm: the BatchNorm statistics and running statistics are the whole batch's;
+  * clip_grad_norm_ + AdamW + ModelEMA on equal gradients leave equal parameters and EMA.
+
+fp32, DETRPose-N, ranks spawned as separate processes (each loads the HIP library)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+WORLD = 2
+SIZES = [2, 2]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _targets(dev):
+    g = torch.Generator().manual_seed(21)
+    out = []
+    for b, n in enumerate(SIZES):
+        c = torch.rand(n, 2, generator=g) * 0.6 + 0.2
+        wh = torch.rand(n, 2, generator=g) * 0.3 + 0.05
+        xy = (c[:, None] + (torch.rand(n, 17, 2, generator=g) - 0.5) * wh[:, None]).clamp(0, 1)
+        vis = (torch.rand(n, 17, generator=g) > 0.25).float()
+        out.append({"labels": ((torch.arange(n) + b) % 2).to(dev), "boxes": torch.cat([c - wh / 2, c + wh / 2], 1).to(dev),
+                    "keypoints": torch.cat([xy.flatten(1), vis], 1).to(dev), "area": (wh.prod(1) * 0.53).to(dev)})
+    return out
+
+
+def _run(rows, dn=None):
+    """Trainer.step (fp32, scope 'full') on the images `rows` of the two-image batch. dn: the DN
+    draws (labels, refs, mask) of the one-process run to feed in (rows of it); None: draw them
+    (dp_cdn_build) and return them."""
+    from detrpose_amd import build_model
+    from detrpose_amd.synthetic import load_synthetic, synthetic_images
+    from detrpose_amd.train import Trainer
+    dev = torch.device("cuda", 0)
+    model, _ = build_model("n", dtype="fp32")
+    load_synthetic(model, seed=0)
+    tr = Trainer(model, dtype="fp32", device=dev, grad_accum_steps=1)
+    images = synthetic_images(2, seed=1).to(dev)[rows]
+    ts = _targets(dev)[rows]
+    drawn = {}
+    orig = tr._draw_dn
+
+    def draw(plan, packed, images_, pad, groups, single):
+        orig(plan, packed, images_, pad, groups, single)
+        if dn is None:
+            drawn.update(label=plan.dn_label.cpu().numpy(), ref=plan.dn_ref.cpu().numpy(), mask=plan.mask.cpu().numpy(),
+                         pad=pad)
+        else:
+            assert pad == dn["pad"]
+            plan.set_dn(torch.as_tensor(dn["label"][rows]).to(dev), torch.as_tensor(dn["ref"][rows]).to(dev),
+                        torch.as_tensor(dn["mask"]).to(dev))
+
+    tr._draw_dn = draw
+    keys, vals = tr.step(images, ts)
+    torch.cuda.synchronize()
+    eng = tr.eng
+    return {"keys": keys, "losses": vals.cpu().numpy(), "grad": eng.grad_flat.cpu().numpy(),
+            "master": eng.master.cpu().numpy(), "ema": eng.ema.cpu().numpy(),
+            "running": {k: v.cpu().numpy() for k, v in eng.running.items()}, "dn": drawn}
+
+
+def _rank_main(rank, port, dn, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    try:
+        torch.distributed.init_process_group("gloo", rank=rank, world_size=WORLD)
+        torch.cuda.set_device(0)
+        r = _run(slice(rank, rank + 1), dn)
+        q.put((rank, r))
+        torch.distributed.barrier()
+    finally:
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
+
+
+def test_trainer_step_two_ranks_equal_one_process():
+    ref = _run(slice(0, 2))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, port, ref["dn"], q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # losses: the ranks' mean is the one-process value (num_boxes all-reduced / world)
+    mean = (res[0]["losses"].astype(np.float64) + res[1]["losses"]) / 2
+    rel = np.abs(mean - ref["losses"]) / np.maximum(np.abs(ref["losses"]), 1.0)
+    worst = int(np.argmax(rel))
+    print(f"losses: ranks' mean vs one process, worst rel err {rel[worst]:.3g} ({ref['keys'][worst]})")
+    assert res[0]["keys"] == ref["keys"]
+    assert rel.max() <= 1e-4
+    # the all-reduced mean gradient (identical on both ranks) vs the one-process gradient
+    g0, g1, gr = res[0]["grad"], res[1]["grad"], ref["grad"]
+    assert np.array_equal(g0, g1)
+    e = float(np.abs(g0 - gr).max() / np.abs(gr).max())
+    l2 = float(np.linalg.norm(g0 - gr) / np.linalg.norm(gr))
+    print(f"DDP mean gradient vs one process: max {e:.3g} of scale, rel L2 {l2:.3g}")
+    assert e <= 1e-3 and l2 <= 1e-3
+    # parameters after clip + AdamW and the EMA: identical across ranks, equal to one process
+    for k in ("master", "ema"):
+        assert np.array_equal(res[0][k], res[1][k]), k
+        d = np.abs(res[0][k] - ref[k])
+        frac = float((d > 1e-6).mean())
+        print(f"{k}: max |rank - one process| {d.max():.3g}, fraction above 1e-6 {frac:.3g}")
+        # the first AdamW step moves a parameter by ~lr (1e-4) x g / (|g| + eps): an entry whose
+        # gradient is ~0 (rounding-level, sign not determined) may move either way, by <= 2 lr
+        assert d.max() <= 2.5e-4 and frac <= 1e-3, k
+    for k, v in ref["running"].items():
+        np.testing.assert_allclose(res[0]["running"][k], v, rtol=1e-4, atol=1e-6, err_msg=k)
+        np.testing.assert_array_equal(res[0]["running"][k], res[1]["running"][k], err_msg=k)

@@ -207,12 +207,18 @@ def sub_dn_inputs(g, p):
             "num_group": int(g[p + "dn_num_group"])}
 
 
-def oracle_train_step_full(size, g, dtype=torch.float32):
+def oracle_train_step_full(size, g, dtype=torch.float32, force=None, split=True, cut_loc=False):
     """The whole of config 5 on the oracle: backbone (FrozenBatchNorm2d, every conv and LAB
     parameter trained: freeze_at=-1), encoder in training mode, transformer with the golden DN
     draws, criterion, backward — once per sub-batch of the fixture, gradients accumulated
     (engine.py:43-59). Returns (per-sub-batch losses, grads keyed like the golden, per-sub-batch
-    backbone outputs, per-sub-batch encoder outputs, running stats)."""
+    backbone outputs, per-sub-batch encoder outputs, running stats).
+
+    force: per sub-batch {"topk": (B, nq) two-stage indices, "match": (H, B, nq) per-head
+    assignments} to use instead of the oracle's own (the bf16 step's selection, so a bf16 run is
+    compared query by query); split=False runs the whole network in one graph even when the
+    fixture holds the reference's d memory; cut_loc: train_transformer's variant without the
+    gradient through the sampling locations."""
     cfg = get_config(size)
     model, _ = build_model(size)
     params = {k for k, v in model.named_parameters() if v.requires_grad}
@@ -230,7 +236,7 @@ def oracle_train_step_full(size, g, dtype=torch.float32):
     prev = torch.get_default_dtype()
     torch.set_default_dtype(dtype)   # the oracle's freshly made tensors (zeros, anchors) in dtype
     try:
-        _full_sub_batches(g, P, images, stats, cfg, bc, sizes, lab, kps, area, lds, bbs, encs)
+        _full_sub_batches(g, P, images, stats, cfg, bc, sizes, lab, kps, area, lds, bbs, encs, force, split, cut_loc)
     finally:
         torch.set_default_dtype(prev)
     grads = {}
@@ -240,16 +246,26 @@ def oracle_train_step_full(size, g, dtype=torch.float32):
     return lds, grads, bbs, encs, stats
 
 
-def _full_sub_batches(g, P, images, stats, cfg, bc, sizes, lab, kps, area, lds, bbs, encs):
+def _full_sub_batches(g, P, images, stats, cfg, bc, sizes, lab, kps, area, lds, bbs, encs, force=None, split=True,
+                      cut_loc=False):
     from oracle.detrpose_cpu import backbone
     from oracle.train_cpu import losses, train_encoder, train_transformer
     own_match = []
     dmems = []
     K, ncls = cfg["transformer"]["num_body_points"], cfg["transformer"]["num_classes"]
-    for rs, ts, p in sub_batches(g):
+    for j, (rs, ts, p) in enumerate(sub_batches(g)):
         feats = backbone(images[rs], P, bc["name"], bc["return_idx"], bc["use_lab"])
         enc = train_encoder(feats, P, cfg["encoder"], stats)
-        if p + "dmem" in g.files:
+        if force is not None:
+            res = train_transformer(enc, P, cfg["transformer"], dn=sub_dn_inputs(g, p), force_topk=force[j]["topk"],
+                                    cut_loc=cut_loc)
+            ld, _, _ = losses(res, sizes[rs], lab[ts], kps[ts], area[ts], K, ncls, force_match=force[j]["match"])
+            sum(ld.values()).backward()
+            lds.append(ld)
+            bbs.append([f.detach() for f in feats])
+            encs.append([e.detach() for e in enc])
+            continue
+        if split and p + "dmem" in g.files:
             # split at the encoder output (see full_step_split): the transformer on detached encoder
             # outputs (its own d memory kept), then the encoder + backbone backward driven by the
             # reference's d memory
