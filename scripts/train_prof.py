@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--out", default="gpurun_out/train_ops.json")
+    ap.add_argument("--accum", type=int, default=None, help="grad_accum_steps (default: the config's)")
     a = ap.parse_args()
     from bench import synthetic_targets
     from detrpose_amd import build_model
@@ -55,7 +56,7 @@ def main():
     dev = torch.device("cuda")
     model, _ = build_model(a.size, dtype=a.dtype)
     load_synthetic(model, 0)
-    tr = Trainer(model, dtype=a.dtype, device=dev)
+    tr = Trainer(model, dtype=a.dtype, device=dev, grad_accum_steps=a.accum)
     images = synthetic_images(a.batch, seed=11).to(dev)
     ts = synthetic_targets(a.batch, dev=dev)
     for _ in range(2):
@@ -65,16 +66,18 @@ def main():
     tr.step(images, ts)
     torch.cuda.synchronize()
     step_ms = (time.perf_counter() - t0) * 1e3
-    plan = next(iter(tr.eng.plans.values()))
+    plan = tr.plan   # the last sub-batch's
+    sub = a.batch // tr.grad_accum_steps
     tapes = {"backbone_fwd": tr.bb.fw, "encoder_fwd": tr.ep.fw, "transformer_fwd": plan.fw,
              "transformer_bwd": plan.bw, "encoder_bwd": tr.ep.bw, "backbone_bwd": tr.bb.bw}
-    out = {"size": a.size, "batch": a.batch, "dtype": a.dtype, "step_ms": round(step_ms, 2), "tapes": {}}
+    out = {"size": a.size, "batch": a.batch, "grad_accum_steps": tr.grad_accum_steps, "dtype": a.dtype,
+           "step_ms": round(step_ms, 2), "tapes_of_one_sub_batch": sub, "tapes": {}}
     allops = []
     for tname, tape in tapes.items():
         if tname == "transformer_bwd":   # the backward reads the criterion's hand-off
             from detrpose_amd.criterion import pack_targets
             from detrpose_amd.train import dn_meta
-            packed = pack_targets(ts, 17, dev)
+            packed = pack_targets(ts[a.batch - sub:], 17, dev)
             plan.criterion(packed, packed.sizes, dn_meta(packed.sizes)[1])
         ops = timed_run(tape)
         fam = {}
