@@ -885,6 +885,19 @@ extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, flo
     }                                                                                                     \
   } while (0)
 
+// bf16 MFMA kernels for sequences of <= 128 tokens (train_attn.hip); false = not covered
+bool dp_attn_fwd_mfma(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out, int32_t ld_o,
+                      float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
+                      int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, float scale, hipStream_t s);
+bool dp_attn_bwd_mfma(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, const float* p_save,
+                      const void* dout, const void* out, int32_t ld_o, void* dq, int32_t ld_dq, void* dk, void* dv,
+                      int32_t ld_dkv, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si, int64_t st,
+                      int32_t seqlen, int32_t nhead, int32_t dh, float scale, hipStream_t s);
+static bool attn_scalar_forced() {   // A/B switch: DETRPOSE_ATTN_SCALAR=1 keeps the scalar bf16 kernels
+  static const bool f = getenv("DETRPOSE_ATTN_SCALAR") != nullptr;
+  return f;
+}
+
 extern "C" int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out,
                            int32_t ld_o, float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner,
                            int64_t so, int64_t si, int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, int32_t dtype,
@@ -896,6 +909,10 @@ extern "C" int dp_attn_fwd(const void* q, int32_t ld_q, const void* k, const voi
   const float scale = 1.f / sqrtf((float)dh);
   dim3 grid((unsigned)(n_outer * n_inner * nhead), (unsigned)((seqlen + ACH - 1) / ACH));
   hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16 && !attn_scalar_forced() &&
+      dp_attn_fwd_mfma(q, ld_q, k, v, ld_kv, out, ld_o, p_save, mask, n_outer, n_inner, so, si, st, seqlen, nhead, dh,
+                       scale, s))
+    return dp_check_launch("dp_attn_fwd");
   if (dtype == DP_BF16)
     ATT_LAUNCH(attn_fwd_kernel, bf16_t, grid, dim3(64), 0, s, (const bf16_t*)q, ld_q, (const bf16_t*)k,
                        (const bf16_t*)v, ld_kv, (bf16_t*)out, ld_o, p_save, mask, n_inner, so, si, st, seqlen, nhead,
@@ -918,6 +935,10 @@ extern "C" int dp_attn_bwd(const void* q, int32_t ld_q, const void* k, const voi
   const float scale = 1.f / sqrtf((float)dh);
   dim3 grid((unsigned)(n_outer * n_inner * nhead), (unsigned)((seqlen + ACH - 1) / ACH));
   hipStream_t s = as_stream(stream);
+  if (dtype == DP_BF16 && !attn_scalar_forced() &&
+      dp_attn_bwd_mfma(q, ld_q, k, v, ld_kv, p_save, dout, out, ld_o, dq, ld_dq, dk, dv, ld_dkv, n_outer, n_inner, so,
+                       si, st, seqlen, nhead, dh, scale, s))
+    return dp_check_launch("dp_attn_bwd");
   if (dtype == DP_BF16) {
     ATT_LAUNCH(attn_bwd_q_kernel, bf16_t, grid, dim3(64), 0, s, (const bf16_t*)k, (const bf16_t*)v, ld_kv,
                        p_save, (const bf16_t*)dout, (const bf16_t*)out, ld_o, (bf16_t*)dq, ld_dq, n_inner, so, si, st,

@@ -136,6 +136,54 @@ def test_attention_fwd_bwd(L, dh, masked):
     assert torch.allclose(dqkv, q.grad, atol=1e-4), (dqkv - q.grad).abs().max()
 
 
+@pytest.mark.parametrize("L,dh,masked", [(18, 32, False), (18, 16, False), (60, 32, True), (96, 32, True),
+                                          (101, 32, True), (128, 48, False), (33, 64, True)])
+def test_attention_fwd_bwd_bf16_mfma(L, dh, masked):
+    """The bf16 MFMA attention kernels (csrc/train_attn.hip: sequences <= 128 tokens, the decoder's
+    within (18) and across (60 + DN) attentions) against torch fp32 autograd on the same bf16
+    inputs: outputs within 1e-2 and dq / dk / dv within 2e-2 of their scale (bf16 P and dS as MFMA
+    operands; measured ~3e-3 / ~6e-3), P saved equal to the softmax within 2e-3."""
+    lib = _lib.load()
+    torch.manual_seed(4)
+    nh, B, Ti = 4, 2, 3
+    Cc = nh * dh
+    rows = B * Ti * L
+    qkv = torch.randn(rows, 3 * Cc, device=DEV).to(torch.bfloat16)
+    mask = (torch.rand(L, L, device=DEV) < 0.3) if masked else torch.zeros(L, L, dtype=torch.bool, device=DEV)
+    mask.fill_diagonal_(False)
+    if masked:
+        mask[L // 2] = True   # one query sees nothing: P = 0, O = 0 (the scalar kernel's convention)
+    out = torch.empty(rows, Cc, device=DEV, dtype=torch.bfloat16)
+    P = torch.empty(B * Ti * nh * L * L, device=DEV)
+    m8 = mask.to(torch.uint8).contiguous()
+    args = (B, Ti, L * Ti, 1, Ti, L, nh, dh, DP_BF16)
+    _lib.check(lib.dp_attn_fwd(qkv.data_ptr(), 3 * Cc, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), 3 * Cc,
+                               out.data_ptr(), Cc, P.data_ptr(), m8.data_ptr() if masked else None, *args, _s()), "attn")
+    q = qkv.float().detach().clone().requires_grad_(True)
+    x = q.view(B, L, Ti, 3, nh, dh).permute(3, 0, 2, 4, 1, 5)
+    sc = (x[0] / dh ** 0.5) @ x[1].transpose(-1, -2)
+    sc = sc.masked_fill(mask, float("-inf"))
+    pr = torch.nan_to_num(torch.softmax(sc, -1), nan=0.0)
+    o = pr @ x[2]
+    ref = o.permute(0, 3, 1, 2, 4).reshape(rows, Cc)
+    torch.cuda.synchronize()
+    e_o = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    e_p = (P.view(B, Ti, nh, L, L).transpose(-1, -2) - pr).abs().max().item()
+    dout = torch.randn(rows, Cc, device=DEV).to(torch.bfloat16)
+    ref.backward(dout.float())
+    dqkv = torch.empty(rows, 3 * Cc, device=DEV, dtype=torch.bfloat16)
+    _lib.check(lib.dp_attn_bwd(qkv.data_ptr(), 3 * Cc, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), 3 * Cc,
+                               P.data_ptr(), dout.data_ptr(), out.data_ptr(), Cc, dqkv.data_ptr(), 3 * Cc,
+                               dqkv[:, Cc:].data_ptr(), dqkv[:, 2 * Cc:].data_ptr(), 3 * Cc, *args, _s()), "attn_bwd")
+    torch.cuda.synchronize()
+    errs = []
+    for part in range(3):
+        g, r = dqkv[:, part * Cc:(part + 1) * Cc].float(), q.grad[:, part * Cc:(part + 1) * Cc]
+        errs.append((g - r).abs().max().item() / r.abs().max().item())
+    print(f"L={L} dh={dh} masked={masked}: out {e_o:.3g}, P {e_p:.3g}, dq/dk/dv {[round(e, 5) for e in errs]}")
+    assert e_o <= 1e-2 and e_p <= 2e-3 and max(errs) <= 2e-2
+
+
 def test_gate_fwd_bwd():
     lib = _lib.load()
     torch.manual_seed(4)
