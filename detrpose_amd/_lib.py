@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DETRPOSE_HIP_LIB", os.path.join(_HERE, "lib", "libdetrpose_hip.so"))
 
 DP_F32, DP_BF16 = 0, 1
+DP_SQNORM_PARTS = 1024   # dp_grad_sqnorm's out holds 1 + DP_SQNORM_PARTS floats
 DP_ACT_NONE, DP_ACT_RELU, DP_ACT_SILU, DP_ACT_GELU = 0, 1, 2, 3
 DP_MSDA_OFFATTN_F32 = 0x100
 ACT = {None: 0, "none": 0, "relu": 1, "silu": 2, "gelu": 3}
@@ -98,6 +99,9 @@ _SIGS = {
     "dp_msda_core_fwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "dp_msda_core_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, i32, vp]),
     "dp_msda_bwd": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, i32, vp]),
+    "dp_msda_bwd_ws_bytes": (i64, [i32, i32, vp, i32, i32, i32, i32]),
+    "dp_msda_bwd_sorted": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, i64,
+                                 i32, vp]),
     "dp_topk": (i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
     "dp_class_max": (i32, [vp, i32, i32, vp, vp, i32, vp, i32, vp]),
     "dp_gather_rows": (i32, [vp, i64, vp, i32, i32, i32, vp, i32, vp]),

@@ -15,6 +15,8 @@
 // the inference path), loc [N][Lq][nH][L][P][2], attn [N][Lq][nH][L][P], out / grad_out
 // [N][Lq][nH*Dh]. Lanes: CPT consecutive lanes own one (token, head), 16 bytes of channels
 // each; the three per-point dot products are reduced over those lanes with shuffles.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -333,6 +335,482 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_cl_kernel(const T* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same backward with the value gradient summed WITHOUT float atomics (dp_msda_bwd_sorted).
+// The atomic kernel above is bound by the chip's global float-atomic rate: every (token, head,
+// point, corner) adds a dh-float row segment (340 M f32 adds per DETRPose-L b16 layer, ~1 ms).
+// Here each sampling point is filed under its CELL, the top-left corner (x0, y0) of its bilinear
+// footprint (x0 in [-1, W-1], y0 in [-1, H-1]: a (W+1) x (H+1) grid per level), and a value pixel
+// (x, y) sums the lists of the four cells whose footprint covers it, as corner k of each:
+// (x - (k & 1), y - (k >> 1)) for k = 00, 01, 10, 11. Per segment (image, head):
+//   KS msda_sort_kernel        one block per (segment, level), all in LDS: the softmax statistics
+//                              of the segment's tokens; count the level's points per cell (LDS
+//                              int atomics), scan, place (token, a, fx, fy) entries in cell order
+//                              (a second atomic pass on the scanned cursors), copy the cell-ordered
+//                              list out coalesced; offsets / counts per cell; the work items
+//                              (pixel, chunk of <= SORT_CHUNK entries of its four lists)
+//   K2 msda_sorted_bwd_kernel  the gather backward for d offsets, d logits, d ref (16-byte lanes;
+//                              each lane keeps the results of every cpt-th point and stores them
+//                              at the end, so a wave's stores are contiguous runs)
+//   K3 msda_value_sum_kernel   per item: sum over the pixel's four lists of
+//                              a * w_k(fx, fy) * grad_out[token row, head] in registers, then ONE
+//                              read-add-write of the pixel's dh-float segment (float atomics only
+//                              for the rare pixels whose lists span several items)
+// No global counters and no scattered list writes: the sort lives in LDS. Work is mapped
+// segment-major with every segment's blocks on one XCD (workgroup i runs on XCD i % 8), so a
+// segment's value rows, lists and grad_out slice stay in one L2. K2 is independent of KS / K3.
+constexpr int SORT_CHUNK = 32;   // list entries per K3 round (one per lane slot)
+constexpr int SORT_ITEM = 256;   // list entries per K3 work item (a hot pixel's lists split in items
+                                 // of this size meet in float atomics)
+
+struct SortWs {
+  float4* list;        // [NS][L * lq * P] (token as int bits, a, fx, fy) in cell order (level-major)
+  int4* item;          // [NS][isz][2] (pixel | chunk, list prefixes, entries, list bases), level-major
+  int32_t* nitem;      // [NS][L]
+  int isz;
+  int spx, segmap;     // segments per XCD; 1 (default): XCD x serves segments [x * spx, (x + 1) * spx)
+                       // (whole images per XCD), 0: segments s = x mod 8 (one head per XCD)
+  int ibase[MAXL];     // first item slot of each level
+  int bps[MAXL];       // K3 blocks per (segment, level)
+};
+
+// <a, b> over one 16-byte lane slice: bf16 pairs on v_dot2 (f32 accumulate), f32 on FMA
+__device__ __forceinline__ float corner_dot(const Vec16<bf16_t>& a, const Vec16<bf16_t>& b) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const uint4 x = *reinterpret_cast<const uint4*>(&a.v), y = *reinterpret_cast<const uint4*>(&b.v);
+  float acc = 0.f;
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, x.x), __builtin_bit_cast(bf2, y.x), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, x.y), __builtin_bit_cast(bf2, y.y), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, x.z), __builtin_bit_cast(bf2, y.z), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, x.w), __builtin_bit_cast(bf2, y.w), acc, false);
+  return acc;
+}
+__device__ __forceinline__ float corner_dot(const Vec16<float>& a, const Vec16<float>& b) {
+  return a.v[0] * b.v[0] + a.v[1] * b.v[1] + a.v[2] * b.v[2] + a.v[3] * b.v[3];
+}
+
+// lane g0 + s of the lane's G-lane group (G <= 4: one DPP quad permute; else ds_bpermute)
+template <int G>
+__device__ __forceinline__ int group_bcast(int v, int s, int g0) {
+  if constexpr (G == 4) {
+    switch (s) {
+      case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xf, 0xf, false);
+      case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xf, 0xf, false);
+      case 2: return __builtin_amdgcn_mov_dpp(v, 0xaa, 0xf, 0xf, false);
+      default: return __builtin_amdgcn_mov_dpp(v, 0xff, 0xf, 0xf, false);
+    }
+  } else if constexpr (G == 2) {
+    return s == 0 ? __builtin_amdgcn_mov_dpp(v, 0xa0, 0xf, 0xf, false)    // [0, 0, 2, 2]
+                  : __builtin_amdgcn_mov_dpp(v, 0xf5, 0xf, 0xf, false);   // [1, 1, 3, 3]
+  } else if constexpr (G == 1) {
+    return v;
+  } else {
+    return __shfl(v, g0 + s, 64);
+  }
+}
+
+__device__ __forceinline__ int seg_of(int xcd, int k, int spx, int segmap) {
+  return segmap ? xcd * spx + k : k * 8 + xcd;
+}
+
+__device__ __forceinline__ void msda_xy(float rx, float ry, float ox, float oy, int H, int W, float& x, float& y) {
+#pragma clang fp contract(off)
+  x = (rx + ox / W) * W - 0.5f;
+  y = (ry + oy / H) * H - 0.5f;
+}
+
+// exclusive prefix of v over a 1024-thread block; the block total to `total`
+__device__ __forceinline__ int block_excl_scan(int v, int* wsum, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int s = wsum[i];
+    pre += i < w ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  total = tot;
+  return pre + x - v;
+}
+
+// LDS: softmax (max, 1/den) [lq] float2 | cell offsets [ncell + 1] int (counts, then offsets,
+// then cursors). Each thread owns the points tid + u * 1024 (u < PPT) of the level and keeps their
+// cell, fractions and logit in registers between the two passes; every loop issues all its loads
+// before the first use.
+constexpr int SORT_PPT = 8;   // points per thread: lq * P <= 8192
+
+__global__ __launch_bounds__(1024) void msda_sort_kernel(TLevels lv, int L, int P, const float* __restrict__ oa,
+                                                         const float* __restrict__ ref, int lq, int nh, int nseg,
+                                                         SortWs ws) {
+  extern __shared__ float2 smx[];
+  __shared__ int wsum[16];
+  const int xcd = blockIdx.x & 7, i = blockIdx.x >> 3;
+  const int seg = seg_of(xcd, i / L, ws.spx, ws.segmap), l = i - (i / L) * L;
+  if (seg >= nseg) return;
+  const int b = seg / nh, h = seg - b * nh;
+  const int H = lv.h[l], W = lv.w[l], W1 = W + 1, ncell = (H + 1) * W1;
+  const int LP = L * P, npt = lq * P, tid = threadIdx.x;
+  const int ncol = nh * LP * 3;
+  const float* oab = oa + (int64_t)b * lq * ncol;
+  int* cnt = reinterpret_cast<int*>(smx + lq);
+  for (int c = tid; c <= ncell; c += 1024) cnt[c] = 0;
+  for (int t = tid; t < lq; t += 1024) {   // softmax over the token's L*P (<= 16) logits of head h
+    const float* lg = oab + (int64_t)t * ncol + nh * LP * 2 + h * LP;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = lg[min(j, LP - 1)];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mx = j < LP ? fmaxf(mx, v[j]) : mx;
+    float den = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) den += j < LP ? expf(v[j] - mx) : 0.f;
+    smx[t] = make_float2(mx, 1.f / den);
+  }
+  // pass 1: the cells of this thread's points
+  int key[SORT_PPT];
+  float pfx[SORT_PPT], pfy[SORT_PPT], plg[SORT_PPT];
+  {
+    float rx[SORT_PPT], ry[SORT_PPT], ox[SORT_PPT], oy[SORT_PPT];
+#pragma unroll
+    for (int u = 0; u < SORT_PPT; ++u) {
+      const int pt = min(tid + u * 1024, npt - 1);
+      const int t = pt / P, j = l * P + pt - t * P;
+      const float* orow = oab + (int64_t)t * ncol;
+      rx[u] = ref[2 * (b * lq + t)];
+      ry[u] = ref[2 * (b * lq + t) + 1];
+      ox[u] = orow[(h * LP + j) * 2];
+      oy[u] = orow[(h * LP + j) * 2 + 1];
+      plg[u] = orow[nh * LP * 2 + h * LP + j];
+    }
+#pragma unroll
+    for (int u = 0; u < SORT_PPT; ++u) {
+      float x, y;
+      msda_xy(rx[u], ry[u], ox[u], oy[u], H, W, x, y);
+      const float fx0 = floorf(x), fy0 = floorf(y);
+      const int x0 = (int)fx0, y0 = (int)fy0;
+      pfx[u] = x - fx0;
+      pfy[u] = y - fy0;
+      key[u] = tid + u * 1024 < npt && x0 >= -1 && x0 < W && y0 >= -1 && y0 < H ? (y0 + 1) * W1 + x0 + 1 : -1;
+    }
+  }
+  __syncthreads();   // counters zeroed
+#pragma unroll
+  for (int u = 0; u < SORT_PPT; ++u)
+    if (key[u] >= 0) atomicAdd(cnt + key[u], 1);
+  __syncthreads();
+  // counts -> exclusive offsets (a contiguous range per thread), cnt[ncell] = the total
+  const int per = (ncell + 1023) / 1024, c0 = min(ncell, tid * per), c1 = min(ncell, c0 + per);
+  int s = 0;
+  for (int c = c0; c < c1; ++c) s += cnt[c];
+  int tot;
+  int o = block_excl_scan(s, wsum, tot);
+  for (int c = c0; c < c1; ++c) {
+    const int n = cnt[c];
+    cnt[c] = o;
+    o += n;
+  }
+  if (tid == 0) cnt[ncell] = tot;
+  __syncthreads();
+  // work items: pixel p's entries = its four cells' lists (the pixel is corner k of cell
+  // (x - (k & 1), y - (k >> 1))), in chunks of SORT_ITEM; each item carries its lists' bounds.
+  // Pixels tid + k * 1024 per thread (item order is free: every item gets its own slot).
+  const int lbase = l * npt;
+  const int npix = H * W;
+  auto pix_cell = [&](int p) { const int py = p / W; return (py + 1) * W1 + p - py * W + 1; };
+  int si = 0;
+  for (int p = tid; p < npix; p += 1024) {
+    const int c = pix_cell(p);
+    si += (cnt[c + 1] - cnt[c - 1] + cnt[c - W1 + 1] - cnt[c - W1 - 1] + SORT_ITEM - 1) / SORT_ITEM;
+  }
+  int itot;
+  int ipre = block_excl_scan(si, wsum, itot);
+  int4* item = ws.item + ((int64_t)seg * ws.isz + ws.ibase[l]) * 2;
+  for (int p = tid; p < npix; p += 1024) {
+    const int c = pix_cell(p);
+    const int cell[4] = {c, c - 1, c - W1, c - W1 - 1};
+    int pr[4], base[4], n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pr[k] = n;
+      base[k] = lbase + cnt[cell[k]] - n;
+      n += cnt[cell[k] + 1] - cnt[cell[k]];
+    }
+    for (int k = 0; k * SORT_ITEM < n; ++k, ++ipre) {
+      item[2 * ipre] = make_int4(p | (k << 16), pr[1] | (pr[2] << 16), pr[3] | (n << 16), base[0]);
+      item[2 * ipre + 1] = make_int4(base[1], base[2], base[3], 0);
+    }
+  }
+  if (tid == 0) ws.nitem[seg * L + l] = itot;
+  __syncthreads();   // the offsets become cursors below
+  // pass 2: (token, a, fx, fy) at the point's slot of its cell's list (16-byte stores into this
+  // block's own lq * P * 16-byte slab: its lines fill in L2)
+  float4* gl = ws.list + (int64_t)seg * L * npt + lbase;
+  int slot[SORT_PPT];
+#pragma unroll
+  for (int u = 0; u < SORT_PPT; ++u) slot[u] = key[u] >= 0 ? atomicAdd(cnt + key[u], 1) : 0;
+#pragma unroll
+  for (int u = 0; u < SORT_PPT; ++u) {
+    if (key[u] < 0) continue;
+    const int pt = tid + u * 1024, t = pt / P;
+    const float2 st = smx[t];
+    gl[slot[u]] = make_float4(__int_as_float(t), expf(plg[u] - st.x) * st.y, pfx[u], pfy[u]);
+  }
+}
+
+// msda_fused_bwd_kernel's gather backward for d offsets / d logits / d ref (16-byte lanes,
+// CPT = dh / VEC lanes per (token, head)), segment-major (a wave's ppw pairs are consecutive tokens
+// of one (image, head)). The points go CPT at a time; after the butterfly sums every lane of a
+// pair holds each point's results and lane u keeps point u of the group, so the pair's results
+// leave as contiguous runs at the end (no per-point scattered stores, no read-back for the
+// softmax backward).
+template <typename T, int CPT, int LPM>
+__global__ __launch_bounds__(256) void msda_sorted_bwd_kernel(const T* __restrict__ value, int S, TLevels lv, int L,
+                                                              int P, const float* __restrict__ oa,
+                                                              const float* __restrict__ ref,
+                                                              const T* __restrict__ gout, int ldg,
+                                                              float* __restrict__ goa, float* __restrict__ gref,
+                                                              int lq, int nh, int nseg, int bps, int spx, int segmap) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int PPW = 64 / CPT;
+  constexpr int KMAX = (LPM + CPT - 1) / CPT;   // kept points per lane, L * P <= LPM
+  const int xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
+  const int seg = seg_of(xcd, bi / bps, spx, segmap), tb = bi - (bi / bps) * bps;
+  if (seg >= nseg) return;
+  const int lane = threadIdx.x & 63;
+  const int slot = lane / CPT, c = lane - slot * CPT;
+  const int t0 = (tb * 4 + (threadIdx.x >> 6)) * PPW;
+  if (t0 >= lq) return;                           // whole waves leave together
+  const int t = min(t0 + slot, lq - 1);           // a ragged last wave repeats its last token...
+  const bool live = t0 + slot < lq;               // ...without storing anything
+  const int b = seg / nh, h = seg - b * nh;
+  const int r = b * lq + t;
+  const int dh = CPT * VEC;
+  const int C = nh * dh;
+  const int LP = L * P;
+  const int ncol = nh * LP * 3;
+  const int ch = h * dh + c * VEC;
+  const T* vb = value + (int64_t)b * S * C + ch;
+  const float* orow = oa + (int64_t)r * ncol;
+  const float* lg = orow + nh * LP * 2 + h * LP;
+  const Vec16<T> gor = load16(gout + (int64_t)r * ldg + ch);
+  // every point's logit and offsets up front (clamped indices: unconditional loads), so the loop
+  // below waits only on the value rows
+  constexpr int LPMAX = KMAX * CPT;
+  float lgv[LPMAX], oxy[2 * LPMAX];
+  if (LP == LPMAX && LPMAX % 4 == 0) {   // 16-byte loads (the head's offsets and logits are 16-byte aligned runs)
+#pragma unroll
+    for (int j = 0; j < 2 * LPMAX; j += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(orow + h * LPMAX * 2 + j);
+      oxy[j] = x.x; oxy[j + 1] = x.y; oxy[j + 2] = x.z; oxy[j + 3] = x.w;
+    }
+#pragma unroll
+    for (int j = 0; j < LPMAX; j += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(lg + j);
+      lgv[j] = x.x; lgv[j + 1] = x.y; lgv[j + 2] = x.z; lgv[j + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < LPMAX; ++j) {
+      const int jc = min(j, LP - 1);
+      lgv[j] = lg[jc];
+      oxy[2 * j] = orow[(h * LP + jc) * 2];
+      oxy[2 * j + 1] = orow[(h * LP + jc) * 2 + 1];
+    }
+  }
+  const float rx = ref[2 * r], ry = ref[2 * r + 1];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < LPMAX; ++j) mx = j < LP ? fmaxf(mx, lgv[j]) : mx;
+  float den = 0.f;
+#pragma unroll
+  for (int j = 0; j < LPMAX; ++j) den += j < LP ? expf(lgv[j] - mx) : 0.f;
+  const float inv = 1.f / den;
+  float dot = 0.f, grx = 0.f, gry = 0.f;
+  float ka[KMAX], kga[KMAX], kgx[KMAX], kgy[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) ka[i] = kga[i] = kgx[i] = kgy[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    if (i * CPT >= LP) break;   // (uniform; between groups only)
+    // the group's CPT points: corners and weights, then all 4 * CPT row loads, then the math
+    float fxu[CPT], fyu[CPT], au[CPT], Wu[CPT], Hu[CPT];
+    int rcu[CPT][4];
+    bool oku[CPT][4];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const int j = i * CPT + u;
+      const int l = min(j, LP - 1) / P;
+      const int H = lv.h[l], W = lv.w[l];
+      float x, y;
+      msda_xy(rx, ry, oxy[2 * j], oxy[2 * j + 1], H, W, x, y);
+      const float fx0 = floorf(x), fy0 = floorf(y);
+      const int x0 = (int)fx0, y0 = (int)fy0;
+      fxu[u] = x - fx0;
+      fyu[u] = y - fy0;
+      au[u] = j < LP ? expf(lgv[j] - mx) * inv : 0.f;   // a point past L*P contributes nothing
+      Wu[u] = W;
+      Hu[u] = H;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {   // unconditional loads at a clamped row, zeroed outside the map
+        const int xi = x0 + (k & 1), yi = y0 + (k >> 1);
+        oku[u][k] = xi >= 0 && xi < W && yi >= 0 && yi < H;
+        rcu[u][k] = lv.start[l] + min(max(yi, 0), H - 1) * W + min(max(xi, 0), W - 1);
+      }
+    }
+    Vec16<T> v[CPT][4];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[u][k] = load16(vb + (int64_t)rcu[u][k] * C);
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const float fx = fxu[u], fy = fyu[u], a = au[u];
+      // d_k = <grad_out, corner k's channels> (the lane's VEC channels), 0 outside the map; then
+      // the three point sums are bilinear forms in d: ga = sum w_k d_k, gx / gy its fx / fy slopes
+      float d[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = oku[u][k] ? corner_dot(gor, v[u][k]) : 0.f;
+      const float ga0 = (1.f - fx) * (1.f - fy) * d[0] + fx * (1.f - fy) * d[1] + (1.f - fx) * fy * d[2] + fx * fy * d[3];
+      float ga = ga0;
+      float gx = (d[1] - d[0]) * (1.f - fy) + (d[3] - d[2]) * fy;
+      float gy = (d[2] - d[0]) * (1.f - fx) + (d[3] - d[1]) * fx;
+#pragma unroll
+      for (int o = CPT >> 1; o > 0; o >>= 1) {
+        ga += __shfl_xor(ga, o, 64);
+        gx += __shfl_xor(gx, o, 64);
+        gy += __shfl_xor(gy, o, 64);
+      }
+      dot += a * ga;
+      grx += a * gx * Wu[u];
+      gry += a * gy * Hu[u];
+      if (c == u) {
+        ka[i] = a;
+        kga[i] = ga;
+        kgx[i] = a * gx;
+        kgy[i] = a * gy;
+      }
+    }
+  }
+  if (!live) return;
+  float* grow = goa + (int64_t)r * ncol;
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const int j = i * CPT + c;
+    if (j < LP) {
+      *reinterpret_cast<float2*>(grow + (h * LP + j) * 2) = make_float2(kgx[i], kgy[i]);
+      grow[nh * LP * 2 + h * LP + j] = ka[i] * (kga[i] - dot);   // softmax backward
+    }
+  }
+  if (gref && c == 0) {
+    unsafeAtomicAdd(gref + 2 * r, grx);
+    unsafeAtomicAdd(gref + 2 * r + 1, gry);
+  }
+}
+
+// K3: a group of G = dh / VEC lanes per work item (pixel, chunk), 16 bytes of channels per lane
+// (16 items per wave at dh 32 bf16). The chunk's <= SORT_CHUNK entries of the pixel's four cell
+// lists are loaded up front (G per step, one per lane) and turned into (token row, a * w_k), then
+// broadcast one at a time from their lane while the grad_out row loads of consecutive entries are
+// in flight (unconditional: a dead entry has weight 0 and row 0).
+template <typename T, int G>
+__global__ __launch_bounds__(256) void msda_value_sum_kernel(const T* __restrict__ gout, int ldg,
+                                                             float* __restrict__ gvalue, TLevels lv, int S, int L,
+                                                             int P, int lq, int nh, int nseg, int bps_seg,
+                                                             SortWs ws) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int IPW = 64 / G;             // items per wave
+  constexpr int EPL = SORT_CHUNK / G;     // entries per lane
+  const int xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
+  const int seg = seg_of(xcd, bi / bps_seg, ws.spx, ws.segmap);
+  if (seg >= nseg) return;
+  int tb = bi - (bi / bps_seg) * bps_seg, l = 0;
+  while (l + 1 < L && tb >= ws.bps[l]) tb -= ws.bps[l++];
+  const int lane = threadIdx.x & 63;
+  const int gi = lane / G, q = lane - gi * G, g0 = lane - q;
+  const int wbase = (tb * 4 + (threadIdx.x >> 6)) * IPW;
+  const int nitem = ws.nitem[seg * L + l];
+  if (wbase >= nitem) return;              // whole waves past the item list leave
+  const int it = min(wbase + gi, nitem - 1);
+  const bool live = wbase + gi < nitem;
+  const int4* ip = ws.item + ((int64_t)seg * ws.isz + ws.ibase[l] + it) * 2;
+  const int4 ia = ip[0], ib = ip[1];
+  const int p = ia.x & 0xffff, chunk = ia.x >> 16, total = ia.z >> 16;
+  const int pr1 = ia.y & 0xffff, pr2 = ia.y >> 16, pr3 = ia.z & 0xffff;
+  const int n = live ? min(SORT_ITEM, total - chunk * SORT_ITEM) : 0;
+  const int b = seg / nh, h = seg - b * nh;
+  const int dh = G * VEC;
+  float* gp = gvalue + ((int64_t)b * S + lv.start[l] + p) * (nh * dh) + h * dh + VEC * q;
+  float gold[VEC];   // the pixel's current gradient, loaded with the list entries
+#pragma unroll
+  for (int e = 0; e < VEC; e += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(gp + e);
+    gold[e] = x.x; gold[e + 1] = x.y; gold[e + 2] = x.z; gold[e + 3] = x.w;
+  }
+  int nmax = n;   // the wave's longest chunk bounds the list and broadcast loops
+#pragma unroll
+  for (int s = G; s < 64; s <<= 1) nmax = max(nmax, __shfl_xor(nmax, s, 64));
+  const T* gcol = gout + h * dh + VEC * q;
+  float acc[VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
+  const float4* lst = ws.list + (int64_t)seg * L * lq * P;
+  for (int r0 = 0; r0 < nmax; r0 += SORT_CHUNK) {   // rounds of SORT_CHUNK entries (uniform)
+    int er[EPL];
+    float ew[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      er[e] = 0;
+      ew[e] = 0.f;
+      if (r0 + e * G >= nmax) continue;   // (uniform)
+      const int ie = e * G + q;
+      const int ii = chunk * SORT_ITEM + r0 + ie;
+      const int k = (ii >= pr1) + (ii >= pr2) + (ii >= pr3);
+      const int sl = (k == 0 ? ia.w : k == 1 ? ib.x : k == 2 ? ib.y : ib.z) + ii;
+      const bool ok = r0 + ie < n;
+      const float4 en = lst[ok ? sl : 0];   // unconditional load (slot 0 for a dead entry), value dropped
+      const float wx = (k & 1) ? en.z : 1.f - en.z, wy = (k & 2) ? en.w : 1.f - en.w;
+      er[e] = b * lq + (ok ? __float_as_int(en.x) : 0);
+      ew[e] = ok ? en.y * (wx * wy) : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      if (r0 + e * G >= nmax) break;
+      float gv[G][VEC];
+#pragma unroll
+      for (int s = 0; s < G; ++s) {
+        const int rr = group_bcast<G>(er[e], s, g0);
+        load_vec(gcol + (int64_t)rr * ldg, gv[s]);
+      }
+#pragma unroll
+      for (int s = 0; s < G; ++s) {
+        const float w = __int_as_float(group_bcast<G>(__float_as_int(ew[e]), s, g0));
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) acc[c] += w * gv[s][c];
+      }
+    }
+  }
+  if (n <= 0) return;
+  if (total > SORT_ITEM) {   // the pixel's lists span several items: they meet in float atomics
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) unsafeAtomicAdd(gp + c, acc[c]);
+  } else {                    // the only writer of this segment of the pixel's row
+#pragma unroll
+    for (int e = 0; e < VEC; e += 4)
+      *reinterpret_cast<float4*>(gp + e) =
+          make_float4(gold[e] + acc[e], gold[e + 1] + acc[e + 1], gold[e + 2] + acc[e + 2], gold[e + 3] + acc[e + 3]);
+  }
+}
+
 template <typename T, bool BWD>
 int launch_core(const void* value, int batch, int S, const TLevels& lv, int L, int P, const float* loc,
                 const float* attn, const void* gout, void* out, float* gvalue, float* gloc, float* gattn, int lq, int nh,
@@ -371,7 +849,152 @@ int check_core(const void* value, int batch, int S, const int32_t* lvl_hw, int n
   return 0;
 }
 
+// dp_msda_bwd_sorted's workspace carved from base (NULL: sizes only); returns the bytes needed.
+// Also fills the per-level cell / item bases and the LDS the KS block needs.
+int64_t sort_ws_layout(int batch, int S, int lq, int nh, const TLevels& lv, int L, int P, char* base, SortWs* ws,
+                       int* ks_lds = nullptr) {
+  const int64_t nseg = (int64_t)batch * nh;
+  const int npt = lq * P;
+  int isz = 0, lds = 0;
+  for (int l = 0; l < L; ++l) {
+    const int cells = (lv.h[l] + 1) * (lv.w[l] + 1);
+    const int items = lv.h[l] * lv.w[l] + (4 * npt + SORT_ITEM - 1) / SORT_ITEM;
+    ws->ibase[l] = isz;
+    isz += items;
+    lds = std::max(lds, lq * 8 + (cells + 1) * 4);
+  }
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t at = o;
+    o += (bytes + 255) / 256 * 256;
+    return base ? base + at : nullptr;
+  };
+  ws->list = reinterpret_cast<float4*>(take(nseg * L * npt * 16));
+  ws->item = reinterpret_cast<int4*>(take(nseg * isz * 32));
+  ws->nitem = reinterpret_cast<int32_t*>(take(nseg * L * 4));
+  ws->isz = isz;
+  if (ks_lds) *ks_lds = lds;
+  return o;
+}
+
+// a shape the sort handles: item fields are 16-bit (pixels per level, a pixel's entries), kept
+// points per lane in K2 bounded (L * P <= 16)
+bool sort_shape_ok(const TLevels& lv, int L, int P, int lq) {
+  if (L * P > 16 || 4 * lq * P >= 65536 || lq * P > 1024 * SORT_PPT) return false;
+  for (int l = 0; l < L; ++l)
+    if (lv.h[l] * lv.w[l] >= 65536) return false;
+  return true;
+}
+
+// LDS the sort block may declare (64 KiB: several blocks per CU)
+constexpr int SORT_LDS_MAX = 64 * 1024 - 256;
+
 }  // namespace
+
+extern "C" int64_t dp_msda_bwd_ws_bytes(int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
+                                        int32_t lq, int32_t nhead, int32_t npoints) {
+  if (batch <= 0 || S <= 0 || lq <= 0 || nhead <= 0 || nlevels <= 0 || nlevels > MAXL || npoints <= 0 || !lvl_hw ||
+      nlevels * npoints > 16)
+    return -1;
+  TLevels lv;
+  for (int l = 0; l < nlevels; ++l) {
+    lv.h[l] = lvl_hw[2 * l];
+    lv.w[l] = lvl_hw[2 * l + 1];
+  }
+  SortWs ws;
+  int lds = 0;
+  const int64_t bytes = sort_ws_layout(batch, S, lq, nhead, lv, nlevels, npoints, nullptr, &ws, &lds);
+  return lds <= SORT_LDS_MAX && sort_shape_ok(lv, nlevels, npoints, lq) ? bytes : -1;
+}
+
+extern "C" int dp_msda_bwd_sorted(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
+                                  const float* offattn, const float* ref, const void* grad_out, int32_t ld_grad_out,
+                                  int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value,
+                                  int32_t accumulate_value, float* grad_offattn, float* grad_ref, void* workspace,
+                                  int64_t workspace_bytes, int32_t dtype, void* stream) {
+  TLevels lv;
+  const int rc = check_core(value, batch, S, lvl_hw, nlevels, offattn, ref, lq, nhead, dh, npoints, dtype, &lv);
+  if (rc) return rc;
+  DP_REQUIRE(grad_out && grad_offattn && grad_value && workspace, "dp_msda_bwd_sorted: null pointer");
+  DP_REQUIRE(dh == 8 || dh == 16 || dh == 32 || dh == 64, "dp_msda_bwd_sorted: dh=%d (8, 16, 32 or 64)", dh);
+  const int VEC = dtype == DP_BF16 ? 8 : 4;
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0 && ld_grad_out % VEC == 0 && ld_grad_out >= nhead * dh,
+             "dp_msda_bwd_sorted: grad_out must be 16-byte aligned per row (ld %d)", ld_grad_out);
+  DP_REQUIRE((reinterpret_cast<uintptr_t>(grad_value) & 15) == 0 && (reinterpret_cast<uintptr_t>(offattn) & 15) == 0,
+             "dp_msda_bwd_sorted: grad_value and offattn must be 16-byte aligned");
+  DP_REQUIRE((int64_t)batch * lq * nhead * nlevels * npoints * 4 < (1ll << 31), "dp_msda_bwd_sorted: too many entries");
+  DP_REQUIRE(sort_shape_ok(lv, nlevels, npoints, lq),
+             "dp_msda_bwd_sorted: shape outside the sort's range (levels x points <= 16, lq points <= 8192, "
+             "H W < 65536 per level)");
+  SortWs ws;
+  int lds = 0;
+  const int64_t need = sort_ws_layout(batch, S, lq, nhead, lv, nlevels, npoints, static_cast<char*>(workspace), &ws,
+                                      &lds);
+  DP_REQUIRE(lds <= SORT_LDS_MAX, "dp_msda_bwd_sorted: a level's cells + tokens need %d bytes of LDS (max %d)", lds,
+             SORT_LDS_MAX);
+  DP_REQUIRE(workspace_bytes >= need, "dp_msda_bwd_sorted: workspace %lld bytes, need %lld",
+             (long long)workspace_bytes, (long long)need);
+  hipStream_t s = as_stream(stream);
+  const int nseg = batch * nhead;
+  const int segs_per_xcd = (nseg + 7) / 8;
+  ws.spx = segs_per_xcd;
+  ws.segmap = getenv("DETRPOSE_MSDA_SEGMAP") ? atoi(getenv("DETRPOSE_MSDA_SEGMAP")) : 1;
+  const size_t vbytes = (size_t)batch * S * nhead * dh * sizeof(float);
+  if ((!accumulate_value && hipMemsetAsync(grad_value, 0, vbytes, s) != hipSuccess) ||
+      (grad_ref && hipMemsetAsync(grad_ref, 0, (size_t)batch * lq * 2 * sizeof(float), s) != hipSuccess))
+    return dp_check_launch("dp_msda_bwd_sorted(memset)");
+  static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_sort_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 SORT_LDS_MAX) == hipSuccess;
+  DP_REQUIRE(lds_ok, "dp_msda_bwd_sorted: cannot raise the sort kernel's LDS limit");
+  hipLaunchKernelGGL(msda_sort_kernel, dim3(8 * segs_per_xcd * nlevels), dim3(1024), lds, s, lv, nlevels, npoints,
+                     offattn, ref, lq, nhead, nseg, ws);
+  {
+    const int cpt = dh / VEC;
+    const int bps = (lq + 4 * (64 / cpt) - 1) / (4 * (64 / cpt));
+    const dim3 grid(8 * segs_per_xcd * bps);
+#define DP_K2(T, CPT)                                                                                              \
+  if (nlevels * npoints <= 12)                                                                                    \
+    hipLaunchKernelGGL((msda_sorted_bwd_kernel<T, CPT, 12>), grid, dim3(256), 0, s, (const T*)value, S, lv,      \
+                       nlevels, npoints, offattn, ref, (const T*)grad_out, ld_grad_out, grad_offattn, grad_ref, lq,   \
+                       nhead, nseg, bps, segs_per_xcd, ws.segmap);                                                \
+  else                                                                                                            \
+    hipLaunchKernelGGL((msda_sorted_bwd_kernel<T, CPT, 16>), grid, dim3(256), 0, s, (const T*)value, S, lv,      \
+                       nlevels, npoints, offattn, ref, (const T*)grad_out, ld_grad_out, grad_offattn, grad_ref, lq,   \
+                       nhead, nseg, bps, segs_per_xcd, ws.segmap)
+    if (dtype == DP_BF16) {
+      if (cpt == 1) { DP_K2(bf16_t, 1); } else if (cpt == 2) { DP_K2(bf16_t, 2); } else if (cpt == 4) { DP_K2(bf16_t, 4); }
+      else { DP_K2(bf16_t, 8); }
+    } else {
+      if (cpt == 2) { DP_K2(float, 2); } else if (cpt == 4) { DP_K2(float, 4); } else if (cpt == 8) { DP_K2(float, 8); }
+      else { DP_K2(float, 16); }
+    }
+#undef DP_K2
+  }
+  {
+    const int G = dh / VEC;
+    const int ipb = 4 * (64 / G);   // items per block
+    int bps_seg = 0;
+    for (int l = 0; l < nlevels; ++l) {
+      const int items = lv.h[l] * lv.w[l] + (4 * lq * npoints + SORT_ITEM - 1) / SORT_ITEM;
+      ws.bps[l] = (items + ipb - 1) / ipb;
+      bps_seg += ws.bps[l];
+    }
+    const dim3 grid(8 * segs_per_xcd * bps_seg);
+#define DP_VSUM(T, GG)                                                                                              \
+  hipLaunchKernelGGL((msda_value_sum_kernel<T, GG>), grid, dim3(256), 0, s, (const T*)grad_out, ld_grad_out,      \
+                     grad_value, lv, S, nlevels, npoints, lq, nhead, nseg, bps_seg, ws)
+    if (dtype == DP_BF16) {
+      if (G == 1) DP_VSUM(bf16_t, 1); else if (G == 2) DP_VSUM(bf16_t, 2); else if (G == 4) DP_VSUM(bf16_t, 4);
+      else DP_VSUM(bf16_t, 8);
+    } else {
+      if (G == 2) DP_VSUM(float, 2); else if (G == 4) DP_VSUM(float, 4); else if (G == 8) DP_VSUM(float, 8);
+      else DP_VSUM(float, 16);
+    }
+#undef DP_VSUM
+  }
+  return dp_check_launch("dp_msda_bwd_sorted");
+}
 
 extern "C" int dp_msda_core_fwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw, int32_t nlevels,
                                 const float* loc, const float* attn, void* out, int32_t lq, int32_t nhead, int32_t dh,

@@ -758,7 +758,11 @@ __global__ void cdn_build_kernel(const int* __restrict__ off, const int* __restr
 }
 
 // ---------------------------------------------------------------- optimizer
-__global__ void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* __restrict__ out) {
+// Squared norm in two fixed-shape passes (no float atomics): DP_SQNORM_PARTS block partials, then
+// one block sums them in a fixed order. The result is bit-identical for identical gradients, so
+// DDP ranks holding the all-reduced gradient clip by the same factor and their parameters stay
+// identical (the replica invariant DDP relies on after its initial broadcast).
+__global__ void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* __restrict__ part) {
   float acc = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     acc = fmaf(g[i], g[i], acc);
@@ -766,7 +770,17 @@ __global__ void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* __r
   __shared__ float red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) unsafeAtomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void sqnorm_final_kernel(const float* __restrict__ part, int nparts, float* __restrict__ out) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  acc = wave_sum(acc);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // torch.optim.AdamW step (decoupled weight decay, bias corrections) after
@@ -1135,10 +1149,9 @@ extern "C" int dp_cdn_build(const int32_t* tgt_off, const int32_t* tgt_label, co
 extern "C" int dp_grad_sqnorm(const float* g, int64_t n, float* out, void* stream) {
   DP_REQUIRE(g && out && n > 0, "dp_grad_sqnorm: bad arguments");
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(out, 0, 4, s) != hipSuccess) return dp_check_launch("dp_grad_sqnorm");
-  int grid = (int)((n + 255) / 256);
-  if (grid > 1024) grid = 1024;
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, s, g, n, out);
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, DP_SQNORM_PARTS);
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, s, g, n, out + 1);
+  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, out + 1, grid, out);
   return dp_check_launch("dp_grad_sqnorm");
 }
 

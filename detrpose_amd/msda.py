@@ -91,7 +91,8 @@ class MSDeformAttnFunction(torch.autograd.Function):
     """The fused op of MSDeformAttn.forward's default branch (ms_deform_attn.py:384-441):
     raw offsets | attention logits + reference points -> softmax, sampling locations,
     bilinear gather, weighted sum. Forward `dp_msda` (the inference kernel), backward
-    `dp_msda_bwd` (softmax and location chain rule fused into the gather backward)."""
+    `dp_msda_bwd_sorted` (softmax and location chain rule fused into the gather backward, the
+    value gradient summed per pixel without float atomics; see msda_bwd)."""
 
     @staticmethod
     def forward(ctx, value, shapes, offattn, ref, n_heads, n_points):
@@ -129,21 +130,40 @@ class MSDeformAttnFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         value, oa, ref = ctx.saved_tensors
-        N, S, Cc = value.shape
-        rows = oa.shape[0]
-        go = grad_out.contiguous().to(value.dtype)
-        gv = torch.empty(N, S, Cc, device=value.device, dtype=torch.float32)
-        goa = torch.empty(oa.shape, device=value.device, dtype=torch.float32)
-        gref = torch.empty(rows, 2, device=value.device, dtype=torch.float32) if ctx.needs_input_grad[3] else None
-        oa32 = oa
-        hw, nl = _shapes_arg(ctx.shapes)
-        lib = _lib.load()
-        s = torch.cuda.current_stream(value.device).cuda_stream
-        _lib.check(lib.dp_msda_bwd(value.data_ptr(), N, S, hw, nl, oa32.data_ptr(), ref.data_ptr(), go.data_ptr(), Cc,
-                                   rows // N, ctx.n_heads, Cc // ctx.n_heads, ctx.n_points, gv.data_ptr(), 0,
-                                   goa.data_ptr(), gref.data_ptr() if gref is not None else None,
-                                   _DT[value.dtype], C.c_void_p(s)), "dp_msda_bwd")
+        gv, goa, gref = msda_bwd(value, ctx.shapes, oa, ref, grad_out, ctx.n_heads, ctx.n_points,
+                                 want_ref=ctx.needs_input_grad[3])
         return gv.to(value.dtype), None, goa, gref, None, None
+
+
+def msda_bwd(value, shapes, offattn, ref, grad_out, n_heads, n_points, want_ref=True, method="sorted"):
+    """The backward of msdeform_attn as a function: (grad_value f32 (N, S, C), grad_offattn f32,
+    grad_ref f32 (rows, 2) or None). method "sorted": dp_msda_bwd_sorted (value gradient by a
+    per-pixel counting sort and register sums; falls to "atomic" outside its shape range),
+    "atomic": dp_msda_bwd (f32 atomics)."""
+    N, S, Cc = value.shape
+    rows = offattn.shape[0]
+    lq = rows // N
+    dh = Cc // n_heads
+    go = grad_out.contiguous().to(value.dtype)
+    oa = offattn.detach().float().contiguous()
+    ref = ref.detach().float().contiguous()
+    gv = torch.empty(N, S, Cc, device=value.device, dtype=torch.float32)
+    goa = torch.empty(oa.shape, device=value.device, dtype=torch.float32)
+    gref = torch.empty(rows, 2, device=value.device, dtype=torch.float32) if want_ref else None
+    hw, nl = _shapes_arg(shapes)
+    lib = _lib.load()
+    s = C.c_void_p(torch.cuda.current_stream(value.device).cuda_stream)
+    args = (value.data_ptr(), N, S, hw, nl, oa.data_ptr(), ref.data_ptr(), go.data_ptr(), Cc, lq, n_heads, dh,
+            n_points, gv.data_ptr(), 0, goa.data_ptr(), gref.data_ptr() if gref is not None else None)
+    nb = int(lib.dp_msda_bwd_ws_bytes(N, S, hw, nl, lq, n_heads, n_points)) if method == "sorted" else -1
+    if nb > 0 and dh in (8, 16, 32, 64):
+        ws = torch.empty(nb, device=value.device, dtype=torch.uint8)
+        _lib.check(lib.dp_msda_bwd_sorted(*args, ws.data_ptr(), nb, _DT[value.dtype], s), "dp_msda_bwd_sorted")
+    elif method in ("sorted", "atomic"):
+        _lib.check(lib.dp_msda_bwd(*args, _DT[value.dtype], s), "dp_msda_bwd")
+    else:
+        raise ValueError(f"msda_bwd: method {method!r}")
+    return gv, goa, gref
 
 
 def msdeform_attn(value, shapes, offattn, ref, n_heads, n_points):

@@ -15,7 +15,7 @@ step's arena, and the backward is written out op by op in reverse:
   nn.LayerNorm         dp_ln_fwd (saves the pre-norm sum and mean / rstd) / dp_ln_bwd
   MultiheadAttention   in_proj / out_proj GEMMs + dp_attn_fwd (saves P) / dp_attn_bwd, with the
                        DN attn_mask in the across attention
-  MSDeformAttn         dp_msda (f32 offsets) / dp_msda_bwd (offsets / logits gradients)
+  MSDeformAttn         dp_msda (f32 offsets) / dp_msda_bwd_sorted (offsets / logits / value gradients)
   Gate                 dp_gate_fwd / dp_gate_bwd + its Linear
   heads                pose / pre / class / LQE MLPs as GEMMs, dp_pose_refine(_bwd),
                        dp_pre_pose + dp_sigmoid_bwd, dp_lqe_stats(_bwd)
@@ -127,7 +127,7 @@ class TrainEngine:
         self.grad_flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.sqnorm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.sqnorm = torch.zeros(1 + _lib.DP_SQNORM_PARTS, dtype=torch.float32, device=dev)   # [norm^2 | partials]
         self.bad = torch.zeros(1, dtype=torch.float32, device=dev)   # step guard (dp_finite_guard)
         self.grad_acc = None   # gradient-accumulation buffer (accumulate_grads)
         self.opt_step = 0
@@ -511,6 +511,10 @@ class TrainPlan:
         self.dn_ref = f32(B, max(P, 1), T, 2)
         self.mask = torch.zeros(Qt, Qt, dtype=torch.uint8, device=dev)
         self.lvl_hw = (C.c_int32 * (2 * len(shapes)))(*[v for hw in shapes for v in hw])
+        # dp_msda_bwd_sorted's workspace (shared by the layers: their backward ops run in order on one
+        # stream); None where the shape is outside the sort's range (dp_msda_bwd's atomics then)
+        nws = int(lib.dp_msda_bwd_ws_bytes(B, S, self.lvl_hw, len(shapes), Qt * T, nh, eng.npnt))
+        self.msda_ws = buf(nws, dtype=torch.uint8) if nws > 0 and Cc // nh in (8, 16, 32, 64) else None
         fw = Tape(lib, dev)
         bw = Tape(lib, dev)
         self.fw, self.bw = fw, bw
@@ -991,9 +995,14 @@ class TrainPlan:
             eng.dgrad(bw, n + ".gate.dx", _p(dG), 2 * Cc, rows, lp + "gateway.gate.weight", _p(dx), 2 * Cc, beta=1.0)
             # MSDA: d offsets / logits (dp_msda_bwd), then the offattn Linear
             doa = f32(rows, ncol)
-            bw.op(n + ".msda_bwd", lib.dp_msda_bwd, _p(self.memory), B, self.S, self.lvl_hw, len(self.shapes),
-                  _p(S_["oa"]), _p(self.refs[l]), _p(dx, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt,
-                  _p(dm) if dm is not None else None, 1, _p(doa), None, code)
+            msda_args = (_p(self.memory), B, self.S, self.lvl_hw, len(self.shapes), _p(S_["oa"]), _p(self.refs[l]),
+                         _p(dx, Cc), 2 * Cc, Qt * T, nh, Cc // nh, eng.npnt, _p(dm) if dm is not None else None, 1,
+                         _p(doa), None)
+            if dm is not None and self.msda_ws is not None:   # value gradient by the per-pixel sort
+                bw.op(n + ".msda_bwd", lib.dp_msda_bwd_sorted, *msda_args, _p(self.msda_ws), self.msda_ws.numel(),
+                      code)
+            else:
+                bw.op(n + ".msda_bwd", lib.dp_msda_bwd, *msda_args, code)
             if self.cut_loc:   # parity-analysis variant: d sampling offsets = 0 (the location columns)
                 nof = eng.nh * eng.nlev * eng.npnt * 2
                 bw.op(n + ".cut_loc", lib.dp_convert_rows, _p(doa), DP_F32, ncol, _p(doa), DP_F32, ncol, rows, nof,

@@ -201,6 +201,23 @@ int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const int32_t* lvl_
                 int32_t lq, int32_t nhead, int32_t dh, int32_t npoints, float* grad_value, int32_t accumulate_value,
                 float* grad_offattn, float* grad_ref, int32_t dtype, void* stream);
 
+/* dp_msda_bwd with the value gradient summed without float atomics (same arguments and
+ * results; grad_value required, dh in {8, 16, 32, 64}): each sampling point is filed under the
+ * top-left corner cell of its bilinear footprint by a per-(image, head, level) counting sort in
+ * LDS, and each value pixel sums the lists of the four cells that cover it in registers, then
+ * adds into grad_value once. workspace: device memory of dp_msda_bwd_ws_bytes(...) bytes
+ * (reusable across calls on one stream); dp_msda_bwd_ws_bytes returns -1 for a shape the sort
+ * cannot hold (a level's (H+1)(W+1) cells + lq*npoints points over 160 KiB of LDS). Same reference
+ * interface as dp_msda_bwd (MSDeformAttn.forward's default branch backward,
+ * ms_deform_attn.py:384-441 / ms_deform_attn_core_pytorch :145-193). */
+int64_t dp_msda_bwd_ws_bytes(int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */, int32_t nlevels,
+                             int32_t lq, int32_t nhead, int32_t npoints);
+int dp_msda_bwd_sorted(const void* value, int32_t batch, int32_t S, const int32_t* lvl_hw /* [L][2] host */,
+                       int32_t nlevels, const float* offattn, const float* ref, const void* grad_out,
+                       int32_t ld_grad_out, int32_t lq, int32_t nhead, int32_t dh, int32_t npoints,
+                       float* grad_value, int32_t accumulate_value, float* grad_offattn, float* grad_ref,
+                       void* workspace, int64_t workspace_bytes, int32_t dtype, void* stream);
+
 /* Input pipeline of the reference benchmark (tools/benchmark/dataset.py:56-61) for one image
  * decoded to uint8 RGB (3, h, w) on the device: T.Resize to (new_h, new_w) (bilinear with
  * antialias, round + clamp to uint8, as torchvision's tensor resize), PadToSize(out_h, out_w)
@@ -538,7 +555,10 @@ int dp_cdn_build(const int32_t* tgt_off, const int32_t* tgt_label, const float* 
                  const float* tgt_boxes, const float* sigmas, int32_t batch, int32_t pad, int32_t single_pad,
                  int32_t nkp, float label_noise_ratio, int32_t num_classes, float img_h, float img_w, uint64_t seed,
                  int32_t* dn_label, float* dn_ref, void* stream);
-/* Squared L2 norm of a gradient buffer (f32 scalar out, zeroed here): clip_grad_norm_'s norm. */
+/* Squared L2 norm of a gradient buffer: clip_grad_norm_'s norm, into out[0]; out holds
+ * 1 + DP_SQNORM_PARTS floats (out[1..] are the block partials). Deterministic (fixed-order
+ * reduction, no float atomics): identical gradients give bit-identical norms on every rank. */
+#define DP_SQNORM_PARTS 1024
 int dp_grad_sqnorm(const float* g, int64_t n, float* out, void* stream);
 /* torch.optim.AdamW step over a flat f32 parameter buffer (decoupled weight decay, bias
  * correction for `step`), after clip_grad_norm_(max_norm) (src/solver/engine.py:78-89) read

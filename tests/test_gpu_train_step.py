@@ -181,7 +181,7 @@ def test_adamw_clip_matches_torch():
     p = torch.randn(n, device="cuda")
     ref = p.clone().requires_grad_(True)
     opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4)
-    m, v, sq = torch.zeros_like(p), torch.zeros_like(p), torch.zeros(1, device="cuda")
+    m, v, sq = torch.zeros_like(p), torch.zeros_like(p), torch.zeros(1 + _lib.DP_SQNORM_PARTS, device="cuda")
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     for step in range(1, 4):
         g = torch.randn(n, device="cuda") * 0.01

@@ -280,3 +280,87 @@ def test_msdeform_attn_module_forward(golden_dir):
     assert (out - want).abs().max().item() <= 1e-4
     out.sum().backward()
     assert q.grad is not None and torch.isfinite(q.grad).all()
+
+
+def _bwd_case(name):
+    """(value, shapes, offattn, ref, grad_out, nH, P) for the sorted-vs-atomic backward checks."""
+    g = torch.Generator().manual_seed(11)
+    if name == "l_b16":        # DETRPose-L b16 decoder rows (100 queries x 18 tokens per image)
+        N, nH, Dh, P, shapes, Lq = 16, 8, 32, 4, [(80, 80), (40, 40), (20, 20)], 1800
+    elif name == "hotspot":    # every reference point near one of three spots: lists of thousands
+        N, nH, Dh, P, shapes, Lq = 2, 8, 32, 4, [(80, 80), (40, 40), (20, 20)], 1800
+    else:                      # ragged: 12 segments (not a multiple of 8 XCDs), dh 16, odd sizes
+        N, nH, Dh, P, shapes, Lq = 3, 4, 16, 3, [(7, 9), (4, 5)], 37
+    L, S = len(shapes), sum(h * w for h, w in shapes)
+    value = torch.randn(N, S, nH * Dh, generator=g)
+    if name == "hotspot":
+        spots = torch.tensor([[0.3, 0.4], [0.62, 0.55], [0.5, 0.8]])
+        ref = spots[torch.randint(0, 3, (N * Lq,), generator=g)] + 0.002 * torch.randn(N * Lq, 2, generator=g)
+        off = torch.randn(N * Lq, nH * L * P * 2, generator=g) * 0.3
+    else:
+        ref = torch.rand(N * Lq, 2, generator=g) * 1.1 - 0.05
+        off = torch.randn(N * Lq, nH * L * P * 2, generator=g) * 3
+    oa = torch.cat([off, torch.randn(N * Lq, nH * L * P, generator=g)], 1)
+    gout = torch.randn(N, Lq, nH * Dh, generator=g)
+    return value, shapes, oa, ref, gout, nH, P
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["l_b16", "hotspot", "ragged"])
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_msda_bwd_sorted_matches_atomic(case, dt):
+    """dp_msda_bwd_sorted (per-pixel counting sort, register sums) vs dp_msda_bwd (f32 atomics) on
+    the same inputs: identical offsets / logits / reference-point gradients up to summation order
+    (1e-5 of scale), the value gradient likewise; hotspot makes pixel lists span several work
+    items (the float-atomic merge path). The ragged case is also checked against autograd of the
+    reference formula."""
+    from detrpose_amd.msda import msda_bwd
+    value, shapes, oa, ref, gout, nH, P = _bwd_case(case)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    v, o, r, go = value.to("cuda", tdt), oa.cuda(), ref.cuda(), gout.to("cuda", tdt)
+    a = msda_bwd(v, shapes, o, r, go, nH, P, method="atomic")
+    b = msda_bwd(v, shapes, o, r, go, nH, P, method="sorted")
+    torch.cuda.synchronize()
+    for name, x, y in zip(("grad_value", "grad_offattn", "grad_ref"), a, b):
+        err = (x - y).abs().max().item()
+        scale = max(1.0, x.abs().max().item())
+        print(f"{case} {dt} {name}: max |sorted - atomic| {err:.3g} (scale {scale:.3g})")
+        assert torch.isfinite(y).all() and err <= 1e-5 * scale, (name, err)
+    if case == "ragged" and dt == "fp32":
+        v0, o0, r0 = (t.clone().requires_grad_(True) for t in (value, oa, ref))
+        _module_ref(v0, shapes, o0, r0, nH, P).backward(gout)
+        for name, x, y in zip(("grad_value", "grad_offattn", "grad_ref"), (v0.grad, o0.grad, r0.grad), b):
+            err = (x - y.cpu()).abs().max().item()
+            assert err <= 1e-4 * max(1.0, x.abs().max().item()), (name, err)
+
+
+@pytest.mark.gpu
+def test_msda_bwd_sorted_accumulates():
+    """accumulate_value=1 adds the value gradient into what grad_value holds (the training tape
+    accumulates every layer's into d memory); workspace reused across calls."""
+    import ctypes as C
+    from detrpose_amd import _lib
+    from detrpose_amd.msda import _shapes_arg, msda_bwd
+    value, shapes, oa, ref, gout, nH, P = _bwd_case("ragged")
+    v, o, r, go = value.cuda(), oa.cuda(), ref.cuda(), gout.cuda()
+    want, _, _ = msda_bwd(v, shapes, o, r, go, nH, P, method="atomic")
+    N, S, Cc = v.shape
+    lq = o.shape[0] // N
+    lib = _lib.load()
+    hw, nl = _shapes_arg(shapes)
+    nb = int(lib.dp_msda_bwd_ws_bytes(N, S, hw, nl, lq, nH, P))
+    ws = torch.empty(nb, device="cuda", dtype=torch.uint8)
+    base = torch.randn(N, S, Cc, device="cuda")
+    gv = base.clone()
+    goa = torch.empty_like(o)
+    for _ in range(2):
+        _lib.check(lib.dp_msda_bwd_sorted(v.data_ptr(), N, S, hw, nl, o.data_ptr(), r.data_ptr(), go.data_ptr(), Cc, lq,
+                                          nH, Cc // nH, P, gv.data_ptr(), 1, goa.data_ptr(), None, ws.data_ptr(), nb,
+                                          _lib.DP_F32, C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                   "dp_msda_bwd_sorted")
+    torch.cuda.synchronize()
+    assert (gv - (base + 2 * want)).abs().max().item() <= 1e-5 * max(1.0, want.abs().max().item())
+    with pytest.raises(RuntimeError, match="workspace"):
+        _lib.check(lib.dp_msda_bwd_sorted(v.data_ptr(), N, S, hw, nl, o.data_ptr(), r.data_ptr(), go.data_ptr(), Cc, lq,
+                                          nH, Cc // nH, P, gv.data_ptr(), 1, goa.data_ptr(), None, ws.data_ptr(), nb - 1,
+                                          _lib.DP_F32, C.c_void_p(0)), "dp_msda_bwd_sorted")
