@@ -290,6 +290,21 @@ def train_leg(size, dtype, dev, batch, steps, warmup=3, rank=0, world=1):
     own = time.perf_counter() - t0
     el = dp.max_over_ranks(own, world, dev)
     ms = el * 1e3 / steps
+    graphs = None
+    if tr.graphs:   # the same steps with every tape launched op by op from Python (no hipGraph replay)
+        tr.graphs = False
+        tr.step(images, ts)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            tr.step(images, ts)
+        torch.cuda.synchronize()
+        eager = (time.perf_counter() - t1) * 1e3 / steps
+        tr.graphs = True
+        tr.step(images, ts)   # tapes back on their graphs for the phase split below
+        torch.cuda.synchronize()
+        graphs = {"tapes_replayed_from_hipgraphs": True, "eager_ms_per_step": round(eager, 3),
+                  "graph_ms_per_step": round(ms, 3), "eager_over_graph": round(eager / ms, 3)}
     comm = None
     if world > 1:   # one instrumented step: every collective synchronised and timed
         encoder_train.COMM_LOG = []
@@ -350,7 +365,7 @@ def train_leg(size, dtype, dev, batch, steps, warmup=3, rank=0, world=1):
                        f"per image)",
            "n_gpus": world, "ms_per_step": round(ms, 3), "images_per_sec": round(batch * world / ms * 1e3, 2),
            "images_per_sec_per_gpu": round(batch / ms * 1e3, 2), "steps": steps, "grad_accum_steps": tr.grad_accum_steps,
-           "dn_pad_last_sub_batch": plan.P, "phase_ms_one_sub_batch": phases,
+           "dn_pad_last_sub_batch": plan.P, "hipgraphs": graphs, "phase_ms_one_sub_batch": phases,
            "tflops_by_part": {k: round(fl[k] / (t[k] * 1e-3) / 1e12, 2) if t[k] > 0 else None for k in fl},
            "sub_batch_tflop": round(sum(fl.values()) / 1e12, 3),
            "losses_finite": bool(torch.isfinite(vals).all()), "update_skipped": tr.eng.step_skipped()}

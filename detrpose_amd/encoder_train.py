@@ -113,10 +113,11 @@ def _all_reduce(t):
 
 
 def _host(fn):
-    """A tape op that runs host code (a collective) in stream order."""
+    """A tape op that runs host code (a collective) in stream order (keeps its tape eager)."""
     def op(stream):
         fn()
         return 0
+    op.host = True
     return op
 
 

@@ -18,6 +18,7 @@ launches up to the memory, BatchNorm in eval mode), only the transformer trained
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -70,7 +71,8 @@ class Trainer:
 
     def __init__(self, model, dtype="bf16", device="cuda", lr=None, betas=None, weight_decay=None,
                  max_norm=None, dn_number=20, label_noise_ratio=0.5, weights=(2.0, 10.0, 4.0), seed=0,
-                 scope="full", backbone_lr=None, ema=True, ema_decay=None, ema_warmups=None, grad_accum_steps=None):
+                 scope="full", backbone_lr=None, ema=True, ema_decay=None, ema_warmups=None, grad_accum_steps=None,
+                 graphs=None):
         from .configs import training_params
         assert scope in ("full", "transformer"), scope
         size = model_size(model)
@@ -93,6 +95,13 @@ class Trainer:
         if ema:
             self.eng.ema_init()
         self.grad_accum_steps = int(pick(grad_accum_steps, "grad_accum_steps"))
+        # tapes replayed from hipGraphs after their first (eager) run; default on at world size 1
+        # (world > 1: the SyncBN collectives are host ops between the encoder's launches)
+        if graphs is None:
+            graphs = os.environ.get("DETRPOSE_TRAIN_GRAPHS", "1") != "0" and not (
+                torch.distributed.is_available() and torch.distributed.is_initialized()
+                and torch.distributed.get_world_size() > 1)
+        self.graphs = bool(graphs)
         self.dn_number, self.label_noise_ratio = dn_number, label_noise_ratio
         self.weights = weights
         self.seed = seed
@@ -149,6 +158,14 @@ class Trainer:
             plan.mask.copy_(torch.from_numpy(dn_attn_mask(pad, groups, single, eng.nq).astype(np.uint8)))
             plan._mask_key = (pad, groups, single)
 
+    def _set_graphs(self, *plans):
+        """Graph replay for the plans' tapes when self.graphs. A backbone with LearnableAffineBlocks
+        (DETRPose-N's B0) keeps both its tapes eager: sync_lab writes the scalars' current values
+        into conv descriptors that its forward and backward launches read by value."""
+        for p in plans:
+            on = self.graphs and not getattr(p, "labs", None)
+            p.fw.use_graph = p.bw.use_graph = on
+
     def sub_step(self, images, targets):
         """Forward + criterion + backward of one sub-batch (engine.py:44-59): the gradients of
         its summed losses in eng.grad_flat (overwritten). Returns (loss names, device losses)."""
@@ -162,6 +179,7 @@ class Trainer:
         full = self.scope == "full"
         plan = eng.plan(B, pad, shapes, memory=memory, d_memory=self.ep.d_memory if full else None)
         self.plan = plan
+        self._set_graphs(plan, *((self.bb, self.ep) if full else ()))
         self._draw_dn(plan, packed, images, pad, groups, single)
         plan.forward()
         keys, vals = plan.criterion(packed, sizes, groups, weights=self.weights)

@@ -25,13 +25,16 @@ step's arena, and the backward is written out op by op in reverse:
                        recomputes enc_output + LN on the selected rows only (the only rows
                        with a gradient)
 
-Scope: the transformer (the encoder memory is an input and is not differentiated: the encoder /
-backbone backward is the next step of BASELINE config 5). BatchNorm is not on this path.
-Parameter gradients accumulate into one f32 buffer (`TrainEngine.grads`, reference names).
+Scope of this tape: the transformer. Its encoder-memory input is differentiated (d memory,
+accumulated by the MSDA value gradient and the two-stage rows) and handed to the encoder tape
+(encoder_train.EncoderTrainPlan), whose backward feeds the backbone tape
+(backbone_train.BackboneTrainPlan): train.Trainer chains the three. BatchNorm is not on this
+tape. Parameter gradients accumulate into one f32 buffer (`TrainEngine.grads`, reference names).
 """
 from __future__ import annotations
 
 import ctypes as C
+import os
 import math
 
 import numpy as np
@@ -57,18 +60,31 @@ def dn_match(sizes, pad_size, num_group):
 
 
 class Tape:
-    """Recorded launches with their descriptors kept alive."""
+    """Recorded launches with their descriptors kept alive.
+
+    use_graph: after one eager run, the launches are captured once into a hipGraph
+    (torch.cuda.CUDAGraph) and later runs replay it (one launch instead of one ctypes call per op).
+    Every op's arguments are fixed buffers and descriptors, so a replay is the eager run; a tape
+    holding host ops (the SyncBN collectives of world > 1) always runs eagerly."""
 
     def __init__(self, lib, device):
         self.lib = lib
         self.device = device
         self.ops = []
         self.keep = []
+        self.use_graph = False
+        self.runs = 0
+        self._graph = None
 
     def op(self, name, fn, *args):
         self.ops.append((name, fn, args))
+        self._graph = None
 
-    def run(self, stream=None, debug=None):
+    @property
+    def graphable(self):
+        return not any(getattr(fn, "host", False) for _, fn, _ in self.ops)
+
+    def _launch(self, stream, debug):
         s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream)
         for name, fn, args in self.ops:
             rc = fn(*args, s)
@@ -77,6 +93,18 @@ class Tape:
             if debug is not None:
                 torch.cuda.synchronize()
                 debug(name)
+
+    def run(self, stream=None, debug=None):
+        if self.use_graph and stream is None and debug is None and self.runs > 0 and self.graphable:
+            if self._graph is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._launch(None, None)
+                self._graph = g
+            self._graph.replay()
+        else:
+            self._launch(stream, debug)
+        self.runs += 1
 
 
 def _p(t, off=0):
@@ -514,7 +542,8 @@ class TrainPlan:
         # dp_msda_bwd_sorted's workspace (shared by the layers: their backward ops run in order on one
         # stream); None where the shape is outside the sort's range (dp_msda_bwd's atomics then)
         nws = int(lib.dp_msda_bwd_ws_bytes(B, S, self.lvl_hw, len(shapes), Qt * T, nh, eng.npnt))
-        self.msda_ws = buf(nws, dtype=torch.uint8) if nws > 0 and Cc // nh in (8, 16, 32, 64) else None
+        sort_ok = nws > 0 and Cc // nh in (8, 16, 32, 64) and os.environ.get("DETRPOSE_MSDA_BWD", "sorted") == "sorted"
+        self.msda_ws = buf(nws, dtype=torch.uint8) if sort_ok else None
         fw = Tape(lib, dev)
         bw = Tape(lib, dev)
         self.fw, self.bw = fw, bw
