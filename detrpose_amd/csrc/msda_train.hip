@@ -717,17 +717,18 @@ __global__ __launch_bounds__(256) void msda_sorted_bwd_kernel(const T* __restric
   }
 }
 
-// K3: a group of G = dh / VEC lanes per work item (pixel, chunk), 16 bytes of channels per lane
-// (16 items per wave at dh 32 bf16). The chunk's <= SORT_CHUNK entries of the pixel's four cell
+// K3: a group of G = dh / CPL lanes per work item (pixel, chunk), CPL channels per lane (32
+// items per wave at dh 32 bf16: CPL 16, two 16-byte loads per entry). The chunk's <= SORT_CHUNK entries of the pixel's four cell
 // lists are loaded up front (G per step, one per lane) and turned into (token row, a * w_k), then
 // broadcast one at a time from their lane while the grad_out row loads of consecutive entries are
 // in flight (unconditional: a dead entry has weight 0 and row 0).
-template <typename T, int G>
+template <typename T, int G, int CPL>
 __global__ __launch_bounds__(256) void msda_value_sum_kernel(const T* __restrict__ gout, int ldg,
                                                              float* __restrict__ gvalue, TLevels lv, int S, int L,
                                                              int P, int lq, int nh, int nseg, int bps_seg,
                                                              SortWs ws) {
   constexpr int VEC = Vec16<T>::N;
+  static_assert(CPL % VEC == 0 && CPL % 4 == 0, "whole 16-byte loads per lane");
   constexpr int IPW = 64 / G;             // items per wave
   constexpr int EPL = SORT_CHUNK / G;     // entries per lane
   const int xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
@@ -748,21 +749,21 @@ __global__ __launch_bounds__(256) void msda_value_sum_kernel(const T* __restrict
   const int pr1 = ia.y & 0xffff, pr2 = ia.y >> 16, pr3 = ia.z & 0xffff;
   const int n = live ? min(SORT_ITEM, total - chunk * SORT_ITEM) : 0;
   const int b = seg / nh, h = seg - b * nh;
-  const int dh = G * VEC;
-  float* gp = gvalue + ((int64_t)b * S + lv.start[l] + p) * (nh * dh) + h * dh + VEC * q;
-  float gold[VEC];   // the pixel's current gradient, loaded with the list entries
+  const int dh = G * CPL;
+  float* gp = gvalue + ((int64_t)b * S + lv.start[l] + p) * (nh * dh) + h * dh + CPL * q;
+  float gold[CPL];   // the pixel's current gradient, loaded with the list entries
 #pragma unroll
-  for (int e = 0; e < VEC; e += 4) {
+  for (int e = 0; e < CPL; e += 4) {
     const float4 x = *reinterpret_cast<const float4*>(gp + e);
     gold[e] = x.x; gold[e + 1] = x.y; gold[e + 2] = x.z; gold[e + 3] = x.w;
   }
   int nmax = n;   // the wave's longest chunk bounds the list and broadcast loops
 #pragma unroll
   for (int s = G; s < 64; s <<= 1) nmax = max(nmax, __shfl_xor(nmax, s, 64));
-  const T* gcol = gout + h * dh + VEC * q;
-  float acc[VEC];
+  const T* gcol = gout + h * dh + CPL * q;
+  float acc[CPL];
 #pragma unroll
-  for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
+  for (int c = 0; c < CPL; ++c) acc[c] = 0.f;
   const float4* lst = ws.list + (int64_t)seg * L * lq * P;
   for (int r0 = 0; r0 < nmax; r0 += SORT_CHUNK) {   // rounds of SORT_CHUNK entries (uniform)
     int er[EPL];
@@ -785,27 +786,28 @@ __global__ __launch_bounds__(256) void msda_value_sum_kernel(const T* __restrict
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       if (r0 + e * G >= nmax) break;
-      float gv[G][VEC];
+      float gv[G][CPL];
 #pragma unroll
       for (int s = 0; s < G; ++s) {
         const int rr = group_bcast<G>(er[e], s, g0);
-        load_vec(gcol + (int64_t)rr * ldg, gv[s]);
+#pragma unroll
+        for (int c = 0; c < CPL; c += VEC) load_vec(gcol + (int64_t)rr * ldg + c, *reinterpret_cast<float(*)[VEC]>(&gv[s][c]));
       }
 #pragma unroll
       for (int s = 0; s < G; ++s) {
         const float w = __int_as_float(group_bcast<G>(__float_as_int(ew[e]), s, g0));
 #pragma unroll
-        for (int c = 0; c < VEC; ++c) acc[c] += w * gv[s][c];
+        for (int c = 0; c < CPL; ++c) acc[c] += w * gv[s][c];
       }
     }
   }
   if (n <= 0) return;
   if (total > SORT_ITEM) {   // the pixel's lists span several items: they meet in float atomics
 #pragma unroll
-    for (int c = 0; c < VEC; ++c) unsafeAtomicAdd(gp + c, acc[c]);
+    for (int c = 0; c < CPL; ++c) unsafeAtomicAdd(gp + c, acc[c]);
   } else {                    // the only writer of this segment of the pixel's row
 #pragma unroll
-    for (int e = 0; e < VEC; e += 4)
+    for (int e = 0; e < CPL; e += 4)
       *reinterpret_cast<float4*>(gp + e) =
           make_float4(gold[e] + acc[e], gold[e + 1] + acc[e + 1], gold[e + 2] + acc[e + 2], gold[e + 3] + acc[e + 3]);
   }
@@ -972,7 +974,12 @@ extern "C" int dp_msda_bwd_sorted(const void* value, int32_t batch, int32_t S, c
 #undef DP_K2
   }
   {
-    const int G = dh / VEC;
+    // channels per lane: 16 for bf16 at dh >= 16 (two 16-byte loads per entry, 32 items per wave
+    // at dh 32), else one 16-byte load; DETRPOSE_MSDA_K3_CPL overrides (A/B)
+    static const int cpl_env = getenv("DETRPOSE_MSDA_K3_CPL") ? atoi(getenv("DETRPOSE_MSDA_K3_CPL")) : 0;
+    int cpl = dtype == DP_BF16 ? (dh >= 16 ? 16 : 8) : 4;
+    if (cpl_env && cpl_env % VEC == 0 && dh % cpl_env == 0 && cpl_env <= 16) cpl = cpl_env;
+    const int G = dh / cpl;
     const int ipb = 4 * (64 / G);   // items per block
     int bps_seg = 0;
     for (int l = 0; l < nlevels; ++l) {
@@ -981,15 +988,26 @@ extern "C" int dp_msda_bwd_sorted(const void* value, int32_t batch, int32_t S, c
       bps_seg += ws.bps[l];
     }
     const dim3 grid(8 * segs_per_xcd * bps_seg);
-#define DP_VSUM(T, GG)                                                                                              \
-  hipLaunchKernelGGL((msda_value_sum_kernel<T, GG>), grid, dim3(256), 0, s, (const T*)grad_out, ld_grad_out,      \
+#define DP_VSUM(T, GG, CC)                                                                                          \
+  hipLaunchKernelGGL((msda_value_sum_kernel<T, GG, CC>), grid, dim3(256), 0, s, (const T*)grad_out, ld_grad_out,  \
                      grad_value, lv, S, nlevels, npoints, lq, nhead, nseg, bps_seg, ws)
     if (dtype == DP_BF16) {
-      if (G == 1) DP_VSUM(bf16_t, 1); else if (G == 2) DP_VSUM(bf16_t, 2); else if (G == 4) DP_VSUM(bf16_t, 4);
-      else DP_VSUM(bf16_t, 8);
+      if (cpl == 16) {
+        if (G == 1) DP_VSUM(bf16_t, 1, 16); else if (G == 2) DP_VSUM(bf16_t, 2, 16); else DP_VSUM(bf16_t, 4, 16);
+      } else {
+        if (G == 1) DP_VSUM(bf16_t, 1, 8); else if (G == 2) DP_VSUM(bf16_t, 2, 8); else if (G == 4) DP_VSUM(bf16_t, 4, 8);
+        else DP_VSUM(bf16_t, 8, 8);
+      }
     } else {
-      if (G == 2) DP_VSUM(float, 2); else if (G == 4) DP_VSUM(float, 4); else if (G == 8) DP_VSUM(float, 8);
-      else DP_VSUM(float, 16);
+      if (cpl == 8) {
+        if (G == 1) DP_VSUM(float, 1, 8); else if (G == 2) DP_VSUM(float, 2, 8); else if (G == 4) DP_VSUM(float, 4, 8);
+        else DP_VSUM(float, 8, 8);
+      } else if (cpl == 16) {
+        if (G == 1) DP_VSUM(float, 1, 16); else if (G == 2) DP_VSUM(float, 2, 16); else DP_VSUM(float, 4, 16);
+      } else {
+        if (G == 2) DP_VSUM(float, 2, 4); else if (G == 4) DP_VSUM(float, 4, 4); else if (G == 8) DP_VSUM(float, 8, 4);
+        else DP_VSUM(float, 16, 4);
+      }
     }
 #undef DP_VSUM
   }

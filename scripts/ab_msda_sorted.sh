@@ -11,7 +11,7 @@ run() {
   cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $R/$OUT/$1 -o run -- python $R/scripts/msda_bwd_bench.py --reps 3 > $R/$OUT/$1.log 2>&1
 }
 run base || exit 1
-DETRPOSE_MSDA_SEGMAP=0 run segmap0 || exit 1
+DETRPOSE_MSDA_K3_CPL=8 run k3cpl8 || exit 1
 for tv in "$@"; do
   tag=${tv%%=*}; lib=${tv#*=}
   DETRPOSE_HIP_LIB=$R/$lib DETRPOSE_ALLOW_STALE_LIB=1 run $tag || exit 1

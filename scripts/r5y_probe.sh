@@ -9,3 +9,5 @@ for cfg in "sorted 1" "atomic 1" "sorted 0"; do
 done
 timeout -k 10 400 python -u -m pytest tests/test_gpu_train_graphs.py -m gpu -v -s --timeout 300 --timeout-method thread > gpurun_out/r5y/pytest.log 2>&1
 tail -3 gpurun_out/r5y/pytest.log; grep -E "max rel|graph - eager|replayed" gpurun_out/r5y/pytest.log
+timeout -k 10 300 python -u -m pytest tests/test_msda_train.py -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/r5y/pytest_msda.log 2>&1; tail -1 gpurun_out/r5y/pytest_msda.log
+bash scripts/ab_msda_sorted.sh gpurun_out/r5y/ab
