@@ -16,6 +16,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------- error reporting
 void dp_set_error(const char* fmt, ...);
 int dp_check_launch(const char* what);
+// stream-ordered zero fill of `bytes` bytes (a kernel: graph-capturable); 0 on success
+int dp_zero_async(void* p, size_t bytes, hipStream_t s);
 
 // dp_conv2d_describe: while a describe buffer is set (this thread), the conv launch sites
 // write the kernel instantiation they would launch and return 0 instead of launching

@@ -61,8 +61,10 @@ struct HaloPool {
 // unrolled and every pixel-fragment address is a lane constant computed once per block (the
 // tile geometry is the same for every tile): no tap-table reads or address arithmetic
 // between the fragment reads of the MFMA loop.
+// NR (streamed weights): depth of the weight ring; the K-step loop keeps NR - 1 steps of weight
+// DMA in flight (a counted vmcnt wait per step instead of a full drain when NR > 2).
 template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false,
-          int NKC = 0>
+          int NKC = 0, int NR = 2>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 2)))
 void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int vec_ok, HaloPool pool) {
   static_assert(!POOL || (KH == 2 && KW == 2 && S == 1 && !DBUF), "pool: 2x2 s1 window, single patch buffer");
@@ -91,7 +93,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   int* const tab = reinterpret_cast<int*>(smem);
   float* const bias_l = reinterpret_cast<float*>(smem + TAB_ENTRY_BYTES);
   char* const wbase = smem + TAB_BYTES;
-  char* const pbase0 = wbase + (RESW ? nk : 2) * BN * 128;
+  char* const pbase0 = wbase + (RESW ? nk : NR) * BN * 128;
   const int r8 = lane >> 3;
   const i32x4 rb_src = make_rsrc(d.weight);
 
@@ -120,6 +122,12 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
       const int o = b_off[t] != OOB ? (b_off[t] + kt * 64) * 2 : OOB;
       dma16(rb_src, dst + (wave + NW * t) * 1024, o);
     }
+  };
+  // the first NR - 1 weight K-steps of a tile (ring slots 0 .. NR-2)
+  auto issue_w_pro = [&]() {
+#pragma unroll
+    for (int i = 0; i < NR - 1; ++i)
+      if (i < nk) issue_w(i, wbase + i * BN * 128);
   };
   auto issue_patch = [&](int tile, char* pb) {
     const int tx = tile % tiles_x, rest = tile / tiles_x;
@@ -183,7 +191,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   // hides behind this tile's epilogue instead of stalling the next tile's start
   constexpr bool EARLY = !DBUF && !POOL;
   if (DBUF || EARLY) issue_patch(L, pbase0);
-  if (EARLY && !RESW) issue_w(0, wbase);
+  if (EARLY && !RESW) issue_w_pro();
   f32x4 acc[TM][TN];
   // stores one wave issues in the epilogue of a whole tile (plain epilogue, vector path): the
   // next tile's wait may leave them in flight, since VMEM ops retire in issue order and the
@@ -220,7 +228,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       issue_patch(tile, pbase0);
-      if (!RESW) issue_w(0, wbase);
+      if (!RESW) issue_w_pro();
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       pbase = pbase0;
@@ -298,12 +306,17 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
           wsl = wbase + kt * BN * 128;
         } else {
           if (kt > 0) {
-            if (!(DP_HALO_ABL & 1)) wait_vmcnt<0>();
+            // step kt's weights landed: NR - 2 later steps may stay in flight (all near the end)
+            if (!(DP_HALO_ABL & 1)) {
+              if (kt + NR - 2 < nk) wait_vmcnt<(NR - 2) * GB>();
+              else wait_vmcnt<0>();
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (!(DP_HALO_ABL & 2)) __builtin_amdgcn_s_barrier();
           }
-          if (kt + 1 < nk) issue_w(kt + 1, wbase + ((kt + 1) & 1) * BN * 128);
-          wsl = wbase + (kt & 1) * BN * 128;
+          // the slot of step kt + NR - 1 held step kt - 1, which every wave is past (barrier)
+          if (kt + NR - 1 < nk) issue_w(kt + NR - 1, wbase + ((kt + NR - 1) % NR) * BN * 128);
+          wsl = wbase + (kt % NR) * BN * 128;
         }
         __builtin_amdgcn_sched_barrier(0);
         bf16x8 wf[2][TN];
@@ -341,7 +354,7 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
       __builtin_amdgcn_s_barrier();
       if (tile + G < ntiles) {
         issue_patch(tile + G, pbase0);
-        if (!RESW) issue_w(0, wbase);
+        if (!RESW) issue_w_pro();
       }
     }
     // epilogue: lane owns pixel (oy0 + yq, ox0 + q), channels lane_chan(g, 0 .. NPL-1)
@@ -419,11 +432,12 @@ void conv_halo_kernel(dp_conv_desc d, int tiles_x, int tiles_y, int ntiles, int 
   wait_vmcnt<0>();
 }
 
-template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false, int NKC = 0>
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF, int ACT, bool POOL = false, int NKC = 0,
+          int NR = 2>
 int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloPool pool = {}) {
-  DP_DESCRIBE("conv_halo_kernel<%d, %d, %d, %d, %d, %d, %s, %s, %d, %s, %d>", TH, NW, KH, KW, S, BN, DP_TF(RESW),
-              DP_TF(DBUF), ACT, DP_TF(POOL), NKC);
-  auto kern = conv_halo_kernel<TH, NW, KH, KW, S, BN, RESW, DBUF, ACT, POOL, NKC>;
+  DP_DESCRIBE("conv_halo_kernel<%d, %d, %d, %d, %d, %d, %s, %s, %d, %s, %d, %d>", TH, NW, KH, KW, S, BN, DP_TF(RESW),
+              DP_TF(DBUF), ACT, DP_TF(POOL), NKC, NR);
+  auto kern = conv_halo_kernel<TH, NW, KH, KW, S, BN, RESW, DBUF, ACT, POOL, NKC, NR>;
   static const int occ = [&] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
@@ -450,15 +464,16 @@ int launch_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloP
   return dp_check_launch("dp_conv2d(halo)");
 }
 
-template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF = false, bool POOL = false, int NKC = 0>
+template <int TH, int NW, int KH, int KW, int S, int BN, bool RESW, bool DBUF = false, bool POOL = false, int NKC = 0,
+          int NR = 2>
 int launch_halo_act(const dp_conv_desc& d, hipStream_t s, int vec_ok, int lds, HaloPool pool = {}) {
   switch (d.act) {
     case DP_ACT_RELU:
-      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_RELU, POOL, NKC>(d, s, vec_ok, lds, pool);
+      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_RELU, POOL, NKC, NR>(d, s, vec_ok, lds, pool);
     case DP_ACT_SILU:
-      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_SILU, POOL, NKC>(d, s, vec_ok, lds, pool);
+      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_SILU, POOL, NKC, NR>(d, s, vec_ok, lds, pool);
     case DP_ACT_NONE:
-      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_NONE, POOL, NKC>(d, s, vec_ok, lds, pool);
+      return launch_halo<TH, NW, KH, KW, S, BN, RESW, DBUF, DP_ACT_NONE, POOL, NKC, NR>(d, s, vec_ok, lds, pool);
     default: return -1;
   }
 }
@@ -490,6 +505,19 @@ int dp_conv2d_halo(const dp_conv_desc& d, hipStream_t s, int vec_ok) {
     if (bn == 64 && lds_res(P16, 2) <= LMAX)
       return launch_halo_act<16, 8, 3, 3, 1, 64, true, true>(d, s, vec_ok, lds_res(P16, 2));
     if (bn == 32 && lds_res(P8, 1) <= 80 * 1024) return launch_halo_act<8, 4, 3, 3, 1, 32, true>(d, s, vec_ok, lds_res(P8, 1));
+    // the 128-channel convs on maps of >= 64 x 64 (the encoder's stride-8 level): 16 x 16 tiles of
+    // 8 waves, one block per CU, a 4-deep weight ring (3 K-steps of weight DMA in flight): the
+    // L b64 80 x 80 shapes 148.5 -> 139.4 us, outputs bit-identical (profiles/r5z_halo_nr_ab.txt);
+    // 40 x 40 is slower this way (tile quantisation: 64 vs 43 us) and keeps the 8-row tiles.
+    // DETRPOSE_HALO_NR = 2 (off) / 3 / 4 overrides (A/B).
+    static const int halo_nr = getenv("DETRPOSE_HALO_NR") ? atoi(getenv("DETRPOSE_HALO_NR")) : 4;
+    if (bn == 128 && (halo_nr == 3 || halo_nr == 4) && d.out_h >= 64 && d.out_w >= 64) {
+      auto lds_nr = [&](int nr) { return TAB_BYTES + nr * bn * 128 + nkc * P16; };
+      if (halo_nr == 3 && lds_nr(3) <= LMAX)
+        return launch_halo_act<16, 8, 3, 3, 1, 128, false, false, false, 0, 3>(d, s, vec_ok, lds_nr(3));
+      if (halo_nr == 4 && lds_nr(4) <= LMAX)
+        return launch_halo_act<16, 8, 3, 3, 1, 128, false, false, false, 0, 4>(d, s, vec_ok, lds_nr(4));
+    }
     if (lds_str(P8) > 80 * 1024) return -1;
     if (bn == 64) return launch_halo_act<8, 4, 3, 3, 1, 64, false>(d, s, vec_ok, lds_str(P8));
     if (bn == 96) return launch_halo_act<8, 4, 3, 3, 1, 96, false>(d, s, vec_ok, lds_str(P8));

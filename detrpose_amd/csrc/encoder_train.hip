@@ -565,7 +565,7 @@ extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, f
                            void* stream) {
   DP_REQUIRE(x && out && rows > 0 && c > 0 && ld >= c, "dp_bn_stats: bad arguments");
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(out + c, 0, 2 * (size_t)c * sizeof(float), s) != hipSuccess) {
+  if (dp_zero_async(out + c, 2 * (size_t)c * sizeof(float), s)) {
     dp_set_error("dp_bn_stats: memset failed");
     return DP_EINVAL;
   }
@@ -611,7 +611,7 @@ extern "C" int dp_bn_act_bwd_reduce(const void* dy, int64_t ld_dy, const void* z
   DP_REQUIRE(dy && z1 && mr1 && g1 && b1 && sums && rows > 0 && c > 0 && (!z2 || (mr2 && g2 && b2)),
              "dp_bn_act_bwd_reduce: bad arguments");
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(sums, 0, 3 * (size_t)c * sizeof(float), s) != hipSuccess) {
+  if (dp_zero_async(sums, 3 * (size_t)c * sizeof(float), s)) {
     dp_set_error("dp_bn_act_bwd_reduce: memset failed");
     return DP_EINVAL;
   }

@@ -607,7 +607,7 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
   DP_REQUIRE(K < (1ll << 31), "dp_conv_wgrad: too many pixels");
   hipStream_t s = as_stream(stream);
   const int taps = kh * kw, N = taps * cin;
-  if (hipMemsetAsync(scratch, 0, (size_t)cout * N * sizeof(float), s) != hipSuccess) {
+  if (dp_zero_async(scratch, (size_t)cout * N * sizeof(float), s)) {
     dp_set_error("dp_conv_wgrad: memset failed");
     return DP_EINVAL;
   }

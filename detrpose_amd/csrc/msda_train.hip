@@ -365,9 +365,14 @@ constexpr int SORT_ITEM = 256;   // list entries per K3 work item (a hot pixel's
 
 struct SortWs {
   float4* list;        // [NS][L * lq * P] (token as int bits, a, fx, fy) in cell order (level-major)
-  int4* item;          // [NS][isz][2] (pixel | chunk, list prefixes, entries, list bases), level-major
+  float* pa;           // [NS][lq][L * P] each point's softmaxed attention weight (K2 writes it)
+  int4* item;          // [NS][isz][2] (pixel | chunk, list prefixes, entries, list bases), level-major:
+                       // slot p = pixel p's first chunk, its further chunks past H * W
   int32_t* nitem;      // [NS][L]
   int isz;
+#ifdef DP_KS_TIMING
+  long long* dbg;      // A/B builds only: per sort block, wall-clock stamps at its phase boundaries
+#endif
   int spx, segmap;     // segments per XCD; 1 (default): XCD x serves segments [x * spx, (x + 1) * spx)
                        // (whole images per XCD), 0: segments s = x mod 8 (one head per XCD)
   int ibase[MAXL];     // first item slot of each level
@@ -442,72 +447,64 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int& total) {
   return pre + x - v;
 }
 
-// LDS: softmax (max, 1/den) [lq] float2 | cell offsets [ncell + 1] int (counts, then offsets,
-// then cursors). Each thread owns the points tid + u * 1024 (u < PPT) of the level and keeps their
-// cell, fractions and logit in registers between the two passes; every loop issues all its loads
-// before the first use.
+#ifdef DP_KS_TIMING
+#define DP_KS_STAMP(k) \
+  if (threadIdx.x == 0) ws.dbg[(int64_t)(seg * L + l) * 8 + (k)] = (long long)wall_clock64()
+#else
+#define DP_KS_STAMP(k)
+#endif
+
+// LDS: cell offsets [ncell + 1] int (counts, then offsets, then cursors). Each thread owns the
+// points tid + u * 1024 (u < PPT) of the level and keeps their cells in registers between the two
+// passes; pass 2 reloads the points' inputs (L2) and the attention weight K2 stored (ws.pa).
 constexpr int SORT_PPT = 8;   // points per thread: lq * P <= 8192
 
 __global__ __launch_bounds__(1024) void msda_sort_kernel(TLevels lv, int L, int P, const float* __restrict__ oa,
                                                          const float* __restrict__ ref, int lq, int nh, int nseg,
                                                          SortWs ws) {
-  extern __shared__ float2 smx[];
+  extern __shared__ int cnt[];
   __shared__ int wsum[16];
+  __shared__ int novf;
   const int xcd = blockIdx.x & 7, i = blockIdx.x >> 3;
   const int seg = seg_of(xcd, i / L, ws.spx, ws.segmap), l = i - (i / L) * L;
   if (seg >= nseg) return;
+  DP_KS_STAMP(0);
   const int b = seg / nh, h = seg - b * nh;
   const int H = lv.h[l], W = lv.w[l], W1 = W + 1, ncell = (H + 1) * W1;
   const int LP = L * P, npt = lq * P, tid = threadIdx.x;
   const int ncol = nh * LP * 3;
   const float* oab = oa + (int64_t)b * lq * ncol;
-  int* cnt = reinterpret_cast<int*>(smx + lq);
   for (int c = tid; c <= ncell; c += 1024) cnt[c] = 0;
-  for (int t = tid; t < lq; t += 1024) {   // softmax over the token's L*P (<= 16) logits of head h
-    const float* lg = oab + (int64_t)t * ncol + nh * LP * 2 + h * LP;
-    float v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = lg[min(j, LP - 1)];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) mx = j < LP ? fmaxf(mx, v[j]) : mx;
-    float den = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) den += j < LP ? expf(v[j] - mx) : 0.f;
-    smx[t] = make_float2(mx, 1.f / den);
-  }
-  // pass 1: the cells of this thread's points
+  if (tid == 0) novf = 0;
+  // pass 1: the cells of this thread's points (half the points' loads in flight at a time)
   int key[SORT_PPT];
-  float pfx[SORT_PPT], pfy[SORT_PPT], plg[SORT_PPT];
-  {
-    float rx[SORT_PPT], ry[SORT_PPT], ox[SORT_PPT], oy[SORT_PPT];
+  auto point_xy = [&](int u, float& x, float& y) {
+    const int pt = min(tid + u * 1024, npt - 1);
+    const int t = pt / P, j = l * P + pt - t * P;
+    const float* orow = oab + (int64_t)t * ncol;
+    msda_xy(ref[2 * (b * lq + t)], ref[2 * (b * lq + t) + 1], orow[(h * LP + j) * 2], orow[(h * LP + j) * 2 + 1], H,
+            W, x, y);
+  };
 #pragma unroll
-    for (int u = 0; u < SORT_PPT; ++u) {
-      const int pt = min(tid + u * 1024, npt - 1);
-      const int t = pt / P, j = l * P + pt - t * P;
-      const float* orow = oab + (int64_t)t * ncol;
-      rx[u] = ref[2 * (b * lq + t)];
-      ry[u] = ref[2 * (b * lq + t) + 1];
-      ox[u] = orow[(h * LP + j) * 2];
-      oy[u] = orow[(h * LP + j) * 2 + 1];
-      plg[u] = orow[nh * LP * 2 + h * LP + j];
-    }
+  for (int u0 = 0; u0 < SORT_PPT; u0 += SORT_PPT / 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    float x[SORT_PPT / 2], y[SORT_PPT / 2];
 #pragma unroll
-    for (int u = 0; u < SORT_PPT; ++u) {
-      float x, y;
-      msda_xy(rx[u], ry[u], ox[u], oy[u], H, W, x, y);
-      const float fx0 = floorf(x), fy0 = floorf(y);
-      const int x0 = (int)fx0, y0 = (int)fy0;
-      pfx[u] = x - fx0;
-      pfy[u] = y - fy0;
-      key[u] = tid + u * 1024 < npt && x0 >= -1 && x0 < W && y0 >= -1 && y0 < H ? (y0 + 1) * W1 + x0 + 1 : -1;
+    for (int u = 0; u < SORT_PPT / 2; ++u) point_xy(u0 + u, x[u], y[u]);
+#pragma unroll
+    for (int u = 0; u < SORT_PPT / 2; ++u) {
+      const int x0 = (int)floorf(x[u]), y0 = (int)floorf(y[u]);
+      key[u0 + u] = tid + (u0 + u) * 1024 < npt && x0 >= -1 && x0 < W && y0 >= -1 && y0 < H ? (y0 + 1) * W1 + x0 + 1
+                                                                                          : -1;
     }
   }
   __syncthreads();   // counters zeroed
+  DP_KS_STAMP(1);
 #pragma unroll
   for (int u = 0; u < SORT_PPT; ++u)
     if (key[u] >= 0) atomicAdd(cnt + key[u], 1);
   __syncthreads();
+  DP_KS_STAMP(2);
   // counts -> exclusive offsets (a contiguous range per thread), cnt[ncell] = the total
   const int per = (ncell + 1023) / 1024, c0 = min(ncell, tid * per), c1 = min(ncell, c0 + per);
   int s = 0;
@@ -521,22 +518,16 @@ __global__ __launch_bounds__(1024) void msda_sort_kernel(TLevels lv, int L, int 
   }
   if (tid == 0) cnt[ncell] = tot;
   __syncthreads();
+  DP_KS_STAMP(3);
   // work items: pixel p's entries = its four cells' lists (the pixel is corner k of cell
   // (x - (k & 1), y - (k >> 1))), in chunks of SORT_ITEM; each item carries its lists' bounds.
-  // Pixels tid + k * 1024 per thread (item order is free: every item gets its own slot).
+  // Item slot p holds pixel p's first chunk (consecutive threads, consecutive 32-byte records;
+  // an empty pixel's item has no entries), further chunks go past npix.
   const int lbase = l * npt;
   const int npix = H * W;
-  auto pix_cell = [&](int p) { const int py = p / W; return (py + 1) * W1 + p - py * W + 1; };
-  int si = 0;
-  for (int p = tid; p < npix; p += 1024) {
-    const int c = pix_cell(p);
-    si += (cnt[c + 1] - cnt[c - 1] + cnt[c - W1 + 1] - cnt[c - W1 - 1] + SORT_ITEM - 1) / SORT_ITEM;
-  }
-  int itot;
-  int ipre = block_excl_scan(si, wsum, itot);
   int4* item = ws.item + ((int64_t)seg * ws.isz + ws.ibase[l]) * 2;
   for (int p = tid; p < npix; p += 1024) {
-    const int c = pix_cell(p);
+    const int py = p / W, c = (py + 1) * W1 + p - py * W + 1;
     const int cell[4] = {c, c - 1, c - W1, c - W1 - 1};
     int pr[4], base[4], n = 0;
 #pragma unroll
@@ -545,26 +536,46 @@ __global__ __launch_bounds__(1024) void msda_sort_kernel(TLevels lv, int L, int 
       base[k] = lbase + cnt[cell[k]] - n;
       n += cnt[cell[k] + 1] - cnt[cell[k]];
     }
-    for (int k = 0; k * SORT_ITEM < n; ++k, ++ipre) {
-      item[2 * ipre] = make_int4(p | (k << 16), pr[1] | (pr[2] << 16), pr[3] | (n << 16), base[0]);
-      item[2 * ipre + 1] = make_int4(base[1], base[2], base[3], 0);
+    const int4 i1 = make_int4(base[1], base[2], base[3], 0);
+    item[2 * p] = make_int4(p, pr[1] | (pr[2] << 16), pr[3] | (n << 16), base[0]);
+    item[2 * p + 1] = i1;
+    for (int k = 1; k * SORT_ITEM < n; ++k) {   // rare: a hot pixel
+      const int q = npix + atomicAdd(&novf, 1);
+      item[2 * q] = make_int4(p | (k << 16), pr[1] | (pr[2] << 16), pr[3] | (n << 16), base[0]);
+      item[2 * q + 1] = i1;
     }
   }
-  if (tid == 0) ws.nitem[seg * L + l] = itot;
-  __syncthreads();   // the offsets become cursors below
+  __syncthreads();   // novf complete; the offsets become cursors below
+  if (tid == 0) ws.nitem[seg * L + l] = npix + novf;
+  DP_KS_STAMP(4);
   // pass 2: (token, a, fx, fy) at the point's slot of its cell's list (16-byte stores into this
   // block's own lq * P * 16-byte slab: its lines fill in L2)
   float4* gl = ws.list + (int64_t)seg * L * npt + lbase;
-  int slot[SORT_PPT];
+  const float* pa = ws.pa + (int64_t)seg * lq * LP;
 #pragma unroll
-  for (int u = 0; u < SORT_PPT; ++u) slot[u] = key[u] >= 0 ? atomicAdd(cnt + key[u], 1) : 0;
+  for (int u0 = 0; u0 < SORT_PPT; u0 += SORT_PPT / 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    float x[SORT_PPT / 2], y[SORT_PPT / 2], aj[SORT_PPT / 2];
+    int slot[SORT_PPT / 2];
 #pragma unroll
-  for (int u = 0; u < SORT_PPT; ++u) {
-    if (key[u] < 0) continue;
-    const int pt = tid + u * 1024, t = pt / P;
-    const float2 st = smx[t];
-    gl[slot[u]] = make_float4(__int_as_float(t), expf(plg[u] - st.x) * st.y, pfx[u], pfy[u]);
+    for (int u = 0; u < SORT_PPT / 2; ++u) {
+      point_xy(u0 + u, x[u], y[u]);
+      const int pt = min(tid + (u0 + u) * 1024, npt - 1);
+      const int t = pt / P;
+      aj[u] = pa[t * LP + l * P + pt - t * P];
+      slot[u] = key[u0 + u] >= 0 ? atomicAdd(cnt + key[u0 + u], 1) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < SORT_PPT / 2; ++u) {
+      if (key[u0 + u] < 0) continue;
+      const int t = (tid + (u0 + u) * 1024) / P;
+      gl[slot[u]] = make_float4(__int_as_float(t), aj[u], x[u] - floorf(x[u]), y[u] - floorf(y[u]));
+    }
   }
+#ifdef DP_KS_TIMING
+  __syncthreads();
+#endif
+  DP_KS_STAMP(5);
 }
 
 // msda_fused_bwd_kernel's gather backward for d offsets / d logits / d ref (16-byte lanes,
@@ -579,7 +590,8 @@ __global__ __launch_bounds__(256) void msda_sorted_bwd_kernel(const T* __restric
                                                               const float* __restrict__ ref,
                                                               const T* __restrict__ gout, int ldg,
                                                               float* __restrict__ goa, float* __restrict__ gref,
-                                                              int lq, int nh, int nseg, int bps, int spx, int segmap) {
+                                                              int lq, int nh, int nseg, int bps, int spx, int segmap,
+                                                              float* __restrict__ pa) {
   constexpr int VEC = Vec16<T>::N;
   constexpr int PPW = 64 / CPT;
   constexpr int KMAX = (LPM + CPT - 1) / CPT;   // kept points per lane, L * P <= LPM
@@ -703,12 +715,14 @@ __global__ __launch_bounds__(256) void msda_sorted_bwd_kernel(const T* __restric
   }
   if (!live) return;
   float* grow = goa + (int64_t)r * ncol;
+  float* pat = pa + ((int64_t)seg * lq + t) * LP;
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
     const int j = i * CPT + c;
     if (j < LP) {
       *reinterpret_cast<float2*>(grow + (h * LP + j) * 2) = make_float2(kgx[i], kgy[i]);
       grow[nh * LP * 2 + h * LP + j] = ka[i] * (kga[i] - dot);   // softmax backward
+      pat[j] = ka[i];                                            // the sort's value-gradient weights
     }
   }
   if (gref && c == 0) {
@@ -717,8 +731,8 @@ __global__ __launch_bounds__(256) void msda_sorted_bwd_kernel(const T* __restric
   }
 }
 
-// K3: a group of G = dh / CPL lanes per work item (pixel, chunk), CPL channels per lane (32
-// items per wave at dh 32 bf16: CPL 16, two 16-byte loads per entry). The chunk's <= SORT_CHUNK entries of the pixel's four cell
+// K3: a group of G = dh / CPL lanes per work item (pixel, chunk), CPL channels per lane (16
+// items per wave at dh 32 bf16: CPL 8, one 16-byte load per entry). The chunk's <= SORT_CHUNK entries of the pixel's four cell
 // lists are loaded up front (G per step, one per lane) and turned into (token row, a * w_k), then
 // broadcast one at a time from their lane while the grad_out row loads of consecutive entries are
 // in flight (unconditional: a dead entry has weight 0 and row 0).
@@ -863,7 +877,7 @@ int64_t sort_ws_layout(int batch, int S, int lq, int nh, const TLevels& lv, int 
     const int items = lv.h[l] * lv.w[l] + (4 * npt + SORT_ITEM - 1) / SORT_ITEM;
     ws->ibase[l] = isz;
     isz += items;
-    lds = std::max(lds, lq * 8 + (cells + 1) * 4);
+    lds = std::max(lds, (cells + 1) * 4);
   }
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -872,8 +886,12 @@ int64_t sort_ws_layout(int batch, int S, int lq, int nh, const TLevels& lv, int 
     return base ? base + at : nullptr;
   };
   ws->list = reinterpret_cast<float4*>(take(nseg * L * npt * 16));
+  ws->pa = reinterpret_cast<float*>(take(nseg * npt * L * 4));
   ws->item = reinterpret_cast<int4*>(take(nseg * isz * 32));
   ws->nitem = reinterpret_cast<int32_t*>(take(nseg * L * 4));
+#ifdef DP_KS_TIMING
+  ws->dbg = reinterpret_cast<long long*>(take(nseg * L * 8 * 8));   // the workspace's last region
+#endif
   ws->isz = isz;
   if (ks_lds) *ks_lds = lds;
   return o;
@@ -942,15 +960,13 @@ extern "C" int dp_msda_bwd_sorted(const void* value, int32_t batch, int32_t S, c
   ws.spx = segs_per_xcd;
   ws.segmap = getenv("DETRPOSE_MSDA_SEGMAP") ? atoi(getenv("DETRPOSE_MSDA_SEGMAP")) : 1;
   const size_t vbytes = (size_t)batch * S * nhead * dh * sizeof(float);
-  if ((!accumulate_value && hipMemsetAsync(grad_value, 0, vbytes, s) != hipSuccess) ||
-      (grad_ref && hipMemsetAsync(grad_ref, 0, (size_t)batch * lq * 2 * sizeof(float), s) != hipSuccess))
+  if ((!accumulate_value && dp_zero_async(grad_value, vbytes, s)) ||
+      (grad_ref && dp_zero_async(grad_ref, (size_t)batch * lq * 2 * sizeof(float), s)))
     return dp_check_launch("dp_msda_bwd_sorted(memset)");
   static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_sort_kernel),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  SORT_LDS_MAX) == hipSuccess;
   DP_REQUIRE(lds_ok, "dp_msda_bwd_sorted: cannot raise the sort kernel's LDS limit");
-  hipLaunchKernelGGL(msda_sort_kernel, dim3(8 * segs_per_xcd * nlevels), dim3(1024), lds, s, lv, nlevels, npoints,
-                     offattn, ref, lq, nhead, nseg, ws);
   {
     const int cpt = dh / VEC;
     const int bps = (lq + 4 * (64 / cpt) - 1) / (4 * (64 / cpt));
@@ -959,11 +975,11 @@ extern "C" int dp_msda_bwd_sorted(const void* value, int32_t batch, int32_t S, c
   if (nlevels * npoints <= 12)                                                                                    \
     hipLaunchKernelGGL((msda_sorted_bwd_kernel<T, CPT, 12>), grid, dim3(256), 0, s, (const T*)value, S, lv,      \
                        nlevels, npoints, offattn, ref, (const T*)grad_out, ld_grad_out, grad_offattn, grad_ref, lq,   \
-                       nhead, nseg, bps, segs_per_xcd, ws.segmap);                                                \
+                       nhead, nseg, bps, segs_per_xcd, ws.segmap, ws.pa);                                         \
   else                                                                                                            \
     hipLaunchKernelGGL((msda_sorted_bwd_kernel<T, CPT, 16>), grid, dim3(256), 0, s, (const T*)value, S, lv,      \
                        nlevels, npoints, offattn, ref, (const T*)grad_out, ld_grad_out, grad_offattn, grad_ref, lq,   \
-                       nhead, nseg, bps, segs_per_xcd, ws.segmap)
+                       nhead, nseg, bps, segs_per_xcd, ws.segmap, ws.pa)
     if (dtype == DP_BF16) {
       if (cpt == 1) { DP_K2(bf16_t, 1); } else if (cpt == 2) { DP_K2(bf16_t, 2); } else if (cpt == 4) { DP_K2(bf16_t, 4); }
       else { DP_K2(bf16_t, 8); }
@@ -973,11 +989,15 @@ extern "C" int dp_msda_bwd_sorted(const void* value, int32_t batch, int32_t S, c
     }
 #undef DP_K2
   }
+  // the sort after K2: it reads the attention weights K2 stored (ws.pa)
+  hipLaunchKernelGGL(msda_sort_kernel, dim3(8 * segs_per_xcd * nlevels), dim3(1024), lds, s, lv, nlevels, npoints,
+                     offattn, ref, lq, nhead, nseg, ws);
   {
-    // channels per lane: 16 for bf16 at dh >= 16 (two 16-byte loads per entry, 32 items per wave
-    // at dh 32), else one 16-byte load; DETRPOSE_MSDA_K3_CPL overrides (A/B)
+    // channels per lane: one 16-byte load per entry (8 bf16 / 4 f32; 16 items per wave at dh 32
+    // bf16). 16 bf16 channels per lane (32 items per wave) measured slower: 172 / 241 vs 141 / 142
+    // us (spread / clustered, r5y). DETRPOSE_MSDA_K3_CPL overrides (A/B)
     static const int cpl_env = getenv("DETRPOSE_MSDA_K3_CPL") ? atoi(getenv("DETRPOSE_MSDA_K3_CPL")) : 0;
-    int cpl = dtype == DP_BF16 ? (dh >= 16 ? 16 : 8) : 4;
+    int cpl = dtype == DP_BF16 ? 8 : 4;
     if (cpl_env && cpl_env % VEC == 0 && dh % cpl_env == 0 && cpl_env <= 16) cpl = cpl_env;
     const int G = dh / cpl;
     const int ipb = 4 * (64 / G);   // items per block
@@ -1040,7 +1060,7 @@ extern "C" int dp_msda_core_bwd(const void* value, int32_t batch, int32_t S, con
   DP_REQUIRE((reinterpret_cast<uintptr_t>(grad_out) & 15) == 0, "dp_msda_core_bwd: grad_out must be 16-byte aligned");
   hipStream_t s = as_stream(stream);
   // grad_value is accumulated by atomics: clear it on the same stream first (graph-capturable)
-  if (hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess)
+  if (dp_zero_async(grad_value, (size_t)batch * S * nhead * dh * sizeof(float), s))
     return dp_check_launch("dp_msda_core_bwd(memset)");
   if (dtype == DP_BF16)
     return launch_core<bf16_t, true>(value, batch, S, lv, nlevels, npoints, loc, attn, grad_out, nullptr, grad_value,
@@ -1064,8 +1084,8 @@ extern "C" int dp_msda_bwd(const void* value, int32_t batch, int32_t S, const in
   hipStream_t s = as_stream(stream);
   // grad_value (and grad_ref) are accumulated by atomics: clear them on the stream first
   if ((grad_value && !accumulate_value &&
-       hipMemsetAsync(grad_value, 0, (size_t)batch * S * nhead * dh * sizeof(float), s) != hipSuccess) ||
-      (grad_ref && hipMemsetAsync(grad_ref, 0, (size_t)batch * lq * 2 * sizeof(float), s) != hipSuccess))
+       dp_zero_async(grad_value, (size_t)batch * S * nhead * dh * sizeof(float), s)) ||
+      (grad_ref && dp_zero_async(grad_ref, (size_t)batch * lq * 2 * sizeof(float), s)))
     return dp_check_launch("dp_msda_bwd(memset)");
   const int pairs = batch * lq * nhead;
   if (grad_value && dh <= 64 && (dh & (dh - 1)) == 0 && !getenv("DETRPOSE_MSDA_BWD_VEC")) {

@@ -871,7 +871,7 @@ extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, flo
                          int32_t dtype, void* stream) {
   DP_REQUIRE(x && out && rows > 0 && n > 0 && ld >= n, "dp_colsum: bad arguments");
   hipStream_t st = as_stream(stream);
-  if (!accumulate && hipMemsetAsync(out, 0, (size_t)n * 4, st) != hipSuccess) return dp_check_launch("dp_colsum");
+  if (!accumulate && dp_zero_async(out, (size_t)n * 4, st)) return dp_check_launch("dp_colsum");
   int lg = 0;
   while ((1 << lg) < n && lg < 8) ++lg;
   const int cw = 1 << lg, gx = (n + cw - 1) / cw;
@@ -1178,8 +1178,31 @@ extern "C" int dp_ema(float* ema, const float* p, int64_t n, float decay, const 
   return dp_check_launch("dp_ema");
 }
 
+// Zero fill as a kernel (16-byte stores over the aligned body): every stream-ordered clear of the
+// library goes through here instead of hipMemsetAsync, whose nodes inside a captured hipGraph
+// (the training tapes' replay) left the cleared buffers wrong in measured runs.
+__global__ void zero_fill_kernel(char* __restrict__ p, size_t bytes) {
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15;
+  const size_t h = head < bytes ? head : bytes;
+  const size_t body = (bytes - h) / 16;
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
+  if (i0 < h) p[i0] = 0;
+  uint4* b = reinterpret_cast<uint4*>(p + h);
+  for (size_t i = i0; i < body; i += st) b[i] = make_uint4(0u, 0u, 0u, 0u);
+  const size_t tail = h + body * 16;
+  if (tail + i0 < bytes) p[tail + i0] = 0;
+}
+
+int dp_zero_async(void* p, size_t bytes, hipStream_t s) {
+  if (!bytes) return 0;
+  const size_t body = bytes / 16 + 1;
+  const unsigned grid = (unsigned)std::min<size_t>((body + 255) / 256, 2048);
+  hipLaunchKernelGGL(zero_fill_kernel, dim3(grid), dim3(256), 0, s, static_cast<char*>(p), bytes);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int dp_zero(void* p, int64_t bytes, void* stream) {
   DP_REQUIRE(p && bytes >= 0, "dp_zero: bad arguments");
-  if (hipMemsetAsync(p, 0, (size_t)bytes, as_stream(stream)) != hipSuccess) return dp_check_launch("dp_zero");
+  if (dp_zero_async(p, (size_t)bytes, as_stream(stream))) return dp_check_launch("dp_zero");
   return 0;
 }

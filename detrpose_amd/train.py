@@ -162,15 +162,20 @@ class Trainer:
         """Graph replay for the plans' tapes when self.graphs. A backbone with LearnableAffineBlocks
         (DETRPose-N's B0) keeps both its tapes eager: sync_lab writes the scalars' current values
         into conv descriptors that its forward and backward launches read by value."""
+        only = os.environ.get("DETRPOSE_GRAPH_TAPES")   # debugging: a comma list of tape names to graph
         for p in plans:
             on = self.graphs and not getattr(p, "labs", None)
-            p.fw.use_graph = p.bw.use_graph = on
+            kind = "bb" if p is getattr(self, "bb", None) else "ep" if p is getattr(self, "ep", None) else "tr"
+            for t, nm in ((p.fw, kind + ".fw"), (p.bw, kind + ".bw")):
+                t.use_graph = on and (only is None or nm in only.split(","))
 
     def sub_step(self, images, targets):
         """Forward + criterion + backward of one sub-batch (engine.py:44-59): the gradients of
         its summed losses in eng.grad_flat (overwritten). Returns (loss names, device losses)."""
         eng = self.eng
         B = images.shape[0]
+        if self.scope == "full" and getattr(self, "bb", None) is not None:
+            self._set_graphs(self.bb, self.ep)   # before their forwards run (the plans are cached per shape)
         memory, shapes = self._memory(images)
         packed = pack_targets(targets, eng.K, self.device)
         sizes = packed.sizes

@@ -58,7 +58,7 @@ def test_plan_costs_and_kernel_names():
         if fn.__name__ == "dp_conv2d":
             k = plan.kernel_of(name)
             assert k.startswith(("conv_halo_kernel<", "conv_stream_kernel<", "conv_direct_kernel<")), (name, k)
-    assert "conv_halo_kernel<8, 4, 3, 3, 1, 128, false, false, 2, false, 0>" in plan.op_kernel.values()
+    assert "conv_halo_kernel<8, 4, 3, 3, 1, 128, false, false, 2, false, 0, 2>" in plan.op_kernel.values()
     # rocprofv3's mangled and demangled spellings reduce to the describe form
     assert canonical_kernel_name("_ZN12_GLOBAL__N_118conv_stream_kernelILi256ELi256ELi2ELi8ELi2ELb1ELi2EDF16bLi0EEEv"
                                  "12dp_conv_desciiii") == "conv_stream_kernel<256, 256, 2, 8, 2, true, 2, bf16, 0>"
