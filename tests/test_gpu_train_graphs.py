@@ -53,6 +53,10 @@ def test_graph_replay_matches_eager_tapes(size, dtype, B):
     ep.forward()
     plan.forward()
     eager = _forward_outputs(tr)
+    bb.forward()                             # eager again: the run-to-run spread of the atomics
+    ep.forward()
+    plan.forward()
+    eager2 = _forward_outputs(tr)
     tr.graphs = True
     tr._set_graphs(plan, bb, ep)
     bb.forward()                             # captured, then replayed
@@ -65,9 +69,12 @@ def test_graph_replay_matches_eager_tapes(size, dtype, B):
         assert torch.equal(a, b), "backbone forward: graph replay differs from the eager launches"
     for k in ("memory", "logits", "kps"):
         d = float((graph[k] - eager[k]).abs().max())
+        d0 = float((eager2[k] - eager[k]).abs().max())
+        nd = int((graph[k] != eager[k]).sum())
         scale = max(float(eager[k].abs().max()), 1e-12)
-        print(f"{size} {dtype} {k}: max |graph - eager| {d:.3g} (scale {scale:.3g})")
-        assert d <= 1e-3 * scale, k
+        print(f"{size} {dtype} {k}: max |graph - eager| {d:.3g} over {nd} of {eager[k].numel()} "
+              f"(eager - eager {d0:.3g}, scale {scale:.3g})")
+        assert d <= max(1e-3 * scale, 2 * d0), k
     # whole steps from the graphs: training goes on
     totals = []
     for _ in range(4):
