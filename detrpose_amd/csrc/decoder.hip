@@ -105,9 +105,11 @@ __device__ __forceinline__ int a_chan(int j, int a) { return (a >> 2) * NV + 4 *
 // Weight-fragment ring of one wave: the fragments of k-step s of the running GEMM sit in
 // f[s % D]; D k-steps are in flight.
 constexpr int D = 4;
-struct WPipe {
-  bf16x8 f[D][TN];
+template <int DD>
+struct WPipeT {
+  bf16x8 f[DD][TN];
 };
+using WPipe = WPipeT<D>;
 
 // Fragment-layout weights: for output-channel block nb (32 channels) and k-step s, the
 // TN fragments of the 64 lanes are 1 KB each, contiguous: frag(nb, s, j) at
@@ -118,9 +120,10 @@ __device__ __forceinline__ const bf16_t* frag_base(const bf16_t* w, int nb, int 
   return w + ((int64_t)(nb * ksteps + s0) * TN * 64 + lane) * 8;
 }
 
-__device__ __forceinline__ void pipe_start(WPipe& p, const bf16_t* wb) {
+template <int DD>
+__device__ __forceinline__ void pipe_start(WPipeT<DD>& p, const bf16_t* wb) {
 #pragma unroll
-  for (int s = 0; s < D; ++s)
+  for (int s = 0; s < DD; ++s)
 #pragma unroll
     for (int j = 0; j < TN; ++j) p.f[s][j] = gld16(wb + (s * TN + j) * 512);
 }
@@ -129,33 +132,41 @@ __device__ __forceinline__ void pipe_start(WPipe& p, const bf16_t* wb) {
 // fragments from global. The pipe holds this GEMM's first D k-steps on entry; as its own
 // steps run out it loads the first D k-steps of the NEXT GEMM (fragment base nx), so the
 // ring never drains between the GEMMs of a kernel. The X fragments of k-step s+1 are read
-// from LDS while the MFMAs of step s run.
-template <int K, int TM>
-__device__ __forceinline__ void wave_gemm(f32x4 (&acc)[TM][TN], const char* xl, const bf16_t* wb, WPipe& p,
+// from LDS while the MFMAs of step s run (XDB; otherwise each step's X fragments are read
+// just before its MFMAs: fewer registers, the latency left to the other waves of the SIMD).
+template <int K, int TM, int DD = D, bool XDB = true>
+__device__ __forceinline__ void wave_gemm(f32x4 (&acc)[TM][TN], const char* xl, const bf16_t* wb, WPipeT<DD>& p,
                                           const bf16_t* nx) {
   constexpr int NS = K / 32;
-  static_assert(NS % D == 0, "k-steps must fill the ring");
+  static_assert(NS % DD == 0, "k-steps must fill the ring");
   const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
-  bf16x8 xf[2][TM];
+  bf16x8 xf[XDB ? 2 : 1][TM];
+  if constexpr (XDB) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i) xf[0][i] = lds16(xl, sw<K>(16 * i + q, g));
+    for (int i = 0; i < TM; ++i) xf[0][i] = lds16(xl, sw<K>(16 * i + q, g));
+  }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     bf16x8 w[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) w[j] = p.f[s % D][j];
+    for (int j = 0; j < TN; ++j) w[j] = p.f[s % DD][j];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
-      p.f[s % D][j] = gld16(s + D < NS ? wb + ((s + D) * TN + j) * 512 : nx + ((s + D - NS) * TN + j) * 512);
-    if (s + 1 < NS) {
+      p.f[s % DD][j] = gld16(s + DD < NS ? wb + ((s + DD) * TN + j) * 512 : nx + ((s + DD - NS) * TN + j) * 512);
+    if constexpr (XDB) {
+      if (s + 1 < NS) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) xf[(s + 1) & 1][i] = lds16(xl, sw<K>(16 * i + q, 4 * (s + 1) + g));
+        for (int i = 0; i < TM; ++i) xf[(s + 1) & 1][i] = lds16(xl, sw<K>(16 * i + q, 4 * (s + 1) + g));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) xf[0][i] = lds16(xl, sw<K>(16 * i + q, 4 * s + g));
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j], xf[s & 1][i], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j], xf[XDB ? (s & 1) : 0][i], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -228,6 +239,70 @@ __device__ __forceinline__ void layernorm_rows(float (&x)[TM][NV], const float (
 #pragma unroll
     for (int e = 0; e < NV; ++e) x[i][e] = (x[i][e] - mean[i]) * rstd * gg[e] + bb[e];
   }
+}
+
+// layernorm_rows in one LDS round: per lane (mean, M2) of its 8 values, merged over the lane
+// groups (xor shuffles) and then the waves (LDS) by the equal-count pairwise update
+// M2 = M2a + M2b + (ma - mb)^2 n / 2 (Chan et al.), in a fixed order. red: NW x BM float2.
+template <int TM, int NW>
+__device__ __forceinline__ void layernorm_rows_1p(float (&x)[TM][NV], const float (&gg)[NV], const float (&bb)[NV],
+                                                  float eps, float* red) {
+  constexpr int BM = 16 * TM;
+  static_assert(NW == 8, "three merge levels over the waves");
+  const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4, w = threadIdx.x >> 6;
+  float2* r2 = reinterpret_cast<float2*>(red);
+  float mean[TM], rstd[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float m = 0.f;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) m += x[i][e];
+    m *= 1.f / NV;
+    float m2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      const float t = x[i][e] - m;
+      m2 = fmaf(t, t, m2);
+    }
+    float n = NV;
+#pragma unroll
+    for (int sh = 16; sh <= 32; sh *= 2) {
+      const float mo = __shfl_xor(m, sh, 64), qo = __shfl_xor(m2, sh, 64);
+      const float d = m - mo;
+      // the same operand order in both lanes of a pair: lower lane first
+      const bool lo = (lane & sh) == 0;
+      const float ma = lo ? m : mo, mb = lo ? mo : m, qa = lo ? m2 : qo, qb = lo ? qo : m2;
+      m2 = qa + qb + d * d * (0.5f * n);
+      m = 0.5f * (ma + mb);
+      n *= 2.f;
+    }
+    if (g == 0) r2[w * BM + 16 * i + q] = make_float2(m, m2);
+  }
+  lds_barrier();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = 16 * i + q;
+    float2 v[NW];
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) v[ww] = r2[ww * BM + row];
+    float n = 32.f;
+#pragma unroll
+    for (int span = 1; span < NW; span *= 2) {
+#pragma unroll
+      for (int a = 0; a < NW; a += 2 * span) {
+        const float d = v[a].x - v[a + span].x;
+        v[a].y = v[a].y + v[a + span].y + d * d * (0.5f * n);
+        v[a].x = 0.5f * (v[a].x + v[a + span].x);
+      }
+      n *= 2.f;
+    }
+    mean[i] = v[0].x;
+    rstd[i] = rsqrtf(v[0].y * (1.f / (32 * NW)) + eps);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < NV; ++e) x[i][e] = (x[i][e] - mean[i]) * rstd[i] * gg[e] + bb[e];
 }
 
 __device__ __forceinline__ void load_bias(const float* __restrict__ b, int cb, float (&v)[NV]) {
@@ -434,8 +509,18 @@ __global__ __launch_bounds__(C * 2) void linear_ln_cls_kernel(bf16_t* out, const
 //      across attention's pos re-add on keypoint rows) -> out.
 // HBM: x read once (+ the residual re-read from L2), out written once: the qkv (3C) and
 // attention-output (C) round trips of the unfused path are gone.
-template <int SEQ, int GB, bool POST, int DHP, bool NEXT>
-__global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, const bf16_t* x, dp_rowmap xm,
+#ifdef DP_MHA_TIMING
+// A/B builds only: wall-clock stamps of each block's wave 0 at the kernel's phase boundaries
+constexpr int MHA_DBG_BLOCKS = 8192, MHA_DBG_N = 12;
+__device__ long long g_mha_dbg[MHA_DBG_BLOCKS * MHA_DBG_N];
+#define MHA_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < MHA_DBG_BLOCKS) g_mha_dbg[blockIdx.x * MHA_DBG_N + (k)] = (long long)wall_clock64()
+#else
+#define MHA_STAMP(k)
+#endif
+
+template <int SEQ, int GB, bool POST, int DHP, bool NEXT, int MODE>
+__global__ __launch_bounds__(512, 2) void mha_ln_kernel(bf16_t* out, dp_rowmap om, const bf16_t* x, dp_rowmap xm,
                                                      int n_inner, int64_t so, int64_t si, int64_t st, int nseq,
                                                      const bf16_t* __restrict__ wqkv, const float* __restrict__ bqkv,
                                                      const bf16_t* __restrict__ wo, const float* __restrict__ bo,
@@ -446,16 +531,20 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
                                                      const float* __restrict__ bn, int nn) {
   constexpr int C = 256, NW = 8, NTH = 512, DH = 32;
   constexpr int RR = SEQ * GB, TM = (RR + 15) / 16, R = 16 * TM;
-  // DHP: V row pitch (elements). 48 makes the transposed reads conflict-free, 32 keeps the
-  // block under 80 KB of LDS (two blocks per CU)
-  constexpr int VR = R + 16;                   // + one zero tile: the last key pair's upper half
+  // LDS: the waves' V slices [NW][R][DHP] (DHP: row pitch in elements, 40 or 48 keep the
+  // transposed reads conflict-free), the X / O image [R][C], the LayerNorm partials. The PV
+  // MFMA of a last odd key tile reads 16 rows past a slice: the next wave's slice, or for
+  // wave 7 the image's first rows -- finite values under zero probabilities either way.
+  // R = 64 / DHP = 40 is 76 KB: two blocks per CU (WPE = 4 waves per SIMD).
   typedef short s4 __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) char smem[R * C * 2 + NW * VR * DHP * 2 + NW * R * 4];
-  char* xl = smem;
+  __shared__ __attribute__((aligned(16))) char smem[NW * R * DHP * 2 + R * C * 2 + NW * R * 8 + R * 4];
+  char* xl = smem + NW * R * DHP * 2;
+  int* rows_l = reinterpret_cast<int*>(xl + R * C * 2 + NW * R * 8);   // row_of(m), for the epilogue
   const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  bf16_t* V = reinterpret_cast<bf16_t*>(smem + R * C * 2) + wv * VR * DHP;
-  float* red = reinterpret_cast<float*>(smem + R * C * 2 + NW * VR * DHP * 2);
+  bf16_t* V = reinterpret_cast<bf16_t*>(smem) + wv * R * DHP;
+  float* red = reinterpret_cast<float*>(xl + R * C * 2);
+  MHA_STAMP(11);
   const int sq0 = blockIdx.x * GB;
   // block row m -> token row (o * so + ii * si + t * st < 2^31, checked by the launcher); -1
   // past the last sequence / padding
@@ -470,12 +559,34 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
   const bf16_t* wk = frag_base(wqkv, NW + wv, C / 32);
   const bf16_t* wvv = frag_base(wqkv, 2 * NW + wv, C / 32);
   const bf16_t* wob = frag_base(wo, wv, C / 32);
-  WPipe p;
-  pipe_start(p, wvv);
-  // ---- X rows -> LDS (zero rows past the block's tokens); the zero V tile
-  {
-    constexpr int CH = C / 8, PER = R * CH / NTH;
-    bf16x8 xv[PER];
+  // MODE 0: the V, K, Q projections as three GEMMs (32 output channels each) through one
+  // weight ring; 1: one GEMM of 96 output channels (each X fragment read from LDS feeds six
+  // MFMAs instead of two)
+  constexpr bool FUSED = MODE == 1;
+  constexpr int MD = D;
+  constexpr bool XDB = true;
+  constexpr int QD = 2;   // FUSED: the projection's ring depth (k-steps of 3 x TN fragments)
+  WPipeT<MD> p;
+  bf16x8 pf[FUSED ? QD : 1][3][TN];
+  auto ring_start = [&]() __attribute__((always_inline)) {
+    if constexpr (FUSED) {
+#pragma unroll
+      for (int s = 0; s < QD; ++s)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          pf[s][0][j] = gld16(wvv + (s * TN + j) * 512);
+          pf[s][1][j] = gld16(wk + (s * TN + j) * 512);
+          pf[s][2][j] = gld16(wq + (s * TN + j) * 512);
+        }
+    } else {
+      pipe_start(p, wvv);
+    }
+  };
+  ring_start();
+  // ---- X rows -> registers -> LDS (zero rows past the block's tokens)
+  constexpr int CH = C / 8, PER = R * CH / NTH;
+  bf16x8 xv[PER];
+  auto load_x = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < PER; ++t) {
       const int e = threadIdx.x + NTH * t;
@@ -483,16 +594,18 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
       const int r = row_of(m);
       xv[t] = r >= 0 ? gld16(x + rowmap_off(xm, r) + c * 8) : bf16x8{};
     }
-#pragma unroll
-    for (int t = 0; t < PER; ++t) {
-      const int e = threadIdx.x + NTH * t;
-      const int m = e / CH, c = e - m * CH;
-      sts16(xl, sw<C>(m, c), xv[t]);
-    }
-    for (int e = lane; e < 16 * DHP / 8; e += 64) sts16(reinterpret_cast<char*>(V + R * DHP), e * 16, bf16x8{});
-  }
+  };
+  load_x();
   const int cb = g * NV;   // the lane's 8 contiguous channels within a 32-channel block
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const int e = threadIdx.x + NTH * t;
+    const int m = e / CH, c = e - m * CH;
+    sts16(xl, sw<C>(m, c), xv[t]);
+  }
+  if (threadIdx.x < R) rows_l[threadIdx.x] = row_of(threadIdx.x);
   lds_barrier();
+  MHA_STAMP(0);
 
   // ---- 1. this head's projections
   bf16x8 qf[TM], kf[TM];
@@ -508,20 +621,76 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
       for (int r = 0; r < 4; ++r) f[4 * j + r] = (bf16_t)(acc[i][j][r] + b[4 * j + r]);
     return f;
   };
-  // V first (to LDS), then K, then Q: the fewest fragments live across a GEMM
-  zero_acc<TM>(acc);
-  wave_gemm<C, TM>(acc, xl, wvv, p, wk);
+  if constexpr (FUSED) {
+    f32x4 a3[3][TM][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) *reinterpret_cast<bf16x8*>(V + (16 * i + q) * DHP + cb) = frag_of(i, 2);
-  zero_acc<TM>(acc);
-  wave_gemm<C, TM>(acc, xl, wk, p, wq);
+    for (int t = 0; t < 3; ++t) zero_acc<TM>(a3[t]);
+    constexpr int NS = C / 32;
+    const bf16_t* wp3[3] = {wvv, wk, wq};
 #pragma unroll
-  for (int i = 0; i < TM; ++i) kf[i] = frag_of(i, 1);
-  zero_acc<TM>(acc);
-  wave_gemm<C, TM>(acc, xl, wq, p, wob);
+    for (int s = 0; s < NS; ++s) {
+      bf16x8 w[3][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) qf[i] = frag_of(i, 0);
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) w[t][j] = pf[s % QD][t][j];
+      if (s + QD < NS) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) pf[s % QD][t][j] = gld16(wp3[t] + ((s + QD) * TN + j) * 512);
+      }
+      bf16x8 xf[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) xf[i] = lds16(xl, sw<C>(16 * i + q, 4 * s + g));
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            a3[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][j], xf[i], a3[t][i][j], 0, 0, 0);
+    }
+    pipe_start(p, wob);   // the out_proj's first k-steps, in flight across the attention
+    MHA_STAMP(1);
+    auto frag3 = [&](int t, int i, int part) __attribute__((always_inline)) {
+      float b[NV];
+      load_bias(bqkv, part * C + 32 * wv + cb, b);
+      bf16x8 f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f[4 * j + r] = (bf16_t)(a3[t][i][j][r] + b[4 * j + r]);
+      return f;
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      *reinterpret_cast<bf16x8*>(V + (16 * i + q) * DHP + cb) = frag3(0, i, 2);
+      kf[i] = frag3(1, i, 1);
+      qf[i] = frag3(2, i, 0);
+    }
+    MHA_STAMP(2);
+    MHA_STAMP(3);
+  } else {
+    // V first (to LDS), then K, then Q: the fewest fragments live across a GEMM
+    zero_acc<TM>(acc);
+    wave_gemm<C, TM, MD, XDB>(acc, xl, wvv, p, wk);
+    MHA_STAMP(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) *reinterpret_cast<bf16x8*>(V + (16 * i + q) * DHP + cb) = frag_of(i, 2);
+    zero_acc<TM>(acc);
+    wave_gemm<C, TM, MD, XDB>(acc, xl, wk, p, wq);
+    MHA_STAMP(2);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) kf[i] = frag_of(i, 1);
+    zero_acc<TM>(acc);
+    wave_gemm<C, TM, MD, XDB>(acc, xl, wq, p, wob);
+    MHA_STAMP(3);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) qf[i] = frag_of(i, 0);
+  }
   lds_barrier();   // every wave is past its projections: the X image may be overwritten by O
+  MHA_STAMP(4);
 
   // ---- 2. attention, one 16-query tile at a time
   const int q4 = (lane & 15) >> 2, p4 = lane & 3;
@@ -596,29 +765,35 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
       *reinterpret_cast<bf16x4*>(xl + sw<C>(qm, ch >> 3) + (ch & 7) * 2) = w;
     }
   }
-  // residual rows for the epilogue, in flight across the barrier and the out_proj GEMM
+  MHA_STAMP(5);
+  // residual rows for the epilogue: in flight across the barrier and the out_proj GEMM (one
+  // block per CU), or fetched after the GEMM (two blocks per CU: registers)
   bf16x8 rv[TM], pv[TM];
   float bias[NV], gg[NV], bb[NV];
-  {
+  auto load_res = [&]() __attribute__((always_inline)) {
     const int ocb = 32 * wv + cb;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int r = max(row_of(16 * i + q), 0);
+      const int r = max(rows_l[16 * i + q], 0);
       rv[i] = gld16(x + rowmap_off(xm, r) + ocb);
       if (POST) {
         const int grp = (int)((unsigned)r / (unsigned)post_group), wi = r - grp * post_group;
         pv[i] = gld16(post + rowmap_off(pm, grp * (post_group - post_skip) + max(wi - post_skip, 0)) + ocb);
       }
     }
-    load_bias(bo, ocb, bias);
-    load_bias(gamma, ocb, gg);
-    load_bias(beta, ocb, bb);
-  }
+  };
+  if constexpr (XDB) load_res();
   lds_barrier();   // the O image is complete
+  MHA_STAMP(6);
 
   // ---- 3. out_proj + bias + residual -> LayerNorm -> out
   zero_acc<TM>(acc);
-  wave_gemm<C, TM>(acc, xl, wob, p, wob);
+  wave_gemm<C, TM, MD, XDB>(acc, xl, wob, p, wob);
+  MHA_STAMP(7);
+  if constexpr (!XDB) load_res();
+  load_bias(bo, 32 * wv + cb, bias);
+  load_bias(gamma, 32 * wv + cb, gg);
+  load_bias(beta, 32 * wv + cb, bb);
   float v[TM][NV];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -627,11 +802,12 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
 #pragma unroll
     for (int e = 0; e < NV; ++e) v[i][e] = a[e] + bias[e] + (float)rv[i][e];
   }
-  layernorm_rows<TM, NW>(v, gg, bb, eps, red);
+  layernorm_rows_1p<TM, NW>(v, gg, bb, eps, red);
+  MHA_STAMP(8);
   const int ocb = 32 * wv + cb;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int r = row_of(16 * i + q);
+    const int r = rows_l[16 * i + q];
     if (r < 0) continue;
     if (POST) {
       const int wi = (int)((unsigned)r % (unsigned)post_group);
@@ -642,6 +818,7 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
     }
     store_row_vals(out + rowmap_off(om, r) + ocb, v[i]);
   }
+  MHA_STAMP(9);
   if constexpr (NEXT) {
     // 4. the next Linear on the rows just stored (the across attention's output + pos is the
     //    MSDA query: its sampling-offset / attention-logit projection, ms_deform_attn.py:
@@ -655,12 +832,12 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
       const bf16_t* wnb = frag_base(wn, nb, C / 32);
       pipe_start(p, wnb);
       zero_acc<TM>(acc);
-      wave_gemm<C, TM>(acc, xl, wnb, p, wnb);
+      wave_gemm<C, TM, MD, XDB>(acc, xl, wnb, p, wnb);
       float nbias[NV];
       load_bias(bn, 32 * nb + cb, nbias);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int r = row_of(16 * i + q);
+        const int r = rows_l[16 * i + q];
         if (r < 0) continue;
         float a[NV];
         lane_vals<TM>(acc, i, a);
@@ -670,6 +847,7 @@ __global__ __launch_bounds__(512) void mha_ln_kernel(bf16_t* out, dp_rowmap om, 
       }
     }
   }
+  MHA_STAMP(10);
 }
 
 // ------------------------------------------------------------------ Gate: Linear + sigmoid mix + LN
@@ -1168,6 +1346,13 @@ extern "C" int dp_pose_mlp(const void* x, dp_rowmap xm, const void* x2, dp_rowma
   return DP_EINVAL;
 }
 
+#ifdef DP_MHA_TIMING
+extern "C" int dp_debug_mha_stamps(long long* host, int32_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mha_dbg), sizeof(long long) * std::min(n, MHA_DBG_BLOCKS * MHA_DBG_N)) ==
+                 hipSuccess ? 0 : DP_EINVAL;
+}
+#endif
+
 extern "C" int dp_mha_layernorm(void* out, dp_rowmap om, const void* x, dp_rowmap xm, int32_t n_outer,
                                 int32_t n_inner, int64_t so, int64_t si, int64_t st, int32_t seqlen, const void* wqkv,
                                 const float* bqkv, const void* wo, const float* bo, const float* gamma,
@@ -1188,28 +1373,34 @@ extern "C" int dp_mha_layernorm(void* out, dp_rowmap om, const void* x, dp_rowma
              "dp_mha_layernorm: token rows exceed 2^31");
   hipStream_t s = as_stream(stream);
   const float scale = 1.f / sqrtf(32.f);
-#ifndef DP_MHA_DHP
-#define DP_MHA_DHP 48   // 32 (two blocks per CU by LDS, but not by registers): 86 -> 130 us within, spills
-#endif
-#ifndef DP_MHA_GBW
-#define DP_MHA_GBW 4
-#endif
-#define DP_MHA_L(SEQ_, GB_, POST_, NEXT_)                                                                          \
-  hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, POST_, DP_MHA_DHP, NEXT_>), grid, dim3(512), 0, s, (bf16_t*)out, om,   \
+  // DETRPOSE_MHA_MODE: 1 (default) the fused V/K/Q projection; 0: three projection GEMMs
+  static const int mode = [] {
+    const char* e = getenv("DETRPOSE_MHA_MODE");
+    return e ? atoi(e) : 1;
+  }();
+#define DP_MHA_L(SEQ_, GB_, POST_, NEXT_, DHP_, WPE_)                                                              \
+  hipLaunchKernelGGL((mha_ln_kernel<SEQ_, GB_, POST_, DHP_, NEXT_, WPE_>), grid, dim3(512), 0, s, (bf16_t*)out, om, \
                      (const bf16_t*)x, xm, n_inner, so, si, st, (int)nseq, (const bf16_t*)wqkv, bqkv,              \
                      (const bf16_t*)wo, bo, gamma, beta, eps, scale, (const bf16_t*)post, pm, POST_ ? post_group : 1, \
                      POST_ ? post_skip : 0, (bf16_t*)next_out, next_ld, (const bf16_t*)next_w, next_b, next_n)
-#define DP_MHA(SEQ_, GB_)                                                                                          \
+#define DP_MHA(SEQ_, GB_, DHP_, WPE_)                                                                              \
   do {                                                                                                             \
-    dim3 grid((unsigned)((nseq + GB_ - 1) / GB_));                                                                 \
-    if (post && next_out) DP_MHA_L(SEQ_, GB_, true, true);                                                         \
-    else if (post) DP_MHA_L(SEQ_, GB_, true, false);                                                               \
-    else if (next_out) DP_MHA_L(SEQ_, GB_, false, true);                                                           \
-    else DP_MHA_L(SEQ_, GB_, false, false);                                                                        \
+    const int64_t tiles_ = (nseq + GB_ - 1) / GB_;                                                                 \
+    dim3 grid((unsigned)tiles_);                                                                                   \
+    if (post && next_out) DP_MHA_L(SEQ_, GB_, true, true, DHP_, WPE_);                                             \
+    else if (post) DP_MHA_L(SEQ_, GB_, true, false, DHP_, WPE_);                                                   \
+    else if (next_out) DP_MHA_L(SEQ_, GB_, false, true, DHP_, WPE_);                                               \
+    else DP_MHA_L(SEQ_, GB_, false, false, DHP_, WPE_);                                                            \
     return dp_check_launch("dp_mha_layernorm");                                                                    \
   } while (0)
-  if (seqlen == 18) DP_MHA(18, DP_MHA_GBW);   // within-instance: the 1 + 17 tokens of a query
-  if (seqlen == 60) DP_MHA(60, 1);   // across-instance: the 60 queries of a token slot
+  // within-instance: the 1 + 17 tokens of a query; across-instance: the 60 queries of a slot
+  if (mode == 0) {
+    if (seqlen == 18) DP_MHA(18, 4, 48, 0);
+    if (seqlen == 60) DP_MHA(60, 1, 48, 0);
+  } else {
+    if (seqlen == 18) DP_MHA(18, 4, 48, 1);
+    if (seqlen == 60) DP_MHA(60, 1, 48, 1);
+  }
 #undef DP_MHA
 #undef DP_MHA_L
   dp_set_error("dp_mha_layernorm: seqlen %d not instantiated (18 / 60)", seqlen);
