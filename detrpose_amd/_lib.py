@@ -154,7 +154,8 @@ _SIGS = {
     "dp_finite_guard": (i32, [vp, i64, vp, vp]),
     "dp_ema": (i32, [vp, vp, i64, f32, vp, vp]),
     # HybridEncoder training (csrc/encoder_train.hip)
-    "dp_bn_stats": (i32, [vp, i64, i32, i32, vp, i32, vp]),
+    "dp_bn_stats": (i32, [vp, i64, i32, i32, vp, vp, i64, i32, vp]),
+    "dp_bn_stats_ws_bytes": (i64, [i32, i32]),
     "dp_bn_finalize": (i32, [vp, i32, f32, i32, f32, f32, vp, vp, vp, vp]),
     "dp_bn_act_fwd": (i32, [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
     "dp_bn_act_bwd_reduce": (i32, [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp,

@@ -38,11 +38,13 @@ __device__ __forceinline__ float act_d(float x, int act) {
 
 // ---------------------------------------------------------------- BatchNorm statistics
 // Column sums over a block of rows, shifted by the column's first-row value K (single-pass
-// variance without the E[x^2] - mean^2 cancellation): out[0] = K, out[1] += sum (x - K),
-// out[2] += sum (x - K)^2. Block: 64 channels (lane) x 4 row phases (wave), 256 rows.
+// variance without the E[x^2] - mean^2 cancellation): part[y][0] = sum (x - K), part[y][1] =
+// sum (x - K)^2 over row slice y. Block: 64 channels (lane) x 4 row phases (wave), 256 rows.
+// No float atomics: bn_stats_reduce_kernel sums the slices in a fixed order, so the forward
+// is deterministic run to run.
 template <typename T>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, int64_t ld, int rows, int c,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ part) {
   __shared__ float red[2][4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + lane;
@@ -62,13 +64,37 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
         s2 = fmaf(d[u], d[u], s2);
       }
   }
-  if (blockIdx.y == 0 && wv == 0 && ch < c) out[ch] = k;
   red[0][wv][lane] = s1;
   red[1][wv][lane] = s2;
   __syncthreads();
   if (wv == 0 && ch < c) {
-    atomicAdd(out + c + ch, red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane]);
-    atomicAdd(out + 2 * c + ch, red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane]);
+    float* pp = part + (int64_t)blockIdx.y * 2 * c;
+    pp[ch] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+    pp[c + ch] = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+  }
+}
+
+// out [3][c] = (K, sum over the ny slices of part[y][0], of part[y][1]): wave w adds slices
+// w, w + 4, ... in order, then the four wave sums are added in order.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_reduce_kernel(const T* __restrict__ x, const float* __restrict__ part,
+                                                              int ny, int c, float* __restrict__ out) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane;
+  const int chc = min(ch, c - 1);
+  float s1 = 0.f, s2 = 0.f;
+  for (int y = wv; y < ny; y += 4) {
+    s1 += part[(int64_t)y * 2 * c + chc];
+    s2 += part[(int64_t)y * 2 * c + c + chc];
+  }
+  red[0][wv][lane] = s1;
+  red[1][wv][lane] = s2;
+  __syncthreads();
+  if (wv == 0 && ch < c) {
+    out[ch] = ld_(x + ch);
+    out[c + ch] = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
+    out[2 * c + ch] = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
   }
 }
 
@@ -561,16 +587,22 @@ int grid_for(int64_t total) {
     }                                  \
   } while (0)
 
-extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, int32_t dtype,
-                           void* stream) {
-  DP_REQUIRE(x && out && rows > 0 && c > 0 && ld >= c, "dp_bn_stats: bad arguments");
+extern "C" int64_t dp_bn_stats_ws_bytes(int32_t rows, int32_t c) {
+  if (rows <= 0 || c <= 0) return -1;
+  return (int64_t)((rows + 255) / 256) * 2 * c * (int64_t)sizeof(float);
+}
+
+extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, float* ws, int64_t ws_bytes,
+                           int32_t dtype, void* stream) {
+  DP_REQUIRE(x && out && ws && rows > 0 && c > 0 && ld >= c, "dp_bn_stats: bad arguments");
+  DP_REQUIRE(ws_bytes >= dp_bn_stats_ws_bytes(rows, c), "dp_bn_stats: workspace of %lld bytes < %lld",
+             (long long)ws_bytes, (long long)dp_bn_stats_ws_bytes(rows, c));
   hipStream_t s = as_stream(stream);
-  if (dp_zero_async(out + c, 2 * (size_t)c * sizeof(float), s)) {
-    dp_set_error("dp_bn_stats: memset failed");
-    return DP_EINVAL;
-  }
-  dim3 grid((c + 63) / 64, (rows + 255) / 256);
-  DP_DT(hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ld, rows, c, out));
+  const int ny = (rows + 255) / 256;
+  dim3 grid((c + 63) / 64, ny);
+  DP_DT(hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ld, rows, c, ws));
+  DP_DT(hipLaunchKernelGGL(bn_stats_reduce_kernel<T>, dim3((c + 63) / 64), dim3(256), 0, s, (const T*)x, ws, ny, c,
+                           out));
   return dp_check_launch("dp_bn_stats");
 }
 

@@ -345,7 +345,9 @@ class TapePlan:
             mr = self.f32(2, c)
             if self.world > 1:
                 fw.op(f"{name}.bn{bi}.zero", lib.dp_zero, _p(parts), parts.numel() * 4)
-            fw.op(f"{name}.bn{bi}.stats", lib.dp_bn_stats, z.xp, z.ld, rows, c, _p(parts[self.rank]), code)
+            ws = self.f32(max(int(lib.dp_bn_stats_ws_bytes(rows, c)), 4) // 4)   # per-slice partial sums
+            fw.op(f"{name}.bn{bi}.stats", lib.dp_bn_stats, z.xp, z.ld, rows, c, _p(parts[self.rank]), _p(ws),
+                  ws.numel() * 4, code)
             if self.world > 1:
                 fw.op(f"{name}.bn{bi}.sync", _host(lambda t=parts: all_reduce(t)))
             rm, rv = eng.running[p + ".running_mean"], eng.running[p + ".running_var"]

@@ -587,8 +587,12 @@ int dp_convert_rows(const void* src, int32_t src_dtype, int64_t ld_src, void* ds
  * f32. Callers: detrpose_amd/encoder_train.py. */
 
 /* nn.BatchNorm2d batch statistics, per rank: out [3][c] = (K = x[0][ch], sum (x - K), sum (x - K)^2)
- * over the rows (single pass, shifted by the first row against cancellation). */
-int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, int32_t dtype, void* stream);
+ * over the rows (single pass, shifted by the first row against cancellation). Per-256-row
+ * partial sums go to ws (dp_bn_stats_ws_bytes) and are added in a fixed order: no float
+ * atomics, the same result on every run. */
+int64_t dp_bn_stats_ws_bytes(int32_t rows, int32_t c);
+int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, float* ws, int64_t ws_bytes,
+                int32_t dtype, void* stream);
 /* Combines nparts per-rank dp_bn_stats outputs (all-gathered: SyncBatchNorm, dist_utils.py:122;
  * `count` rows each) into mean_rstd [2][c] = (mean, 1/sqrt(biased var + eps)) and updates the
  * running statistics as F.batch_norm does (momentum, unbiased variance; NULL: no update). */

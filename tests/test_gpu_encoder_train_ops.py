@@ -41,7 +41,10 @@ def bn_stats(lib, z, count_parts=1):
     per = rows // count_parts
     for p in range(count_parts):
         zp = z[p * per:(p + 1) * per]
-        _lib.check(lib.dp_bn_stats(zp.data_ptr(), c, per, c, parts[p].data_ptr(), DP_F32, _s()), "bn_stats")
+        nb = int(lib.dp_bn_stats_ws_bytes(per, c))
+        ws = torch.empty(nb // 4, device=DEV)
+        _lib.check(lib.dp_bn_stats(zp.data_ptr(), c, per, c, parts[p].data_ptr(), ws.data_ptr(), nb, DP_F32, _s()),
+                   "bn_stats")
     return parts, per
 
 

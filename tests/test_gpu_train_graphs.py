@@ -1,11 +1,12 @@
 """Trainer.step with its tapes replayed from hipGraphs (the default at world size 1).
 
 A graph replay launches exactly the kernels an eager run of the tape does, on the same fixed
-buffers, so on identical inputs it must give the same results: the backbone forward (no atomics)
-bit for bit, the encoder memory and the transformer heads up to float-atomic summation order.
-That is checked tape by tape after one eager step (a comparison of whole training steps would
-not be: a rounding-level difference can flip the two-stage top-k or a Hungarian assignment and
-move a loss by percents, eager run against eager run alike). Then a few steps running entirely
+buffers, and the training forward has no float atomics (BatchNorm statistics are summed per
+row slice in a fixed order, dp_bn_stats), so on identical inputs two eager forwards and the
+graph replay agree BIT FOR BIT: backbone outputs, the encoder memory, the heads' logits and
+keypoints (checked tape by tape after one eager step; whole-step losses are not compared, the
+backward still sums with float atomics and one rounding-level difference can flip the two-stage
+top-k or a Hungarian assignment and move a loss by percents). Then a few steps running entirely
 from graphs must keep training: finite losses and gradient norms, no skipped update.
 fp32 DETRPose-N (its LAB backbone stays eager) and bf16 DETRPose-L (every tape replayed)."""
 import numpy as np
@@ -74,7 +75,7 @@ def test_graph_replay_matches_eager_tapes(size, dtype, B):
         scale = max(float(eager[k].abs().max()), 1e-12)
         print(f"{size} {dtype} {k}: max |graph - eager| {d:.3g} over {nd} of {eager[k].numel()} "
               f"(eager - eager {d0:.3g}, scale {scale:.3g})")
-        assert d <= max(1e-3 * scale, 2 * d0), k
+        assert d0 == 0 and d == 0, (k, d0, d)   # deterministic forward: bit-identical
     # whole steps from the graphs: training goes on
     totals = []
     for _ in range(4):
