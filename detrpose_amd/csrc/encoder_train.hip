@@ -39,20 +39,21 @@ __device__ __forceinline__ float act_d(float x, int act) {
 // ---------------------------------------------------------------- BatchNorm statistics
 // Column sums over a block of rows, shifted by the column's first-row value K (single-pass
 // variance without the E[x^2] - mean^2 cancellation): part[y][0] = sum (x - K), part[y][1] =
-// sum (x - K)^2 over row slice y. Block: 64 channels (lane) x 4 row phases (wave), 256 rows.
+// sum (x - K)^2 over row slice y. Block: 64 channels (lane) x 4 row phases (wave), `slice` rows
+// (a multiple of 32; at most BN_SLICES slices, so the reduction below stays short).
 // No float atomics: bn_stats_reduce_kernel sums the slices in a fixed order, so the forward
 // is deterministic run to run.
 template <typename T>
-__global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, int64_t ld, int rows, int c,
+__global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, int64_t ld, int rows, int c, int slice,
                                                        float* __restrict__ part) {
   __shared__ float red[2][4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + lane;
   const int chc = min(ch, c - 1);
-  const int r0 = blockIdx.y * 256;
+  const int r0 = blockIdx.y * slice;
   float s1 = 0.f, s2 = 0.f;
   const float k = ld_(x + chc);
-  const int r1 = min(r0 + 256, rows);
+  const int r1 = min(r0 + slice, rows);
   for (int r = r0 + wv; r < r1; r += 32) {   // 8 rows per step, loads issued together
     float d[8];
 #pragma unroll
@@ -84,6 +85,7 @@ __global__ __launch_bounds__(256) void bn_stats_reduce_kernel(const T* __restric
   const int ch = blockIdx.x * 64 + lane;
   const int chc = min(ch, c - 1);
   float s1 = 0.f, s2 = 0.f;
+#pragma unroll 4
   for (int y = wv; y < ny; y += 4) {
     s1 += part[(int64_t)y * 2 * c + chc];
     s2 += part[(int64_t)y * 2 * c + c + chc];
@@ -587,9 +589,17 @@ int grid_for(int64_t total) {
     }                                  \
   } while (0)
 
+// row slices of dp_bn_stats: 256-row slices, or BN_SLICES longer ones (multiples of 32 rows)
+constexpr int BN_SLICES = 64;
+inline int bn_slice_rows(int rows) {
+  const int per = (rows + BN_SLICES - 1) / BN_SLICES;
+  return std::max(256, (per + 31) / 32 * 32);
+}
+
 extern "C" int64_t dp_bn_stats_ws_bytes(int32_t rows, int32_t c) {
   if (rows <= 0 || c <= 0) return -1;
-  return (int64_t)((rows + 255) / 256) * 2 * c * (int64_t)sizeof(float);
+  const int sl = bn_slice_rows(rows);
+  return (int64_t)((rows + sl - 1) / sl) * 2 * c * (int64_t)sizeof(float);
 }
 
 extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, float* ws, int64_t ws_bytes,
@@ -598,9 +608,9 @@ extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, f
   DP_REQUIRE(ws_bytes >= dp_bn_stats_ws_bytes(rows, c), "dp_bn_stats: workspace of %lld bytes < %lld",
              (long long)ws_bytes, (long long)dp_bn_stats_ws_bytes(rows, c));
   hipStream_t s = as_stream(stream);
-  const int ny = (rows + 255) / 256;
+  const int sl = bn_slice_rows(rows), ny = (rows + sl - 1) / sl;
   dim3 grid((c + 63) / 64, ny);
-  DP_DT(hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ld, rows, c, ws));
+  DP_DT(hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ld, rows, c, sl, ws));
   DP_DT(hipLaunchKernelGGL(bn_stats_reduce_kernel<T>, dim3((c + 63) / 64), dim3(256), 0, s, (const T*)x, ws, ny, c,
                            out));
   return dp_check_launch("dp_bn_stats");

@@ -587,7 +587,7 @@ int dp_convert_rows(const void* src, int32_t src_dtype, int64_t ld_src, void* ds
  * f32. Callers: detrpose_amd/encoder_train.py. */
 
 /* nn.BatchNorm2d batch statistics, per rank: out [3][c] = (K = x[0][ch], sum (x - K), sum (x - K)^2)
- * over the rows (single pass, shifted by the first row against cancellation). Per-256-row
+ * over the rows (single pass, shifted by the first row against cancellation). Per-row-slice
  * partial sums go to ws (dp_bn_stats_ws_bytes) and are added in a fixed order: no float
  * atomics, the same result on every run. */
 int64_t dp_bn_stats_ws_bytes(int32_t rows, int32_t c);

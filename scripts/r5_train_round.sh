@@ -20,6 +20,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_train -o run --o
   || { tail -20 $OUT/prof_train.log; exit 1; }
 timeout -k 10 400 python -u bench.py --gpus 2 --shared-gpu-rehearsal --batch 8 --steps 5 --warmup 2 $NT \
   --train-batch 4 --train-steps 3 > $OUT/rehearsal2.json 2> $OUT/rehearsal2.err || { tail -20 $OUT/rehearsal2.err; exit 1; }
-python -c "import json; d=json.load(open('$OUT/rehearsal2.json')); print(json.dumps(d['train_step']))"
+python -c "import json; l=[x for x in open('$OUT/rehearsal2.json') if x.startswith('{')][-1]; print(json.dumps(json.loads(l)['train_step']))"
 find $OUT -name '*stats.csv' | head
 echo done
