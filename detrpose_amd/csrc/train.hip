@@ -1187,8 +1187,10 @@ __global__ void zero_fill_kernel(char* __restrict__ p, size_t bytes) {
   const size_t body = (bytes - h) / 16;
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
   if (i0 < h) p[i0] = 0;
-  uint4* b = reinterpret_cast<uint4*>(p + h);
-  for (size_t i = i0; i < body; i += st) b[i] = make_uint4(0u, 0u, 0u, 0u);
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  u32x4_t* b = reinterpret_cast<u32x4_t*>(p + h);
+  // streaming stores: the zeroed buffers are accumulated into much later in the tape
+  for (size_t i = i0; i < body; i += st) __builtin_nontemporal_store(u32x4_t{0u, 0u, 0u, 0u}, b + i);
   const size_t tail = h + body * 16;
   if (tail + i0 < bytes) p[tail + i0] = 0;
 }
@@ -1196,7 +1198,7 @@ __global__ void zero_fill_kernel(char* __restrict__ p, size_t bytes) {
 int dp_zero_async(void* p, size_t bytes, hipStream_t s) {
   if (!bytes) return 0;
   const size_t body = bytes / 16 + 1;
-  const unsigned grid = (unsigned)std::min<size_t>((body + 255) / 256, 2048);
+  const unsigned grid = (unsigned)std::min<size_t>((body + 255) / 256, 16384);
   hipLaunchKernelGGL(zero_fill_kernel, dim3(grid), dim3(256), 0, s, static_cast<char*>(p), bytes);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
