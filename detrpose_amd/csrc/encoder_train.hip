@@ -8,6 +8,8 @@
 // Layout: NHWC activations as [rows][c] with a row stride (channel slices of concat buffers),
 // rows = batch * h * w. f32 statistics. Activations / activation gradients of dtype.
 #include <algorithm>
+#include <stdlib.h>
+#include <type_traits>
 
 #include "common.h"
 
@@ -340,31 +342,66 @@ __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin,
 }
 
 // depthwise conv backward (SCDown's 3x3 s2, hybrid_encoder.py:156-170; HGNetv2's 3x3 s2
-// downsample and 5x5 / 3x3 LightConvBNAct, hgnetv2.py:144-163). A wave = 64 channels (lanes) of one
-// row tile of TW pixels; K, S compile-time so the taps, the tile and the accumulators live in
-// registers. dx (+=): stride 1 slides a register window of the dz row over the tile; dw (+=): a
-// thread sums its channel's K*K taps over the tiles it walks, the block's 64 channels x K*K sums
-// are transposed through LDS so the f32 atomics hit contiguous addresses of the [c][K][K] gradient.
+// downsample and 5x5 / 3x3 LightConvBNAct, hgnetv2.py:144-163). A lane = VC consecutive channels
+// (one VC-element vector load per pixel: 8 bytes for bf16 at VC = 4), a wave = 64 such chunks of
+// one row tile of DW_TW pixels; K, S compile-time so the taps, the tile and the accumulators live
+// in registers. dx (+=): stride 1 slides a register window of the dz row over the tile; dw (+=):
+// a thread sums its channels' K*K taps over the tiles it walks, the block's channels x K*K sums
+// are transposed through LDS so the f32 atomics hit contiguous addresses of the [c][K][K]
+// gradient. VC = 1 is the any-stride / any-alignment form.
 constexpr int DW_TW = 8;
 
-template <typename T, int K, int S>
+template <typename T, int VC>
+__device__ __forceinline__ void ld_vec(const T* p, float (&v)[VC]) {
+  if constexpr (VC == 1) {
+    v[0] = to_f32(*p);
+  } else if constexpr (std::is_same<T, bf16_t>::value) {
+    static_assert(VC == 4, "bf16 vectors of 4");
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(u.x << 16), v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16), v[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+    static_assert(VC == 4, "f32 vectors of 4");
+    const float4 f = *reinterpret_cast<const float4*>(p);
+    v[0] = f.x, v[1] = f.y, v[2] = f.z, v[3] = f.w;
+  }
+}
+template <typename T, int VC>
+__device__ __forceinline__ void st_vec(T* p, const float (&v)[VC]) {
+  if constexpr (VC == 1) {
+    *p = from_f32<T>(v[0]);
+  } else if constexpr (std::is_same<T, bf16_t>::value) {
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (bf16_t)v[e];
+    *reinterpret_cast<bf16x4*>(p) = o;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <typename T, int K, int S, int VC>
 __global__ __launch_bounds__(256) void dw_bwd_data_kernel(const T* __restrict__ dz, int64_t zbs, int zps,
                                                           const float* __restrict__ wt, int h, int w, int c, int pad,
                                                           int oh, int ow, T* __restrict__ dx, int64_t xbs, int xps,
                                                           int ntiles) {
-  const int ch = blockIdx.x * 64 + threadIdx.x;
+  const int ch = (blockIdx.x * 64 + threadIdx.x) * VC;
   if (ch >= c) return;
-  float wk[K * K];
+  float wk[K * K][VC];
 #pragma unroll
-  for (int t = 0; t < K * K; ++t) wk[t] = wt[t * c + ch];
+  for (int t = 0; t < K * K; ++t)
+#pragma unroll
+    for (int v = 0; v < VC; ++v) wk[t][v] = wt[t * c + ch + v];
   const int ntx = (w + DW_TW - 1) / DW_TW;
   for (int tt = blockIdx.y * 4 + threadIdx.y; tt < ntiles; tt += gridDim.y * 4) {
     const int x0 = (tt % ntx) * DW_TW, t2 = tt / ntx;
     const int y = t2 % h, b = t2 / h;
     const T* zb = dz + (int64_t)b * zbs + ch;
-    float acc[DW_TW];
+    float acc[DW_TW][VC];
 #pragma unroll
-    for (int i = 0; i < DW_TW; ++i) acc[i] = 0.f;
+    for (int i = 0; i < DW_TW; ++i)
+#pragma unroll
+      for (int v = 0; v < VC; ++v) acc[i][v] = 0.f;
 #pragma unroll
     for (int ky = 0; ky < K; ++ky) {
       const int ny = y + pad - ky;
@@ -374,17 +411,21 @@ __global__ __launch_bounds__(256) void dw_bwd_data_kernel(const T* __restrict__ 
       const T* zr = zb + (int64_t)oy * ow * zps;
       if (S == 1) {
         // output x0 + i takes dz[ox = x0 + i + pad - kx]: window j = i + K - 1 - kx
-        float zw[DW_TW + K - 1];
+        float zw[DW_TW + K - 1][VC];
 #pragma unroll
         for (int j = 0; j < DW_TW + K - 1; ++j) {
           const int ox = x0 + pad - (K - 1) + j;
-          const float zv = to_f32(zr[(int64_t)min(max(ox, 0), ow - 1) * zps]);
-          zw[j] = (ox >= 0 && ox < ow) ? zv : 0.f;
+          ld_vec<T, VC>(zr + (int64_t)min(max(ox, 0), ow - 1) * zps, zw[j]);
+          if (ox < 0 || ox >= ow)
+#pragma unroll
+            for (int v = 0; v < VC; ++v) zw[j][v] = 0.f;
         }
 #pragma unroll
         for (int i = 0; i < DW_TW; ++i)
 #pragma unroll
-          for (int kx = 0; kx < K; ++kx) acc[i] = fmaf(zw[i + K - 1 - kx], wk[ky * K + kx], acc[i]);
+          for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+            for (int v = 0; v < VC; ++v) acc[i][v] = fmaf(zw[i + K - 1 - kx][v], wk[ky * K + kx][v], acc[i][v]);
       } else {
 #pragma unroll
         for (int i = 0; i < DW_TW; ++i)
@@ -392,92 +433,115 @@ __global__ __launch_bounds__(256) void dw_bwd_data_kernel(const T* __restrict__ 
           for (int kx = 0; kx < K; ++kx) {
             const int nx = x0 + i + pad - kx;
             const int ox = nx / S;
-            const float zv = to_f32(zr[(int64_t)min(max(ox, 0), ow - 1) * zps]);
-            acc[i] = fmaf((nx >= 0 && nx % S == 0 && ox < ow) ? zv : 0.f, wk[ky * K + kx], acc[i]);
+            float zv[VC];
+            ld_vec<T, VC>(zr + (int64_t)min(max(ox, 0), ow - 1) * zps, zv);
+            const bool ok = nx >= 0 && nx % S == 0 && ox < ow;
+#pragma unroll
+            for (int v = 0; v < VC; ++v) acc[i][v] = fmaf(ok ? zv[v] : 0.f, wk[ky * K + kx][v], acc[i][v]);
           }
       }
     }
     T* o = dx + (int64_t)b * xbs + (int64_t)y * w * xps + ch;
-    float prev[DW_TW];
+    float prev[DW_TW][VC];
 #pragma unroll
-    for (int i = 0; i < DW_TW; ++i) prev[i] = to_f32(o[(int64_t)min(x0 + i, w - 1) * xps]);
+    for (int i = 0; i < DW_TW; ++i) ld_vec<T, VC>(o + (int64_t)min(x0 + i, w - 1) * xps, prev[i]);
 #pragma unroll
     for (int i = 0; i < DW_TW; ++i)
-      if (x0 + i < w) o[(int64_t)(x0 + i) * xps] = from_f32<T>(prev[i] + acc[i]);
+      if (x0 + i < w) {
+        float r[VC];
+#pragma unroll
+        for (int v = 0; v < VC; ++v) r[v] = prev[i][v] + acc[i][v];
+        st_vec<T, VC>(o + (int64_t)(x0 + i) * xps, r);
+      }
   }
 }
 
-template <typename T, int K, int S>
+template <typename T, int K, int S, int VC>
 __global__ __launch_bounds__(256) void dw_bwd_weight_kernel(const T* __restrict__ x, int64_t xbs, int xps,
                                                             const T* __restrict__ dz, int64_t zbs, int zps, int h,
                                                             int w, int c, int pad, int oh, int ow, int ntiles,
                                                             float* __restrict__ dw) {
   constexpr int XW = (DW_TW - 1) * S + K;
-  __shared__ float red[4][64 * K * K];
-  const int ch = blockIdx.x * 64 + threadIdx.x;
+  constexpr int CB = 64 * VC;   // the block's channels
+  __shared__ float red[CB * K * K];   // the four waves' sums, added in wave order
+  const int ch = (blockIdx.x * 64 + threadIdx.x) * VC;
   const bool active = ch < c;
-  float acc[K * K];
+  float acc[K * K][VC];
 #pragma unroll
-  for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
+  for (int t = 0; t < K * K; ++t)
+#pragma unroll
+    for (int v = 0; v < VC; ++v) acc[t][v] = 0.f;
   const int ntx = (ow + DW_TW - 1) / DW_TW;
   if (active) {
     for (int tt = blockIdx.y * 4 + threadIdx.y; tt < ntiles; tt += gridDim.y * 4) {
       const int ox0 = (tt % ntx) * DW_TW, t2 = tt / ntx;
       const int oy = t2 % oh, b = t2 / oh;
-      float g[DW_TW];
+      float g[DW_TW][VC];
       const T* zr = dz + (int64_t)b * zbs + (int64_t)oy * ow * zps + ch;
 #pragma unroll
       for (int i = 0; i < DW_TW; ++i) {
-        const float gv = to_f32(zr[(int64_t)min(ox0 + i, ow - 1) * zps]);
-        g[i] = ox0 + i < ow ? gv : 0.f;
+        ld_vec<T, VC>(zr + (int64_t)min(ox0 + i, ow - 1) * zps, g[i]);
+        if (ox0 + i >= ow)
+#pragma unroll
+          for (int v = 0; v < VC; ++v) g[i][v] = 0.f;
       }
 #pragma unroll
       for (int ky = 0; ky < K; ++ky) {
         const int iy = oy * S - pad + ky;
         if (iy < 0 || iy >= h) continue;
         const T* xr = x + (int64_t)b * xbs + (int64_t)iy * w * xps + ch;
-        float xw[XW];
+        float xw[XW][VC];
 #pragma unroll
         for (int j = 0; j < XW; ++j) {
           const int ix = ox0 * S - pad + j;
-          const float xv = to_f32(xr[(int64_t)min(max(ix, 0), w - 1) * xps]);
-          xw[j] = (ix >= 0 && ix < w) ? xv : 0.f;
+          ld_vec<T, VC>(xr + (int64_t)min(max(ix, 0), w - 1) * xps, xw[j]);
+          if (ix < 0 || ix >= w)
+#pragma unroll
+            for (int v = 0; v < VC; ++v) xw[j][v] = 0.f;
         }
 #pragma unroll
         for (int i = 0; i < DW_TW; ++i)
 #pragma unroll
-          for (int kx = 0; kx < K; ++kx) acc[ky * K + kx] = fmaf(g[i], xw[i * S + kx], acc[ky * K + kx]);
+          for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+            for (int v = 0; v < VC; ++v) acc[ky * K + kx][v] = fmaf(g[i][v], xw[i * S + kx][v], acc[ky * K + kx][v]);
       }
     }
   }
+  // [channel][tap] order in LDS: the block's channels ch0 .. own dw[ch0*K*K ..] contiguously
+  for (int wy = 0; wy < 4; ++wy) {
+    if (threadIdx.y == wy) {
 #pragma unroll
-  for (int t = 0; t < K * K; ++t) red[threadIdx.y][threadIdx.x * K * K + t] = acc[t];
-  __syncthreads();
-  // the block's channels ch0 .. ch0+63 own dw[ch0*K*K ..] contiguously
-  const int ch0 = blockIdx.x * 64;
-  const int n = min(64, c - ch0) * K * K;
-  for (int e = threadIdx.y * 64 + threadIdx.x; e < n; e += 256) {
-    const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
-    atomicAdd(dw + (int64_t)ch0 * K * K + e, v);
+      for (int t = 0; t < K * K; ++t)
+#pragma unroll
+        for (int v = 0; v < VC; ++v) {
+          float& r = red[(threadIdx.x * VC + v) * K * K + t];
+          r = wy ? r + acc[t][v] : acc[t][v];
+        }
+    }
+    __syncthreads();
   }
+  const int ch0 = blockIdx.x * CB;
+  const int n = min(CB, c - ch0) * K * K;
+  for (int e = threadIdx.y * 64 + threadIdx.x; e < n; e += 256) atomicAdd(dw + (int64_t)ch0 * K * K + e, red[e]);
 }
 
-template <typename T, int K, int S>
+template <typename T, int K, int S, int VC>
 void dw_bwd_launch(const void* x, int64_t xbs, int xps, const void* dz, int64_t zbs, int zps, const float* wt,
                    int batch, int h, int w, int c, int pad, int oh, int ow, void* dx, int64_t dxbs, int dxps,
                    float* dw, hipStream_t s) {
-  const unsigned gx = (unsigned)((c + 63) / 64);
+  const unsigned gx = (unsigned)((c + 64 * VC - 1) / (64 * VC));
   if (dx) {
     const int ntiles = batch * h * ((w + DW_TW - 1) / DW_TW);
     const unsigned gy = (unsigned)std::min((ntiles + 3) / 4, 65535);
-    hipLaunchKernelGGL((dw_bwd_data_kernel<T, K, S>), dim3(gx, gy), dim3(64, 4), 0, s, (const T*)dz, zbs, zps, wt, h,
-                       w, c, pad, oh, ow, (T*)dx, dxbs, dxps, ntiles);
+    hipLaunchKernelGGL((dw_bwd_data_kernel<T, K, S, VC>), dim3(gx, gy), dim3(64, 4), 0, s, (const T*)dz, zbs, zps, wt,
+                       h, w, c, pad, oh, ow, (T*)dx, dxbs, dxps, ntiles);
   }
   if (dw) {
     const int ntiles = batch * oh * ((ow + DW_TW - 1) / DW_TW);
     // about 4 tiles per thread: enough waves to fill the chip, the atomics a small fraction
     const unsigned gy = (unsigned)std::max(1, std::min((ntiles + 15) / 16, 65535));
-    hipLaunchKernelGGL((dw_bwd_weight_kernel<T, K, S>), dim3(gx, gy), dim3(64, 4), 0, s, (const T*)x, xbs, xps,
+    hipLaunchKernelGGL((dw_bwd_weight_kernel<T, K, S, VC>), dim3(gx, gy), dim3(64, 4), 0, s, (const T*)x, xbs, xps,
                        (const T*)dz, zbs, zps, h, w, c, pad, oh, ow, ntiles, dw);
   }
 }
@@ -729,10 +793,23 @@ extern "C" int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride
   DP_REQUIRE((k == 3 || k == 5) && (stride == 1 || stride == 2), "dp_dwconv_bwd: k %d stride %d (3 / 5, 1 / 2)", k,
              stride);
   hipStream_t s = as_stream(stream);
+  // 4-channel vectors for the stride-2 convs when every row of channels is 4-aligned: L b16 tapes
+  // 0.348 -> 0.314 ms for the downsamples; the 5x5 stride-1 LightConvs are faster scalar (1.13 vs
+  // 1.25 ms: 220-240 VGPRs at 4 channels). DETRPOSE_DW_BWD_VEC = 0 (never) / 2 (always): A/B.
+  static const int vec_env = getenv("DETRPOSE_DW_BWD_VEC") ? atoi(getenv("DETRPOSE_DW_BWD_VEC")) : 1;
+  const int esz = dtype == DP_BF16 ? 2 : 4;
+  auto al = [&](const void* p) { return !p || (reinterpret_cast<uintptr_t>(p) & (4 * esz - 1)) == 0; };
+  const bool vec = (vec_env == 2 || (vec_env == 1 && stride == 2)) && c % 4 == 0 && x_pstride % 4 == 0 && z_pstride % 4 == 0 && dx_pstride % 4 == 0 &&
+                   x_bstride % 4 == 0 && z_bstride % 4 == 0 && dx_bstride % 4 == 0 && al(x) && al(dz) && al(dx) &&
+                   al(wt);
 #define DW_CASE(KK, SS)                                                                                          \
   if (k == KK && stride == SS) {                                                                                 \
-    DP_DT((dw_bwd_launch<T, KK, SS>(x, x_bstride, x_pstride, dz, z_bstride, z_pstride, wt, batch, h, w, c, pad, oh, \
-                                    ow, dx, dx_bstride, dx_pstride, dw, s)));                                   \
+    if (vec)                                                                                                     \
+      DP_DT((dw_bwd_launch<T, KK, SS, 4>(x, x_bstride, x_pstride, dz, z_bstride, z_pstride, wt, batch, h, w, c, pad, \
+                                         oh, ow, dx, dx_bstride, dx_pstride, dw, s)));                          \
+    else                                                                                                         \
+      DP_DT((dw_bwd_launch<T, KK, SS, 1>(x, x_bstride, x_pstride, dz, z_bstride, z_pstride, wt, batch, h, w, c, pad, \
+                                         oh, ow, dx, dx_bstride, dx_pstride, dw, s)));                          \
   }
   DW_CASE(3, 1) else DW_CASE(3, 2) else DW_CASE(5, 1) else DW_CASE(5, 2)
 #undef DW_CASE

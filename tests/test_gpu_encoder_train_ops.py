@@ -177,7 +177,7 @@ def test_conv_pack_forward_dgrad_wgrad(k, cin, cout):
     _close(dW.view(cout, cin, k, k), wr.grad, f"conv{k} wgrad")
 
 
-@pytest.mark.parametrize("k,st,c", [(3, 2, 64), (5, 1, 96), (3, 1, 40), (5, 2, 68)])
+@pytest.mark.parametrize("k,st,c", [(3, 2, 64), (5, 1, 96), (3, 1, 40), (5, 2, 68), (3, 2, 296)])
 def test_depthwise_s2_backward_and_pack(k, st, c):
     """SCDown's depthwise 3x3 stride-2 conv (hybrid_encoder.py:156-170): dp_conv_pack mode 2 +
     dp_dwconv2d forward, dp_dwconv_bwd input and weight gradients vs autograd; also HGNetv2's 5x5 /
@@ -213,6 +213,41 @@ def test_depthwise_s2_backward_and_pack(k, st, c):
     _close(out, y.detach().permute(0, 2, 3, 1), "dw fwd")
     _close(dx, x.grad.permute(0, 2, 3, 1), "dw dx")
     _close(dw, wr.grad.view(c, k, k), "dw dw")
+
+
+@pytest.mark.parametrize("k,st,c", [(5, 1, 192), (3, 2, 384), (5, 2, 42), (3, 1, 36)])
+def test_depthwise_backward_bf16(k, st, c):
+    """dp_dwconv_bwd on bf16 maps (the training tapes' dtype): 4-channel vector lanes for the
+    stride-2 convs when the channel rows allow it (c % 4 == 0), the scalar form otherwise (c = 42,
+    the stride-1 convs), against autograd in fp32 on the
+    same bf16 values; dx accumulates into a nonzero bf16 buffer (one bf16 rounding of the sum),
+    dw in f32."""
+    lib = _lib.load()
+    torch.manual_seed(11)
+    B, h, w = 2, 13, 21
+    p = (k - 1) // 2
+    wt = torch.randn(c, 1, k, k, device=DEV)
+    x = torch.randn(B, c, h, w, device=DEV).bfloat16().float().requires_grad_(True)
+    wr = wt.clone().requires_grad_(True)
+    y = F.conv2d(x, wr, None, st, p, 1, c)
+    dy = torch.randn_like(y).bfloat16().float()
+    y.backward(dy)
+    oh, ow = y.shape[2:]
+    taps = wt.view(c, k * k).t().contiguous()          # [k*k][c] f32, dp_conv_pack mode 2's layout
+    xn = x.detach().permute(0, 2, 3, 1).contiguous().bfloat16()
+    dyn = dy.permute(0, 2, 3, 1).contiguous().bfloat16()
+    dx0 = torch.randn(B, h, w, c, device=DEV).bfloat16()
+    dx = dx0.clone()
+    dw = torch.zeros(c, k, k, device=DEV)
+    _lib.check(lib.dp_dwconv_bwd(xn.data_ptr(), h * w * c, c, dyn.data_ptr(), oh * ow * c, c, taps.data_ptr(), B, h, w,
+                                 c, k, st, p, oh, ow, dx.data_ptr(), h * w * c, c, dw.data_ptr(), DP_BF16, _s()),
+               "dw bwd bf16")
+    torch.cuda.synchronize()
+    ref_dx = dx0.float() + x.grad.permute(0, 2, 3, 1)
+    err = float((dx.float() - ref_dx).abs().max())
+    scale = float(ref_dx.abs().max())
+    assert err <= 2 ** -7 * scale, ("dx", err, scale)       # one bf16 rounding of the sum
+    _close(dw, wr.grad.view(c, k, k), "dw dw bf16")
 
 
 def test_upsample_axpby_gelu_backward():
