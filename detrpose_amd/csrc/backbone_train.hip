@@ -133,10 +133,112 @@ __global__ void col2im_kernel(const T* __restrict__ col, int h, int w, int cin, 
   *o = from_f32<T>(acc ? ldf(o) + sum : sum);
 }
 
+// The same with 16-byte channel vectors (VC channels per thread: 8 bf16 / 4 f32) and 32-bit
+// index arithmetic (total / VC < 2^31, host-checked): the scalar form spends most of its time in
+// 64-bit divisions, one thread per element.
+template <typename T, int VC>
+__global__ __launch_bounds__(256) void col2im_vec_kernel(const T* __restrict__ col, int h, int w, int cin, int kh,
+                                                         int kw, int s, int pad, int oh, int ow, T* __restrict__ dx,
+                                                         int64_t bs, int ps, int acc, unsigned total) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const unsigned nch = (unsigned)(cin / VC);
+  const unsigned p = e / nch;
+  const int ci = (int)(e - p * nch) * VC;
+  const unsigned t = p / (unsigned)w;
+  const int x = (int)(p - t * (unsigned)w);
+  const unsigned b_ = t / (unsigned)h;
+  const int yy = (int)(t - b_ * (unsigned)h), b = (int)b_;
+  const int64_t K = (int64_t)cin * kh * kw;
+  float sum[VC];
+#pragma unroll
+  for (int v = 0; v < VC; ++v) sum[v] = 0.f;
+  for (int ky = (yy + pad) % s; ky < kh; ky += s) {
+    const int ny = yy + pad - ky;
+    if (ny < 0) break;
+    const int oy = ny / s;
+    if (oy >= oh) continue;
+    const T* crow = col + ((int64_t)b * oh + oy) * ow * K + (int64_t)ky * kw * cin + ci;
+    for (int kx = (x + pad) % s; kx < kw; kx += s) {
+      const int nx = x + pad - kx;
+      if (nx < 0) break;
+      const int ox = nx / s;
+      if (ox >= ow) continue;
+      const u32x4_t u = *reinterpret_cast<const u32x4_t*>(crow + ox * K + kx * cin);
+      if constexpr (VC == 8) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sum[2 * q] += __uint_as_float(u[q] << 16);
+          sum[2 * q + 1] += __uint_as_float(u[q] & 0xffff0000u);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sum[q] += __uint_as_float(u[q]);
+      }
+    }
+  }
+  T* o = dx + (int64_t)b * bs + ((int64_t)yy * w + x) * ps + ci;
+  if (acc) {
+    const u32x4_t u = *reinterpret_cast<const u32x4_t*>(o);
+    if constexpr (VC == 8) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        sum[2 * q] += __uint_as_float(u[q] << 16);
+        sum[2 * q + 1] += __uint_as_float(u[q] & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sum[q] += __uint_as_float(u[q]);
+    }
+  }
+  if constexpr (VC == 8) {
+    bf16x8 r;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) r[v] = (bf16_t)sum[v];
+    *reinterpret_cast<bf16x8*>(o) = r;
+  } else {
+    *reinterpret_cast<float4*>(o) = make_float4(sum[0], sum[1], sum[2], sum[3]);
+  }
+}
+
 // F.pad(x, (0,1,0,1)) + MaxPool2d(2, 1, ceil_mode=True) backward (hgnetv2.py:215, 217): each
 // output's gradient goes to its window's first maximum in scan order (max_pool2d's argmax, the
 // pad zeros included: a pad maximum takes the gradient out of the map); gathered per input.
-template <typename T>
+// 16-byte vectors of channels: 8 bf16 or 4 f32 (VC), or one element (VC = 1)
+template <typename T, int VC>
+__device__ __forceinline__ void ld16v(const T* p, float (&v)[VC]) {
+  if constexpr (VC == 1) {
+    v[0] = ldf(p);
+  } else {
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t u = *reinterpret_cast<const u32x4_t*>(p);
+    if constexpr (VC == 8) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[2 * q] = __uint_as_float(u[q] << 16), v[2 * q + 1] = __uint_as_float(u[q] & 0xffff0000u);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = __uint_as_float(u[q]);
+    }
+  }
+}
+template <typename T, int VC>
+__device__ __forceinline__ void st16v(T* p, const float (&v)[VC]) {
+  if constexpr (VC == 1) {
+    *p = from_f32<T>(v[0]);
+  } else if constexpr (VC == 8) {
+    bf16x8 r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = (bf16_t)v[e];
+    *reinterpret_cast<bf16x8*>(p) = r;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// VC channels per thread (16-byte vectors when the rows allow: 8x fewer load instructions);
+// I32: total / VC < 2^31, the index split in 32-bit unsigned arithmetic
+template <typename T, bool I32, int VC>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ x, int64_t xbs, int xps, const T* __restrict__ dout,
                                    int64_t obs, int ops, int h, int w, int c, T* __restrict__ dx, int64_t dbs, int dps,
                                    int64_t total) {
@@ -144,44 +246,64 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ x, int64_t xbs, int xps
   // x and the 2x2 of dout are in flight together
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
-  const int ch = (int)(e % c);
-  const int64_t p = e / c;
-  const int px = (int)(p % w);
-  const int64_t t = p / w;
-  const int py = (int)(t % h), b = (int)(t / h);
+  const int nch = c / VC;
+  int ch, px, py, b;
+  if constexpr (I32) {
+    const unsigned e32 = (unsigned)e, p = e32 / (unsigned)nch, t = p / (unsigned)w, b_ = t / (unsigned)h;
+    ch = (int)(e32 - p * (unsigned)nch) * VC, px = (int)(p - t * (unsigned)w), py = (int)(t - b_ * (unsigned)h);
+    b = (int)b_;
+  } else {
+    ch = (int)(e % nch) * VC;
+    const int64_t p = e / nch;
+    px = (int)(p % w);
+    const int64_t t = p / w;
+    py = (int)(t % h), b = (int)(t / h);
+  }
   const T* xb = x + (int64_t)b * xbs + ch;
-  float xv[3][3];   // x at rows py-1 .. py+1, columns px-1 .. px+1 (0 past the right / bottom edge)
+  float xv[3][3][VC];   // x at rows py-1 .. py+1, columns px-1 .. px+1 (0 past the right / bottom edge)
 #pragma unroll
   for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
     for (int dxx = 0; dxx < 3; ++dxx) {
       const int yy = py - 1 + dy, xx = px - 1 + dxx;
-      const float v = ldf(xb + ((int64_t)min(max(yy, 0), h - 1) * w + min(max(xx, 0), w - 1)) * xps);
-      xv[dy][dxx] = (yy < h && xx < w) ? v : 0.f;   // yy, xx >= 0 wherever a window reads them
+      ld16v<T, VC>(xb + ((int64_t)min(max(yy, 0), h - 1) * w + min(max(xx, 0), w - 1)) * xps, xv[dy][dxx]);
+      if (!(yy < h && xx < w))   // yy, xx >= 0 wherever a window reads them
+#pragma unroll
+        for (int v = 0; v < VC; ++v) xv[dy][dxx][v] = 0.f;
     }
-  float acc = 0.f;
+  float acc[VC];
+#pragma unroll
+  for (int v = 0; v < VC; ++v) acc[v] = 0.f;
 #pragma unroll
   for (int oy = 0; oy < 2; ++oy)
 #pragma unroll
     for (int ox = 0; ox < 2; ++ox) {
       // output (py - 1 + oy, px - 1 + ox): window rows oy .. oy+1, columns ox .. ox+1 of xv
       const int qy = py - 1 + oy, qx = px - 1 + ox;
-      const float g = ldf(dout + (int64_t)b * obs + ((int64_t)max(qy, 0) * w + max(qx, 0)) * ops + ch);
-      float best = -INFINITY;
-      int arg = 0;
+      float g[VC];
+      ld16v<T, VC>(dout + (int64_t)b * obs + ((int64_t)max(qy, 0) * w + max(qx, 0)) * ops + ch, g);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float v = xv[oy + (q >> 1)][ox + (q & 1)];
-        if (v > best) {
-          best = v;
-          arg = q;
+      for (int v = 0; v < VC; ++v) {
+        float best = -INFINITY;
+        int arg = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float xq = xv[oy + (q >> 1)][ox + (q & 1)][v];
+          if (xq > best) {
+            best = xq;
+            arg = q;
+          }
         }
+        // this pixel is the window's (1 - oy, 1 - ox) element
+        if (qy >= 0 && qx >= 0 && arg == ((1 - oy) << 1 | (1 - ox))) acc[v] += g[v];
       }
-      // this pixel is the window's (1 - oy, 1 - ox) element
-      if (qy >= 0 && qx >= 0 && arg == ((1 - oy) << 1 | (1 - ox))) acc += g;
     }
   T* o = dx + (int64_t)b * dbs + ((int64_t)py * w + px) * dps + ch;
-  *o = from_f32<T>(ldf(o) + acc);
+  float prev[VC];
+  ld16v<T, VC>(o, prev);
+#pragma unroll
+  for (int v = 0; v < VC; ++v) prev[v] += acc[v];
+  st16v<T, VC>(o, prev);
 }
 
 int grid_of(int64_t total) {
@@ -241,6 +363,22 @@ extern "C" int dp_col2im(const void* col, int32_t batch, int32_t h, int32_t w, i
   DP_REQUIRE(col && dx && batch > 0 && h > 0 && w > 0 && cin > 0 && kh > 0 && kw > 0 && stride > 0 && oh > 0 && ow > 0,
              "dp_col2im: bad arguments");
   const int64_t total = (int64_t)batch * h * w * cin;
+  const int vc = dtype == DP_BF16 ? 8 : 4, esz = dtype == DP_BF16 ? 2 : 4;
+  const bool vec = cin % vc == 0 && dx_pstride % vc == 0 && dx_bstride % vc == 0 && total / vc < (1ll << 31) &&
+                   (reinterpret_cast<uintptr_t>(col) & 15) == 0 && (reinterpret_cast<uintptr_t>(dx) & 15) == 0 &&
+                   vc * esz == 16;
+  if (vec) {
+    const unsigned n = (unsigned)(total / vc);
+    if (dtype == DP_BF16)
+      hipLaunchKernelGGL((col2im_vec_kernel<bf16_t, 8>), dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                         (const bf16_t*)col, h, w, cin, kh, kw, stride, pad, oh, ow, (bf16_t*)dx, dx_bstride,
+                         dx_pstride, accumulate, n);
+    else
+      hipLaunchKernelGGL((col2im_vec_kernel<float, 4>), dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                         (const float*)col, h, w, cin, kh, kw, stride, pad, oh, ow, (float*)dx, dx_bstride,
+                         dx_pstride, accumulate, n);
+    return dp_check_launch("dp_col2im");
+  }
   DP_DT(hipLaunchKernelGGL(col2im_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
                            (const T*)col, h, w, cin, kh, kw, stride, pad, oh, ow, (T*)dx, dx_bstride, dx_pstride,
                            accumulate, total));
@@ -253,8 +391,30 @@ extern "C" int dp_maxpool2x2_pad_rb_bwd(const void* x, int64_t x_bstride, int32_
                                         int32_t dtype, void* stream) {
   DP_REQUIRE(x && dout && dx && batch > 0 && h > 0 && w > 0 && c > 0, "dp_maxpool2x2_pad_rb_bwd: bad arguments");
   const int64_t total = (int64_t)batch * h * w * c;
-  DP_DT(hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                           as_stream(stream), (const T*)x, x_bstride, x_pstride, (const T*)dout, dout_bstride,
-                           dout_pstride, h, w, c, (T*)dx, dx_bstride, dx_pstride, total));
+  const int vc = dtype == DP_BF16 ? 8 : 4;
+  auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool vec = c % vc == 0 && x_pstride % vc == 0 && dout_pstride % vc == 0 && dx_pstride % vc == 0 &&
+                   x_bstride % vc == 0 && dout_bstride % vc == 0 && dx_bstride % vc == 0 && a16(x) && a16(dout) &&
+                   a16(dx) && total / vc < (1ll << 31);
+  const dim3 blk(256);
+  if (vec) {
+    const int64_t n = total / vc;
+    if (dtype == DP_BF16)
+      hipLaunchKernelGGL((maxpool_bwd_kernel<bf16_t, true, 8>), dim3((unsigned)((n + 255) / 256)), blk, 0,
+                         as_stream(stream), (const bf16_t*)x, x_bstride, x_pstride, (const bf16_t*)dout, dout_bstride,
+                         dout_pstride, h, w, c, (bf16_t*)dx, dx_bstride, dx_pstride, n);
+    else
+      hipLaunchKernelGGL((maxpool_bwd_kernel<float, true, 4>), dim3((unsigned)((n + 255) / 256)), blk, 0,
+                         as_stream(stream), (const float*)x, x_bstride, x_pstride, (const float*)dout, dout_bstride,
+                         dout_pstride, h, w, c, (float*)dx, dx_bstride, dx_pstride, n);
+  } else if (total < (1ll << 31)) {
+    DP_DT(hipLaunchKernelGGL((maxpool_bwd_kernel<T, true, 1>), dim3((unsigned)((total + 255) / 256)), blk, 0,
+                             as_stream(stream), (const T*)x, x_bstride, x_pstride, (const T*)dout, dout_bstride,
+                             dout_pstride, h, w, c, (T*)dx, dx_bstride, dx_pstride, total));
+  } else {
+    DP_DT(hipLaunchKernelGGL((maxpool_bwd_kernel<T, false, 1>), dim3((unsigned)((total + 255) / 256)), blk, 0,
+                             as_stream(stream), (const T*)x, x_bstride, x_pstride, (const T*)dout, dout_bstride,
+                             dout_pstride, h, w, c, (T*)dx, dx_bstride, dx_pstride, total));
+  }
   return dp_check_launch("dp_maxpool2x2_pad_rb_bwd");
 }

@@ -72,11 +72,13 @@ def test_frozen_act_bwd(lab, dtype):
         _close(dl[1], cb.grad[0], "d lab.bias", 1e-4 if dtype == DP_F32 else 2e-2)
 
 
-def test_col2im_strided_dgrad():
-    """StemBlock.stem3 (3x3, stride 2, pad 1): dx = col2im(dz W) == F.conv2d's input gradient."""
+@pytest.mark.parametrize("bf16,cin", [(False, 32), (False, 30), (True, 64), (True, 36)])
+def test_col2im_strided_dgrad(bf16, cin):
+    """StemBlock.stem3 (3x3, stride 2, pad 1): dx = col2im(dz W) == F.conv2d's input gradient;
+    16-byte channel vectors when cin allows (32 f32, 64 bf16), the scalar form otherwise."""
     lib = _lib.load()
     torch.manual_seed(6)
-    B, cin, cout, h, w = 2, 32, 24, 17, 22
+    B, cout, h, w = 2, 24, 17, 22
     x = torch.randn(B, cin, h, w, device=DEV).requires_grad_(True)
     wt = torch.randn(cout, cin, 3, 3, device=DEV)
     y = F.conv2d(x, wt, None, 2, 1)
@@ -85,6 +87,26 @@ def test_col2im_strided_dgrad():
     oh, ow = y.shape[2:]
     # columns tap-major (ky, kx, ci), the order dp_conv_pack mode 4 packs W^T in
     dcol = dy.permute(0, 2, 3, 1).reshape(-1, cout) @ wt.permute(0, 2, 3, 1).reshape(cout, -1)
+    if bf16:
+        dcol = dcol.bfloat16()
+        dx = torch.ones(B, h, w, cin, device=DEV, dtype=torch.bfloat16)
+        _lib.check(lib.dp_col2im(dcol.contiguous().data_ptr(), B, h, w, cin, 3, 3, 2, 1, oh, ow, dx.data_ptr(),
+                                 h * w * cin, cin, 1, DP_BF16, _s()), "col2im bf16")
+        torch.cuda.synchronize()
+        # reference from the same bf16 columns, summed in f32, one bf16 rounding
+        ref = torch.ones(B, h, w, cin, device=DEV)
+        dc = dcol.float().reshape(B, oh, ow, 3, 3, cin)
+        for ky in range(3):
+            for kx in range(3):
+                for oy in range(oh):
+                    y_ = 2 * oy - 1 + ky
+                    if 0 <= y_ < h:
+                        xs = [2 * ox - 1 + kx for ox in range(ow)]
+                        ok = [i for i, x_ in enumerate(xs) if 0 <= x_ < w]
+                        ref[:, y_, [xs[i] for i in ok]] += dc[:, oy, ok, ky, kx]
+        err = float((dx.float() - ref).abs().max())
+        assert err <= 2 ** -7 * float(ref.abs().max()), err
+        return
     dx = torch.ones(B, h, w, cin, device=DEV)
     _lib.check(lib.dp_col2im(dcol.contiguous().data_ptr(), B, h, w, cin, 3, 3, 2, 1, oh, ow, dx.data_ptr(), h * w * cin,
                              cin, 1, DP_F32, _s()), "col2im")
@@ -101,14 +123,14 @@ def test_col2im_strided_dgrad():
     assert torch.equal(wp, ref)
 
 
-@pytest.mark.parametrize("dtype", [DP_F32, DP_BF16])
-def test_maxpool_pad_rb_bwd_with_ties(dtype):
+@pytest.mark.parametrize("dtype,c", [(DP_F32, 16), (DP_BF16, 16), (DP_BF16, 12), (DP_F32, 6)])
+def test_maxpool_pad_rb_bwd_with_ties(dtype, c):
     """F.pad(0,1,0,1) + MaxPool2d(2, 1, ceil_mode=True) backward, ReLU'd input (many tied zeros,
-    the pad zeros included)."""
+    the pad zeros included); 16-byte channel vectors (c = 16) and the one-channel form."""
     lib = _lib.load()
     torch.manual_seed(7)
     td = torch.float32 if dtype == DP_F32 else torch.bfloat16
-    B, c, h, w = 2, 16, 13, 11
+    B, h, w = 2, 13, 11
     x = F.relu(torch.randn(B, c, h, w, device=DEV)).to(td).float().requires_grad_(True)
     y = F.max_pool2d(F.pad(x, (0, 1, 0, 1)), 2, 1, ceil_mode=True)
     dy = torch.randn_like(y)
