@@ -42,7 +42,7 @@ __device__ __forceinline__ float act_d(float x, int act) {
 // Column sums over a block of rows, shifted by the column's first-row value K (single-pass
 // variance without the E[x^2] - mean^2 cancellation): part[y][0] = sum (x - K), part[y][1] =
 // sum (x - K)^2 over row slice y. Block: 64 channels (lane) x 4 row phases (wave), `slice` rows
-// (a multiple of 32; at most BN_SLICES slices, so the reduction below stays short).
+// (a multiple of 32; see bn_slice_rows: enough slices to fill the chip, few enough for a short reduction).
 // No float atomics: bn_stats_reduce_kernel sums the slices in a fixed order, so the forward
 // is deterministic run to run.
 template <typename T>
@@ -77,18 +77,19 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
   }
 }
 
-// out [3][c] = (K, sum over the ny slices of part[y][0], of part[y][1]): wave w adds slices
-// w, w + 4, ... in order, then the four wave sums are added in order.
+// out [3][c] = (K, sum over the ny slices of part[y][0], of part[y][1]): wave w of 16 adds
+// slices w, w + 16, ... in order, then the 16 wave sums are added in order.
 template <typename T>
-__global__ __launch_bounds__(256) void bn_stats_reduce_kernel(const T* __restrict__ x, const float* __restrict__ part,
-                                                              int ny, int c, float* __restrict__ out) {
-  __shared__ float red[2][4][64];
+__global__ __launch_bounds__(1024) void bn_stats_reduce_kernel(const T* __restrict__ x, const float* __restrict__ part,
+                                                               int ny, int c, float* __restrict__ out) {
+  constexpr int NWV = 16;
+  __shared__ float red[2][NWV][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + lane;
   const int chc = min(ch, c - 1);
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll 4
-  for (int y = wv; y < ny; y += 4) {
+  for (int y = wv; y < ny; y += NWV) {
     s1 += part[(int64_t)y * 2 * c + chc];
     s2 += part[(int64_t)y * 2 * c + c + chc];
   }
@@ -96,9 +97,12 @@ __global__ __launch_bounds__(256) void bn_stats_reduce_kernel(const T* __restric
   red[1][wv][lane] = s2;
   __syncthreads();
   if (wv == 0 && ch < c) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NWV; ++k) t1 += red[0][k][lane], t2 += red[1][k][lane];
     out[ch] = ld_(x + ch);
-    out[c + ch] = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
-    out[2 * c + ch] = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
+    out[c + ch] = t1;
+    out[2 * c + ch] = t2;
   }
 }
 
@@ -653,16 +657,18 @@ int grid_for(int64_t total) {
     }                                  \
   } while (0)
 
-// row slices of dp_bn_stats: 256-row slices, or BN_SLICES longer ones (multiples of 32 rows)
-constexpr int BN_SLICES = 64;
-inline int bn_slice_rows(int rows) {
-  const int per = (rows + BN_SLICES - 1) / BN_SLICES;
+// row slices of dp_bn_stats: 256-row slices, or longer ones (multiples of 32 rows) when a map
+// would need more than max(64, 2048 / channel blocks) of them: about 2048 blocks fill the chip,
+// and the reduction stays a few rounds of loads per wave
+inline int bn_slice_rows(int rows, int c) {
+  const int cb = (c + 63) / 64, cap = std::max(64, 2048 / cb);
+  const int per = (rows + cap - 1) / cap;
   return std::max(256, (per + 31) / 32 * 32);
 }
 
 extern "C" int64_t dp_bn_stats_ws_bytes(int32_t rows, int32_t c) {
   if (rows <= 0 || c <= 0) return -1;
-  const int sl = bn_slice_rows(rows);
+  const int sl = bn_slice_rows(rows, c);
   return (int64_t)((rows + sl - 1) / sl) * 2 * c * (int64_t)sizeof(float);
 }
 
@@ -672,10 +678,10 @@ extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, f
   DP_REQUIRE(ws_bytes >= dp_bn_stats_ws_bytes(rows, c), "dp_bn_stats: workspace of %lld bytes < %lld",
              (long long)ws_bytes, (long long)dp_bn_stats_ws_bytes(rows, c));
   hipStream_t s = as_stream(stream);
-  const int sl = bn_slice_rows(rows), ny = (rows + sl - 1) / sl;
+  const int sl = bn_slice_rows(rows, c), ny = (rows + sl - 1) / sl;
   dim3 grid((c + 63) / 64, ny);
   DP_DT(hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ld, rows, c, sl, ws));
-  DP_DT(hipLaunchKernelGGL(bn_stats_reduce_kernel<T>, dim3((c + 63) / 64), dim3(256), 0, s, (const T*)x, ws, ny, c,
+  DP_DT(hipLaunchKernelGGL(bn_stats_reduce_kernel<T>, dim3((c + 63) / 64), dim3(1024), 0, s, (const T*)x, ws, ny, c,
                            out));
   return dp_check_launch("dp_bn_stats");
 }
