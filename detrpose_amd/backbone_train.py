@@ -268,7 +268,7 @@ class BackboneTrainPlan(TapePlan):
             t = torch.zeros(K, kpad, dtype=self.dt, device=self.dev)
             self.arena.append(t)
             self._packs[key] = (t, kpad)
-            self.fw.op(f"pack.{wkey}.T", self.lib.dp_conv_pack, _p(w), cout, cin, k, k, _p(t), kpad, 0, 4, None,
+            self.pk.op(f"pack.{wkey}.T", self.lib.dp_conv_pack, _p(w), cout, cin, k, k, _p(t), kpad, 0, 4, None,
                        self.code)
         t, kpad = self._packs[key]
         d = ConvDesc()
@@ -323,6 +323,9 @@ class BackboneTrainPlan(TapePlan):
         if images.data_ptr() != self.image.data_ptr():
             self.image.copy_(images.to(torch.float32))
 
-    def forward(self, debug=None):
+    def forward(self, debug=None, pack=True):
+        """pack=False: the weight packs of an earlier sub-batch of the same step are current."""
         self.sync_lab()
+        if pack:
+            self.pk.run(debug=debug)
         self.fw.run(debug=debug)

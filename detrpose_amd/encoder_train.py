@@ -141,6 +141,9 @@ class TapePlan:
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             self.world, self.rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
         self.fw, self.bw = _lib_tape(self.lib, self.dev), _lib_tape(self.lib, self.dev)
+        # the weight packs (bf16 copies / conv layouts of the f32 master) on a tape of their own:
+        # run once per optimizer step, not once per grad_accum sub-batch (forward(pack=False))
+        self.pk = _lib_tape(self.lib, self.dev)
         self._packs = {}
         self._col = None
 
@@ -193,7 +196,7 @@ class TapePlan:
             t = torch.empty(src.numel(), dtype=self.dt, device=self.dev)
             self.arena.append(t)
             self._packs[key] = t
-            self.fw.op("pack." + key, self.lib.dp_convert_rows, _p(src), DP_F32, src.numel(), _p(t), self.code,
+            self.pk.op("pack." + key, self.lib.dp_convert_rows, _p(src), DP_F32, src.numel(), _p(t), self.code,
                        src.numel(), 1, src.numel(), C.c_float(1.0), 0)
         return _p(self._packs[key])
 
@@ -213,7 +216,7 @@ class TapePlan:
                 t = torch.zeros(rows_p, kpad, dtype=self.dt, device=self.dev)
             self.arena.append(t)
             self._packs[k2] = (t, kpad)
-            self.fw.op(f"pack.{key}.{mode}", self.lib.dp_conv_pack, _p(w), cout, cin, kh, kw, _p(t), kpad, kc, mode,
+            self.pk.op(f"pack.{key}.{mode}", self.lib.dp_conv_pack, _p(w), cout, cin, kh, kw, _p(t), kpad, kc, mode,
                        _p(scale) if scale is not None else None, self.code if mode < 2 else DP_F32)
         return self._packs[k2]
 
@@ -398,7 +401,10 @@ class TapePlan:
             t = f.permute(0, 2, 3, 1) if f.dim() == 4 and f.shape[1] == v.c and f.shape[-1] != v.c else f
             v.buf.x[:, :v.c].copy_(t.reshape(v.rows, v.c).to(self.dt))
 
-    def forward(self, debug=None):
+    def forward(self, debug=None, pack=True):
+        """pack=False: the weight packs of an earlier sub-batch of the same step are current."""
+        if pack:
+            self.pk.run(debug=debug)
         self.fw.run(debug=debug)
 
     def backward(self, debug=None):

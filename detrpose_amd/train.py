@@ -121,8 +121,8 @@ class Trainer:
             bb.set_image(images)
             shapes = [(v.H, v.W) for v in bb.outs]
             ep = self.eng.encoder_plan(B, shapes, feats=bb.outs, feats_plan=bb)
-            bb.forward()
-            ep.forward()
+            bb.forward(pack=self._pack_due(bb))
+            ep.forward(pack=self._pack_due(ep))
             self.bb, self.ep = bb, ep
             return ep.memory, shapes
         plan = self.inf.plan(B)
@@ -158,6 +158,14 @@ class Trainer:
             plan.mask.copy_(torch.from_numpy(dn_attn_mask(pad, groups, single, eng.nq).astype(np.uint8)))
             plan._mask_key = (pad, groups, single)
 
+    def _pack_due(self, p):
+        """Whether plan p's weight-pack tape must run: once per optimizer step (the master weights
+        change only in the update), so the later grad_accum sub-batches reuse the packs."""
+        if getattr(p, "_packed_at", None) == self.steps:
+            return False
+        p._packed_at = self.steps
+        return True
+
     def _set_graphs(self, *plans):
         """Graph replay for the plans' tapes when self.graphs. A backbone with LearnableAffineBlocks
         (DETRPose-N's B0) keeps both its tapes eager: sync_lab writes the scalars' current values
@@ -166,7 +174,10 @@ class Trainer:
         for p in plans:
             on = self.graphs and not getattr(p, "labs", None)
             kind = "bb" if p is getattr(self, "bb", None) else "ep" if p is getattr(self, "ep", None) else "tr"
-            for t, nm in ((p.fw, kind + ".fw"), (p.bw, kind + ".bw")):
+            tapes = [(p.fw, kind + ".fw"), (p.bw, kind + ".bw")]
+            if getattr(p, "pk", None) is not None:
+                tapes.append((p.pk, kind + ".pk"))
+            for t, nm in tapes:
                 t.use_graph = on and (only is None or nm in only.split(","))
 
     def sub_step(self, images, targets):

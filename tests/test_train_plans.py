@@ -52,7 +52,10 @@ def test_every_parameter_gets_a_gradient(size, B):
     # the d memory hand-off and the backbone outputs' gradients are wired
     assert ep.d_memory.data_ptr() in _pointers(plan.bw)
     assert all(v.buf.g is not None for v in bb.outs)
-    assert len(bb.fw.ops) > 100 and len(ep.bw.ops) > 100
+    assert len(bb.fw.ops) > 30 and len(ep.bw.ops) > 100
+    # the weight packs on their own tapes (run once per optimizer step), none left in the forwards
+    assert len(bb.pk.ops) > 30 and len(ep.pk.ops) > 30
+    assert not any(n.startswith("pack.") for n, _, _ in bb.fw.ops + ep.fw.ops)
 
 
 def test_bf16_tapes_route_to_the_fast_kernels():
