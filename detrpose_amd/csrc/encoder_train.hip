@@ -133,6 +133,46 @@ __global__ void bn_finalize_kernel(const float* __restrict__ parts, int np, floa
   }
 }
 
+// VC-element vector loads / stores of a row chunk (VC = 1, or 16 / 8 bytes)
+template <typename T, int VC>
+__device__ __forceinline__ void ld_vec(const T* p, float (&v)[VC]) {
+  if constexpr (VC == 1) {
+    v[0] = to_f32(*p);
+  } else if constexpr (std::is_same<T, bf16_t>::value && VC == 8) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const unsigned w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[2 * q] = __uint_as_float(w4[q] << 16), v[2 * q + 1] = __uint_as_float(w4[q] & 0xffff0000u);
+  } else if constexpr (std::is_same<T, bf16_t>::value) {
+    static_assert(VC == 4, "bf16 vectors of 4 or 8");
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(u.x << 16), v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16), v[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+    static_assert(VC == 4, "f32 vectors of 4");
+    const float4 f = *reinterpret_cast<const float4*>(p);
+    v[0] = f.x, v[1] = f.y, v[2] = f.z, v[3] = f.w;
+  }
+}
+template <typename T, int VC>
+__device__ __forceinline__ void st_vec(T* p, const float (&v)[VC]) {
+  if constexpr (VC == 1) {
+    *p = from_f32<T>(v[0]);
+  } else if constexpr (std::is_same<T, bf16_t>::value && VC == 8) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16_t)v[e];
+    *reinterpret_cast<bf16x8*>(p) = o;
+  } else if constexpr (std::is_same<T, bf16_t>::value) {
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (bf16_t)v[e];
+    *reinterpret_cast<bf16x4*>(p) = o;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 struct BnBranch {
   const void* z;
   int64_t ld;
@@ -354,35 +394,6 @@ __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin,
 // are transposed through LDS so the f32 atomics hit contiguous addresses of the [c][K][K]
 // gradient. VC = 1 is the any-stride / any-alignment form.
 constexpr int DW_TW = 8;
-
-template <typename T, int VC>
-__device__ __forceinline__ void ld_vec(const T* p, float (&v)[VC]) {
-  if constexpr (VC == 1) {
-    v[0] = to_f32(*p);
-  } else if constexpr (std::is_same<T, bf16_t>::value) {
-    static_assert(VC == 4, "bf16 vectors of 4");
-    const uint2 u = *reinterpret_cast<const uint2*>(p);
-    v[0] = __uint_as_float(u.x << 16), v[1] = __uint_as_float(u.x & 0xffff0000u);
-    v[2] = __uint_as_float(u.y << 16), v[3] = __uint_as_float(u.y & 0xffff0000u);
-  } else {
-    static_assert(VC == 4, "f32 vectors of 4");
-    const float4 f = *reinterpret_cast<const float4*>(p);
-    v[0] = f.x, v[1] = f.y, v[2] = f.z, v[3] = f.w;
-  }
-}
-template <typename T, int VC>
-__device__ __forceinline__ void st_vec(T* p, const float (&v)[VC]) {
-  if constexpr (VC == 1) {
-    *p = from_f32<T>(v[0]);
-  } else if constexpr (std::is_same<T, bf16_t>::value) {
-    bf16x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (bf16_t)v[e];
-    *reinterpret_cast<bf16x4*>(p) = o;
-  } else {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
 
 template <typename T, int K, int S, int VC>
 __global__ __launch_bounds__(256) void dw_bwd_data_kernel(const T* __restrict__ dz, int64_t zbs, int zps,

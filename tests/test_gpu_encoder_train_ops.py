@@ -113,6 +113,71 @@ def test_bn_act_train_forward_backward(two, act, nparts):
         _close(db2, b2.grad, "dbeta2")
 
 
+@pytest.mark.parametrize("two,act,c,res", [(False, "silu", 96, False), (True, "relu", 256, True),
+                                            (True, "silu", 16, False), (False, None, 392, True)])
+def test_bn_act_bf16_rows(two, act, c, res):
+    """The BatchNorm row kernels on bf16 maps (the training tapes' dtype) against torch fp32
+    autograd on the same bf16 values: statistics, forward (+ CSP residual) and the backward reduce
+    / apply, ragged channel blocks included. bf16 outputs within 1e-2 of scale (their rounding),
+    f32 sums and parameter gradients within 2e-4. (A 16-byte-vector form of these kernels
+    measured no faster in the L b16 tapes and was not kept.)"""
+    lib = _lib.load()
+    torch.manual_seed(21 + c)
+    B, H, W = 3, 11, 13
+    rows = B * H * W
+    bf = lambda t: t.bfloat16().float()
+    z1 = bf(torch.randn(rows, c, device=DEV) * 2 + 3).requires_grad_(True)
+    z2 = bf(torch.randn(rows, c, device=DEV) - 1).requires_grad_(True)
+    rs = bf(torch.randn(rows, c, device=DEV))
+    g1, b1 = torch.randn(c, device=DEV).requires_grad_(True), torch.randn(c, device=DEV).requires_grad_(True)
+    g2, b2 = torch.randn(c, device=DEV).requires_grad_(True), torch.randn(c, device=DEV).requires_grad_(True)
+    pre = F.batch_norm(z1, None, None, g1, b1, True, 0.1, 1e-5)
+    if two:
+        pre = pre + F.batch_norm(z2, None, None, g2, b2, True, 0.1, 1e-5)
+    y_ref = _act(pre, act) + (rs if res else 0)
+    dy = bf(torch.randn_like(y_ref))
+    y_ref.backward(dy)
+    # statistics as the tapes compute them (f32 over the bf16 maps)
+    mr1, mr2 = torch.empty(2, c, device=DEV), torch.empty(2, c, device=DEV)
+    zb1, zb2, rsb, dyb = (t.detach().bfloat16().contiguous() for t in (z1, z2, rs, dy))
+    for zb, mr in ((zb1, mr1), (zb2, mr2)):
+        parts = torch.zeros(1, 3, c, device=DEV)
+        nb = int(lib.dp_bn_stats_ws_bytes(rows, c))
+        ws = torch.empty(nb // 4, device=DEV)
+        _lib.check(lib.dp_bn_stats(zb.data_ptr(), c, rows, c, parts.data_ptr(), ws.data_ptr(), nb, DP_BF16, _s()), "st")
+        _lib.check(lib.dp_bn_finalize(parts.data_ptr(), 1, float(rows), c, 1e-5, 0.1, None, None, mr.data_ptr(), _s()),
+                   "fin")
+    y = torch.empty(rows, c, device=DEV, dtype=torch.bfloat16)
+    _lib.check(lib.dp_bn_act_fwd(y.data_ptr(), c, zb1.data_ptr(), c, mr1.data_ptr(), g1.detach().data_ptr(),
+                                 b1.detach().data_ptr(), zb2.data_ptr() if two else None, c,
+                                 mr2.data_ptr() if two else None, g2.detach().data_ptr() if two else None,
+                                 b2.detach().data_ptr() if two else None, rsb.data_ptr() if res else None, c, rows, c,
+                                 ACTS[act], DP_BF16, _s()), "bn_act_fwd bf16")
+    sums = torch.empty(3, c, device=DEV)
+    dg1, db1, dg2, db2 = (torch.zeros(c, device=DEV) for _ in range(4))
+    _lib.check(lib.dp_bn_act_bwd_reduce(dyb.data_ptr(), c, zb1.data_ptr(), c, mr1.data_ptr(), g1.detach().data_ptr(),
+                                        b1.detach().data_ptr(), zb2.data_ptr() if two else None, c,
+                                        mr2.data_ptr() if two else None, g2.detach().data_ptr() if two else None,
+                                        b2.detach().data_ptr() if two else None, rows, c, ACTS[act], sums.data_ptr(),
+                                        dg1.data_ptr(), db1.data_ptr(), dg2.data_ptr() if two else None,
+                                        db2.data_ptr() if two else None, DP_BF16, _s()), "reduce bf16")
+    dz1, dz2 = (torch.empty(rows, c, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    _lib.check(lib.dp_bn_act_bwd_apply(dz1.data_ptr(), c, dz2.data_ptr() if two else None, c, dyb.data_ptr(), c,
+                                       zb1.data_ptr(), c, mr1.data_ptr(), g1.detach().data_ptr(), b1.detach().data_ptr(),
+                                       zb2.data_ptr() if two else None, c, mr2.data_ptr() if two else None,
+                                       g2.detach().data_ptr() if two else None, b2.detach().data_ptr() if two else None,
+                                       rows, c, ACTS[act], sums.data_ptr(), float(rows), DP_BF16, _s()), "apply bf16")
+    torch.cuda.synchronize()
+    _close(y, y_ref, f"bn fwd bf16 c{c}", 1e-2)
+    _close(dz1, z1.grad, "dz1 bf16", 1e-2)
+    _close(dg1, g1.grad, "dgamma1 bf16")
+    _close(db1, b1.grad, "dbeta1 bf16")
+    if two:
+        _close(dz2, z2.grad, "dz2 bf16", 1e-2)
+        _close(dg2, g2.grad, "dgamma2 bf16")
+        _close(db2, b2.grad, "dbeta2 bf16")
+
+
 def _conv_desc(x, w_packed, kpad, cin, cout, h, w, k, out, res=None, B=2):
     d = ConvDesc()
     d.in_, d.in_bstride, d.in_pstride, d.in_h, d.in_w, d.cin = x.data_ptr(), h * w * cin, cin, h, w, cin
