@@ -155,6 +155,53 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
   }
 }
 
+// The same over 16-byte column vectors (VC = 8 bf16 / 4 f32 columns per thread): 8x / 4x fewer
+// load instructions than one column per lane.
+template <typename T, int VC>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(const T* __restrict__ x, int64_t ld, int rows, int n,
+                                                         float* __restrict__ out, int rows_per, int cw_log2) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  __shared__ float red[256][VC];
+  const int cw = 1 << cw_log2, nph = 256 >> cw_log2;
+  const int jl = threadIdx.x & (cw - 1), ph = threadIdx.x >> cw_log2;
+  const int nv = n / VC;
+  const int j = blockIdx.x * cw + jl;
+  const int jc = min(j, nv - 1);
+  const int r0 = blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
+  float acc[VC];
+#pragma unroll
+  for (int v = 0; v < VC; ++v) acc[v] = 0.f;
+  for (int r = r0 + ph; r < r1; r += 4 * nph) {
+    u32x4_t u[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      u[q] = *reinterpret_cast<const u32x4_t*>(x + (int64_t)min(r + q * nph, r1 - 1) * ld + (int64_t)jc * VC);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (r + q * nph >= r1) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if constexpr (VC == 8) {
+          acc[2 * e] += __uint_as_float(u[q][e] << 16);
+          acc[2 * e + 1] += __uint_as_float(u[q][e] & 0xffff0000u);
+        } else {
+          acc[e] += __uint_as_float(u[q][e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VC; ++v) red[threadIdx.x][v] = acc[v];
+  __syncthreads();
+  for (int pr = threadIdx.x; pr < cw * VC; pr += 256) {   // (vector, element) pairs of the block
+    const int pl = pr / VC, v = pr - pl * VC, jj = blockIdx.x * cw + pl;
+    if (jj >= nv) continue;
+    float t = 0.f;
+    for (int q = 0; q < nph; ++q) t += red[q * cw + pl][v];
+    unsafeAtomicAdd(out + jj * VC + v, t);
+  }
+}
+
 // ---------------------------------------------------------------- attention core
 // One wave per (sequence, head, 64-row block): lane = a query (forward, dQ) or a key (dK, dV) of
 // the block, so every sequence length keeps the chip busy (the AIFI layer's 400 tokens give 7
@@ -872,6 +919,24 @@ extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, flo
   DP_REQUIRE(x && out && rows > 0 && n > 0 && ld >= n, "dp_colsum: bad arguments");
   hipStream_t st = as_stream(stream);
   if (!accumulate && dp_zero_async(out, (size_t)n * 4, st)) return dp_check_launch("dp_colsum");
+  const int vc = dtype == DP_BF16 ? 8 : 4;
+  if (n % vc == 0 && ld % vc == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const int nv = n / vc;
+    int lg = 0;
+    while ((1 << lg) < nv && lg < 8) ++lg;
+    const int cw = 1 << lg, gx = (nv + cw - 1) / cw, nph = 256 / cw;
+    int chunks = std::max(1, std::min((rows + 4 * nph - 1) / (4 * nph), std::max(1, 1024 / gx)));
+    const int per = (rows + chunks - 1) / chunks;
+    chunks = (rows + per - 1) / per;
+    dim3 grid((unsigned)gx, (unsigned)chunks);
+    if (dtype == DP_BF16)
+      hipLaunchKernelGGL((colsum_vec_kernel<bf16_t, 8>), grid, dim3(256), 0, st, (const bf16_t*)x, ld, rows, n, out,
+                         per, lg);
+    else
+      hipLaunchKernelGGL((colsum_vec_kernel<float, 4>), grid, dim3(256), 0, st, (const float*)x, ld, rows, n, out,
+                         per, lg);
+    return dp_check_launch("dp_colsum");
+  }
   int lg = 0;
   while ((1 << lg) < n && lg < 8) ++lg;
   const int cw = 1 << lg, gx = (n + cw - 1) / cw;

@@ -1,7 +1,8 @@
-// Training attention core on MFMA (bf16, sequences of at most 128 tokens): the decoder's
-// within-instance (18 tokens) and across-instance (60 + DN tokens, with the DN attn_mask)
-// nn.MultiheadAttention cores of the training step (transformer.py:403-419; dn_component.py:
-// 155-167), behind dp_attn_fwd / dp_attn_bwd (train.hip) for dtype bf16. Same interface and
+// Training attention core on MFMA (bf16, sequences of at most 128 tokens, or 400 with 32-wide
+// heads): the decoder's within-instance (18 tokens) and across-instance (60 + DN tokens, with the
+// DN attn_mask) nn.MultiheadAttention cores of the training step (transformer.py:403-419;
+// dn_component.py:155-167) and the encoder's AIFI layer (hybrid_encoder.py:276-279, the 20 x 20
+// map), behind dp_attn_fwd / dp_attn_bwd (train.hip) for dtype bf16. Same interface and
 // saved tensor as the scalar kernels in train.hip: P f32 [pair][key][query].
 //
 // All three kernels run one wave per (sequence, head, 16-row tile) on v_mfma_f32_16x16x32_bf16,
@@ -25,7 +26,9 @@
 
 namespace {
 
-constexpr int WPB = 4;   // waves per block
+// waves per block: 4, or 2 for the 400-token AIFI instantiation (its per-wave LDS slices)
+template <int KT>
+constexpr int wpb_of() { return KT > 8 ? 2 : 4; }
 
 __device__ __forceinline__ int64_t row_base(int pair, int nhead, int n_inner, int64_t so, int64_t si) {
   const int sq = pair / nhead;
@@ -78,9 +81,10 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16_t* __rest
                                                             int64_t si, int64_t st, int L, int nhead, int items,
                                                             float scale) {
   constexpr int KS = (DH + 31) / 32, ND = DH / 16, NK = 16 * KT, VP = NK + 8, NM = (KT + 1) / 2;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[WPB][DH * VP];
+  static_assert(KT % 2 == 0, "tiles are read in pairs: an odd KT would read past a V^T row");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[wpb_of<KT>()][DH * VP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int item = blockIdx.x * WPB + wave;
+  const int item = blockIdx.x * wpb_of<KT>() + wave;
   if (item >= items) return;   // wave-uniform
   const int nqt = (L + 15) / 16;
   const int pair = item / nqt, it = item - pair * nqt;
@@ -176,9 +180,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_mfma_kernel(const bf16_t* __re
                                                               int64_t so, int64_t si, int64_t st, int L, int nhead,
                                                               int items, float scale) {
   constexpr int KS = (DH + 31) / 32, ND = DH / 16, NK = 16 * KT, VP = NK + 8, NM = (KT + 1) / 2;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[WPB][DH * VP];
+  static_assert(KT % 2 == 0, "tiles are read in pairs: an odd KT would read past a V^T row");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[wpb_of<KT>()][DH * VP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int item = blockIdx.x * WPB + wave;
+  const int item = blockIdx.x * wpb_of<KT>() + wave;
   if (item >= items) return;
   const int nqt = (L + 15) / 16;
   const int pair = item / nqt, it = item - pair * nqt;
@@ -254,10 +259,11 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_mfma_kernel(const bf16_t* __r
                                                                int lddkv, int n_inner, int64_t so, int64_t si,
                                                                int64_t st, int L, int nhead, int items, float scale) {
   constexpr int KS = (DH + 31) / 32, ND = DH / 16, NK = 16 * KT, VP = NK + 8, NM = (KT + 1) / 2;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[WPB][2 * DH * VP];
-  __shared__ float Ds[WPB][NK];
+  static_assert(KT % 2 == 0, "tiles are read in pairs: an odd KT would read past a V^T row");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[wpb_of<KT>()][2 * DH * VP];
+  __shared__ float Ds[wpb_of<KT>()][NK];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int item = blockIdx.x * WPB + wave;
+  const int item = blockIdx.x * wpb_of<KT>() + wave;
   if (item >= items) return;
   const int nkt = (L + 15) / 16;
   const int pair = item / nkt, jt = item - pair * nkt;
@@ -347,6 +353,7 @@ void launch_fwd(const bf16_t* q, int ldq, const bf16_t* k, const bf16_t* v, int 
                 const uint8_t* mask, int npairs, int n_inner, int64_t so, int64_t si, int64_t st, int L, int nhead,
                 float scale, hipStream_t s) {
   const int items = npairs * ((L + 15) / 16);
+  constexpr int WPB = wpb_of<KT>();
   hipLaunchKernelGGL((attn_fwd_mfma_kernel<DH, KT>), dim3((items + WPB - 1) / WPB), dim3(64 * WPB), 0, s, q, ldq, k, v,
                      ldkv, out, ldo, ps, mask, n_inner, so, si, st, L, nhead, items, scale);
 }
@@ -357,6 +364,7 @@ void launch_bwd(const bf16_t* q, int ldq, const bf16_t* k, const bf16_t* v, int 
                 int npairs, int n_inner, int64_t so, int64_t si, int64_t st, int L, int nhead, float scale,
                 hipStream_t s) {
   const int items = npairs * ((L + 15) / 16);
+  constexpr int WPB = wpb_of<KT>();
   const dim3 grid((items + WPB - 1) / WPB), block(64 * WPB);
   hipLaunchKernelGGL((attn_bwd_q_mfma_kernel<DH, KT>), grid, block, 0, s, k, v, ldkv, ps, dout, out, ldo, dq, lddq,
                      n_inner, so, si, st, L, nhead, items, scale);
@@ -384,6 +392,10 @@ bool dispatch_kt(int L, bool bwd, const void* const* a, const int64_t* n, float 
   DP_ATT_KT(2)
   DP_ATT_KT(4)
   DP_ATT_KT(8)
+  // AIFI (hybrid_encoder.py:276-279): the 20 x 20 = 400 tokens of the stride-32 map, 32-wide heads
+  if constexpr (DH == 32) {
+    DP_ATT_KT(26)   // even: the PV step reads key tiles in pairs (V^T rows of 16 KT + 8)
+  }
 #undef DP_ATT_KT
   return false;
 }
@@ -395,7 +407,7 @@ bool dispatch_kt(int L, bool bwd, const void* const* a, const int64_t* n, float 
 bool dp_attn_fwd_mfma(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out, int32_t ld_o,
                       float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
                       int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, float scale, hipStream_t s) {
-  if (seqlen > 128) return false;
+  if (seqlen > (dh == 32 ? 400 : 128)) return false;
   const void* a[6] = {q, k, v, out, p_save, mask};
   const int64_t n[9] = {ld_q, ld_kv, ld_o, (int64_t)n_outer * n_inner * nhead, n_inner, so, si, st, nhead};
   switch (dh) {
@@ -411,7 +423,7 @@ bool dp_attn_bwd_mfma(const void* q, int32_t ld_q, const void* k, const void* v,
                       const void* dout, const void* out, int32_t ld_o, void* dq, int32_t ld_dq, void* dk, void* dv,
                       int32_t ld_dkv, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si, int64_t st,
                       int32_t seqlen, int32_t nhead, int32_t dh, float scale, hipStream_t s) {
-  if (seqlen > 128) return false;
+  if (seqlen > (dh == 32 ? 400 : 128)) return false;
   const void* a[9] = {q, k, v, p_save, dout, out, dq, dk, dv};
   const int64_t n[11] = {ld_q, ld_kv, ld_o, ld_dq, (int64_t)n_outer * n_inner * nhead, n_inner, so, si, st, ld_dkv,
                          nhead};

@@ -137,10 +137,12 @@ def test_attention_fwd_bwd(L, dh, masked):
 
 
 @pytest.mark.parametrize("L,dh,masked", [(18, 32, False), (18, 16, False), (60, 32, True), (96, 32, True),
-                                          (101, 32, True), (128, 48, False), (33, 64, True)])
+                                          (101, 32, True), (128, 48, False), (33, 64, True), (400, 32, False),
+                                          (257, 32, True)])
 def test_attention_fwd_bwd_bf16_mfma(L, dh, masked):
     """The bf16 MFMA attention kernels (csrc/train_attn.hip: sequences <= 128 tokens, the decoder's
-    within (18) and across (60 + DN) attentions) against torch fp32 autograd on the same bf16
+    within (18) and across (60 + DN) attentions; <= 400 with 32-wide heads, the AIFI layer's 20 x
+    20 map, 257 ragged) against torch fp32 autograd on the same bf16
     inputs: outputs within 1e-2 and dq / dk / dv within 2e-2 of their scale (bf16 P and dS as MFMA
     operands; measured ~3e-3 / ~6e-3), P saved equal to the softmax within 2e-3."""
     lib = _lib.load()
@@ -241,3 +243,22 @@ def test_pose_refine_and_lqe_bwd():
                                     h * w * c, DP_F32, _s()), "lqe_bwd")
     assert torch.allclose(dkp.cpu(), kpc.grad, atol=1e-3), (dkp.cpu() - kpc.grad).abs().max()
     assert torch.allclose(dfeat.cpu(), featc.grad, atol=1e-5), (dfeat.cpu() - featc.grad).abs().max()
+
+
+@pytest.mark.parametrize("dtype,rows,n,ld,acc", [(DP_BF16, 26112, 256, 256, False), (DP_F32, 26112, 256, 288, True),
+                                                 (DP_BF16, 1000, 72, 80, True), (DP_F32, 777, 34, 34, False),
+                                                 (DP_BF16, 50, 2048, 2048, False)])
+def test_colsum_bias_gradient(dtype, rows, n, ld, acc):
+    """dp_colsum (nn.Linear's bias gradient, db = sum over rows of dy): 16-byte column vectors when
+    n and the row stride allow (8 bf16 / 4 f32 columns per thread), one column per lane otherwise
+    (n = 34); accumulate adds to the existing gradient. Within 1e-5 of sum |dy| per column."""
+    lib = _lib.load()
+    torch.manual_seed(rows + n)
+    td = torch.bfloat16 if dtype == DP_BF16 else torch.float32
+    x = torch.randn(rows, ld, device=DEV).to(td)
+    out = torch.randn(n, device=DEV) if acc else torch.full((n,), 7.0, device=DEV)
+    ref = x[:, :n].double().sum(0) + (out.double() if acc else 0)
+    _lib.check(lib.dp_colsum(x.data_ptr(), ld, rows, n, out.data_ptr(), 1 if acc else 0, dtype, _s()), "colsum")
+    torch.cuda.synchronize()
+    tol = 1e-5 * x[:, :n].double().abs().sum(0) + 1e-6
+    assert ((out.double() - ref).abs() <= tol).all(), float((out.double() - ref).abs().max())
