@@ -4,6 +4,8 @@
 // dp_msda / dp_msda_bwd (msda.hip, msda_train.hip). Reference lines on each entry point in
 // include/detrpose_hip.h. f32 math everywhere; activations / activation gradients of dtype.
 #include <algorithm>
+#include <stdlib.h>
+#include <initializer_list>
 
 #include "common.h"
 
@@ -123,6 +125,135 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(T* __restrict__ dx, const T
     unsafeAtomicAdd(dgamma + j, red[0][0][j] + red[0][1][j] + red[0][2][j] + red[0][3][j]);
     unsafeAtomicAdd(dbeta + j, red[1][0][j] + red[1][1][j] + red[1][2][j] + red[1][3][j]);
   }
+}
+
+// The same two kernels with each lane owning E = c / 64 CONTIGUOUS channels (c = 128 / 256 / 512):
+// one E-element vector load per row and operand instead of E masked 2-byte loads (the strided
+// form above runs its LN_E = 8 slots for every c, half of them masked at c = 256).
+template <typename T, int E>
+__device__ __forceinline__ void ldE(const T* p, float (&v)[E]) {
+  typedef T VT __attribute__((ext_vector_type(E)));
+  const VT u = *reinterpret_cast<const VT*>(p);
+#pragma unroll
+  for (int e = 0; e < E; ++e) v[e] = to_f32(u[e]);
+}
+template <typename T, int E>
+__device__ __forceinline__ void stE(T* p, const float (&v)[E]) {
+  typedef T VT __attribute__((ext_vector_type(E)));
+  VT u;
+#pragma unroll
+  for (int e = 0; e < E; ++e) u[e] = from_f32<T>(v[e]);
+  *reinterpret_cast<VT*>(p) = u;
+}
+
+template <typename T, int E>
+__global__ __launch_bounds__(256) void ln_fwd_vec_kernel(T* __restrict__ y, int ld_y, const T* __restrict__ x,
+                                                         const T* __restrict__ res, T* __restrict__ s,
+                                                         float* __restrict__ stats, const float* __restrict__ g,
+                                                         const float* __restrict__ bt, float eps, int rows,
+                                                         const T* __restrict__ post, int pgroup, int pskip) {
+  constexpr int c = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int j0 = E * lane;
+  float v[E];
+  ldE<T, E>(x + (int64_t)r * c + j0, v);
+  if (res) {
+    float rv[E];
+    ldE<T, E>(res + (int64_t)r * c + j0, rv);
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] += rv[e];
+  }
+  if (s) stE<T, E>(s + (int64_t)r * c + j0, v);
+  float sum = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) sum += v[e];
+  const float mean = wave_sum(sum) / c;
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) q += (v[e] - mean) * (v[e] - mean);
+  const float rstd = rsqrtf(wave_sum(q) / c + eps);
+  if (lane == 0) {
+    stats[2 * (int64_t)r] = mean;
+    stats[2 * (int64_t)r + 1] = rstd;
+  }
+  float pv[E];
+  bool addp = false;
+  if (post) {
+    const int gi = r % pgroup;
+    if (gi >= pskip) {
+      ldE<T, E>(post + ((int64_t)(r / pgroup) * (pgroup - pskip) + gi - pskip) * c + j0, pv);
+      addp = true;
+    }
+  }
+  float o[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) o[e] = (v[e] - mean) * rstd * g[j0 + e] + bt[j0 + e] + (addp ? pv[e] : 0.f);
+  stE<T, E>(y + (int64_t)r * ld_y + j0, o);
+}
+
+template <typename T, int E>
+__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(T* __restrict__ dx, const T* __restrict__ dy, int ld_dy,
+                                                         const T* __restrict__ s, const float* __restrict__ stats,
+                                                         const float* __restrict__ g, int rows,
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta, int acc) {
+  constexpr int c = 64 * E;
+  __shared__ float red[2][4][c];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j0 = E * lane;
+  float gw[E], pg[E], pb[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) gw[e] = g[j0 + e], pg[e] = pb[e] = 0.f;
+  for (int r = blockIdx.x * 4 + wave; r < rows; r += gridDim.x * 4) {
+    const float mean = stats[2 * (int64_t)r], rstd = stats[2 * (int64_t)r + 1];
+    float d[E], xh[E], gy[E];
+    ldE<T, E>(dy + (int64_t)r * ld_dy + j0, d);
+    ldE<T, E>(s + (int64_t)r * c + j0, xh);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xh[e] = (xh[e] - mean) * rstd;
+      gy[e] = d[e] * gw[e];
+      s1 += gy[e];
+      s2 += gy[e] * xh[e];
+      pg[e] += d[e] * xh[e];
+      pb[e] += d[e];
+    }
+    s1 = wave_sum(s1) / c;
+    s2 = wave_sum(s2) / c;
+    float o[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) o[e] = rstd * (gy[e] - s1 - xh[e] * s2);
+    T* p = dx + (int64_t)r * c + j0;
+    if (acc) {
+      float pr[E];
+      ldE<T, E>(p, pr);
+#pragma unroll
+      for (int e = 0; e < E; ++e) o[e] += pr[e];
+    }
+    stE<T, E>(p, o);
+  }
+  if (!dgamma) return;
+#pragma unroll
+  for (int e = 0; e < E; ++e) red[0][wave][j0 + e] = pg[e], red[1][wave][j0 + e] = pb[e];
+  __syncthreads();
+  for (int j = threadIdx.x; j < c; j += 256) {
+    unsafeAtomicAdd(dgamma + j, red[0][0][j] + red[0][1][j] + red[0][2][j] + red[0][3][j]);
+    unsafeAtomicAdd(dbeta + j, red[1][0][j] + red[1][1][j] + red[1][2][j] + red[1][3][j]);
+  }
+}
+
+// E (elements per lane) for the vector forms: c = 64 E, rows and pointers E-element aligned
+inline int ln_vec_e(int c, int esz, std::initializer_list<int64_t> lds, std::initializer_list<const void*> ptrs) {
+  static const bool off = getenv("DETRPOSE_LN_VEC") && atoi(getenv("DETRPOSE_LN_VEC")) == 0;   // A/B
+  const int e = c / 64;
+  if (off || c % 64 || (e != 2 && e != 4 && e != 8)) return 0;
+  for (int64_t l : lds)
+    if (l % e) return 0;
+  for (const void* q : ptrs)
+    if (q && (reinterpret_cast<uintptr_t>(q) % (uintptr_t)(e * esz))) return 0;
+  return e;
 }
 
 // ---------------------------------------------------------------- column sums (bias grads)
@@ -885,6 +1016,19 @@ extern "C" int dp_ln_fwd(void* y, int32_t ld_y, const void* x, const void* res, 
   DP_REQUIRE(c > 0 && c <= 64 * LN_E && rows > 0 && ld_y >= c, "dp_ln_fwd: c=%d rows=%d ld_y=%d", c, rows, ld_y);
   DP_REQUIRE(!post || (post_group > post_skip && post_skip >= 0), "dp_ln_fwd: bad post map");
   hipStream_t st = as_stream(stream);
+  const int esz = dtype == DP_BF16 ? 2 : 4;
+  if (const int e = ln_vec_e(c, esz, {ld_y}, {y, x, res, s, post})) {
+#define LNF(T_, E_)                                                                                              \
+  hipLaunchKernelGGL((ln_fwd_vec_kernel<T_, E_>), dim3(nblk(rows, 4)), dim3(256), 0, st, (T_*)y, ld_y, (const T_*)x, \
+                     (const T_*)res, (T_*)s, stats, gamma, beta, eps, rows, (const T_*)post, post_group, post_skip)
+    if (dtype == DP_BF16) {
+      if (e == 2) LNF(bf16_t, 2); else if (e == 4) LNF(bf16_t, 4); else LNF(bf16_t, 8);
+    } else {
+      if (e == 2) LNF(float, 2); else if (e == 4) LNF(float, 4); else LNF(float, 8);
+    }
+#undef LNF
+    return dp_check_launch("dp_ln_fwd");
+  }
   if (dtype == DP_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(nblk(rows, 4)), dim3(256), 0, st, (bf16_t*)y, ld_y,
                        (const bf16_t*)x, (const bf16_t*)res, (bf16_t*)s, stats, gamma, beta, eps, rows, c,
@@ -905,6 +1049,19 @@ extern "C" int dp_ln_bwd(void* dx, const void* dy, int32_t ld_dy, const void* s,
   int grid = (rows + 3) / 4;
   if (grid > 2048) grid = 2048;
   hipStream_t st = as_stream(stream);
+  const int esz = dtype == DP_BF16 ? 2 : 4;
+  if (const int e = ln_vec_e(c, esz, {ld_dy}, {dx, dy, s})) {
+#define LNB(T_, E_)                                                                                               \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<T_, E_>), dim3(grid), dim3(256), 0, st, (T_*)dx, (const T_*)dy, ld_dy,      \
+                     (const T_*)s, stats, gamma, rows, dgamma, dbeta, accumulate)
+    if (dtype == DP_BF16) {
+      if (e == 2) LNB(bf16_t, 2); else if (e == 4) LNB(bf16_t, 4); else LNB(bf16_t, 8);
+    } else {
+      if (e == 2) LNB(float, 2); else if (e == 4) LNB(float, 4); else LNB(float, 8);
+    }
+#undef LNB
+    return dp_check_launch("dp_ln_bwd");
+  }
   if (dtype == DP_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, (bf16_t*)dx, (const bf16_t*)dy, ld_dy,
                        (const bf16_t*)s, stats, gamma, rows, c, dgamma, dbeta, accumulate);
