@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(T* __restrict__ y, int6
 // xh2, and the parameter gradients dg1 += sum dp xh1, db1 += sum dp (dg2 / db2 likewise)
 template <typename T, bool TWO>
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restrict__ dy, int64_t ldy, BnBranch p1,
-                                                                BnBranch p2, int rows, int c, int act,
+                                                                BnBranch p2, int rows, int c, int act, int per,
                                                                 float* __restrict__ sums, float* __restrict__ dg1,
                                                                 float* __restrict__ db1, float* __restrict__ dg2,
                                                                 float* __restrict__ db2) {
@@ -231,14 +231,14 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restr
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + lane;
   const int chc = min(ch, c - 1);
-  const int r0 = blockIdx.y * 256;
+  const int r0 = blockIdx.y * per;
   const float m1 = p1.mr[chc], s1 = p1.mr[c + chc], g1 = p1.g[chc], b1 = p1.b[chc];
   const float m2 = TWO ? p2.mr[chc] : 0.f, s2 = TWO ? p2.mr[c + chc] : 0.f, g2 = TWO ? p2.g[chc] : 0.f,
               b2 = TWO ? p2.b[chc] : 0.f;
   const T* z1 = reinterpret_cast<const T*>(p1.z) + chc;
   const T* z2 = reinterpret_cast<const T*>(p2.z) + chc;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-  const int r1 = min(r0 + 256, rows);
+  const int r1 = min(r0 + per, rows);
   for (int r = r0 + wv; r < r1; r += 4 * RU) {
     float x1[RU], x2[RU], g[RU];
 #pragma unroll
@@ -739,13 +739,16 @@ extern "C" int dp_bn_act_bwd_reduce(const void* dy, int64_t ld_dy, const void* z
     return DP_EINVAL;
   }
   const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
-  dim3 grid((c + 63) / 64, (rows + 255) / 256);
+  // 256-row slices (capping the block count to shorten the same-address atomic chains, as
+  // dp_colsum / dp_ln_bwd do, measured slower here: too few waves for the row loop)
+  const int cb = (c + 63) / 64, per = 256;
+  dim3 grid(cb, (rows + per - 1) / per);
   if (z2)
     DP_DT(hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, s, (const T*)dy, ld_dy, p1, p2,
-                             rows, c, act, sums, dg1, db1, dg2, db2));
+                             rows, c, act, per, sums, dg1, db1, dg2, db2));
   else
     DP_DT(hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, s, (const T*)dy, ld_dy, p1, p2,
-                             rows, c, act, sums, dg1, db1, dg2, db2));
+                             rows, c, act, per, sums, dg1, db1, dg2, db2));
   return dp_check_launch("dp_bn_act_bwd_reduce");
 }
 

@@ -1046,8 +1046,10 @@ extern "C" int dp_ln_bwd(void* dx, const void* dy, int32_t ld_dy, const void* s,
   DP_REQUIRE(dx && dy && s && stats && gamma, "dp_ln_bwd: null pointer");
   DP_REQUIRE(c > 0 && c <= 64 * LN_E && rows > 0 && ld_dy >= c, "dp_ln_bwd: c=%d rows=%d", c, rows);
   DP_REQUIRE((dgamma == nullptr) == (dbeta == nullptr), "dp_ln_bwd: dgamma / dbeta both or neither");
+  // every block adds its dgamma / dbeta partials with one atomic per column: 256 blocks (one per
+  // CU) keep the same-address atomic chains short (2048 blocks cost ~2x the kernel)
   int grid = (rows + 3) / 4;
-  if (grid > 2048) grid = 2048;
+  if (grid > 256) grid = 256;
   hipStream_t st = as_stream(stream);
   const int esz = dtype == DP_BF16 ? 2 : 4;
   if (const int e = ln_vec_e(c, esz, {ld_dy}, {dx, dy, s})) {
@@ -1082,7 +1084,7 @@ extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, flo
     int lg = 0;
     while ((1 << lg) < nv && lg < 8) ++lg;
     const int cw = 1 << lg, gx = (nv + cw - 1) / cw, nph = 256 / cw;
-    int chunks = std::max(1, std::min((rows + 4 * nph - 1) / (4 * nph), std::max(1, 1024 / gx)));
+    int chunks = std::max(1, std::min((rows + 4 * nph - 1) / (4 * nph), std::max(1, 256 / gx)));   // one block per CU: each column takes <= 256 atomics
     const int per = (rows + chunks - 1) / chunks;
     chunks = (rows + per - 1) / per;
     dim3 grid((unsigned)gx, (unsigned)chunks);
@@ -1099,7 +1101,7 @@ extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, flo
   const int cw = 1 << lg, gx = (n + cw - 1) / cw;
   // about 1024 blocks, each at least 8 row steps of its phases
   const int nph = 256 / cw;
-  int chunks = std::max(1, std::min((rows + 8 * nph - 1) / (8 * nph), std::max(1, 1024 / gx)));
+  int chunks = std::max(1, std::min((rows + 8 * nph - 1) / (8 * nph), std::max(1, 256 / gx)));   // <= 256 atomics per column
   const int per = (rows + chunks - 1) / chunks;
   chunks = (rows + per - 1) / per;
   dim3 grid((unsigned)gx, (unsigned)chunks);
