@@ -555,6 +555,7 @@ void dw_bwd_launch(const void* x, int64_t xbs, int xps, const void* dz, int64_t 
   if (dw) {
     const int ntiles = batch * oh * ((ow + DW_TW - 1) / DW_TW);
     // about 4 tiles per thread: enough waves to fill the chip, the atomics a small fraction
+    // (capping the row blocks at 64 / 32 to shorten the atomic chains measured 1.4x / 2.1x slower)
     const unsigned gy = (unsigned)std::max(1, std::min((ntiles + 15) / 16, 65535));
     hipLaunchKernelGGL((dw_bwd_weight_kernel<T, K, S, VC>), dim3(gx, gy), dim3(64, 4), 0, s, (const T*)x, xbs, xps,
                        (const T*)dz, zbs, zps, h, w, c, pad, oh, ow, ntiles, dw);
