@@ -7,6 +7,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -95,6 +96,85 @@ __global__ __launch_bounds__(256) void frozen_act_bwd_kernel(const T* __restrict
   if (threadIdx.x == 0) {
     atomicAdd(dlab_a, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
     atomicAdd(dlab_b, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+// 16-byte vectors of channels: 8 bf16 or 4 f32 (VC), or one element (VC = 1)
+template <typename T, int VC>
+__device__ __forceinline__ void ld16v(const T* p, float (&v)[VC]) {
+  if constexpr (VC == 1) {
+    v[0] = ldf(p);
+  } else {
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t u = *reinterpret_cast<const u32x4_t*>(p);
+    if constexpr (VC == 8) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[2 * q] = __uint_as_float(u[q] << 16), v[2 * q + 1] = __uint_as_float(u[q] & 0xffff0000u);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = __uint_as_float(u[q]);
+    }
+  }
+}
+template <typename T, int VC>
+__device__ __forceinline__ void st16v(T* p, const float (&v)[VC]) {
+  if constexpr (VC == 1) {
+    *p = from_f32<T>(v[0]);
+  } else if constexpr (VC == 8) {
+    bf16x8 r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = (bf16_t)v[e];
+    *reinterpret_cast<bf16x8*>(p) = r;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// The bf16 non-LAB case (every DETRPose-L / X backbone conv) over 16-byte channel vectors: a
+// thread owns 8 channels of RU rows; a block = (256 / cw) rows x cw chunks (cw = c / 8 rounded
+// up to a power of two).
+template <bool RELU, bool RES>
+__global__ __launch_bounds__(256) void frozen_act_bwd_vec_kernel(const bf16_t* __restrict__ y, int64_t ldy,
+                                                                 const bf16_t* __restrict__ res, int64_t ldr,
+                                                                 const bf16_t* __restrict__ dy, int64_t lddy,
+                                                                 bf16_t* __restrict__ dz, int64_t lddz, int rows, int c,
+                                                                 int cw_log2, const float* __restrict__ scale) {
+  constexpr int RU = 4;
+  const int cw = 1 << cw_log2, rpb = 256 >> cw_log2;
+  const int ck = blockIdx.y * cw + (threadIdx.x & (cw - 1));
+  const int rsub = threadIdx.x >> cw_log2;
+  if (ck * 8 >= c) return;
+  const int ch = ck * 8;
+  constexpr float eps = 3.90625e-3f;   // bf16 rounding of the stored output (see above)
+  float sc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sc[e] = scale ? scale[ch + e] : 1.f;
+  const int step = gridDim.x * rpb * RU;
+  for (int r0 = blockIdx.x * rpb * RU + rsub; r0 < rows; r0 += step) {
+    float g[RU][8], yv[RU][8], rv[RU][8];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t r = min(r0 + u * rpb, rows - 1);
+      ld16v<bf16_t, 8>(dy + r * lddy + ch, g[u]);
+      if (RELU) ld16v<bf16_t, 8>(y + r * ldy + ch, yv[u]);
+      if (RES) ld16v<bf16_t, 8>(res + r * ldr + ch, rv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      if (r0 + u * rpb >= rows) continue;
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        d[e] = g[u][e];
+        if (RELU) {
+          const float v = yv[u][e] - (RES ? rv[u][e] : 0.f);
+          const float tol = RES ? eps * (fabsf(yv[u][e]) + fabsf(rv[u][e])) : 0.f;
+          d[e] = v > tol ? g[u][e] : 0.f;
+        }
+        d[e] *= sc[e];
+      }
+      st16v<bf16_t, 8>(dz + (int64_t)(r0 + u * rpb) * lddz + ch, d);
+    }
   }
 }
 
@@ -205,37 +285,6 @@ __global__ __launch_bounds__(256) void col2im_vec_kernel(const T* __restrict__ c
 // F.pad(x, (0,1,0,1)) + MaxPool2d(2, 1, ceil_mode=True) backward (hgnetv2.py:215, 217): each
 // output's gradient goes to its window's first maximum in scan order (max_pool2d's argmax, the
 // pad zeros included: a pad maximum takes the gradient out of the map); gathered per input.
-// 16-byte vectors of channels: 8 bf16 or 4 f32 (VC), or one element (VC = 1)
-template <typename T, int VC>
-__device__ __forceinline__ void ld16v(const T* p, float (&v)[VC]) {
-  if constexpr (VC == 1) {
-    v[0] = ldf(p);
-  } else {
-    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-    const u32x4_t u = *reinterpret_cast<const u32x4_t*>(p);
-    if constexpr (VC == 8) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[2 * q] = __uint_as_float(u[q] << 16), v[2 * q + 1] = __uint_as_float(u[q] & 0xffff0000u);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = __uint_as_float(u[q]);
-    }
-  }
-}
-template <typename T, int VC>
-__device__ __forceinline__ void st16v(T* p, const float (&v)[VC]) {
-  if constexpr (VC == 1) {
-    *p = from_f32<T>(v[0]);
-  } else if constexpr (VC == 8) {
-    bf16x8 r;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) r[e] = (bf16_t)v[e];
-    *reinterpret_cast<bf16x8*>(p) = r;
-  } else {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-
 // VC channels per thread (16-byte vectors when the rows allow: 8x fewer load instructions);
 // I32: total / VC < 2^31, the index split in 32-bit unsigned arithmetic
 template <typename T, bool I32, int VC>
@@ -337,6 +386,25 @@ extern "C" int dp_frozen_act_bwd(const void* y, int64_t ld_y, const void* res, i
   const int gx = std::max(1, std::min((rows + rpb * 4 - 1) / (rpb * 4), std::max(1, 4096 / gy)));
   const bool relu = act == DP_ACT_RELU, hres = relu && res, lab = lab_a != nullptr;
   hipStream_t s = as_stream(stream);
+  auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  static const bool vec_off = getenv("DETRPOSE_FAB_VEC") && atoi(getenv("DETRPOSE_FAB_VEC")) == 0;   // A/B
+  if (!vec_off && dtype == DP_BF16 && !lab && c % 8 == 0 && ld_dy % 8 == 0 && ld_dz % 8 == 0 &&
+      (!relu || ld_y % 8 == 0) && (!hres || ld_res % 8 == 0) && a16(dy) && a16(dz) && a16(relu ? y : nullptr) &&
+      a16(hres ? res : nullptr)) {
+    const int nck = c / 8;
+    int lv = 0;
+    while ((1 << lv) < nck && lv < 8) ++lv;
+    const int cwv = 1 << lv, rpv = 256 / cwv, gyv = (nck + cwv - 1) / cwv;
+    const int gxv = std::max(1, std::min((rows + rpv * 4 - 1) / (rpv * 4), std::max(1, 4096 / gyv)));
+#define FABV(R_, S_)                                                                                           \
+  hipLaunchKernelGGL((frozen_act_bwd_vec_kernel<R_, S_>), dim3(gxv, gyv), dim3(256), 0, s, (const bf16_t*)y, ld_y, \
+                     (const bf16_t*)res, ld_res, (const bf16_t*)dy, ld_dy, (bf16_t*)dz, ld_dz, rows, c, lv, scale)
+    if (!relu) FABV(false, false);
+    else if (!hres) FABV(true, false);
+    else FABV(true, true);
+#undef FABV
+    return dp_check_launch("dp_frozen_act_bwd");
+  }
 #define FAB(T_, R_, S_, L_)                                                                                      \
   hipLaunchKernelGGL((frozen_act_bwd_kernel<T_, R_, S_, L_>), dim3(gx, gy), dim3(256), 0, s, (const T_*)y, ld_y, \
                      (const T_*)res, ld_res, (const T_*)dy, ld_dy, (T_*)dz, ld_dz, rows, c, lg, lab_a, lab_b, scale, \

@@ -28,8 +28,11 @@ def _close(got, ref, what, tol=2e-4):
     assert err <= tol * scale, (what, err, scale)
 
 
-@pytest.mark.parametrize("lab,dtype", [(False, DP_F32), (True, DP_F32), (True, DP_BF16)])
-def test_frozen_act_bwd(lab, dtype):
+@pytest.mark.parametrize("lab,dtype,bres", [(False, DP_F32, False), (True, DP_F32, False), (True, DP_BF16, False),
+                                           (False, DP_BF16, False), (False, DP_BF16, True)])
+def test_frozen_act_bwd(lab, dtype, bres):
+    """FrozenBatchNorm2d + ReLU (+ LAB, + the HG block's identity) backward; bf16 without LAB runs
+    the 16-byte channel-vector kernel."""
     lib = _lib.load()
     torch.manual_seed(5)
     rows, c = 3000, 48
@@ -46,8 +49,9 @@ def test_frozen_act_bwd(lab, dtype):
     dz = torch.empty(rows, c, device=DEV, dtype=td)
     dl = torch.zeros(2, device=DEV)
     res = torch.randn(rows, c, device=DEV).to(td)   # an HG-block identity added after the act
-    yd = (yd.float() + res.float()).to(td) if dtype == DP_F32 else yd
-    _lib.check(lib.dp_frozen_act_bwd(yd.data_ptr(), c, res.data_ptr() if dtype == DP_F32 else None, c, dyd.data_ptr(),
+    use_res = dtype == DP_F32 or bres
+    yd = (yd.float() + res.float()).to(td) if use_res else yd
+    _lib.check(lib.dp_frozen_act_bwd(yd.data_ptr(), c, res.data_ptr() if use_res else None, c, dyd.data_ptr(),
                                      c, dz.data_ptr(), c, rows, c, _lib.DP_ACT_RELU,
                                      a.detach().data_ptr() if lab else None, cb.detach().data_ptr() if lab else None,
                                      s.data_ptr(), dl.data_ptr() if lab else None, dl.data_ptr() + 4 if lab else None,
@@ -62,11 +66,13 @@ def test_frozen_act_bwd(lab, dtype):
     else:
         # bf16 storage of y = a r + cb cannot tell r > 0 from r == 0 within cb's rounding: the
         # ReLU mask may differ only there (|u| within a few bf16 ulps of cb / a)
+        # (with the identity added: within y + res's rounding, a few bf16 ulps of |res|)
         err = (dz.float() - want).abs()
         bad = err > 1e-2 * float(want.abs().max())
-        print(f"bf16 LAB: {int(bad.sum())} of {bad.numel()} differ, max |u| there "
+        print(f"bf16 lab={lab} res={bres}: {int(bad.sum())} of {bad.numel()} differ, max |u| there "
               f"{float(u.detach().abs()[bad].max()) if bad.any() else 0.0:.3g}")
-        assert bad.float().mean() < 1e-2 and (not bad.any() or float(u.detach().abs()[bad].max()) < 0.01)
+        umax = 0.05 if bres else 0.01
+        assert bad.float().mean() < 1e-2 and (not bad.any() or float(u.detach().abs()[bad].max()) < umax)
     if lab:
         _close(dl[0], a.grad[0], "d lab.scale", 1e-4 if dtype == DP_F32 else 2e-2)
         _close(dl[1], cb.grad[0], "d lab.bias", 1e-4 if dtype == DP_F32 else 2e-2)
