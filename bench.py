@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline-seconds", type=float, default=25.0, help="cap on the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-gemm-peak", action="store_true", help="skip the measured bf16 GEMM peak (BASELINE.md's "
+                    "denominator of the end-to-end MFMA fraction)")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step leg (BASELINE configs[4])")
     ap.add_argument("--train-batch", type=int, default=16, help="images per GPU of the training-step leg")
@@ -374,6 +376,30 @@ def train_leg(size, dtype, dev, batch, steps, warmup=3, rank=0, world=1):
     return out
 
 
+def gemm_peak(dev, n=8192, reps=20):
+    """BASELINE.md's denominator for the end-to-end MFMA fraction: the bf16 GEMM rate this GPU
+    reaches on a large square product (torch.matmul = hipBLASLt, n^3, median of reps launches
+    timed with HIP events, after warm-up). Timed outside the benchmark's region."""
+    torch.manual_seed(0)
+    x = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    y = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    for _ in range(5):
+        torch.matmul(x, y)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.matmul(x, y)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ms = statistics.median(ts)
+    del x, y
+    return {"tflops": round(2.0 * n ** 3 / (ms * 1e-3) / 1e12, 1), "shape": f"{n}x{n}x{n} bf16",
+            "how": "torch.matmul (hipBLASLt), median of %d launches, HIP events" % reps}
+
+
 def latency_bs1(model, pp, dev, runs, warmup):
     """tools/benchmark/torch_benchmark.py:29-51 on the HIP path: Model(images, sizes) at
     batch 1 (one hipGraph replay incl. the input copy), synchronised around every call."""
@@ -547,6 +573,7 @@ def main():
             "outputs_finite": finite,
             "roofline": roofline,
             "e2e_mfma_frac": round(value / world * gflop * 1e9 / (peak * 1e12), 4),
+            "gflop_per_image": gflop,
             "kernel_ms_per_step": {k: round(v, 3) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])},
             "msda_algorithmic_gbs": round(msda_gbs, 1) if msda_gbs else None,
         }
@@ -557,6 +584,12 @@ def main():
         if a.shared_gpu_rehearsal:
             out["rehearsal"] = (f"{world} ranks sharing one GPU, gloo collectives with host staging: checks the "
                                 "N-rank launch/barrier/gather path on real kernels; not a scaling number")
+        if not a.no_gemm_peak:
+            # "achieved fraction of the MFMA roofline, computed as img/s x GFLOP/img /
+            # measured peak bf16 GEMM FLOP/s" (per GPU)
+            gp = gemm_peak(dev)
+            out["gemm_peak_measured"] = gp
+            out["e2e_frac_of_measured_gemm_peak"] = round(value / world * gflop * 1e9 / (gp["tflops"] * 1e12), 4)
         if world == 1 and not a.no_latency:
             out["latency_bs1"] = latency_bs1(model, pp, dev, a.latency_runs, a.latency_warmup)
         if world == 1 and not a.no_secondary:

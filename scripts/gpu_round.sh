@@ -18,12 +18,12 @@ if [ "$SKIP_TESTS" != 1 ]; then
 fi
 timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-PB="--steps 10 --warmup 3 --no-cpu-baseline --no-latency --no-secondary --no-train"
+PB="--steps 10 --warmup 3 --no-cpu-baseline --no-latency --no-secondary --no-train --no-gemm-peak"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
   python3 bench.py $PB --profile-ops $OUT/ops.json > $OUT/prof_bench.json 2> $OUT/prof.err \
   || { tail -20 $OUT/prof.err; exit 1; }
 if [ "${SKIP_PMC:-0}" != 1 ]; then
-  PP="--steps 2 --warmup 1 --no-cpu-baseline --no-latency --no-secondary --no-train"
+  PP="--steps 2 --warmup 1 --no-cpu-baseline --no-latency --no-secondary --no-train --no-gemm-peak"
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- \
     python3 bench.py $PP > /dev/null 2> $OUT/pmc_fetch.err
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- \
