@@ -159,7 +159,8 @@ _SIGS = {
     "dp_bn_finalize": (i32, [vp, i32, f32, i32, f32, f32, vp, vp, vp, vp]),
     "dp_bn_act_fwd": (i32, [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
     "dp_bn_act_bwd_reduce": (i32, [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp,
-                                   vp, i32, vp]),
+                                   vp, vp, i64, i32, vp]),
+    "dp_bn_act_bwd_reduce_ws_bytes": (i64, [i32, i32]),
     "dp_bn_act_bwd_apply": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32,
                                   vp, f32, i32, vp]),
     "dp_im2col": (i32, [vp, i64, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp]),

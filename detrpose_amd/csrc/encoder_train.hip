@@ -219,14 +219,12 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(T* __restrict__ y, int6
   }
 }
 
-// dp = dy * act'(pre): column sums sums[0] += sum dp, sums[1] += sum dp xh1, sums[2] += sum dp
-// xh2, and the parameter gradients dg1 += sum dp xh1, db1 += sum dp (dg2 / db2 likewise)
+// dp = dy * act'(pre): per row slice y the column sums part[y] = (sum dp, sum dp xh1, sum dp xh2)
+// (no float atomics: bn_act_bwd_sum_kernel adds the slices in a fixed order)
 template <typename T, bool TWO>
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restrict__ dy, int64_t ldy, BnBranch p1,
                                                                 BnBranch p2, int rows, int c, int act, int per,
-                                                                float* __restrict__ sums, float* __restrict__ dg1,
-                                                                float* __restrict__ db1, float* __restrict__ dg2,
-                                                                float* __restrict__ db2) {
+                                                                float* __restrict__ part) {
   __shared__ float red[3][4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + lane;
@@ -264,16 +262,46 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restr
   red[2][wv][lane] = a2;
   __syncthreads();
   if (wv == 0 && ch < c) {
-    const float t0 = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
-    const float t1 = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
-    const float t2 = red[2][0][lane] + red[2][1][lane] + red[2][2][lane] + red[2][3][lane];
-    atomicAdd(sums + ch, t0);
-    atomicAdd(sums + c + ch, t1);
-    atomicAdd(sums + 2 * c + ch, t2);
-    if (dg1) atomicAdd(dg1 + ch, t1);
-    if (db1) atomicAdd(db1 + ch, t0);
-    if (dg2) atomicAdd(dg2 + ch, t2);
-    if (db2) atomicAdd(db2 + ch, t0);
+    float* pp = part + (int64_t)blockIdx.y * 3 * c;
+    pp[ch] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+    pp[c + ch] = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+    pp[2 * c + ch] = red[2][0][lane] + red[2][1][lane] + red[2][2][lane] + red[2][3][lane];
+  }
+}
+
+// sums [3][c] = the slices' sums in a fixed order (wave w of 16 takes slices w, w + 16, ...), and
+// the parameter gradients from them: dg1 += sums[1], db1 += sums[0], dg2 += sums[2], db2 += sums[0]
+__global__ __launch_bounds__(1024) void bn_act_bwd_sum_kernel(const float* __restrict__ part, int ny, int c,
+                                                              float* __restrict__ sums, float* __restrict__ dg1,
+                                                              float* __restrict__ db1, float* __restrict__ dg2,
+                                                              float* __restrict__ db2) {
+  constexpr int NWV = 16;
+  __shared__ float red[3][NWV][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane;
+  const int chc = min(ch, c - 1);
+  float t[3] = {0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int y = wv; y < ny; y += NWV) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] += part[((int64_t)y * 3 + k) * c + chc];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) red[k][wv][lane] = t[k];
+  __syncthreads();
+  if (wv == 0 && ch < c) {
+    float u[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) u[k] += red[k][w][lane];
+    sums[ch] = u[0];
+    sums[c + ch] = u[1];
+    sums[2 * c + ch] = u[2];
+    if (dg1) dg1[ch] += u[1];
+    if (db1) db1[ch] += u[0];
+    if (dg2) dg2[ch] += u[2];
+    if (db2) db2[ch] += u[0];
   }
 }
 
@@ -727,29 +755,33 @@ extern "C" int dp_bn_act_fwd(void* y, int64_t ld_y, const void* z1, int64_t ld1,
   return dp_check_launch("dp_bn_act_fwd");
 }
 
+extern "C" int64_t dp_bn_act_bwd_reduce_ws_bytes(int32_t rows, int32_t c) {
+  if (rows <= 0 || c <= 0) return -1;
+  return (int64_t)((rows + 255) / 256) * 3 * c * (int64_t)sizeof(float);
+}
+
 extern "C" int dp_bn_act_bwd_reduce(const void* dy, int64_t ld_dy, const void* z1, int64_t ld1, const float* mr1,
                                     const float* g1, const float* b1, const void* z2, int64_t ld2, const float* mr2,
                                     const float* g2, const float* b2, int32_t rows, int32_t c, int32_t act,
-                                    float* sums, float* dg1, float* db1, float* dg2, float* db2, int32_t dtype,
-                                    void* stream) {
-  DP_REQUIRE(dy && z1 && mr1 && g1 && b1 && sums && rows > 0 && c > 0 && (!z2 || (mr2 && g2 && b2)),
+                                    float* sums, float* dg1, float* db1, float* dg2, float* db2, float* ws,
+                                    int64_t ws_bytes, int32_t dtype, void* stream) {
+  DP_REQUIRE(dy && z1 && mr1 && g1 && b1 && sums && ws && rows > 0 && c > 0 && (!z2 || (mr2 && g2 && b2)),
              "dp_bn_act_bwd_reduce: bad arguments");
+  DP_REQUIRE(ws_bytes >= dp_bn_act_bwd_reduce_ws_bytes(rows, c), "dp_bn_act_bwd_reduce: workspace of %lld bytes < %lld",
+             (long long)ws_bytes, (long long)dp_bn_act_bwd_reduce_ws_bytes(rows, c));
   hipStream_t s = as_stream(stream);
-  if (dp_zero_async(sums, 3 * (size_t)c * sizeof(float), s)) {
-    dp_set_error("dp_bn_act_bwd_reduce: memset failed");
-    return DP_EINVAL;
-  }
   const BnBranch p1{z1, ld1, mr1, g1, b1}, p2{z2, ld2, mr2, g2, b2};
-  // 256-row slices (capping the block count to shorten the same-address atomic chains, as
-  // dp_colsum / dp_ln_bwd do, measured slower here: too few waves for the row loop)
-  const int cb = (c + 63) / 64, per = 256;
-  dim3 grid(cb, (rows + per - 1) / per);
+  // 256-row slices into the workspace, then one fixed-order pass over them (no float atomics:
+  // the same sums on every run; capping the slices instead measured slower)
+  const int cb = (c + 63) / 64, per = 256, ny = (rows + per - 1) / per;
+  dim3 grid(cb, ny);
   if (z2)
     DP_DT(hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, s, (const T*)dy, ld_dy, p1, p2,
-                             rows, c, act, per, sums, dg1, db1, dg2, db2));
+                             rows, c, act, per, ws));
   else
     DP_DT(hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, s, (const T*)dy, ld_dy, p1, p2,
-                             rows, c, act, per, sums, dg1, db1, dg2, db2));
+                             rows, c, act, per, ws));
+  hipLaunchKernelGGL(bn_act_bwd_sum_kernel, dim3(cb), dim3(1024), 0, s, ws, ny, c, sums, dg1, db1, dg2, db2);
   return dp_check_launch("dp_bn_act_bwd_reduce");
 }
 

@@ -373,10 +373,11 @@ class TapePlan:
             if res is not None:   # the CSP sum: d res += d out
                 bw.op(name + ".dres", lib.dp_axpby_rows, res.gp, res.ld, out.gp, out.ld, C.c_float(1.0), N, 0,
                       C.c_float(0.0), rows, c, 1, code)
+            rws = self.f32(max(int(lib.dp_bn_act_bwd_reduce_ws_bytes(rows, c)), 4) // 4)   # per-slice partials
             bw.op(name + ".bn_reduce", lib.dp_bn_act_bwd_reduce, out.gp, out.ld, z1.xp, z1.ld, _p(mr1), _p(g1), _p(b1),
                   z2.xp if two else N, z2.ld if two else 0, _p(mr2) if two else N, _p(g2) if two else N,
                   _p(b2) if two else N, rows, c, ACT[act], _p(sums), _p(dg1), _p(db1), _p(dg2) if two else N,
-                  _p(db2) if two else N, code)
+                  _p(db2) if two else N, _p(rws), rws.numel() * 4, code)
             if self.world > 1:
                 bw.op(name + ".bn_sync", _host(lambda: all_reduce(sums)))
             bw.op(name + ".bn_apply", lib.dp_bn_act_bwd_apply, z1.gp, z1.ld, z2.gp if two else N, z2.ld if two else 0,

@@ -605,13 +605,17 @@ int dp_bn_act_fwd(void* y, int64_t ld_y, const void* z1, int64_t ld1, const floa
                   const float* b1, const void* z2, int64_t ld2, const float* mr2, const float* g2, const float* b2,
                   const void* res, int64_t ld_res, int32_t rows, int32_t c, int32_t act, int32_t dtype, void* stream);
 /* Its backward, first pass: dp = dy * act'(pre) (pre recomputed from z / statistics); sums [3][c] =
- * (sum dp, sum dp xhat1, sum dp xhat2) over this rank's rows (zeroed here; all-reduce them for
+ * (sum dp, sum dp xhat1, sum dp xhat2) over this rank's rows (overwritten; all-reduce them for
  * SyncBN before the second pass) and, from the LOCAL sums, dg_k += sum dp xhat_k, db_k += sum dp
- * (NULL to skip). */
+ * (NULL to skip). Per-256-row partials in ws (dp_bn_act_bwd_reduce_ws_bytes), summed in a fixed
+ * order: the same result on every run. */
 int dp_bn_act_bwd_reduce(const void* dy, int64_t ld_dy, const void* z1, int64_t ld1, const float* mr1,
                          const float* g1, const float* b1, const void* z2, int64_t ld2, const float* mr2,
                          const float* g2, const float* b2, int32_t rows, int32_t c, int32_t act, float* sums,
-                         float* dg1, float* db1, float* dg2, float* db2, int32_t dtype, void* stream);
+                         float* dg1, float* db1, float* dg2, float* db2, float* ws, int64_t ws_bytes, int32_t dtype,
+                         void* stream);
+/* Per-256-row-slice partials of dp_bn_act_bwd_reduce (summed in a fixed order: no float atomics). */
+int64_t dp_bn_act_bwd_reduce_ws_bytes(int32_t rows, int32_t c);
 /* Second pass: dz_k = g_k rstd_k (dp - sum dp / count - xhat_k sum (dp xhat_k) / count), count =
  * the rows of all ranks (batch_norm_backward_elemt). */
 int dp_bn_act_bwd_apply(void* dz1, int64_t ld_dz1, void* dz2, int64_t ld_dz2, const void* dy, int64_t ld_dy,

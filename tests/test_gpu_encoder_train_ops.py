@@ -34,6 +34,16 @@ def _act(x, a):
     return {"silu": F.silu, "relu": F.relu, None: lambda t: t}[a](x)
 
 
+_RWS = []
+
+
+def _rws(lib, rows, c):
+    """A workspace for dp_bn_act_bwd_reduce's per-slice partials (kept alive past the launch)."""
+    t = torch.empty(int(lib.dp_bn_act_bwd_reduce_ws_bytes(rows, c)) // 4, device=DEV)
+    _RWS.append(t)
+    return t
+
+
 def bn_stats(lib, z, count_parts=1):
     """per-part dp_bn_stats over row splits, then dp_bn_finalize: (mean_rstd, parts)."""
     rows, c = z.shape
@@ -95,7 +105,8 @@ def test_bn_act_train_forward_backward(two, act, nparts):
                                         g2.detach().data_ptr() if two else None,
                                         b2.detach().data_ptr() if two else None, rows, c, ACTS[act], sums.data_ptr(),
                                         dg1.data_ptr(), db1.data_ptr(), dg2.data_ptr() if two else None,
-                                        db2.data_ptr() if two else None, DP_F32, _s()), "bn_bwd_reduce")
+                                        db2.data_ptr() if two else None, _rws(lib, rows, c).data_ptr(),
+                                        int(lib.dp_bn_act_bwd_reduce_ws_bytes(rows, c)), DP_F32, _s()), "bn_bwd_reduce")
     dz1, dz2 = torch.empty(rows, c, device=DEV), torch.empty(rows, c, device=DEV)
     _lib.check(lib.dp_bn_act_bwd_apply(dz1.data_ptr(), c, dz2.data_ptr() if two else None, c, dy.data_ptr(), c,
                                        z1.detach().data_ptr(), c, mr1.data_ptr(), g1.detach().data_ptr(),
@@ -160,7 +171,8 @@ def test_bn_act_bf16_rows(two, act, c, res):
                                         mr2.data_ptr() if two else None, g2.detach().data_ptr() if two else None,
                                         b2.detach().data_ptr() if two else None, rows, c, ACTS[act], sums.data_ptr(),
                                         dg1.data_ptr(), db1.data_ptr(), dg2.data_ptr() if two else None,
-                                        db2.data_ptr() if two else None, DP_BF16, _s()), "reduce bf16")
+                                        db2.data_ptr() if two else None, _rws(lib, rows, c).data_ptr(),
+                                        int(lib.dp_bn_act_bwd_reduce_ws_bytes(rows, c)), DP_BF16, _s()), "reduce bf16")
     dz1, dz2 = (torch.empty(rows, c, device=DEV, dtype=torch.bfloat16) for _ in range(2))
     _lib.check(lib.dp_bn_act_bwd_apply(dz1.data_ptr(), c, dz2.data_ptr() if two else None, c, dyb.data_ptr(), c,
                                        zb1.data_ptr(), c, mr1.data_ptr(), g1.detach().data_ptr(), b1.detach().data_ptr(),
