@@ -478,6 +478,11 @@ extern "C" int dp_dwconv2d(const dp_conv_desc* dp, void* stream) {
   hipStream_t s = as_stream(stream);
   static const bool no_lds = getenv("DETRPOSE_DW_NO_LDS") != nullptr;
   if (d.dtype == DP_BF16 && d.cin % 64 == 0 && !no_lds) {
+    // maps at most 20 wide (HGNetv2 stage 4's 20x20 5x5s): one 4 x 20 tile per block, 4 outputs
+    // per thread (86 VGPRs, 31 KB LDS: 5 blocks per CU) measured 22.5 vs 26.6 us for the
+    // persistent 8 x 20 form at L b64; the 40x40 maps keep the persistent form (35.4 vs 38.0),
+    // profiles/r5_dw5_ab.txt
+    if (d.kh == 5 && d.kw == 5 && d.stride == 1 && d.out_w <= 20) return launch_dw_tile<5, 1, 4, 20, 4>(d, s);
     if (d.kh == 5 && d.kw == 5 && d.stride == 1) return launch_dw_lds<5, 1, DP_DW5_TH, 20, 5, true>(d, s);
     if (d.kh == 3 && d.kw == 3 && d.stride == 1) return launch_dw_lds<3, 1, 8, 20, 5, true>(d, s);
     if (d.kh == 3 && d.kw == 3 && d.stride == 2) return launch_dw_tile<3, 2, DP_DWS2_TH, 16, 2>(d, s);

@@ -279,6 +279,24 @@ def test_dwconv_model_shapes(k, s, c, hw):
     _close(out, ref.permute(0, 2, 3, 1), "bf16", f"dw{k}s{s}c{c}")
 
 
+@pytest.mark.parametrize("h,w,c", [(37, 23, 128), (50, 19, 64), (9, 40, 192), (41, 40, 64), (3, 7, 64)])
+def test_dwconv5_ragged(h, w, c):
+    """Both bf16 5x5 paths on ragged rectangles: maps at most 20 wide (one 4 x 20 tile per block,
+    4 outputs per thread: 50x19, 3x7) and wider ones (persistent 8 x 20 tiles: 37x23, 9x40,
+    41x40): partial tiles in both directions, fewer rows than one tile."""
+    torch.manual_seed(h * w)
+    pk = Packer({}, "bf16", torch.device("cuda"))
+    x = torch.randn(2, c, h, w).bfloat16().float()
+    wt = torch.randn(c, 1, 5, 5) / 5
+    b = torch.randn(c) * 0.1
+    pc = pk.dwconv(wt.double(), b.double(), 1, act="relu")
+    ref = F.relu(F.conv2d(x, wt, b, 1, 2, groups=c))
+    out = torch.full((2, h, w, c), 7.0, device="cuda", dtype=torch.bfloat16)
+    _run_conv(pc, _nhwc(x, "bf16"), out, "bf16")
+    torch.cuda.synchronize()
+    _close(out, ref.permute(0, 2, 3, 1), "bf16", f"dw5 rows {h}x{w}c{c}")
+
+
 @pytest.mark.parametrize("dt", DT)
 def test_stem_conv_and_pool(dt):
     lib = _lib.load()
