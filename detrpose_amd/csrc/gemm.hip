@@ -283,6 +283,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs g) {
 //     written with 16-byte stores and read back with ds_read_b64_tr_b16 (two 4-k reads per
 //     fragment: lane group g takes k = 8g .. 8g+7, the same k slots as the b128 reads).
 constexpr int BT = 128, BKB = 64, P0 = 72;
+// Two waves per SIMD (the LDS allows two blocks per CU): holds every instantiation at <= 256
+// VGPRs (the both-transposed <1, 1> had 272, i.e. one block per CU). DP_GEMM128_WPE=0: no bound (A/B)
+#ifndef DP_GEMM128_WPE
+#define DP_GEMM128_WPE 2
+#endif
+#if DP_GEMM128_WPE
+#define DP_G128_ATTR __attribute__((amdgpu_waves_per_eu(DP_GEMM128_WPE)))
+#else
+#define DP_G128_ATTR
+#endif
 constexpr int IMG = BT * P0 > BKB * BT ? BT * P0 : BKB * BT;   // elements per operand image
 
 __device__ __forceinline__ int swz_off(int r, int ch) {   // bytes of chunk ch of k-row r
@@ -326,6 +336,8 @@ __device__ __forceinline__ void load_tile2(Tile2Regs& t, const Operand& op, int 
       gr = r0 + (c & 15) * 8;
       if (gk < K && gr + 8 <= op.rows) {
         t.v[i] = *reinterpret_cast<const uint4*>(p + (int64_t)gk * op.ks + gr);
+      } else if (gk >= K || gr >= op.rows) {   // wholly outside (e.g. rows past a 48-channel cout)
+        t.v[i] = uint4{0u, 0u, 0u, 0u};
       } else {
         bf16_t e8[8];
 #pragma unroll
@@ -339,22 +351,50 @@ __device__ __forceinline__ void load_tile2(Tile2Regs& t, const Operand& op, int 
 // B tile of mode 3: k rows kabs .. kabs+63 (output pixels), n columns n0 .. n0+127 (tap-major:
 // n = tap * cin + ci; cin % 8 == 0 so a 16-byte chunk is 8 channels of one tap). Every load is
 // issued (address clamped into the map), the chunk zeroed where the tap falls outside it.
-__device__ __forceinline__ void load_tile_im(Tile2Regs& t, const GemmArgs& g, int kabs, int n0, int kend) {
+// A thread's four chunks share one column n (c & 15 == tid & 15), so its tap / channel split is
+// computed once per block (ImLane); the pixel index is split by float reciprocals with a
+// one-step correction (exact for K < 2^24, host check) instead of runtime integer divisions,
+// which had made the gather VALU-bound (six divisions per chunk against 32 MFMAs per wave).
+struct ImLane {
+  int dy, dx, cic;   // tap offsets (ky - pad, kx - pad) and channel of this thread's column
+  bool nok;          // column inside N
+  float inv_w, inv_h;
+};
+
+__device__ __forceinline__ int fdivi(int a, int d, float inv) {   // a / d for 0 <= a < 2^24
+  int q = (int)((float)a * inv);
+  const int r = a - q * d;
+  q += r >= d ? 1 : 0;
+  q -= r < 0 ? 1 : 0;
+  return q;
+}
+
+__device__ __forceinline__ ImLane im_lane(const GemmArgs& g, int n0) {
+  ImLane L;
+  const int n = n0 + (threadIdx.x & 15) * 8;
+  L.nok = n < g.N;
+  const int nn = L.nok ? n : 0;
+  const int tap = nn / g.icin, ky = tap / g.ikw;
+  L.cic = nn - tap * g.icin;
+  L.dy = ky - g.ipad;
+  L.dx = tap - ky * g.ikw - g.ipad;
+  L.inv_w = 1.f / (float)g.iow;
+  L.inv_h = 1.f / (float)g.ioh;
+  return L;
+}
+
+__device__ __forceinline__ void load_tile_im(Tile2Regs& t, const GemmArgs& g, int kabs, int kend, const ImLane& L) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int c = tid + 256 * i;
-    const int p = kabs + (c >> 4), n = n0 + (c & 15) * 8;
+    const int p = kabs + (tid >> 4) + 16 * i;
     const int pc = min(p, kend - 1);
-    const int ox = pc % g.iow, t2 = pc / g.iow;
-    const int oy = t2 % g.ioh, b = t2 / g.ioh;
-    const int tap = n / g.icin, ci = n - tap * g.icin;
-    const int ky = tap / g.ikw, kx = tap - ky * g.ikw;
-    const int y = oy * g.istride - g.ipad + ky, x = ox * g.istride - g.ipad + kx;
-    const bool ok = p < kend && n < g.N && (unsigned)y < (unsigned)g.ih && (unsigned)x < (unsigned)g.iw;
+    const int t2 = fdivi(pc, g.iow, L.inv_w), ox = pc - t2 * g.iow;
+    const int b = fdivi(t2, g.ioh, L.inv_h), oy = t2 - b * g.ioh;
+    const int y = oy * g.istride + L.dy, x = ox * g.istride + L.dx;
+    const bool ok = p < kend && L.nok && (unsigned)y < (unsigned)g.ih && (unsigned)x < (unsigned)g.iw;
     const int yc = min(max(y, 0), g.ih - 1), xc = min(max(x, 0), g.iw - 1);
-    const int cic = n < g.N ? ci : 0;
-    const uint4 v = *reinterpret_cast<const uint4*>(g.ix + (int64_t)b * g.ix_bs + ((int64_t)yc * g.iw + xc) * g.ix_ps + cic);
+    const uint4 v = *reinterpret_cast<const uint4*>(g.ix + (int64_t)b * g.ix_bs + ((int64_t)yc * g.iw + xc) * g.ix_ps + L.cic);
     t.v[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
   }
 }
@@ -389,7 +429,7 @@ __device__ __forceinline__ bf16x8 frag2(const bf16_t* img, int mode, int r0, int
 
 // MA / MB: the operands' modes as compile-time constants (no branch in the fragment reads)
 template <int MA, int MB>
-__global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
+__global__ __launch_bounds__(256) DP_G128_ATTR void gemm128_kernel(const GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem128[];   // [buffer][A | B][IMG]
   bf16_t(*sm)[2][IMG] = reinterpret_cast<bf16_t(*)[2][IMG]>(smem128);
   const int tile = blockIdx.x;
@@ -409,25 +449,20 @@ __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
   const Operand A = g.A, B = g.B;
   const int64_t aoff = (int64_t)bidx * A.bs + (int64_t)kb * A.ks, boff = (int64_t)bidx * B.bs + (int64_t)kb * B.ks;
   const int KC = ke - kb;
-  Tile2Regs ra, rb;
-  if (KC > 0) {
-    load_tile2(ra, A, MA, aoff, m0, 0, KC);
-    if constexpr (MB == 3) load_tile_im(rb, g, kb, n0, ke);
-    else load_tile2(rb, B, MB, boff, n0, 0, KC);
-    store_tile2(ra, sm[0][0], MA);
-    store_tile2(rb, sm[0][1], MB == 3 ? 1 : MB);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int k0 = 0; k0 < KC; k0 += BKB) {
-    const bool more = k0 + BKB < KC;
-    if (more) {
-      load_tile2(ra, A, MA, aoff, m0, k0 + BKB, KC);
-      if constexpr (MB == 3) load_tile_im(rb, g, kb + k0 + BKB, n0, ke);
-      else load_tile2(rb, B, MB, boff, n0, k0 + BKB, KC);
-    }
-    const bf16_t* Ai = sm[cur][0];
-    const bf16_t* Bi = sm[cur][1];
+  ImLane il{};
+  if constexpr (MB == 3) il = im_lane(g, n0);
+  auto load_step = [&](Tile2Regs& ra, Tile2Regs& rb, int k0) __attribute__((always_inline)) {
+    load_tile2(ra, A, MA, aoff, m0, k0, KC);
+    if constexpr (MB == 3) load_tile_im(rb, g, kb + k0, ke, il);
+    else load_tile2(rb, B, MB, boff, n0, k0, KC);
+  };
+  auto store_step = [&](const Tile2Regs& ra, const Tile2Regs& rb, int buf) __attribute__((always_inline)) {
+    store_tile2(ra, sm[buf][0], MA);
+    store_tile2(rb, sm[buf][1], MB == 3 ? 1 : MB);
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const bf16_t* Ai = sm[buf][0];
+    const bf16_t* Bi = sm[buf][1];
 #pragma unroll
     for (int ks = 0; ks < BKB / 32; ++ks) {
       bf16x8 af[4], bfr[4];
@@ -440,10 +475,20 @@ __global__ __launch_bounds__(256) void gemm128_kernel(const GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) {   // the other buffer's readers passed the previous iteration's barrier
-      store_tile2(ra, sm[cur ^ 1][0], MA);
-      store_tile2(rb, sm[cur ^ 1][1], MB == 3 ? 1 : MB);
-    }
+  };
+  const int nst = (KC + BKB - 1) / BKB;   // K steps of this split
+  Tile2Regs ra, rb;
+  if (nst > 0) {
+    load_step(ra, rb, 0);
+    store_step(ra, rb, 0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int st = 0; st < nst; ++st) {
+    const bool more = st + 1 < nst;
+    if (more) load_step(ra, rb, (st + 1) * BKB);
+    compute(cur);
+    if (more) store_step(ra, rb, cur ^ 1);   // the other buffer's readers passed the last barrier
     __syncthreads();
     cur ^= 1;
   }
@@ -604,7 +649,8 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
              "dp_conv_wgrad: bf16, cin %% 8 == 0, 16-byte aligned pixels (cin %d, pstride %d, ld %lld)", cin,
              x_pstride, (long long)dz_ld);
   const int64_t K = (int64_t)batch * oh * ow;
-  DP_REQUIRE(K < (1ll << 31), "dp_conv_wgrad: too many pixels");
+  DP_REQUIRE(K < (1ll << 24), "dp_conv_wgrad: %lld output pixels (the gather's float-reciprocal split needs < 2^24)",
+             (long long)K);
   hipStream_t s = as_stream(stream);
   const int taps = kh * kw, N = taps * cin;
   if (dp_zero_async(scratch, (size_t)cout * N * sizeof(float), s)) {

@@ -396,7 +396,11 @@ def test_attention_400_tokens(C_, nh):
 
 
 @pytest.mark.parametrize("B,h,w,cin,cout,k,st,pad,xpad", [(2, 17, 12, 48, 48, 3, 1, 1, 0), (2, 20, 20, 64, 130, 3, 2, 1, 8),
-                                                         (3, 9, 13, 96, 96, 3, 1, 1, 16), (2, 10, 11, 16, 24, 2, 1, 0, 0)])
+                                                         (3, 9, 13, 96, 96, 3, 1, 1, 16), (2, 10, 11, 16, 24, 2, 1, 0, 0),
+                                                         # HGNetv2-L stage 0 at b16 (409,600 pixels: the gather's
+                                                         # float-reciprocal pixel split far from small integers)
+                                                         (16, 160, 160, 48, 48, 3, 1, 1, 0),
+                                                         (5, 81, 79, 128, 128, 3, 1, 1, 0), (7, 61, 67, 32, 16, 3, 2, 1, 0)])
 def test_conv_wgrad_implicit(B, h, w, cin, cout, k, st, pad, xpad):
     """dp_conv_wgrad (implicit-GEMM weight gradient, the training step's 3x3 / 2x2 convs) vs the
     fp32 autograd weight gradient on the same bf16-rounded x and dz; padded pixel strides, an
