@@ -603,10 +603,12 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
     const int target = big ? 512 : 4096, kmin = big ? 4 : 8;
     splits = (int)((target + tiles - 1) / tiles);
     if (splits > ksteps / kmin) splits = ksteps / kmin;
-    // at most 1024 float-atomic adds per output address (stem1's 32 x 27 weight gradient over
-    // 1.6 M pixels had 3200: 0.245 -> 0.195 ms; 256 measured slower there,
-    // profiles/r5_gemm_split_cap_ab.txt); DETRPOSE_GEMM_SPLIT_CAP overrides (A/B, 0 = none)
-    static const int cap = getenv("DETRPOSE_GEMM_SPLIT_CAP") ? atoi(getenv("DETRPOSE_GEMM_SPLIT_CAP")) : 1024;
+    // bounded float-atomic adds per output address: 512 for a one-tile output (stem1's 32 x 27
+    // weight gradient over 1.6 M pixels had 3200 splits: 0.245 -> 0.177 ms; 256 measured 0.295),
+    // 256 otherwise (the encoder / aggregation weight gradients: -0.14 ms per b16 sub-batch);
+    // profiles/r5_gemm_split_cap_ab.txt. DETRPOSE_GEMM_SPLIT_CAP overrides (A/B, 0 = none)
+    static const int cap_env = getenv("DETRPOSE_GEMM_SPLIT_CAP") ? atoi(getenv("DETRPOSE_GEMM_SPLIT_CAP")) : -1;
+    const int cap = cap_env >= 0 ? cap_env : (tiles > 1 ? 256 : 512);
     if (cap > 0 && splits > cap) splits = cap;
     if (splits < 1) splits = 1;
   }
