@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DETRPOSE_HIP_LIB", os.path.join(_HERE, "lib", "libdetrpose_hip.so"))
 
 DP_F32, DP_BF16 = 0, 1
-DP_SQNORM_PARTS = 1024   # dp_grad_sqnorm's out holds 1 + DP_SQNORM_PARTS floats
+DP_SQNORM_PARTS = 1024   # upper bound of dp_grad_sqnorm_ws_floats(n)
 DP_ACT_NONE, DP_ACT_RELU, DP_ACT_SILU, DP_ACT_GELU = 0, 1, 2, 3
 DP_MSDA_OFFATTN_F32 = 0x100
 ACT = {None: 0, "none": 0, "relu": 1, "silu": 2, "gelu": 3}
@@ -67,6 +67,12 @@ class GemmDesc(C.Structure):
                 ("bias", vp), ("alpha", f32), ("beta", f32), ("act", i32),
                 ("gate", vp), ("gate_bs", i64), ("gate_rs", i64), ("gate_dtype", i32),
                 ("split_k", i32)]
+
+
+class PackDesc(C.Structure):
+    """Mirror of dp_pack_desc."""
+    _fields_ = [("w", vp), ("out", vp), ("scale", vp), ("cout", i32), ("cin", i32), ("kh", i32), ("kw", i32),
+                ("kpad", i32), ("kc", i32), ("mode", i32), ("dtype", i32)]
 
 
 def rowmap(base=0, group=1, stride_g=0, stride_r=0) -> RowMap:
@@ -149,7 +155,8 @@ _SIGS = {
     "dp_convert_rows": (i32, [vp, i32, i64, vp, i32, i64, i32, i32, f32, i32, vp]),
     "dp_zero": (i32, [vp, i64, vp]),
     "dp_cdn_build": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, i32, f32, f32, C.c_uint64, vp, vp, vp]),
-    "dp_grad_sqnorm": (i32, [vp, i64, vp, vp]),
+    "dp_grad_sqnorm": (i32, [vp, i64, vp, vp, i64, vp]),
+    "dp_grad_sqnorm_ws_floats": (i64, [i64]),
     "dp_adamw": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp, vp, vp]),
     "dp_finite_guard": (i32, [vp, i64, vp, vp]),
     "dp_ema": (i32, [vp, vp, i64, f32, vp, vp]),
@@ -165,6 +172,8 @@ _SIGS = {
                                   vp, f32, i32, vp]),
     "dp_im2col": (i32, [vp, i64, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp]),
     "dp_conv_pack": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, vp, i32, vp]),
+    "dp_conv_pack_check": (i32, [vp, i32]),
+    "dp_conv_pack_batch": (i32, [vp, i32, i32, vp]),
     "dp_frozen_act_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp]),
     "dp_col2im": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, i32, i32, i32, vp]),
     "dp_maxpool2x2_pad_rb_bwd": (i32, [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, vp]),

@@ -107,6 +107,7 @@ class BackboneTrainPlan(TapePlan):
             if si in bb.return_idx:
                 self.outs.append(x_src)
         self._record_backward(zero=False)   # zeroed by the encoder's backward, which runs first
+        self.batch_packs()
         eng.cur = prev
 
     # ------------------------------------------------------------------ frozen BN
@@ -133,6 +134,7 @@ class BackboneTrainPlan(TapePlan):
     def stem1(self, p, out, sd):
         """StemBlock.stem1: 3x3 s2 conv of the f32 NCHW image (dp_stem_conv), wgrad only."""
         lib = self.lib
+        self.taps[p] = out
         B, H, W = self.B, self.H, self.W
         wkey = p + ".conv.weight"
         s, sh = self._frozen(p, sd, out.cp)
@@ -173,6 +175,7 @@ class BackboneTrainPlan(TapePlan):
     def cba(self, p, x, out, sd, k=1, stride=1, pad=None, dw=False, act=True, res=None):
         """ConvBNAct (hgnetv2.py:82-134) from x into out (+ res, the HG block's identity)."""
         lib = self.lib
+        self.taps[p] = out
         name = p[len(B_):]
         wkey = p + ".conv.weight"
         w = self.eng.params[wkey]

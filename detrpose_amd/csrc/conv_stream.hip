@@ -33,6 +33,9 @@
 #ifndef DP_STREAM_PRIO
 #define DP_STREAM_PRIO 1   // s_setprio(1) around each K-step's fragment reads + MFMAs (fpn1.cv1 +3.5%, s2.sq +2.4%, others flat)
 #endif
+#ifndef DP_STREAM_PIPE
+#define DP_STREAM_PIPE 1   // K loop pipelined across the per-step barrier (0: the unpipelined loop, A/B only)
+#endif
 #ifndef DP_ABL_NOMFMA
 #define DP_ABL_NOMFMA 0    // ... drop the MFMAs (fragment reads kept live)
 #endif
@@ -197,7 +200,14 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
   // then 2 x 1 KB bias slots (tile parity): the tile's BN f32 biases, DMA'd by wave 0 in
   // front of the tile's first weight K-step, so the epilogue reads them from LDS and the
   // compiler never has a VMEM load of its own to wait for behind the in-flight DMAs.
-  __shared__ __attribute__((aligned(1024))) char smem[SB * BBYTES + SA * ABYTES + 2048];
+  // (pipelined loop: 4 bias slots, since with one K-step per tile the bias of tile t+2 is issued
+  // before tile t's epilogue)
+  // Only the 192-row tile pipelines (deep-K GEMMs on 8 waves: s2 squeeze 273 -> 256 us, the
+  // decoder GEMMs 1-3 %); elsewhere it measured neutral to -2 % (profiles/r6a_conv_ab.txt), and
+  // the 256 x 256 tile spills with it (its 256 registers hold the accumulators and one K-step)
+  constexpr bool PIPE = DP_STREAM_PIPE && BM == 192;
+  constexpr int NBS = PIPE ? 4 : 2;
+  __shared__ __attribute__((aligned(1024))) char smem[SB * BBYTES + SA * ABYTES + NBS * 1024];
   char* const sa_base = smem + SB * BBYTES;
   char* const bias_base = sa_base + SA * ABYTES;
   static_assert(BN * 4 <= 1024, "bias slot");
@@ -300,7 +310,7 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
       // the tile's biases (older than its first weight K-step: covered by the same wait)
       const int n0 = (b_tile - (b_tile / nt_n) * nt_n) * BN;
       const int o = (d.bias && n0 + 4 * lane < d.cout && 4 * lane < BN) ? (n0 + 4 * lane) * 4 : OOB;
-      if (!DP_ABL_NODMA) dma16(make_rsrc(d.bias), bias_base + (b_t & 1) * 1024, o);
+      if (!DP_ABL_NODMA) dma16(make_rsrc(d.bias), bias_base + (b_t % NBS) * 1024, o);
     }
 #pragma unroll
     for (int t = 0; t < GB; ++t) {
@@ -392,12 +402,97 @@ void conv_stream_kernel(dp_conv_desc d, int M, int nt_n, int ntiles, int vec_ok)
     ++c;
   };
   int t_n = 0;
+  if constexpr (!PIPE) {
+    for (int ctile = L; ctile < ntiles; ctile += G, ++t_n) {
+      step(std::true_type{});
+      for (int kt = 1; kt < nk; ++kt) step(std::false_type{});
+      const int tm = ctile / nt_n, tn = ctile - tm * nt_n;
+      const int mw = tm * BM + wm * WM;
+      const float* bias_w = reinterpret_cast<const float*>(bias_base + (t_n % NBS) * 1024) + wn * WN;
+      dirty = stream_epilogue<ACT, TO, TM, TN, EPI>(d, acc, bias_w, M, mw, tn * BN + wn * WN, vec_ok) ? 1 : 2;
+    }
+    wait_vmcnt<0>();
+    return;
+  }
+  // Pipelined K loop: the per-step barrier sits between the two MFMA halves of a K-step. The
+  // barrier in step c publishes A(c+1) / B(c+1) (the waits of the unpipelined step c+1, same
+  // counts) and frees step c's ring slots; half 0 of step c+1's fragments is then read under
+  // the half-1 MFMAs of step c, half 1 of a step under its own half-0 MFMAs. No MFMA waits for
+  // an LDS read issued after a barrier (the unpipelined step read both halves there, every
+  // wave at once, before its first MFMA). A tile's epilogue follows its last half-1 MFMAs, after
+  // the barrier that issued the next tile's first DMAs, so those stay older than its stores.
+  bf16x8 wf0[TN], pf0[TM], wf1[TN], pf1[TM];
+  auto read_half = [&](int cs, int ks, bf16x8 (&wf)[TN], bf16x8 (&pf)[TM]) {
+    const char* sbw = smem + (cs % SB) * BBYTES;
+    const char* sbp = sa_base + (cs % SA) * ABYTES;
+    const int cc = 4 * ks + lg;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r = wrow + 16 * j;
+      wf[j] = *reinterpret_cast<const bf16x8*>(sbw + r * 128 + ((cc ^ (r & 7)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = prow + 16 * i;
+      pf[i] = *reinterpret_cast<const bf16x8*>(sbp + r * 128 + ((cc ^ (r & 7)) << 4));
+    }
+  };
+  auto mfma_half = [&](const bf16x8 (&wf)[TN], const bf16x8 (&pf)[TM], bool zero) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#if DP_ABL_NOMFMA
+      {
+        asm volatile("" ::"v"(wf[j]), "v"(pf[i]));
+        if (zero) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#else
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], zero ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j],
+                                                            0, 0, 0);
+#endif
+  };
+  // wait for A(cn) and B(cn) (cn = the step the next fragment reads belong to), publish them,
+  // refill both rings: the unpipelined step's head with c = cn
+  auto publish = [&](int cn) {
+    const int younger = SA == 2 ? 0 : (cn == 0 ? min(SA - 2, a_n - 1) : (a_n > cn + SA - 2 ? 1 : 0));
+    if (dirty == 2) wait_vmcnt<0>();
+    else if (dirty == 1) {
+      if (younger <= 0) wait_vmcnt<EPIV>();
+      else if (younger == 1) wait_vmcnt<(EPIV + GA > 63 ? 63 : EPIV + GA)>();
+      else wait_vmcnt<(EPIV + 2 * GA > 63 ? 63 : EPIV + 2 * GA)>();
+    } else if (younger <= 0) wait_vmcnt<0>();
+    else if (younger == 1) wait_vmcnt<GA>();
+    else wait_vmcnt<2 * GA>();
+    dirty = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (b_n < total) issue_b();
+    if (a_n < total) issue_a();
+  };
+  publish(0);
+  read_half(0, 0, wf0, pf0);
   for (int ctile = L; ctile < ntiles; ctile += G, ++t_n) {
-    step(std::true_type{});
-    for (int kt = 1; kt < nk; ++kt) step(std::false_type{});
+    for (int kt = 0; kt < nk; ++kt) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (DP_STREAM_PRIO) __builtin_amdgcn_s_setprio(1);
+      read_half(c, 1, wf1, pf1);
+      mfma_half(wf0, pf0, kt == 0);
+      if (DP_STREAM_PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      // unconditional on the block's last step (its reads of step c+1's slots are harmless: every
+      // DMA has landed): a branch around the reads would merge wait states before the MFMAs below
+      publish(c + 1);
+      if (DP_STREAM_PRIO) __builtin_amdgcn_s_setprio(1);
+      read_half(c + 1, 0, wf0, pf0);
+      mfma_half(wf1, pf1, false);
+      if (DP_STREAM_PRIO) __builtin_amdgcn_s_setprio(0);
+      ++c;
+    }
     const int tm = ctile / nt_n, tn = ctile - tm * nt_n;
     const int mw = tm * BM + wm * WM;
-    const float* bias_w = reinterpret_cast<const float*>(bias_base + (t_n & 1) * 1024) + wn * WN;
+    const float* bias_w = reinterpret_cast<const float*>(bias_base + (t_n % NBS) * 1024) + wn * WN;
     dirty = stream_epilogue<ACT, TO, TM, TN, EPI>(d, acc, bias_w, M, mw, tn * BN + wn * WN, vec_ok) ? 1 : 2;
   }
   wait_vmcnt<0>();
@@ -427,8 +522,9 @@ template <int BM, int BN, int NW>
 constexpr int ring_a() {
   if (DP_NARROW_SA && BN <= 64) return DP_NARROW_SA;
   constexpr int want = BM == 192 ? 3 : DP_STREAM_SA;   // the 192-row tile has LDS for a 3rd A stage
-  constexpr int blocks2 = (160 * 1024) / ((2 * BM + 2 * BN) * 128 + 2048);     // + the 2 KB bias slots
-  constexpr int blocksw = (160 * 1024) / ((want * BM + 2 * BN) * 128 + 2048);
+  constexpr int bias = (DP_STREAM_PIPE && BM == 192) ? 4096 : 2048;   // + the bias slots
+  constexpr int blocks2 = (160 * 1024) / ((2 * BM + 2 * BN) * 128 + bias);
+  constexpr int blocksw = (160 * 1024) / ((want * BM + 2 * BN) * 128 + bias);
   return (blocksw >= 1 && blocksw >= blocks2) ? want : 2;
 }
 

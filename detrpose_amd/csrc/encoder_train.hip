@@ -375,33 +375,66 @@ __global__ void im2col_kernel(const TI* __restrict__ x, int64_t bs, int ps, int6
 // (rows = kh*kw*cin in tap-major order (ky, kx, ci), K over cout, taps not flipped: dcol = dz W
 // in the order dp_col2im reads). kc: the K dimension's channel stride (>= the real channel count:
 // maps whose channels are padded to a vector multiple), zero in the pads
+// elements pack_elem writes for one pack (mode 5: a plain f32 -> dtype copy of cout elements)
+__host__ __device__ inline int64_t pack_total(int cout, int cin, int kh, int kw, int kpad, int mode) {
+  return mode == 2 ? (int64_t)cout * kh * kw
+         : mode == 3 ? (int64_t)cout * cin * kh * kw
+         : mode == 4 ? (int64_t)kh * kw * cin * kpad
+         : mode == 5 ? (int64_t)cout
+                     : (int64_t)(mode == 0 ? cout : cin) * kpad;
+}
+
+template <typename T>
+__device__ __forceinline__ void pack_elem(int64_t e, const float* __restrict__ w, int cout, int cin, int kh, int kw,
+                                          void* __restrict__ out, int kpad, int kc, int mode,
+                                          const float* __restrict__ scale);
+
 template <typename T>
 __global__ void conv_pack_kernel(const float* __restrict__ w, int cout, int cin, int kh, int kw, void* __restrict__ out,
                                  int kpad, int kc, int mode, const float* __restrict__ scale) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= pack_total(cout, cin, kh, kw, kpad, mode)) return;
+  pack_elem<T>(e, w, cout, cin, kh, kw, out, kpad, kc, mode, scale);
+}
+
+// every pack of a training plan's pack tape in one launch: block row y = pack y of the table,
+// the x blocks stride over its elements (the dtype per entry, uniform per block)
+__global__ void conv_pack_batch_kernel(const dp_pack_desc* __restrict__ tab) {
+  const dp_pack_desc d = tab[blockIdx.y];
+  const int64_t total = pack_total(d.cout, d.cin, d.kh, d.kw, d.kpad, d.mode);
+  const int kc = d.kc > 0 ? d.kc : (d.mode == 0 ? d.cin : d.cout);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    if (d.dtype == DP_BF16) pack_elem<bf16_t>(e, d.w, d.cout, d.cin, d.kh, d.kw, d.out, d.kpad, kc, d.mode, d.scale);
+    else pack_elem<float>(e, d.w, d.cout, d.cin, d.kh, d.kw, d.out, d.kpad, kc, d.mode, d.scale);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void pack_elem(int64_t e, const float* __restrict__ w, int cout, int cin, int kh, int kw,
+                                          void* __restrict__ out, int kpad, int kc, int mode,
+                                          const float* __restrict__ scale) {
+  if (mode == 5) {
+    reinterpret_cast<T*>(out)[e] = from_f32<T>(w[e]);
+    return;
+  }
   if (mode == 2) {
-    if (e >= (int64_t)cout * kh * kw) return;
     const int tap = (int)(e / cout), ch = (int)(e % cout);
     reinterpret_cast<float*>(out)[e] = w[(int64_t)ch * kh * kw + tap] * (scale ? scale[ch] : 1.f);
     return;
   }
   if (mode == 3) {
     const int K = cin * kh * kw;
-    if (e >= (int64_t)cout * K) return;
     reinterpret_cast<float*>(out)[e] = w[e] * (scale ? scale[e / K] : 1.f);
     return;
   }
   if (mode == 4) {
-    if (e >= (int64_t)kh * kw * cin * kpad) return;
     const int r = (int)(e / kpad), j = (int)(e % kpad);
     const int tap = r / cin, ci = r - tap * cin;
     const float v = j < cout ? w[((int64_t)j * cin + ci) * kh * kw + tap] * (scale ? scale[j] : 1.f) : 0.f;
     reinterpret_cast<T*>(out)[e] = from_f32<T>(v);
     return;
   }
-  const int rows = mode == 0 ? cout : cin;
   const int inner = mode == 0 ? cin : cout;
-  if (e >= (int64_t)rows * kpad) return;
   const int r = (int)(e / kpad), k = (int)(e % kpad);
   float v = 0.f;
   const int tap = k / kc, j = k - tap * kc;
@@ -835,6 +868,32 @@ extern "C" int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t k
   DP_DT(hipLaunchKernelGGL(conv_pack_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
                            w, cout, cin, kh, kw, out, kpad, kc, mode, scale));
   return dp_check_launch("dp_conv_pack");
+}
+
+// the pack table's entries as dp_conv_pack would accept them one by one (mode 5: cout elements
+// copied f32 -> dtype); mode 2 / 3 pack f32
+extern "C" int dp_conv_pack_check(const dp_pack_desc* tab, int32_t n) {
+  DP_REQUIRE(tab && n > 0 && n < 65536, "dp_conv_pack_check: bad table");
+  for (int i = 0; i < n; ++i) {
+    const dp_pack_desc& d = tab[i];
+    const int kc = d.kc > 0 ? d.kc : (d.mode == 0 ? d.cin : d.cout);
+    const bool ok = d.w && d.out && d.cout > 0 && d.cin > 0 && d.kh > 0 && d.kw > 0 && d.mode >= 0 && d.mode <= 5 &&
+                    (d.dtype == DP_BF16 || d.dtype == DP_F32) && (d.mode != 2 && d.mode != 3 || d.dtype == DP_F32) &&
+                    (d.mode == 2 ? d.cin == 1
+                     : d.mode == 3 || d.mode == 5 ? true
+                     : d.mode == 4 ? d.kpad >= d.cout
+                                   : kc >= (d.mode == 0 ? d.cin : d.cout) && d.kpad >= d.kh * d.kw * kc);
+    DP_REQUIRE(ok, "dp_conv_pack_check: entry %d (mode %d, cout %d, cin %d, k %dx%d, kpad %d, kc %d, dtype %d)", i, d.mode,
+               d.cout, d.cin, d.kh, d.kw, d.kpad, d.kc, d.dtype);
+  }
+  return 0;
+}
+
+extern "C" int dp_conv_pack_batch(const dp_pack_desc* tab_dev, int32_t n, int32_t blocks_per_pack, void* stream) {
+  DP_REQUIRE(tab_dev && n > 0 && n < 65536 && blocks_per_pack > 0, "dp_conv_pack_batch: bad arguments");
+  hipLaunchKernelGGL(conv_pack_batch_kernel, dim3((unsigned)blocks_per_pack, (unsigned)n), dim3(256), 0,
+                     as_stream(stream), tab_dev);
+  return dp_check_launch("dp_conv_pack_batch");
 }
 
 extern "C" int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride, const void* dz, int64_t z_bstride,

@@ -19,6 +19,7 @@
 // Split-K (when the M x N grid cannot fill the chip, e.g. wgrad over 10^5 rows): each block
 // adds alpha * its partial product into f32 C with atomics (C pre-initialised by the caller).
 #include "common.h"
+#include "conv_lds.h"
 
 namespace {
 
@@ -532,6 +533,150 @@ int operand_mode(const Operand& op, int vec, int64_t align_bytes_ok) {
 }
 
 
+// ---------------------------------------------------------------- weight-gradient GEMM on an LDS-DMA ring
+// C[m][n] += alpha * sum_k A[k][m] B[k][n] with both operands row-contiguous in k-major rows
+// (mode 1 / 1: dW = dy^T x of every 1x1 conv and Linear, dy [P][M], x [P][N], P = pixels or
+// tokens of 10^4 - 10^6), bf16 in, f32 C accumulated with float atomics over K splits. The
+// register-staged 128 x 128 kernel above reaches 6-20 % of MFMA peak here: its one K-step of
+// register prefetch cannot cover the HBM latency of a K-major stream. Here 128 x 256 tiles of
+// 8 waves (64 x 64 each) stream through a 3-deep LDS ring filled by buffer_load ... lds (no
+// staging registers; conv_lds.h): each 16-byte DMA lane fetches the global chunk that belongs
+// at its LDS slot under the [64 k][128 col] XOR swizzle of swz_off, so the ds_read_b64_tr_b16
+// fragment reads of frag2 apply unchanged. One block per CU (144 KB of LDS); the block order
+// is XCD-sliced so the tiles of one K split (which read the same rows of A and B) share an L2.
+constexpr int WT_BM = 128, WT_BN = 256, WT_NS = 3;
+constexpr int WT_SUB = 64 * 256;               // bytes of one [64 k][128 col] sub-image
+constexpr int WT_STAGE = 3 * WT_SUB;           // A | B cols 0-127 | B cols 128-255
+constexpr int WT_DMA = 6;                      // DMA instructions per wave per K-step (2 A + 4 B)
+
+// IM: B is dp_conv_wgrad's implicit im2col (mode 3: B(k = output pixel p, n = tap * cin + ci) =
+// x at the tap's input pixel of p, zero outside the map): each B DMA lane gathers the 16-byte
+// chunk of 8 channels of its column's tap at its row's pixel (an out-of-map pixel is an OOB
+// offset: zeros).
+template <bool IM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+void wgrad_tt_kernel(const GemmArgs g, int ntiles, int tiles_n) {
+  using namespace dpconv;
+  extern __shared__ __attribute__((aligned(1024))) char smw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;                       // multiple of 8
+  const int Lb = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int tile = Lb % ntiles, split = Lb / ntiles;
+  if (split >= g.splits) return;
+  const int kb = split * g.kchunk;
+  const int nst = (min(g.K, kb + g.kchunk) - kb + 63) / 64;
+  if (nst <= 0) return;
+  const int krem = min(g.K, kb + g.kchunk) - kb;   // rows of this split
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * WT_BM, n0 = tn * WT_BN;
+  const bf16_t* pa = reinterpret_cast<const bf16_t*>(g.A.p) + (int64_t)kb * g.A.ks;
+  const bf16_t* pb = IM ? g.ix : reinterpret_cast<const bf16_t*>(g.B.p) + (int64_t)kb * g.B.ks;
+  const i32x4 ra = make_rsrc(pa), rb = make_rsrc(pb);
+  // this wave's DMA instructions: t = 0, 1 -> A k-row groups 4 (2 wave + t); t = 2 .. 5 -> B
+  // instruction q = 4 wave + t - 2: sub-image q / 16, k-row group 4 (q % 16). Lane: row kr + rr,
+  // LDS slot s = lane % 16 holding logical chunk s ^ swizzle(row).
+  const int rr = lane >> 4, sl = lane & 15;
+  int row[WT_DMA], colb[WT_DMA], ldso[WT_DMA];
+  bool cok[WT_DMA];
+  int tdy[WT_DMA], tdx[WT_DMA];   // IM: the B column's tap offsets (colb: its channel, bytes)
+#pragma unroll
+  for (int t = 0; t < WT_DMA; ++t) {
+    int sub, kr;
+    if (t < 2) {
+      sub = 0, kr = 4 * (2 * wave + t);
+    } else {
+      const int q = 4 * wave + t - 2;
+      sub = 1 + q / 16, kr = 4 * (q % 16);
+    }
+    const int r = kr + rr;
+    const int ch = sl ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    const int col = (sub == 0 ? m0 : n0 + 128 * (sub - 1)) + 8 * ch;
+    row[t] = r;
+    colb[t] = col * 2;
+    cok[t] = col < (sub == 0 ? g.M : g.N);
+    ldso[t] = sub * WT_SUB + kr * 256;
+    tdy[t] = tdx[t] = 0;
+    if (IM && sub > 0) {
+      const int nn = cok[t] ? col : 0;
+      const int tap = nn / g.icin, ky = tap / g.ikw;
+      colb[t] = (nn - tap * g.icin) * 2;
+      tdy[t] = ky - g.ipad;
+      tdx[t] = tap - ky * g.ikw - g.ipad;
+    }
+  }
+  const float inv_w = 1.f / (float)g.iow, inv_h = 1.f / (float)g.ioh;
+  const int64_t a_step = (int64_t)g.A.ks * 2, b_step = (int64_t)g.B.ks * 2;   // bytes per k row
+  auto issue = [&](int st) {
+    char* base = smw + (st % WT_NS) * WT_STAGE;
+#pragma unroll
+    for (int t = 0; t < WT_DMA; ++t) {
+      const int k = st * 64 + row[t];
+      bool ok = cok[t] && k < krem;
+      int o;
+      if (IM && t >= 2) {
+        // output pixel p -> (image, oy, ox) -> the tap's input pixel (p < 2^24: fdivi exact)
+        const int pp = min(kb + k, g.K - 1);
+        const int t2 = fdivi(pp, g.iow, inv_w), ox = pp - t2 * g.iow;
+        const int b = fdivi(t2, g.ioh, inv_h), oy = t2 - b * g.ioh;
+        const int y = oy * g.istride + tdy[t], x = ox * g.istride + tdx[t];
+        ok = ok && (unsigned)y < (unsigned)g.ih && (unsigned)x < (unsigned)g.iw;
+        o = ok ? (int)((b * g.ix_bs + (int64_t)(y * g.iw + x) * g.ix_ps) * 2) + colb[t] : OOB;
+      } else {
+        o = ok ? (int)(k * (t < 2 ? a_step : b_step)) + colb[t] : OOB;
+      }
+      dma16(t < 2 ? ra : rb, base + ldso[t], o);
+    }
+  };
+  const int wm = (wave >> 2) * 64, wn = (wave & 3) * 64;
+  const int bsub = 1 + (wn >> 7), bcol = wn & 127;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < WT_NS - 1; ++p)
+    if (p < nst) issue(p);
+  for (int st = 0; st < nst; ++st) {
+    // stage st landed: the younger stages in flight are st+1 .. st+NS-2 (each WT_DMA per wave)
+    if (st + WT_NS - 2 < nst) wait_vmcnt<(WT_NS - 2) * WT_DMA>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // the slot of st + NS - 1 held st - 1, which every wave is past (barrier)
+    if (st + WT_NS - 1 < nst) issue(st + WT_NS - 1);
+    const char* base = smw + (st % WT_NS) * WT_STAGE;
+    const bf16_t* Ai = reinterpret_cast<const bf16_t*>(base);
+    const bf16_t* Bi = reinterpret_cast<const bf16_t*>(base + bsub * WT_SUB);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag2(Ai, 1, wm + 16 * i, 32 * ks);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag2(Bi, 1, bcol + 16 * j, 32 * ks);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn + 16 * j + (lane & 15);
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+        if (m < g.M) unsafeAtomicAdd(g.cf + (int64_t)m * g.c_rs + n, g.alpha * acc[i][j][r]);
+      }
+    }
+}
+
 // dw[co][ci][tap] += s[co][tap][ci] (the reference's [cout][cin][kh][kw] from the tap-major sums)
 __global__ void wgrad_permute_kernel(const float* __restrict__ s, float* __restrict__ dw, int cout, int cin, int taps) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over dw
@@ -586,6 +731,32 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
                           d.k >= 8 * 64;
   const bool big = !force64 && d.in_dtype == DP_BF16 && g.modeA < 2 && g.modeB < 2 && d.m >= 128 && d.n >= 96 &&
                    ((int64_t)d.m * d.n >= (int64_t)128 * 128 * 64 || (splittable && d.split_k == 0));
+  // weight gradients (both operands k-major rows, f32 C accumulated): the LDS-DMA ring kernel
+  // (DETRPOSE_WGRAD_TT=0 keeps the 128 x 128 kernel, A/B)
+  static const bool tt_off = getenv("DETRPOSE_WGRAD_TT") && atoi(getenv("DETRPOSE_WGRAD_TT")) == 0;
+  if (!tt_off && big && splittable && d.split_k == 0 && d.batch == 1 && g.modeA == 1 && g.modeB == 1 &&
+      d.m % 8 == 0 && d.n % 8 == 0 && d.k >= 4096) {
+    const int tmw = (d.m + WT_BM - 1) / WT_BM, tnw = (d.n + WT_BN - 1) / WT_BN;
+    const int ntl = tmw * tnw;
+    const int ksteps64 = (d.k + 63) / 64;
+    int sp = (dpconv::num_cus() + ntl - 1) / ntl;   // one block per CU, one round
+    if (sp > ksteps64 / 4) sp = ksteps64 / 4;
+    if (sp < 1) sp = 1;
+    const int kchunk = ((ksteps64 + sp - 1) / sp) * 64;
+    // 32-bit buffer offsets from each split's first row
+    if (((int64_t)kchunk * d.a_ks + d.m) * 2 < 0x7ff00000ll && ((int64_t)kchunk * d.b_ks + d.n) * 2 < 0x7ff00000ll) {
+      g.splits = sp;
+      g.kchunk = kchunk;
+      static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_tt_kernel<false>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   WT_NS * WT_STAGE) == hipSuccess;
+      DP_REQUIRE(attr, "dp_gemm: cannot set the weight-gradient kernel's LDS size");
+      const int nb = (ntl * sp + 7) / 8 * 8;
+      hipLaunchKernelGGL(wgrad_tt_kernel<false>, dim3((unsigned)nb), dim3(512), WT_NS * WT_STAGE, as_stream(stream), g,
+                         ntl, tnw);
+      return dp_check_launch("dp_gemm(wgrad)");
+    }
+  }
   const int TMs = big ? BT : TM, TNs = big ? BT : TN;
   const int tm = (d.m + TMs - 1) / TMs, tn = (d.n + TNs - 1) / TNs;
   g.tiles_n = tn;
@@ -655,9 +826,11 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
                  (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(dz) & 15) == 0,
              "dp_conv_wgrad: bf16, cin %% 8 == 0, 16-byte aligned pixels (cin %d, pstride %d, ld %lld)", cin,
              x_pstride, (long long)dz_ld);
-  const int64_t K = (int64_t)batch * oh * ow;
-  DP_REQUIRE(K < (1ll << 24), "dp_conv_wgrad: %lld output pixels (the gather's float-reciprocal split needs < 2^24)",
-             (long long)K);
+  // the gather splits a pixel index with a float reciprocal, exact below 2^24: larger batches run
+  // as consecutive image chunks accumulating into the same scratch (beta = 1)
+  const int64_t ppi = (int64_t)oh * ow;
+  DP_REQUIRE(ppi < (1ll << 24), "dp_conv_wgrad: %lld output pixels per image (needs < 2^24)", (long long)ppi);
+  const int chunk = (int)std::min<int64_t>(batch, ((1ll << 24) - 1) / ppi);
   hipStream_t s = as_stream(stream);
   const int taps = kh * kw, N = taps * cin;
   if (dp_zero_async(scratch, (size_t)cout * N * sizeof(float), s)) {
@@ -673,7 +846,7 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
   g.cb = nullptr;
   g.c_bs = 0;
   g.c_rs = N;
-  g.M = cout, g.N = N, g.K = (int)K, g.batch = 1;
+  g.M = cout, g.N = N, g.batch = 1;
   g.alpha = 1.f;
   g.beta = 1.f;
   g.act = DP_ACT_NONE;
@@ -683,17 +856,45 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
   g.ih = h, g.iw = w, g.icin = cin, g.ioh = oh, g.iow = ow, g.ikw = kw, g.istride = stride, g.ipad = pad;
   const int tm = (cout + BT - 1) / BT, tn = (N + BT - 1) / BT;
   g.tiles_n = tn;
-  const int ksteps = (int)((K + BKB - 1) / BKB);
-  int splits = (512 + tm * tn - 1) / (tm * tn);
-  if (splits > ksteps / 4) splits = ksteps / 4;
-  if (splits < 1) splits = 1;
-  g.splits = splits;
-  g.kchunk = ((ksteps + splits - 1) / splits) * BKB;
   constexpr size_t lds = sizeof(bf16_t) * 4 * IMG;
   static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm128_kernel<1, 3>),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   DP_REQUIRE(attr_ok, "dp_conv_wgrad: cannot set the kernel's LDS size");
-  hipLaunchKernelGGL((gemm128_kernel<1, 3>), dim3((unsigned)(tm * tn), (unsigned)splits), dim3(256), lds, s, g);
+  static const bool tt_off = getenv("DETRPOSE_WGRAD_TT") && atoi(getenv("DETRPOSE_WGRAD_TT")) == 0;
+  for (int b0 = 0; b0 < batch; b0 += chunk) {
+    const int nb = std::min(chunk, batch - b0);
+    const int64_t K = (int64_t)nb * ppi;
+    g.A.p = reinterpret_cast<const bf16_t*>(dz) + (int64_t)b0 * ppi * dz_ld;
+    g.ix = reinterpret_cast<const bf16_t*>(x) + (int64_t)b0 * x_bstride;
+    g.B.p = g.ix;
+    g.K = (int)K;
+    // the LDS-DMA ring kernel (wgrad_tt_kernel<true>) where its 32-bit buffer offsets reach
+    if (!tt_off && K >= 4096 && cout % 8 == 0 && N % 8 == 0 && (int64_t)nb * x_bstride * 2 < 0x7ff00000ll &&
+        (K * dz_ld + cout) * 2 < 0x7ff00000ll) {
+      const int tmw = (cout + WT_BM - 1) / WT_BM, tnw = (N + WT_BN - 1) / WT_BN;
+      const int ntl = tmw * tnw;
+      const int ks64 = (int)((K + 63) / 64);
+      int sp = (dpconv::num_cus() + ntl - 1) / ntl;
+      if (sp > ks64 / 4) sp = ks64 / 4;
+      if (sp < 1) sp = 1;
+      g.splits = sp;
+      g.kchunk = ((ks64 + sp - 1) / sp) * 64;
+      static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_tt_kernel<true>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   WT_NS * WT_STAGE) == hipSuccess;
+      DP_REQUIRE(attr, "dp_conv_wgrad: cannot set the weight-gradient kernel's LDS size");
+      hipLaunchKernelGGL(wgrad_tt_kernel<true>, dim3((unsigned)((ntl * sp + 7) / 8 * 8)), dim3(512),
+                         WT_NS * WT_STAGE, s, g, ntl, tnw);
+      continue;
+    }
+    const int ksteps = (int)((K + BKB - 1) / BKB);
+    int splits = (512 + tm * tn - 1) / (tm * tn);
+    if (splits > ksteps / 4) splits = ksteps / 4;
+    if (splits < 1) splits = 1;
+    g.splits = splits;
+    g.kchunk = ((ksteps + splits - 1) / splits) * BKB;
+    hipLaunchKernelGGL((gemm128_kernel<1, 3>), dim3((unsigned)(tm * tn), (unsigned)splits), dim3(256), lds, s, g);
+  }
   const int64_t total = (int64_t)cout * N;
   hipLaunchKernelGGL(wgrad_permute_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, scratch, dw, cout,
                      cin, taps);

@@ -1370,12 +1370,18 @@ extern "C" int dp_cdn_build(const int32_t* tgt_off, const int32_t* tgt_label, co
   return dp_check_launch("dp_cdn_build");
 }
 
-extern "C" int dp_grad_sqnorm(const float* g, int64_t n, float* out, void* stream) {
-  DP_REQUIRE(g && out && n > 0, "dp_grad_sqnorm: bad arguments");
+extern "C" int64_t dp_grad_sqnorm_ws_floats(int64_t n) {
+  return n > 0 ? std::min<int64_t>((n + 255) / 256, DP_SQNORM_PARTS) : 0;
+}
+
+extern "C" int dp_grad_sqnorm(const float* g, int64_t n, float* out, float* ws, int64_t ws_floats, void* stream) {
+  DP_REQUIRE(g && out && ws && n > 0, "dp_grad_sqnorm: bad arguments");
+  const int64_t grid = dp_grad_sqnorm_ws_floats(n);
+  DP_REQUIRE(ws_floats >= grid, "dp_grad_sqnorm: workspace holds %lld floats, needs dp_grad_sqnorm_ws_floats(n) = %lld",
+             (long long)ws_floats, (long long)grid);
   hipStream_t s = as_stream(stream);
-  const int grid = (int)std::min<int64_t>((n + 255) / 256, DP_SQNORM_PARTS);
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, s, g, n, out + 1);
-  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, out + 1, grid, out);
+  hipLaunchKernelGGL(sqnorm_kernel, dim3((int)grid), dim3(256), 0, s, g, n, ws);
+  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, ws, (int)grid, out);
   return dp_check_launch("dp_grad_sqnorm");
 }
 

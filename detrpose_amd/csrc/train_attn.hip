@@ -404,10 +404,17 @@ bool dispatch_kt(int L, bool bwd, const void* const* a, const int64_t* n, float 
 
 // Called by dp_attn_fwd / dp_attn_bwd (train.hip) for bf16: false when the shape is not covered
 // (sequence > 128 tokens, head dim not 16 / 32 / 48 / 64) and the scalar kernels run instead.
+// every row start of a bf16 operand with row pitch ld (elements) is 16-byte aligned
+static bool rows16(const void* p, int64_t ld) {
+  return p != nullptr && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0;
+}
+
 bool dp_attn_fwd_mfma(const void* q, int32_t ld_q, const void* k, const void* v, int32_t ld_kv, void* out, int32_t ld_o,
                       float* p_save, const uint8_t* mask, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si,
                       int64_t st, int32_t seqlen, int32_t nhead, int32_t dh, float scale, hipStream_t s) {
   if (seqlen > (dh == 32 ? 400 : 128)) return false;
+  // 16-byte bf16x8 / 8-byte bf16x4 rows: other layouts take the scalar kernels
+  if (!rows16(q, ld_q) || !rows16(k, ld_kv) || !rows16(v, ld_kv) || !rows16(out, ld_o)) return false;
   const void* a[6] = {q, k, v, out, p_save, mask};
   const int64_t n[9] = {ld_q, ld_kv, ld_o, (int64_t)n_outer * n_inner * nhead, n_inner, so, si, st, nhead};
   switch (dh) {
@@ -424,6 +431,9 @@ bool dp_attn_bwd_mfma(const void* q, int32_t ld_q, const void* k, const void* v,
                       int32_t ld_dkv, int32_t n_outer, int32_t n_inner, int64_t so, int64_t si, int64_t st,
                       int32_t seqlen, int32_t nhead, int32_t dh, float scale, hipStream_t s) {
   if (seqlen > (dh == 32 ? 400 : 128)) return false;
+  if (!rows16(q, ld_q) || !rows16(k, ld_kv) || !rows16(v, ld_kv) || !rows16(out, ld_o) || !rows16(dout, ld_o) ||
+      !rows16(dq, ld_dq) || !rows16(dk, ld_dkv) || !rows16(dv, ld_dkv))
+    return false;
   const void* a[9] = {q, k, v, p_save, dout, out, dq, dk, dv};
   const int64_t n[11] = {ld_q, ld_kv, ld_o, ld_dq, (int64_t)n_outer * n_inner * nhead, n_inner, so, si, st, ld_dkv,
                          nhead};

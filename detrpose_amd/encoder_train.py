@@ -36,6 +36,7 @@ their gradients f32 (the TrainEngine's flat buffers, reference names).
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -89,27 +90,29 @@ class V:
 COMM_LOG = None   # when a list: every all_reduce is synchronised and timed into it (bench.py's train leg)
 
 
-def all_reduce(t):
+def all_reduce(t, async_op=False, group=None):
     """Sum over the ranks in place (RCCL on device tensors; host-staged under gloo, whose
-    collectives take host tensors: the one-GPU multi-rank rehearsal and tests)."""
+    collectives take host tensors: the one-GPU multi-rank rehearsal and tests). async_op: return
+    the RCCL work handle (wait() before reading t); host-staged reductions complete here (None)."""
     if COMM_LOG is not None:
         import time
         torch.cuda.synchronize(t.device) if t.is_cuda else None
         t0 = time.perf_counter()
-        _all_reduce(t)
+        _all_reduce(t, False, group)
         torch.cuda.synchronize(t.device) if t.is_cuda else None
         COMM_LOG.append((t.numel() * t.element_size(), time.perf_counter() - t0))
-        return
-    _all_reduce(t)
+        return None
+    return _all_reduce(t, async_op, group)
 
 
-def _all_reduce(t):
-    if torch.distributed.get_backend() == "gloo" and t.is_cuda:
+def _all_reduce(t, async_op, group=None):
+    if torch.distributed.get_backend(group) == "gloo" and t.is_cuda:
         h = t.cpu()
-        torch.distributed.all_reduce(h)
+        torch.distributed.all_reduce(h, group=group)
         t.copy_(h)
-    else:
-        torch.distributed.all_reduce(t)
+        return None
+    w = torch.distributed.all_reduce(t, async_op=async_op, group=group)
+    return w if async_op else None
 
 
 def _host(fn):
@@ -135,6 +138,9 @@ class TapePlan:
         self.vec = 8 if self.code == DP_BF16 else 4
         self.dev = eng.device
         self.op_flops = {}
+        # stored layer outputs by reference prefix (the forced-state parity test reads them,
+        # tests/test_gpu_full_train_step_l.py; the oracle's TAP names)
+        self.taps = {}
         self.arena, self.bufs = [], []
         self._bwd = []
         self.world, self.rank = 1, 0
@@ -168,6 +174,12 @@ class TapePlan:
 
     def cost(self, name, flops):
         self.op_flops[name] = self.op_flops.get(name, 0.0) + flops
+
+    def batch_packs(self):
+        """The pack tape's launches merged into one (Tape.batch_packs; DETRPOSE_PACK_BATCH=0 keeps
+        one launch per weight, A/B)."""
+        if os.environ.get("DETRPOSE_PACK_BATCH", "1") != "0":
+            self.pk.batch_packs()
 
     def _record_backward(self, zero=True, extra_zero=()):
         """Gradient buffers for every stored map (one arena), then the ops in reverse. The
@@ -334,10 +346,17 @@ class TapePlan:
         self._bwd.append(bwd)
         return z
 
-    def bn(self, name, branches, out, act, res=None):
+    def bn(self, name, branches, out, act, res=None, tap=None):
         """out = act(sum_k BN_k(z_k)) [+ res], BatchNorm2d on batch statistics (SyncBN over the
-        ranks), running statistics updated. branches: [(z view, BN prefix)] (one or two)."""
+        ranks), running statistics updated. branches: [(z view, BN prefix)] (one or two). tap:
+        the reference prefix `out` is stored under in self.taps (default: the layer's, from the
+        BN prefix)."""
         lib, eng = self.lib, self.eng
+        if tap is None:
+            tap = branches[0][1][:-len(".norm")]
+            if len(branches) > 1:
+                tap = tap[:-len(".conv1")]
+        self.taps[tap] = out
         c = out.c
         rows = out.rows
         code = self.code
@@ -502,6 +521,7 @@ class EncoderTrainPlan(TapePlan):
                 lv.gp, self.code, n, B, n, C.c_float(1.0), 1))
         self._record_backward(extra_zero=[feats_plan.grad_arena] if feats_plan is not None else ())
         self.d_feats = [f.buf.g for f in self.feats]
+        self.batch_packs()
         eng.cur = prev
 
     def csp(self, name, p, x, out):
@@ -523,7 +543,7 @@ class EncoderTrainPlan(TapePlan):
             z1 = self.conv(f"{name}.vgg{i}.c1", q + ".conv2.conv.weight", [(cur, 0, c4)], c4)
             dst = out if i == nb - 1 else self.view(B, H, W, c4)
             self.bn(f"{name}.vgg{i}", [(z3, q + ".conv1.norm"), (z1, q + ".conv2.norm")], dst, enc.act,
-                    res=x2 if i == nb - 1 else None)
+                    res=x2 if i == nb - 1 else None, tap=p if i == nb - 1 else None)
             cur = dst
 
     def elan(self, name, p, x, out):
@@ -609,6 +629,7 @@ class EncoderTrainPlan(TapePlan):
         self.gemm(fw, f"aifi{i}.linear1.act", x1.xp, Cc, 1, W1p, 1, Cc, h.xp, F_, rows, F_, Cc, bias=_p(b1), act=act)
         f = self.view(1, 1, rows, Cc)
         self.gemm(fw, f"aifi{i}.linear2", h.xp, F_, 1, W2p, 1, F_, f.xp, Cc, rows, Cc, F_, bias=_p(b2))
+        self.taps[lp] = out
         s2, st2 = self.view(1, 1, rows, Cc), self.f32(rows, 2)
         n2g, n2b = eng.params[lp + ".norm2.weight"], eng.params[lp + ".norm2.bias"]
         fw.op(f"aifi{i}.norm2", lib.dp_ln_fwd, out.xp, Cc, x1.xp, f.xp, s2.xp, _p(st2), _p(n2g), _p(n2b),

@@ -95,12 +95,11 @@ class Trainer:
         if ema:
             self.eng.ema_init()
         self.grad_accum_steps = int(pick(grad_accum_steps, "grad_accum_steps"))
-        # tapes replayed from hipGraphs after their first (eager) run; default on at world size 1
-        # (world > 1: the SyncBN collectives are host ops between the encoder's launches)
+        # tapes replayed from hipGraphs after their first (eager) run, at every world size (at
+        # world > 1 the SyncBN collectives are host ops that cut the encoder's tapes into graph
+        # segments: graph -> collective -> graph, train_engine.Tape)
         if graphs is None:
-            graphs = os.environ.get("DETRPOSE_TRAIN_GRAPHS", "1") != "0" and not (
-                torch.distributed.is_available() and torch.distributed.is_initialized()
-                and torch.distributed.get_world_size() > 1)
+            graphs = os.environ.get("DETRPOSE_TRAIN_GRAPHS", "1") != "0"
         self.graphs = bool(graphs)
         self.dn_number, self.label_noise_ratio = dn_number, label_noise_ratio
         self.weights = weights
@@ -180,9 +179,12 @@ class Trainer:
             for t, nm in tapes:
                 t.use_graph = on and (only is None or nm in only.split(","))
 
-    def sub_step(self, images, targets):
+    def sub_step(self, images, targets, after=None):
         """Forward + criterion + backward of one sub-batch (engine.py:44-59): the gradients of
-        its summed losses in eng.grad_flat (overwritten). Returns (loss names, device losses)."""
+        its summed losses in eng.grad_flat (overwritten). after(part): called as each part's
+        backward finishes ('transformer', 'encoder', 'backbone'; the DDP buckets). Returns (loss
+        names, device losses)."""
+        after = after or (lambda part: None)
         eng = self.eng
         B = images.shape[0]
         if self.scope == "full" and getattr(self, "bb", None) is not None:
@@ -200,9 +202,12 @@ class Trainer:
         plan.forward()
         keys, vals = plan.criterion(packed, sizes, groups, weights=self.weights)
         plan.backward()
+        after("transformer")
         if full:
             self.ep.backward()
+            after("encoder")
             self.bb.backward()
+            after("backbone")
         return keys, vals
 
     def step(self, images, targets, update=True):
@@ -221,18 +226,48 @@ class Trainer:
         sub = B // n
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         eng.step_ok_reset()
+        world = torch.distributed.get_world_size() if (torch.distributed.is_available() and
+                                                       torch.distributed.is_initialized()) else 1
+        buckets = {p: (lo, hi) for p, lo, hi in eng.grad_buckets()}
+        works = []
+        if world > 1 and getattr(self, "_ddp_group", None) is None:
+            # the buckets' own communicator (every rank creates it at its first step): on one
+            # communicator RCCL runs collectives in issue order, and the encoder backward's SyncBN
+            # reductions would queue behind the transformer bucket instead of overlapping it
+            self._ddp_group = torch.distributed.new_group(list(range(world)))
+
+        def bucket_done(first):
+            # DDP's bucketed all-reduce overlapped with the backward (dist_utils.py:111-133 wraps
+            # the model in DDP, whose hooks reduce each bucket as its gradients are ready): as a
+            # part's backward of the LAST sub-batch finishes, its range gets the accumulated
+            # sub-batch sum and its all-reduce starts (RCCL: async on the collective stream, while
+            # the next part's backward runs; gloo: host-staged, in order)
+            def hook(part):
+                lo, hi = buckets[part]
+                eng.accumulate_grads(first=first, last=True, lo=lo, hi=hi)
+                works.append(all_reduce(eng.grad_flat[lo:hi], async_op=True, group=self._ddp_group))
+            return hook
+
         for j in range(n):
-            keys, vals = self.sub_step(images[j * sub:(j + 1) * sub], targets[j * sub:(j + 1) * sub])
+            last = j == n - 1
+            ddp = world > 1 and last
+            keys, vals = self.sub_step(images[j * sub:(j + 1) * sub], targets[j * sub:(j + 1) * sub],
+                                       after=bucket_done(j == 0) if ddp else None)
             eng.check_finite(vals)
-            eng.accumulate_grads(first=j == 0, last=j == n - 1)
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            world = torch.distributed.get_world_size()
-            if world > 1:
-                # DDP: mean of the ranks' gradients (one all-reduce of the flat f32 buffer)
-                all_reduce(eng.grad_flat)
-                _lib.check(lib.dp_convert_rows(_p(eng.grad_flat), 0, eng.grad_flat.numel(), _p(eng.grad_flat), 0,
-                                               eng.grad_flat.numel(), 1, eng.grad_flat.numel(), 1.0 / world, 0, s),
-                           "grad mean")
+            if not ddp:
+                eng.accumulate_grads(first=j == 0, last=last)
+        if world > 1:
+            # the step guard over every rank's losses (4 bytes): the reference checks the
+            # rank-reduced loss (engine.py:63-71), so all ranks skip or update together and the
+            # replicas stay identical
+            all_reduce(eng.bad)
+            for w in works:
+                if w is not None:
+                    w.wait()
+            # DDP: the mean of the ranks' gradients
+            _lib.check(lib.dp_convert_rows(_p(eng.grad_flat), 0, eng.grad_flat.numel(), _p(eng.grad_flat), 0,
+                                           eng.grad_flat.numel(), 1, eng.grad_flat.numel(), 1.0 / world, 0, s),
+                       "grad mean")
         if update:
             eng.optimizer_step(**self.opt)
             if self.ema is not None:

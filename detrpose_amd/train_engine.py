@@ -62,10 +62,12 @@ def dn_match(sizes, pad_size, num_group):
 class Tape:
     """Recorded launches with their descriptors kept alive.
 
-    use_graph: after one eager run, the launches are captured once into a hipGraph
-    (torch.cuda.CUDAGraph) and later runs replay it (one launch instead of one ctypes call per op).
-    Every op's arguments are fixed buffers and descriptors, so a replay is the eager run; a tape
-    holding host ops (the SyncBN collectives of world > 1) always runs eagerly."""
+    use_graph: after one eager run, the launches are captured once into hipGraphs
+    (torch.cuda.CUDAGraph) and later runs replay them (one launch instead of one ctypes call per
+    op). Every op's arguments are fixed buffers and descriptors, so a replay is the eager run. A
+    tape holding host ops (the SyncBN collectives of world > 1) is cut at them into segments:
+    each run of device ops between two host ops is its own graph, and the host ops run between
+    the replays in stream order (graph -> collective -> graph), so world > 1 keeps the replay."""
 
     def __init__(self, lib, device):
         self.lib = lib
@@ -74,19 +76,25 @@ class Tape:
         self.keep = []
         self.use_graph = False
         self.runs = 0
-        self._graph = None
+        self._graph = None   # [("graph", CUDAGraph) | ("host", fn)] once captured
 
     def op(self, name, fn, *args):
         self.ops.append((name, fn, args))
         self._graph = None
 
     @property
-    def graphable(self):
-        return not any(getattr(fn, "host", False) for _, fn, _ in self.ops)
+    def n_host(self):
+        """Host ops on the tape (each one a cut between two graph segments)."""
+        return sum(1 for _, fn, _ in self.ops if getattr(fn, "host", False))
 
-    def _launch(self, stream, debug):
+    @property
+    def n_graphs(self):
+        """Graph segments of the captured tape (0 before capture)."""
+        return sum(1 for k, _ in self._graph if k == "graph") if self._graph else 0
+
+    def _launch(self, stream, debug, ops=None):
         s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream)
-        for name, fn, args in self.ops:
+        for name, fn, args in (self.ops if ops is None else ops):
             rc = fn(*args, s)
             if rc:
                 _lib.check(rc, name)
@@ -94,14 +102,73 @@ class Tape:
                 torch.cuda.synchronize()
                 debug(name)
 
-    def run(self, stream=None, debug=None):
-        if self.use_graph and stream is None and debug is None and self.runs > 0 and self.graphable:
-            if self._graph is None:
+    def batch_packs(self):
+        """Replace the tape's weight packs (dp_conv_pack calls, and the dp_convert_rows f32 ->
+        dtype copies of whole weights) by ONE dp_conv_pack_batch launch over a device table of
+        their descriptors. Every pack writes its own output from the f32 master, so their order is
+        free; the tape's other ops keep theirs, after the batch."""
+        lib = self.lib
+        rows, rest = [], []
+        for name, fn, args in self.ops:
+            if fn is lib.dp_conv_pack:
+                w, cout, cin, kh, kw, out, kpad, kc, mode, scale, dt = args
+                rows.append((w, out, scale, cout, cin, kh, kw, kpad, kc, mode, dt))
+            elif (fn is lib.dp_convert_rows and len(args) == 10 and args[1] == _lib.DP_F32 and args[6] == 1 and
+                  args[2] == args[5] == args[7] and not args[9] and getattr(args[8], "value", args[8]) == 1.0):
+                # dp_convert_rows(src, F32, n, dst, code, n, 1, n, 1.0, 0): a whole-weight copy
+                rows.append((args[0], args[3], None, args[2], 1, 1, 1, 0, 0, 5, args[4]))
+            else:
+                rest.append((name, fn, args))
+        if len(rows) < 2:
+            return
+        n = len(rows)
+        tab = (_lib.PackDesc * n)()
+        for i, (w, out, scale, cout, cin, kh, kw, kpad, kc, mode, dt) in enumerate(rows):
+            tab[i] = _lib.PackDesc(w, out, scale, cout, cin, kh, kw, kpad, kc, mode, dt)
+        _lib.check(lib.dp_conv_pack_check(tab, n), "pack table")
+        dev = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(self.device)
+        self.keep.append(dev)
+        self.ops = [("pack.batch", lib.dp_conv_pack_batch, (_p(dev), n, 64))] + rest
+        self._graph = None
+
+    @staticmethod
+    def segments(ops):
+        """The tape cut at its host ops: [("device", [ops...]) | ("host", op)] in tape order, no
+        empty device runs."""
+        segs, run = [], []
+        for op in ops:
+            if getattr(op[1], "host", False):
+                if run:
+                    segs.append(("device", run))
+                    run = []
+                segs.append(("host", op))
+            else:
+                run.append(op)
+        if run:
+            segs.append(("device", run))
+        return segs
+
+    def _capture(self):
+        out = []
+        for kind, x in self.segments(self.ops):
+            if kind == "device":
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self._launch(None, None)
-                self._graph = g
-            self._graph.replay()
+                    self._launch(None, None, x)
+                out.append(("graph", g))
+            else:
+                out.append(("host", x))
+        return out
+
+    def run(self, stream=None, debug=None):
+        if self.use_graph and stream is None and debug is None and self.runs > 0:
+            if self._graph is None:
+                self._graph = self._capture()
+            for kind, x in self._graph:
+                if kind == "graph":
+                    x.replay()
+                else:
+                    self._launch(None, None, [x])
         else:
             self._launch(stream, debug)
         self.runs += 1
@@ -155,7 +222,8 @@ class TrainEngine:
         self.grad_flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.sqnorm = torch.zeros(1 + _lib.DP_SQNORM_PARTS, dtype=torch.float32, device=dev)   # [norm^2 | partials]
+        self.sqnorm = torch.zeros(1, dtype=torch.float32, device=dev)   # ||g||^2 (dp_grad_sqnorm)
+        self.sqnorm_ws = torch.zeros(max(1, self.lib.dp_grad_sqnorm_ws_floats(total)), dtype=torch.float32, device=dev)
         self.bad = torch.zeros(1, dtype=torch.float32, device=dev)   # step guard (dp_finite_guard)
         self.grad_acc = None   # gradient-accumulation buffer (accumulate_grads)
         self.opt_step = 0
@@ -272,9 +340,14 @@ class TrainEngine:
         lib = self.lib
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         n = self.master.numel()
+        # host counters (AdamW bias correction here, the EMA warm-up in ema_update): a step the
+        # device guard skips still advances them. The reference never continues past a
+        # non-finite loss (engine.py:62-66 exits), so no reference behaviour is matched or broken
+        # by it; keeping them host-side keeps the update free of host synchronisation.
         self.opt_step += 1
         if max_norm and max_norm > 0:
-            _lib.check(lib.dp_grad_sqnorm(_p(self.grad_flat), n, _p(self.sqnorm), s), "dp_grad_sqnorm")
+            _lib.check(lib.dp_grad_sqnorm(_p(self.grad_flat), n, _p(self.sqnorm), _p(self.sqnorm_ws),
+                                              self.sqnorm_ws.numel(), s), "dp_grad_sqnorm")
             _lib.check(lib.dp_finite_guard(_p(self.sqnorm), 1, _p(self.bad), s), "dp_finite_guard")
         for o0, o1, lr_ in ((0, self.bb_end, backbone_lr), (self.bb_end, n, lr)):
             if o1 > o0:
@@ -298,20 +371,36 @@ class TrainEngine:
         """Whether the last optimizer step was skipped by the guard (synchronises)."""
         return float(self.bad) != 0.0
 
-    def accumulate_grads(self, first: bool, last: bool):
+    def accumulate_grads(self, first: bool, last: bool, lo: int = 0, hi: int = None):
         """Gradient accumulation over sub-batches (engine.py:43-59: .grad sums over the loop's
         backward calls): every backward overwrites grad_flat, so sub-batch j's gradient is added
         into grad_acc, and the last one's grad_flat receives the sum (2 passes over the flat
-        buffer per step for 2 sub-batches)."""
+        buffer per step for 2 sub-batches). [lo, hi): one range of the flat buffer (a DDP bucket)."""
         if first and last:
             return
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        n = self.grad_flat.numel()
+        hi = self.grad_flat.numel() if hi is None else hi
+        n = hi - lo
         if self.grad_acc is None:
             self.grad_acc = torch.empty_like(self.grad_flat)
         src, dst, acc = (self.grad_acc, self.grad_flat, 1) if last else (self.grad_flat, self.grad_acc, 0 if first else 1)
-        _lib.check(self.lib.dp_convert_rows(_p(src), DP_F32, n, _p(dst), DP_F32, n, 1, n, C.c_float(1.0), acc, s),
-                   "grad accumulate")
+        _lib.check(self.lib.dp_convert_rows(_p(src, lo), DP_F32, n, _p(dst, lo), DP_F32, n, 1, n, C.c_float(1.0), acc,
+                                            s), "grad accumulate")
+
+    def grad_buckets(self):
+        """DDP buckets of the flat gradient in the order the backward finishes them: [(part, lo,
+        hi)] for the transformer, the encoder, the backbone (each part's parameters are one range
+        of the flat buffer, module order backbone | encoder | transformer)."""
+        out = []
+        for pre in ("transformer.", "encoder.", "backbone."):
+            ns = [n for n in self.pnames if n.startswith(pre)]
+            if not ns:
+                continue
+            i0 = self.pnames.index(ns[0])
+            assert self.pnames[i0:i0 + len(ns)] == ns, f"{pre} parameters are not one range of the flat buffer"
+            out.append((pre[:-1], self.offsets[ns[0]][0], self.offsets[ns[-1]][1]))
+        assert sum(h - l for _, l, h in out) == sum(b - a for a, b in self.offsets.values())
+        return out
 
     def ema_init(self):
         self.ema = self.master.clone()

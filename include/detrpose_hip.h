@@ -555,11 +555,13 @@ int dp_cdn_build(const int32_t* tgt_off, const int32_t* tgt_label, const float* 
                  const float* tgt_boxes, const float* sigmas, int32_t batch, int32_t pad, int32_t single_pad,
                  int32_t nkp, float label_noise_ratio, int32_t num_classes, float img_h, float img_w, uint64_t seed,
                  int32_t* dn_label, float* dn_ref, void* stream);
-/* Squared L2 norm of a gradient buffer: clip_grad_norm_'s norm, into out[0]; out holds
- * 1 + DP_SQNORM_PARTS floats (out[1..] are the block partials). Deterministic (fixed-order
- * reduction, no float atomics): identical gradients give bit-identical norms on every rank. */
+/* Squared L2 norm of a gradient buffer: clip_grad_norm_'s norm, into out[0]. ws receives the
+ * block partials: it must hold dp_grad_sqnorm_ws_floats(n) floats (at most DP_SQNORM_PARTS;
+ * checked, an error otherwise). Deterministic (fixed-order reduction, no float atomics):
+ * identical gradients give bit-identical norms on every rank. */
 #define DP_SQNORM_PARTS 1024
-int dp_grad_sqnorm(const float* g, int64_t n, float* out, void* stream);
+int64_t dp_grad_sqnorm_ws_floats(int64_t n);
+int dp_grad_sqnorm(const float* g, int64_t n, float* out, float* ws, int64_t ws_floats, void* stream);
 /* torch.optim.AdamW step over a flat f32 parameter buffer (decoupled weight decay, bias
  * correction for `step`), after clip_grad_norm_(max_norm) (src/solver/engine.py:78-89) read
  * from grad_sqnorm on the device (max_norm <= 0: no clipping). Parameters and moments are left
@@ -641,6 +643,19 @@ int dp_im2col(const void* x, int64_t bstride, int32_t pstride, int64_t cstride, 
  * multiplied by it (FrozenBatchNorm2d's scale folded into the conv, hgnetv2.py:51-61). */
 int dp_conv_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out, int32_t kpad,
                  int32_t kc, int32_t mode, const float* scale, int32_t dtype, void* stream);
+/* One dp_conv_pack call per entry (same fields; mode 5: a plain f32 -> dtype copy of `cout`
+ * elements, the bf16 copy of a linear weight), all in ONE launch: a training plan's weight packs
+ * of one optimizer step. dp_conv_pack_check validates a host copy of the table (once, when the
+ * plan is built); dp_conv_pack_batch reads the table from device memory (tab_dev), its x blocks
+ * striding over each pack's elements (blocks_per_pack of them). */
+typedef struct dp_pack_desc {
+  const float* w;
+  void* out;
+  const float* scale;
+  int32_t cout, cin, kh, kw, kpad, kc, mode, dtype;
+} dp_pack_desc;
+int dp_conv_pack_check(const dp_pack_desc* tab, int32_t n);
+int dp_conv_pack_batch(const dp_pack_desc* tab_dev, int32_t n, int32_t blocks_per_pack, void* stream);
 /* Depthwise conv backward (k <= 5, any stride / pad): dx (+=, NULL to skip) and dw f32
  * [c][k][k] (+=, NULL to skip) from dz. x / dz / dx: NHWC with image and pixel strides. */
 int dp_dwconv_bwd(const void* x, int64_t x_bstride, int32_t x_pstride, const void* dz, int64_t z_bstride,

@@ -27,6 +27,17 @@ import torch.nn.functional as F
 
 # ----------------------------------------------------------------------------- helpers
 
+# Test hook (tests/test_gpu_full_train_step_l.py, "teacher forcing"): when set, TAP(name, y) is
+# applied to every stored layer output of the backbone / training encoder (name = the layer's
+# reference prefix) and returns the tensor to continue with. The forced-state check returns
+# y + (gpu_value - y).detach(): the GPU run's stored forward value, with y's gradient path.
+TAP = None
+
+
+def tap(name, y):
+    return y if TAP is None else TAP(name, y)
+
+
 
 def _bn_eval(x, sd, p, eps=1e-5):
     """nn.BatchNorm2d in eval == (x-mean)/sqrt(var+eps)*w+b (NCHW)."""
@@ -170,20 +181,21 @@ def backbone(x, sd, name, return_idx, use_lab):
     HG_Block 319-329 (agg='se': squeeze 1x1 -> excitation 1x1), LightConvBNAct 163-166."""
     stem_ch, stages = ARCH[name]
     p = "backbone.stem"
-    x = conv_bn_act(x, sd, p + ".stem1", stride=2, lab=use_lab)
+    x = tap(p + ".stem1", conv_bn_act(x, sd, p + ".stem1", stride=2, lab=use_lab))
     x = F.pad(x, (0, 1, 0, 1))
-    x2 = conv_bn_act(x, sd, p + ".stem2a", lab=use_lab)
+    x2 = tap(p + ".stem2a", conv_bn_act(x, sd, p + ".stem2a", lab=use_lab))
     x2 = F.pad(x2, (0, 1, 0, 1))
-    x2 = conv_bn_act(x2, sd, p + ".stem2b", lab=use_lab)
+    x2 = tap(p + ".stem2b", conv_bn_act(x2, sd, p + ".stem2b", lab=use_lab))
     x1 = F.max_pool2d(x, 2, 1, ceil_mode=True)
     x = torch.cat([x1, x2], 1)
-    x = conv_bn_act(x, sd, p + ".stem3", stride=2, lab=use_lab)
-    x = conv_bn_act(x, sd, p + ".stem4", lab=use_lab)
+    x = tap(p + ".stem3", conv_bn_act(x, sd, p + ".stem3", stride=2, lab=use_lab))
+    x = tap(p + ".stem4", conv_bn_act(x, sd, p + ".stem4", lab=use_lab))
     outs = []
     for si, (cin, mid, cout, nblk, down, light, k, nlayer) in enumerate(stages):
         sp = f"backbone.stages.{si}"
         if down:
-            x = conv_bn_act(x, sd, sp + ".downsample", stride=2, groups=cin, act=False, lab=use_lab)
+            x = tap(sp + ".downsample",
+                    conv_bn_act(x, sd, sp + ".downsample", stride=2, groups=cin, act=False, lab=use_lab))
         for bi in range(nblk):
             bp = f"{sp}.blocks.{bi}"
             identity = x
@@ -191,16 +203,17 @@ def backbone(x, sd, name, return_idx, use_lab):
             for li in range(nlayer):
                 lp = f"{bp}.layers.{li}"
                 if light:
-                    x = conv_bn_act(x, sd, lp + ".conv1", act=False, lab=use_lab)
-                    x = conv_bn_act(x, sd, lp + ".conv2", groups=x.shape[1], lab=use_lab)
+                    x = tap(lp + ".conv1", conv_bn_act(x, sd, lp + ".conv1", act=False, lab=use_lab))
+                    x = tap(lp + ".conv2", conv_bn_act(x, sd, lp + ".conv2", groups=x.shape[1], lab=use_lab))
                 else:
-                    x = conv_bn_act(x, sd, lp, lab=use_lab)
+                    x = tap(lp, conv_bn_act(x, sd, lp, lab=use_lab))
                 feats.append(x)
             x = torch.cat(feats, 1)
-            x = conv_bn_act(x, sd, bp + ".aggregation.0", lab=use_lab)
+            x = tap(bp + ".aggregation.0", conv_bn_act(x, sd, bp + ".aggregation.0", lab=use_lab))
             x = conv_bn_act(x, sd, bp + ".aggregation.1", lab=use_lab)
             if bi > 0:
                 x = x + identity
+            x = tap(bp + ".aggregation.1", x)
         if si in return_idx:
             outs.append(x)
     return outs

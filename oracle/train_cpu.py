@@ -29,7 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from oracle import criterion_cpu as crit
-from oracle.detrpose_cpu import (anchors_and_mask, bilinear_gather, inverse_sigmoid, msda_core, sine_embedding,
+from oracle.detrpose_cpu import (anchors_and_mask, bilinear_gather, inverse_sigmoid, msda_core, sine_embedding, tap,
                                  weighting_function)
 
 T_ = "transformer."
@@ -280,6 +280,11 @@ def _conv_norm_t(x, P, p, stats, stride=1, groups=1, act=None):
     return _act(_bn_train(x, P, p + ".norm", stats), act)
 
 
+def _conv_norm_tap(x, P, p, stats, stride=1, groups=1, act=None):
+    """_conv_norm_t, its output a stored layer output (the test hook oracle.detrpose_cpu.TAP)."""
+    return tap(p, _conv_norm_t(x, P, p, stats, stride, groups, act))
+
+
 def _vgg_t(x, P, p, stats, act):
     """VGGBlock.forward, training (hybrid_encoder.py:139-154): act(BN(conv3x3) + BN(conv1x1))."""
     return _act(_conv_norm_t(x, P, p + ".conv1", stats) + _conv_norm_t(x, P, p + ".conv2", stats), act)
@@ -287,22 +292,24 @@ def _vgg_t(x, P, p, stats, act):
 
 def _csp_t(x, P, p, stats, nblk, act):
     """CSPLayer.forward (hybrid_encoder.py:215-240)."""
-    x1 = _conv_norm_t(x, P, p + ".conv1", stats, act=act)
+    x1 = _conv_norm_tap(x, P, p + ".conv1", stats, act=act)
     for i in range(nblk):
         x1 = _vgg_t(x1, P, f"{p}.bottlenecks.{i}", stats, act)
-    return x1 + _conv_norm_t(x, P, p + ".conv2", stats, act=act)
+        if i < nblk - 1:   # the last block's output is stored with the conv2 branch added
+            x1 = tap(f"{p}.bottlenecks.{i}", x1)
+    return tap(p, x1 + _conv_norm_tap(x, P, p + ".conv2", stats, act=act))
 
 
 def _elan_t(x, P, p, stats, nblk, act="silu"):
     """RepNCSPELAN4.forward (hybrid_encoder.py:192-212)."""
-    y = _conv_norm_t(x, P, p + ".cv1", stats, act=act)
+    y = _conv_norm_tap(x, P, p + ".cv1", stats, act=act)
     c = y.shape[1] // 2
     ys = [y[:, :c], y[:, c:]]
     z = _csp_t(ys[-1], P, p + ".cv2.0", stats, nblk, act)
-    ys.append(_conv_norm_t(z, P, p + ".cv2.1", stats, act=act))
+    ys.append(_conv_norm_tap(z, P, p + ".cv2.1", stats, act=act))
     z = _csp_t(ys[-1], P, p + ".cv3.0", stats, nblk, act)
-    ys.append(_conv_norm_t(z, P, p + ".cv3.1", stats, act=act))
-    return _conv_norm_t(torch.cat(ys, 1), P, p + ".cv4", stats, act=act)
+    ys.append(_conv_norm_tap(z, P, p + ".cv3.1", stats, act=act))
+    return _conv_norm_tap(torch.cat(ys, 1), P, p + ".cv4", stats, act=act)
 
 
 def train_encoder(feats, P, cfg, stats=None):
@@ -317,7 +324,8 @@ def train_encoder(feats, P, cfg, stats=None):
     nblk = round(3 * cfg["depth_mult"])
     enc_idx = cfg.get("use_encoder_idx", [2])
     E = "encoder."
-    proj = [_bn_train(F.conv2d(f, P[f"{E}input_proj.{i}.conv.weight"]), P, f"{E}input_proj.{i}.norm", stats)
+    proj = [tap(f"{E}input_proj.{i}",
+                _bn_train(F.conv2d(f, P[f"{E}input_proj.{i}.conv.weight"]), P, f"{E}input_proj.{i}.norm", stats))
             for i, f in enumerate(feats)]
     for i, ei in enumerate(enc_idx):
         B, _, H, W = proj[ei].shape
@@ -336,17 +344,17 @@ def train_encoder(feats, P, cfg, stats=None):
         src = _ln(src + s2, P, p + ".norm1")
         s2 = _lin(_act(_lin(src, P, p + ".linear1"), cfg["enc_act"]), P, p + ".linear2")
         src = _ln(src + s2, P, p + ".norm2")
-        proj[ei] = src.permute(0, 2, 1).reshape(B, C, H, W)
+        proj[ei] = tap(p, src.permute(0, 2, 1).reshape(B, C, H, W))
     inner = [proj[-1]]
     for idx in range(nlev - 1, 0, -1):
         j = nlev - 1 - idx
-        high = _conv_norm_t(inner[0], P, f"{E}lateral_convs.{j}", stats, act=cfg["act"])
+        high = _conv_norm_tap(inner[0], P, f"{E}lateral_convs.{j}", stats, act=cfg["act"])
         inner[0] = high
         up = F.interpolate(high, scale_factor=2.0, mode="nearest")
         inner.insert(0, _elan_t(torch.cat([up, proj[idx - 1]], 1), P, f"{E}fpn_blocks.{j}", stats, nblk))
     outs = [inner[0]]
     for idx in range(nlev - 1):
-        d = _conv_norm_t(outs[-1], P, f"{E}downsample_convs.{idx}.0.cv1", stats)
-        d = _conv_norm_t(d, P, f"{E}downsample_convs.{idx}.0.cv2", stats, stride=2, groups=d.shape[1])
+        d = _conv_norm_tap(outs[-1], P, f"{E}downsample_convs.{idx}.0.cv1", stats)
+        d = _conv_norm_tap(d, P, f"{E}downsample_convs.{idx}.0.cv2", stats, stride=2, groups=d.shape[1])
         outs.append(_elan_t(torch.cat([d, inner[idx + 1]], 1), P, f"{E}pan_blocks.{idx}", stats, nblk))
     return outs

@@ -429,3 +429,25 @@ def test_conv_wgrad_implicit(B, h, w, cin, cout, k, st, pad, xpad):
     ref = wr.grad + 0.5
     err = (dw - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-3, err
+
+
+def test_conv_wgrad_more_than_2p24_pixels():
+    """dp_conv_wgrad past 2^24 output pixels (its gather's float-reciprocal split is exact below
+    2^24): the batch runs as image chunks accumulating into one scratch. 4100 images of 64 x 64
+    (16.8 M pixels, two chunks) vs the fp32 autograd weight gradient."""
+    lib = _lib.load()
+    torch.manual_seed(9)
+    B, h, w, cin, cout, k = 4100, 64, 64, 8, 16, 3
+    assert B * h * w >= 1 << 24
+    x = torch.randn(B, h, w, cin, device=DEV).bfloat16()
+    dz = torch.randn(B * h * w, cout, device=DEV).bfloat16()
+    with torch.backends.cudnn.flags(enabled=True, allow_tf32=False):
+        ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (cout, cin, k, k),
+                                          dz.float().view(B, h, w, cout).permute(0, 3, 1, 2), 1, 1)
+    dw = torch.zeros(cout, cin, k, k, device=DEV)
+    scratch = torch.empty(cout * cin * k * k, device=DEV)
+    _lib.check(lib.dp_conv_wgrad(x.data_ptr(), h * w * cin, cin, B, h, w, cin, dz.data_ptr(), cout, h, w, cout, k, k,
+                                 1, 1, scratch.data_ptr(), dw.data_ptr(), DP_BF16, _s()), "conv_wgrad 2^24")
+    torch.cuda.synchronize()
+    err = (dw - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-3, err

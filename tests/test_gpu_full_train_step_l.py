@@ -40,14 +40,16 @@ def _nchw(v, buf):
     return buf[:, v.off:v.off + v.c].reshape(v.B, v.H, v.W, v.c).permute(0, 3, 1, 2)
 
 
-def run_full_accum(g, size, dtype="fp32", split=True, cut=False):
+def run_full_accum(g, size, dtype="fp32", split=True, cut=False, snap=False):
     """The training step of the fixture on the HIP tapes, one sub-batch after the other.
 
     split: after each sub-batch's transformer backward, the encoder + backbone backward runs
     on the reference's own d memory (g["s{j}.dmem"]) instead of the tapes' (recorded first).
     cut: the TrainPlan variant without the gradient through the sampling locations
-    (cut_location_grads). Returns a dict of host copies: losses, matchings, top-k, d memory,
-    sampled backbone / encoder outputs, and the engine."""
+    (cut_location_grads). snap: also keep every stored backbone / encoder layer output of each
+    sub-batch (out["taps"][j]: reference prefix -> NCHW f32 host copy, the plans' `taps`).
+    Returns a dict of host copies: losses, matchings, top-k, d memory, sampled backbone / encoder
+    outputs, and the engine."""
     from detrpose_amd.train_engine import TrainEngine
     dev = torch.device("cuda")
     model, _ = build_model(size, dtype=dtype)
@@ -57,7 +59,7 @@ def run_full_accum(g, size, dtype="fp32", split=True, cut=False):
     images = synthetic_images(B, seed=int(g["meta"][2])).to(dev)
     sizes, ts = _targets(g, dev)
     subs = sub_batches(g)
-    out = {"losses": [], "match": [], "topk": [], "dmem": [], "outs": {}}
+    out = {"losses": [], "match": [], "topk": [], "dmem": [], "outs": {}, "taps": []}
     for j, (rs, tsl, p) in enumerate(subs):
         sb = rs.stop - rs.start
         bb = eng.backbone_plan(sb, images.shape[2], images.shape[3])
@@ -75,6 +77,9 @@ def run_full_accum(g, size, dtype="fp32", split=True, cut=False):
         for tag, views in (("bb", bb.outs), ("enc", ep.levels)):
             for i, v in enumerate(views):
                 out["outs"][f"{p}{tag}{i}"] = _nchw(v, v.buf.x).double().cpu().reshape(-1).numpy()
+        if snap:
+            out["taps"].append({k: _nchw(v, v.buf.x).float().cpu() for k, v in list(bb.taps.items()) +
+                                list(ep.taps.items())})
         keys, vals = plan.criterion(pack_targets(ts[rs], eng.K, dev), sizes[rs], int(g[p + "dn_num_group"]))
         plan.backward()
         torch.cuda.synchronize()
@@ -285,9 +290,13 @@ FP32_CUT_BOUNDS = {"transformer": 1e-2, "encoder": 5e-2, "backbone": 5e-2}
 # fixture's small synthetic persons (area down to 1e-3 of the image), which bf16's ~1e-2
 # keypoint error reaches: single losses move by up to 18 % with the selection and matching
 # forced ("Training parity at DETRPose-L").
+# At L the backbone / encoder worst parameters sit above 1.0 relative L2 end to end, so only the
+# medians are bounded there, below 1.0 (a zero gradient has relative L2 = 1 for every parameter
+# and fails them); test_l_step_bf16_split_backbone_encoder is the check that pins the bf16
+# backbone + encoder backward per parameter.
 BF16_BOUNDS = {
     "n": {"transformer": (0.03, 0.75), "encoder": (0.27, 0.6), "backbone": (0.32, 0.8), "backbone.lab": (0.32, None)},
-    "l": {"transformer": (0.06, 0.75), "encoder": (0.9, 1.5), "backbone": (1.1, 1.7)},
+    "l": {"transformer": (0.06, 0.75), "encoder": (0.9, None), "backbone": (0.97, None)},
 }
 BF16_LOSS_BOUND = {"n": 8e-2, "l": 0.25}   # measured N 1.4-5.2 % (over runs), L 18-20 %
 
@@ -315,3 +324,112 @@ def test_l_step_bf16_per_parameter_location_cut(golden_l):
     fam = per_parameter_table(rel, "L bf16 cut")
     assert worst[0][0] <= BF16_LOSS_BOUND["l"], worst[:5]
     check_bf16_families(fam, "l")
+
+
+# The backbone + encoder backward on the GPU run's OWN forward state ("teacher forcing"). At L this
+# fixture's backbone / encoder gradients are ill-conditioned in the forward state: on the fp32
+# oracle with the reference's d memory, 0.4 % noise on the input image moves them by 15 % (median
+# relative L2), rounding the backbone + encoder weights to bf16 by 45 % / 38 %, rounding only the
+# AIFI layer's weights by 5 % ("Training parity at DETRPose-L"). A bf16 forward's state
+# differs from fp32 by bf16 storage at every layer, so against the fp32 gradients no bf16
+# implementation can come within a few 1e-2. Instead the fp32 oracle runs its backbone + encoder
+# forward with every stored layer output replaced by the GPU run's stored value
+# (oracle.detrpose_cpu.TAP: y + (gpu - y).detach(), the oracle's own gradient path), so its
+# backward (driven by the reference's d memory, as the GPU's) is the fp32 backward AT the GPU's
+# forward state: what is left is the rounding of the GPU's backward itself. Bounds: (median,
+# worst) relative L2 per family over whole parameter tensors, from the MI355X measurement the
+# test prints.
+FORCED_BOUNDS = {"fp32": {"encoder": (1e-3, 2e-2), "backbone": (1e-3, 2e-2)},
+                 "bf16": {"encoder": (0.3, 1.0), "backbone": (0.3, 1.0)}}
+
+
+def forced_oracle_grads(g, size, run):
+    """The fp32 oracle's accumulated backbone + encoder gradients of the fixture's step with every
+    stored layer output forced to the GPU run's (run["taps"][j] per sub-batch) and the backward
+    from the reference's d memory. Returns ({name: gradient}, {tap names the oracle read})."""
+    import oracle.detrpose_cpu as OD
+    from test_train_oracle import oracle_train_step_full
+    state = {"j": -1, "used": set()}
+
+    def force(name, y):
+        if name == "backbone.stem.stem1":
+            state["j"] += 1
+        gv = run["taps"][state["j"]][name]
+        assert tuple(gv.shape) == tuple(y.shape), (name, tuple(gv.shape), tuple(y.shape))
+        state["used"].add(name)
+        return y + (gv.to(y.dtype) - y).detach()
+
+    OD.TAP = force
+    try:
+        _, grads, _, _, _ = oracle_train_step_full(size, g, split=True)
+    finally:
+        OD.TAP = None
+    assert state["j"] == len(run["taps"]) - 1
+    return {k[len("grad."):]: v.detach() for k, v in grads.items() if k.startswith(("grad.backbone.", "grad.encoder."))}, \
+        state["used"]
+
+
+def forced_rows(ref, grads, zero=(), all_zero=False):
+    """Per backbone / encoder parameter: (relative L2 of the GPU gradient against the forced
+    oracle's, name); `zero` names (or every parameter, all_zero) read as zero gradients (the
+    negative controls). Parameters whose oracle gradient vanishes analytically (a conv bias ahead of
+    a training-mode BatchNorm) are skipped."""
+    rows = []
+    for k, v in ref.items():
+        r = v.double().reshape(-1).numpy()
+        nr = np.linalg.norm(r)
+        if nr < 1e-6 * max(1.0, r.size ** 0.5):
+            continue
+        got = grads[k].double().cpu().reshape(-1).numpy()
+        if all_zero or k in zero:
+            got = np.zeros_like(got)
+        rows.append((float(np.linalg.norm(got - r) / nr), k))
+    return rows
+
+
+def forced_check(rows, bounds, verbose=False):
+    """None when every family meets its (median, worst) bounds, else the first failure."""
+    fam = {}
+    for r_ in rows:
+        fam.setdefault(r_[1].split(".")[0], []).append(r_)
+    fails = []
+    for f, rs in sorted(fam.items()):
+        rs.sort(reverse=True)
+        med = float(np.median([r_[0] for r_ in rs]))
+        if verbose:
+            print(f"forced-state per-parameter rel L2 [{f}] n={len(rs)} median {med:.3g} worst "
+                  f"{[(round(r_[0], 5), r_[1]) for r_ in rs[:4]]}")
+        if med > bounds[f][0]:
+            fails.append((f, "median", med))
+        if rs[0][0] > bounds[f][1]:
+            fails.append((f, "worst", rs[:3]))
+    return fails[0] if fails else None
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_l_step_backbone_encoder_backward_at_own_forward_state(golden_l, dtype):
+    """DETRPose-L backbone + encoder backward, per parameter, on the run's own forward state: the
+    tapes run the step's forward (both sub-batches), then their encoder + backbone backward from
+    the REFERENCE's d memory of each sub-batch; the fp32 oracle (pinned to the reference) runs
+    the same step with every stored layer output forced to the GPU's (FORCED_BOUNDS comment) and
+    the same d memory. Every backbone / encoder parameter's accumulated gradient (whole tensors)
+    within its family's (median, worst) relative-L2 bound. Negative controls, which must FAIL the
+    same check: an all-zero gradient arena, and the real gradients with one parameter zeroed (the
+    deepest, stem1's weight; an encoder FPN conv)."""
+    g = golden_l
+    r = run_full_accum(g, "l", dtype=dtype, split=True, snap=True)
+    eng = r["eng"]
+    ref, used = forced_oracle_grads(g, "l", r)
+    taps = set(r["taps"][0])
+    assert used == taps, (sorted(taps - used)[:5], sorted(used - taps)[:5])
+    rows = forced_rows(ref, eng.grads)
+    assert sum(k.startswith("backbone.") for _, k in rows) >= 80
+    assert sum(k.startswith("encoder.") for _, k in rows) >= 100
+    b = FORCED_BOUNDS[dtype]
+    print(f"{dtype}: {len(used)} stored layer outputs forced per sub-batch")
+    fail = forced_check(rows, b, verbose=True)
+    assert fail is None, fail
+    assert forced_check(forced_rows(ref, eng.grads, all_zero=True), b) is not None, "zero-gradient control passed"
+    for probe in ("backbone.stem.stem1.conv.weight", "encoder.fpn_blocks.0.cv4.conv.weight"):
+        assert any(k == probe for _, k in rows), probe
+        assert forced_check(forced_rows(ref, eng.grads, zero=(probe,)), b) is not None, f"zeroed {probe} passed"

@@ -199,6 +199,29 @@ def test_conv2d_1x1_large_m(cin, cout, H, W, ld, off, mode, act):
         _close(up, F.interpolate(ref, scale_factor=2.0, mode="nearest").permute(0, 2, 3, 1), "bf16", "1x1 up")
 
 
+@pytest.mark.parametrize("B,cin,cout,H,W,act", [
+    (64, 128, 128, 80, 80, "silu"), (16, 128, 128, 40, 40, "silu"), (8, 128, 128, 20, 20, None),
+    (4, 128, 128, 64, 70, "relu"), (16, 64, 64, 40, 40, "relu"), (8, 96, 96, 33, 35, "silu")])
+def test_conv2d_halo_streamed_plain(B, cin, cout, H, W, act):
+    """The streamed-weight halo tiles as the encoder runs them: no residual, every output channel
+    present, so a block's next tile starts on the counted vmcnt waits that leave the previous
+    tile's epilogue stores in flight (the pipelined K loop's per-step counts included); batches
+    with several tiles per persistent block (L b64 80x80: 1600 tiles), ragged edges."""
+    torch.manual_seed(B * H + cin)
+    pk = Packer({}, "bf16", torch.device("cuda"))
+    x = torch.randn(B, cin, H, W).bfloat16().float()
+    w = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pk.conv(w.double(), b.double(), act=act)
+    with torch.backends.cudnn.flags(enabled=True, allow_tf32=False):   # fp32 reference, no xf32
+        ref = F.conv2d(x.cuda(), _rb(w, "bf16").cuda(), b.cuda(), 1, 1)
+    ref = {"relu": F.relu, "silu": F.silu, None: lambda t: t}[act](ref)
+    out = torch.full((B, H, W, cout), 7.0, device="cuda", dtype=torch.bfloat16)
+    _run_conv(pc, _nhwc(x, "bf16"), out, "bf16")
+    torch.cuda.synchronize()
+    _close(out, ref.permute(0, 2, 3, 1), "bf16", f"halo {cin}->{cout} {H}x{W} b{B}")
+
+
 @pytest.mark.parametrize("H,W,act", [(50, 53, "relu"), (160, 160, "silu"), (17, 9, None)])
 def test_conv2d_halo_48(H, W, act):
     """The 48-wide natural-order halo tile (HG stage-0 3x3 48->48 convs, no residual) writing a

@@ -64,6 +64,25 @@ def test_gemm_linear_dgrad_wgrad(dt, m, n, k):
     assert (dW - rdW).abs().max() <= 1e-4 * max(1.0, rdW.abs().max().item())
 
 
+@pytest.mark.parametrize("m,n,k,lda,ldb", [(512, 1536, 25600, 520, 1552), (136, 104, 9999, 136, 104),
+                                            (256, 256, 409600, 256, 256), (1024, 264, 6400, 1032, 264)])
+def test_gemm_wgrad_dma_ring(m, n, k, lda, ldb):
+    """dp_gemm's weight-gradient route (wgrad_tt_kernel: C += alpha dy^T x with dy [k][m] and x
+    [k][n] in k-major rows, LDS-DMA ring, split-K float atomics) vs torch fp32 on the same bf16
+    operands: padded row pitches, ragged M / N / K tiles, 409,600 rows (the stride-4 map of a b16
+    batch), C accumulated onto existing values with alpha != 1."""
+    torch.manual_seed(m + n)
+    dy = torch.randn(k, lda, device=DEV).to(torch.bfloat16)
+    x = torch.randn(k, ldb, device=DEV).to(torch.bfloat16)
+    c0 = torch.randn(m, n, device=DEV)
+    dW = c0.clone()
+    gemm(dy, (1, lda), x, (ldb, 1), dW, n, m, n, k, alpha=0.5, beta=1.0)
+    ref = c0 + 0.5 * (dy[:, :m].float().t() @ x[:, :n].float())
+    err = (dW - ref).abs().max().item() / ref.abs().max().item()
+    print(f"wgrad {m}x{n} over {k}: max err {err:.3g} of scale")
+    assert err <= 1e-4
+
+
 def test_gemm_generic_strides_and_forced_split():
     torch.manual_seed(1)
     A = torch.randn(50, 30, device=DEV)[:, ::3]      # (50, 10), strides (30, 3): generic
@@ -152,10 +171,13 @@ def test_attention_fwd_bwd(L, dh, masked):
     assert torch.allclose(dqkv, q.grad, atol=1e-4), (dqkv - q.grad).abs().max()
 
 
-@pytest.mark.parametrize("L,dh,masked", [(18, 32, False), (18, 16, False), (60, 32, True), (96, 32, True),
-                                          (101, 32, True), (128, 48, False), (33, 64, True), (400, 32, False),
-                                          (257, 32, True)])
-def test_attention_fwd_bwd_bf16_mfma(L, dh, masked):
+@pytest.mark.parametrize("L,dh,masked,mis", [(18, 32, False, 0), (18, 16, False, 0), (60, 32, True, 0), (96, 32, True, 0),
+                                              (101, 32, True, 0), (128, 48, False, 0), (33, 64, True, 0),
+                                              (400, 32, False, 0), (257, 32, True, 0),
+                                              # q / k / v rows not 16-byte aligned (pitch and base one
+                                              # element off): the MFMA route declines, the scalar kernels run
+                                              (18, 32, False, 1), (60, 32, True, 1)])
+def test_attention_fwd_bwd_bf16_mfma(L, dh, masked, mis):
     """The bf16 MFMA attention kernels (csrc/train_attn.hip: sequences <= 128 tokens, the decoder's
     within (18) and across (60 + DN) attentions; <= 400 with 32-wide heads, the AIFI layer's 20 x
     20 map, 257 ragged) against torch fp32 autograd on the same bf16
@@ -166,7 +188,9 @@ def test_attention_fwd_bwd_bf16_mfma(L, dh, masked):
     nh, B, Ti = 4, 2, 3
     Cc = nh * dh
     rows = B * Ti * L
-    qkv = torch.randn(rows, 3 * Cc, device=DEV).to(torch.bfloat16)
+    ld = 3 * Cc + mis
+    flat = torch.randn(rows * ld + mis, device=DEV).to(torch.bfloat16)
+    qkv = flat[mis:].view(rows, ld)[:, :3 * Cc]
     mask = (torch.rand(L, L, device=DEV) < 0.3) if masked else torch.zeros(L, L, dtype=torch.bool, device=DEV)
     mask.fill_diagonal_(False)
     if masked:
@@ -175,9 +199,9 @@ def test_attention_fwd_bwd_bf16_mfma(L, dh, masked):
     P = torch.empty(B * Ti * nh * L * L, device=DEV)
     m8 = mask.to(torch.uint8).contiguous()
     args = (B, Ti, L * Ti, 1, Ti, L, nh, dh, DP_BF16)
-    _lib.check(lib.dp_attn_fwd(qkv.data_ptr(), 3 * Cc, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), 3 * Cc,
+    _lib.check(lib.dp_attn_fwd(qkv.data_ptr(), ld, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), ld,
                                out.data_ptr(), Cc, P.data_ptr(), m8.data_ptr() if masked else None, *args, _s()), "attn")
-    q = qkv.float().detach().clone().requires_grad_(True)
+    q = qkv.float().contiguous().detach().clone().requires_grad_(True)
     x = q.view(B, L, Ti, 3, nh, dh).permute(3, 0, 2, 4, 1, 5)
     sc = (x[0] / dh ** 0.5) @ x[1].transpose(-1, -2)
     sc = sc.masked_fill(mask, float("-inf"))
@@ -190,7 +214,7 @@ def test_attention_fwd_bwd_bf16_mfma(L, dh, masked):
     dout = torch.randn(rows, Cc, device=DEV).to(torch.bfloat16)
     ref.backward(dout.float())
     dqkv = torch.empty(rows, 3 * Cc, device=DEV, dtype=torch.bfloat16)
-    _lib.check(lib.dp_attn_bwd(qkv.data_ptr(), 3 * Cc, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), 3 * Cc,
+    _lib.check(lib.dp_attn_bwd(qkv.data_ptr(), ld, qkv[:, Cc:].data_ptr(), qkv[:, 2 * Cc:].data_ptr(), ld,
                                P.data_ptr(), dout.data_ptr(), out.data_ptr(), Cc, dqkv.data_ptr(), 3 * Cc,
                                dqkv[:, Cc:].data_ptr(), dqkv[:, 2 * Cc:].data_ptr(), 3 * Cc, *args, _s()), "attn_bwd")
     torch.cuda.synchronize()

@@ -181,14 +181,15 @@ def test_adamw_clip_matches_torch():
     p = torch.randn(n, device="cuda")
     ref = p.clone().requires_grad_(True)
     opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4)
-    m, v, sq = torch.zeros_like(p), torch.zeros_like(p), torch.zeros(1 + _lib.DP_SQNORM_PARTS, device="cuda")
+    m, v, sq = torch.zeros_like(p), torch.zeros_like(p), torch.zeros(1, device="cuda")
+    ws = torch.zeros(lib.dp_grad_sqnorm_ws_floats(n), device="cuda")
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     for step in range(1, 4):
         g = torch.randn(n, device="cuda") * 0.01
         ref.grad = g.clone()
         torch.nn.utils.clip_grad_norm_([ref], 0.1)
         opt.step()
-        _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), s), "sq")
+        _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), ws.data_ptr(), ws.numel(), s), "sq")
         _lib.check(lib.dp_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8,
                                 1e-4, step, 0.1, sq.data_ptr(), None, s), "adamw")
     assert torch.allclose(p, ref.detach(), atol=1e-6, rtol=1e-5), (p - ref).abs().max()
@@ -207,10 +208,13 @@ def test_step_guard_skips_non_finite_updates():
     m, v, e = torch.zeros_like(p), torch.zeros_like(p), p.clone()
     g = torch.randn(n, device="cuda")
     sq, bad = torch.zeros(1, device="cuda"), torch.zeros(1, device="cuda")
+    ws = torch.zeros(lib.dp_grad_sqnorm_ws_floats(n), device="cuda")
+    # the workspace size is checked: one float short is an error, not an out-of-bounds write
+    assert lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), ws.data_ptr(), ws.numel() - 1, s) != 0
     losses = torch.tensor([1.0, float("nan"), 2.0], device="cuda")
     p0 = p.clone()
     _lib.check(lib.dp_finite_guard(losses.data_ptr(), 3, bad.data_ptr(), s), "guard")
-    _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), s), "sq")
+    _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), ws.data_ptr(), ws.numel(), s), "sq")
     _lib.check(lib.dp_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1,
                             0.1, sq.data_ptr(), bad.data_ptr(), s), "adamw")
     _lib.check(lib.dp_ema(e.data_ptr(), g.data_ptr(), n, 0.5, bad.data_ptr(), s), "ema")
@@ -219,7 +223,7 @@ def test_step_guard_skips_non_finite_updates():
     # a NaN gradient: the norm is NaN, the update is skipped even without the flag
     g2 = g.clone()
     g2[7] = float("nan")
-    _lib.check(lib.dp_grad_sqnorm(g2.data_ptr(), n, sq.data_ptr(), s), "sq")
+    _lib.check(lib.dp_grad_sqnorm(g2.data_ptr(), n, sq.data_ptr(), ws.data_ptr(), ws.numel(), s), "sq")
     _lib.check(lib.dp_adamw(p.data_ptr(), g2.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1,
                             0.1, sq.data_ptr(), None, s), "adamw")
     torch.cuda.synchronize()
@@ -227,7 +231,7 @@ def test_step_guard_skips_non_finite_updates():
     bad.zero_()
     ok = torch.tensor([1.0, 2.0], device="cuda")
     _lib.check(lib.dp_finite_guard(ok.data_ptr(), 2, bad.data_ptr(), s), "guard")
-    _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), s), "sq")
+    _lib.check(lib.dp_grad_sqnorm(g.data_ptr(), n, sq.data_ptr(), ws.data_ptr(), ws.numel(), s), "sq")
     _lib.check(lib.dp_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1,
                             0.1, sq.data_ptr(), bad.data_ptr(), s), "adamw")
     _lib.check(lib.dp_ema(e.data_ptr(), g.data_ptr(), n, 0.5, bad.data_ptr(), s), "ema")

@@ -436,3 +436,42 @@ def test_lab_scalar_gradients_fp64_fixture(golden_dir):
     worst = int(np.argmax(rel))
     print(f"reference fp32 vs fp64 LAB gradients: worst {rel[worst]:.3g} ({names[worst]}), median {np.median(rel):.3g}")
     assert len(names) == 60
+
+
+def test_forced_state_hook_is_identity_on_own_values(golden_dir):
+    """The forced-state hook (oracle.detrpose_cpu.TAP, tests/test_gpu_full_train_step_l.py) fed
+    the oracle's OWN stored layer outputs changes nothing: the L step's backbone / encoder
+    gradients equal the unforced ones (the substitution keeps the oracle's gradient path)."""
+    import oracle.detrpose_cpu as OD
+    g = np.load(os.path.join(golden_dir, "train_full_l_b2a2.npz"))
+    rec = []
+
+    def record(name, y):
+        if name == "backbone.stem.stem1":
+            rec.append({})
+        rec[-1][name] = y.detach().clone()
+        return y
+    OD.TAP = record
+    try:
+        _, g0, _, _, _ = oracle_train_step_full("l", g)
+    finally:
+        OD.TAP = None
+    state = {"j": -1}
+
+    def force(name, y):
+        if name == "backbone.stem.stem1":
+            state["j"] += 1
+        return y + (rec[state["j"]][name] - y).detach()
+    OD.TAP = force
+    try:
+        _, g1, _, _, _ = oracle_train_step_full("l", g)
+    finally:
+        OD.TAP = None
+    assert len(rec) == 2 and len(rec[0]) > 120
+    keys = [k for k in g0 if k.startswith(("grad.backbone.", "grad.encoder."))]
+    assert len(keys) > 300
+    for k in keys:
+        if float(g0[k].norm()) < 1e-6 * max(1.0, g0[k].numel() ** 0.5):
+            continue   # analytically zero (a bias ahead of a training-mode BatchNorm): rounding noise
+        err = float((g1[k] - g0[k]).abs().max() / g0[k].abs().max())
+        assert err <= 1e-5, (k, err)
