@@ -339,8 +339,13 @@ def test_l_step_bf16_per_parameter_location_cut(golden_l):
 # forward state: what is left is the rounding of the GPU's backward itself. Bounds: (median,
 # worst) relative L2 per family over whole parameter tensors, from the MI355X measurement the
 # test prints.
-FORCED_BOUNDS = {"fp32": {"encoder": (1e-3, 2e-2), "backbone": (1e-3, 2e-2)},
-                 "bf16": {"encoder": (0.3, 1.0), "backbone": (0.3, 1.0)}}
+# Measured on MI355X (profiles/r6b_pytest_forced.txt): fp32 backbone median 2.4e-4 / worst 8.5e-4,
+# encoder 3.8e-6 / 1.6e-4; bf16 backbone 0.098 / 0.20 (the backbone's ~40 layers of bf16 activation
+# gradients compound), encoder 0.015 / 0.56 (the two downsample cv1 BatchNorm weights, 0.56 / 0.38:
+# a dgamma = sum(dy x_hat) that cancels; they sit at the same ~40x the family median in fp32). A
+# missing or zeroed gradient has relative L2 1.0: above every worst bound.
+FORCED_BOUNDS = {"fp32": {"encoder": (1e-4, 2e-3), "backbone": (1e-3, 5e-3)},
+                 "bf16": {"encoder": (0.025, 0.8), "backbone": (0.15, 0.3)}}
 
 
 def forced_oracle_grads(g, size, run):
@@ -372,13 +377,20 @@ def forced_oracle_grads(g, size, run):
 def forced_rows(ref, grads, zero=(), all_zero=False):
     """Per backbone / encoder parameter: (relative L2 of the GPU gradient against the forced
     oracle's, name); `zero` names (or every parameter, all_zero) read as zero gradients (the
-    negative controls). Parameters whose oracle gradient vanishes analytically (a conv bias ahead of
-    a training-mode BatchNorm) are skipped."""
+    negative controls). Parameters whose oracle gradient vanishes analytically are skipped: a bias
+    whose every consumer normalises it away (input_proj's BatchNorm bias and the AIFI's last
+    LayerNorm bias, each followed only by convs into a training-mode BatchNorm), recognised by a
+    gradient RMS below 1e-4 of its family's median (rounding noise)."""
+    rms = {k: float(v.double().norm()) / max(1, v.numel()) ** 0.5 for k, v in ref.items()}
+    fam_rms = {}
+    for k, r in rms.items():
+        fam_rms.setdefault(k.split(".")[0], []).append(r)
+    fam_rms = {f: float(np.median(v)) for f, v in fam_rms.items()}
     rows = []
     for k, v in ref.items():
         r = v.double().reshape(-1).numpy()
         nr = np.linalg.norm(r)
-        if nr < 1e-6 * max(1.0, r.size ** 0.5):
+        if rms[k] < 1e-4 * fam_rms[k.split(".")[0]]:
             continue
         got = grads[k].double().cpu().reshape(-1).numpy()
         if all_zero or k in zero:
