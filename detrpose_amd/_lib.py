@@ -66,7 +66,7 @@ class GemmDesc(C.Structure):
                 ("in_dtype", i32), ("out_dtype", i32),
                 ("bias", vp), ("alpha", f32), ("beta", f32), ("act", i32),
                 ("gate", vp), ("gate_bs", i64), ("gate_rs", i64), ("gate_dtype", i32),
-                ("split_k", i32)]
+                ("split_k", i32), ("colsum", vp)]
 
 
 class PackDesc(C.Structure):
@@ -164,6 +164,7 @@ _SIGS = {
     "dp_bn_stats": (i32, [vp, i64, i32, i32, vp, vp, i64, i32, vp]),
     "dp_bn_stats_ws_bytes": (i64, [i32, i32]),
     "dp_bn_finalize": (i32, [vp, i32, f32, i32, f32, f32, vp, vp, vp, vp]),
+    "dp_bn_stats_finalize": (i32, [vp, i64, i32, i32, vp, vp, i64, f32, f32, vp, vp, vp, i32, vp]),
     "dp_bn_act_fwd": (i32, [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
     "dp_bn_act_bwd_reduce": (i32, [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp,
                                    vp, vp, i64, i32, vp]),

@@ -79,9 +79,39 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
 
 // out [3][c] = (K, sum over the ny slices of part[y][0], of part[y][1]): wave w of 16 adds
 // slices w, w + 16, ... in order, then the 16 wave sums are added in order.
+// parts [np][3][c] (one per rank: K, S1, S2 over `count` rows each) -> mr [2][c] = (mean, rstd)
+// of the union (Chan's parallel combination), biased variance; running statistics updated as
+// F.batch_norm does (momentum, unbiased variance). One channel.
+__device__ __forceinline__ void bn_finalize_ch(const float* __restrict__ parts, int np, float count, int c, int ch,
+                                               float eps, float momentum, float* __restrict__ rmean,
+                                               float* __restrict__ rvar, float* __restrict__ mr) {
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int p = 0; p < np; ++p) {
+    const float* q = parts + (int64_t)p * 3 * c;
+    const double k = q[ch], s1 = q[c + ch], s2 = q[2 * c + ch];
+    const double mi = k + s1 / count, m2i = s2 - s1 * s1 / count;
+    const double nn = n + count, delta = mi - mean;
+    mean += delta * count / nn;
+    m2 += m2i + delta * delta * n * count / nn;
+    n = nn;
+  }
+  const double var = m2 / n;
+  mr[ch] = (float)mean;
+  mr[c + ch] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) {
+    rmean[ch] = (float)((1.0 - momentum) * rmean[ch] + momentum * mean);
+    rvar[ch] = (float)((1.0 - momentum) * rvar[ch] + momentum * (n > 1.0 ? m2 / (n - 1.0) : var));
+  }
+}
+
+struct BnFin {   // the finalize of dp_bn_stats_finalize (mr == nullptr: none)
+  float count, eps, momentum;
+  float *rmean, *rvar, *mr;
+};
+
 template <typename T>
 __global__ __launch_bounds__(1024) void bn_stats_reduce_kernel(const T* __restrict__ x, const float* __restrict__ part,
-                                                               int ny, int c, float* __restrict__ out) {
+                                                               int ny, int c, float* __restrict__ out, BnFin fin) {
   constexpr int NWV = 16;
   __shared__ float red[2][NWV][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -103,34 +133,18 @@ __global__ __launch_bounds__(1024) void bn_stats_reduce_kernel(const T* __restri
     out[ch] = ld_(x + ch);
     out[c + ch] = t1;
     out[2 * c + ch] = t2;
+    // one rank (no SyncBN exchange between the statistics and their finalize): finalize here, from
+    // the values this thread just stored (the same arithmetic as bn_finalize_kernel's)
+    if (fin.mr) bn_finalize_ch(out, 1, fin.count, c, ch, fin.eps, fin.momentum, fin.rmean, fin.rvar, fin.mr);
   }
 }
 
-// parts [np][3][c] (one per rank: K, S1, S2 over `count` rows each) -> mr [2][c] = (mean, rstd)
-// of the union (Chan's parallel combination), biased variance; running statistics updated as
-// F.batch_norm does (momentum, unbiased variance)
 __global__ void bn_finalize_kernel(const float* __restrict__ parts, int np, float count, int c, float eps,
                                    float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
                                    float* __restrict__ mr) {
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= c) return;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int p = 0; p < np; ++p) {
-    const float* q = parts + (int64_t)p * 3 * c;
-    const double k = q[ch], s1 = q[c + ch], s2 = q[2 * c + ch];
-    const double mi = k + s1 / count, m2i = s2 - s1 * s1 / count;
-    const double nn = n + count, delta = mi - mean;
-    mean += delta * count / nn;
-    m2 += m2i + delta * delta * n * count / nn;
-    n = nn;
-  }
-  const double var = m2 / n;
-  mr[ch] = (float)mean;
-  mr[c + ch] = (float)(1.0 / sqrt(var + (double)eps));
-  if (rmean) {
-    rmean[ch] = (float)((1.0 - momentum) * rmean[ch] + momentum * mean);
-    rvar[ch] = (float)((1.0 - momentum) * rvar[ch] + momentum * (n > 1.0 ? m2 / (n - 1.0) : var));
-  }
+  bn_finalize_ch(parts, np, count, c, ch, eps, momentum, rmean, rvar, mr);
 }
 
 // VC-element vector loads / stores of a row chunk (VC = 1, or 16 / 8 bytes)
@@ -745,18 +759,31 @@ extern "C" int64_t dp_bn_stats_ws_bytes(int32_t rows, int32_t c) {
   return (int64_t)((rows + sl - 1) / sl) * 2 * c * (int64_t)sizeof(float);
 }
 
-extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, float* ws, int64_t ws_bytes,
-                           int32_t dtype, void* stream) {
+static int bn_stats_launch(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, float* ws,
+                           int64_t ws_bytes, int32_t dtype, hipStream_t s, const BnFin& fin) {
   DP_REQUIRE(x && out && ws && rows > 0 && c > 0 && ld >= c, "dp_bn_stats: bad arguments");
   DP_REQUIRE(ws_bytes >= dp_bn_stats_ws_bytes(rows, c), "dp_bn_stats: workspace of %lld bytes < %lld",
              (long long)ws_bytes, (long long)dp_bn_stats_ws_bytes(rows, c));
-  hipStream_t s = as_stream(stream);
   const int sl = bn_slice_rows(rows, c), ny = (rows + sl - 1) / sl;
   dim3 grid((c + 63) / 64, ny);
   DP_DT(hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ld, rows, c, sl, ws));
   DP_DT(hipLaunchKernelGGL(bn_stats_reduce_kernel<T>, dim3((c + 63) / 64), dim3(1024), 0, s, (const T*)x, ws, ny, c,
-                           out));
+                           out, fin));
   return dp_check_launch("dp_bn_stats");
+}
+
+extern "C" int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, float* ws, int64_t ws_bytes,
+                           int32_t dtype, void* stream) {
+  return bn_stats_launch(x, ld, rows, c, out, ws, ws_bytes, dtype, as_stream(stream), BnFin{0.f, 0.f, 0.f, nullptr,
+                                                                                           nullptr, nullptr});
+}
+
+extern "C" int dp_bn_stats_finalize(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, float* ws,
+                                    int64_t ws_bytes, float eps, float momentum, float* running_mean,
+                                    float* running_var, float* mean_rstd, int32_t dtype, void* stream) {
+  DP_REQUIRE(mean_rstd && (!running_mean == !running_var), "dp_bn_stats_finalize: bad arguments");
+  return bn_stats_launch(x, ld, rows, c, out, ws, ws_bytes, dtype, as_stream(stream),
+                         BnFin{(float)rows, eps, momentum, running_mean, running_var, mean_rstd});
 }
 
 extern "C" int dp_bn_finalize(const float* parts, int32_t nparts, float count, int32_t c, float eps, float momentum,

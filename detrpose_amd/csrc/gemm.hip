@@ -21,6 +21,9 @@
 #include "common.h"
 #include "conv_lds.h"
 
+extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, float* out, int32_t accumulate,
+                         int32_t dtype, void* stream);
+
 namespace {
 
 constexpr int TM = 64, TN = 64;
@@ -157,6 +160,7 @@ struct GemmArgs {
   int gate_bf16;
   int modeA, modeB;
   int tiles_n;
+  float* colsum;   // wgrad_tt_kernel: colsum[m] += alpha * sum_k A(m, k) (bias gradient), or NULL
   // B operand mode 3 (dp_conv_wgrad): B(k = output pixel p, n = tap * cin + ci) = x at the
   // tap's input pixel of p (zero outside the map) -- im2col on the fly
   const bf16_t* ix;
@@ -630,6 +634,10 @@ void wgrad_tt_kernel(const GemmArgs g, int ntiles, int tiles_n) {
   };
   const int wm = (wave >> 2) * 64, wn = (wave & 3) * 64;
   const int bsub = 1 + (wn >> 7), bcol = wn & 127;
+  // the bias gradient (A's column sums over k) from the A fragments this wave reads anyway: the
+  // waves of the first N-tile column (wn == 0) of the tiles at n0 == 0, each over its 64 rows
+  const bool csum = !IM && g.colsum != nullptr && tn == 0 && (wave & 3) == 0;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -657,6 +665,12 @@ void wgrad_tt_kernel(const GemmArgs g, int ntiles, int tiles_n) {
       for (int i = 0; i < 4; ++i) af[i] = frag2(Ai, 1, wm + 16 * i, 32 * ks);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = frag2(Bi, 1, bcol + 16 * j, 32 * ks);
+      if (csum) {   // lane: row m = wm + 16 i + lane % 16, k = 32 ks + 8 (lane / 16) .. + 7
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[i] += (float)af[i][e];
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -675,6 +689,16 @@ void wgrad_tt_kernel(const GemmArgs g, int ntiles, int tiles_n) {
         if (m < g.M) unsafeAtomicAdd(g.cf + (int64_t)m * g.c_rs + n, g.alpha * acc[i][j][r]);
       }
     }
+  if (csum) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = cs[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int m = m0 + wm + 16 * i + (lane & 15);
+      if (lane < 16 && m < g.M) unsafeAtomicAdd(g.colsum + m, g.alpha * v);
+    }
+  }
 }
 
 // dw[co][ci][tap] += s[co][tap][ci] (the reference's [cout][cin][kh][kw] from the tap-major sums)
@@ -701,6 +725,8 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
   DP_REQUIRE(d.act == DP_ACT_NONE || d.act == DP_ACT_RELU || d.act == DP_ACT_GELU, "dp_gemm: act %d (none / relu / gelu)",
              d.act);
   DP_REQUIRE(d.split_k >= 0, "dp_gemm: split_k %d", d.split_k);
+  DP_REQUIRE(!d.colsum || (d.batch == 1 && d.alpha == 1.f && d.a_rs == 1 && d.a_ks >= d.m),
+             "dp_gemm: colsum needs batch 1, alpha 1 and A(m, k) = a[k * a_ks + m]");
   const int es = d.in_dtype == DP_BF16 ? 2 : 4;
   const int vec = 16 / es;
   const int BK = d.in_dtype == DP_BF16 ? 64 : 32;
@@ -734,8 +760,11 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
   // weight gradients (both operands k-major rows, f32 C accumulated): the LDS-DMA ring kernel
   // (DETRPOSE_WGRAD_TT=0 keeps the 128 x 128 kernel, A/B)
   static const bool tt_off = getenv("DETRPOSE_WGRAD_TT") && atoi(getenv("DETRPOSE_WGRAD_TT")) == 0;
-  if (!tt_off && big && splittable && d.split_k == 0 && d.batch == 1 && g.modeA == 1 && g.modeB == 1 &&
-      d.m % 8 == 0 && d.n % 8 == 0 && d.k >= 4096) {
+  // (mode 1 rows are 16-byte aligned with ld % 8 == 0, so a 16-byte chunk never straddles two k
+  // rows: a chunk past M / N reads the row's padding, which feeds only discarded C rows / columns)
+  g.colsum = nullptr;
+  if (!tt_off && !force64 && d.in_dtype == DP_BF16 && splittable && d.split_k == 0 && d.batch == 1 && g.modeA == 1 &&
+      g.modeB == 1 && d.k >= 2048) {
     const int tmw = (d.m + WT_BM - 1) / WT_BM, tnw = (d.n + WT_BN - 1) / WT_BN;
     const int ntl = tmw * tnw;
     const int ksteps64 = (d.k + 63) / 64;
@@ -747,6 +776,7 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
     if (((int64_t)kchunk * d.a_ks + d.m) * 2 < 0x7ff00000ll && ((int64_t)kchunk * d.b_ks + d.n) * 2 < 0x7ff00000ll) {
       g.splits = sp;
       g.kchunk = kchunk;
+      g.colsum = d.colsum;
       static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_tt_kernel<false>),
                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    WT_NS * WT_STAGE) == hipSuccess;
@@ -812,6 +842,10 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
     hipLaunchKernelGGL(gemm_kernel<bf16_t>, grid, block, 0, s, g);
   else
     hipLaunchKernelGGL(gemm_kernel<float>, grid, block, 0, s, g);
+  if (d.colsum) {   // the kernels above do not fuse it: the bias gradient on its own kernel
+    const int rc = dp_colsum(d.a, d.a_ks, d.k, d.m, d.colsum, 1, d.in_dtype, stream);
+    if (rc) return rc;
+  }
   return dp_check_launch("dp_gemm");
 }
 
@@ -833,6 +867,12 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
   const int chunk = (int)std::min<int64_t>(batch, ((1ll << 24) - 1) / ppi);
   hipStream_t s = as_stream(stream);
   const int taps = kh * kw, N = taps * cin;
+  // the LDS-DMA ring kernel (wgrad_tt_kernel<true>) wherever its 32-bit buffer offsets reach. Its
+  // float atomics go to the tap-major scratch (contiguous columns), permuted into dw after: adding
+  // straight into dw[co][ci][tap] (columns 9 floats apart) measured 3.9 -> 18.8 ms per L step.
+  static const bool tt_off = getenv("DETRPOSE_WGRAD_TT") && atoi(getenv("DETRPOSE_WGRAD_TT")) == 0;
+  const bool tt = !tt_off && cout % 8 == 0 && N % 8 == 0 && (int64_t)chunk * x_bstride * 2 < 0x7ff00000ll &&
+                  ((int64_t)chunk * ppi * dz_ld + cout) * 2 < 0x7ff00000ll;
   if (dp_zero_async(scratch, (size_t)cout * N * sizeof(float), s)) {
     dp_set_error("dp_conv_wgrad: memset failed");
     return DP_EINVAL;
@@ -860,7 +900,6 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
   static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm128_kernel<1, 3>),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   DP_REQUIRE(attr_ok, "dp_conv_wgrad: cannot set the kernel's LDS size");
-  static const bool tt_off = getenv("DETRPOSE_WGRAD_TT") && atoi(getenv("DETRPOSE_WGRAD_TT")) == 0;
   for (int b0 = 0; b0 < batch; b0 += chunk) {
     const int nb = std::min(chunk, batch - b0);
     const int64_t K = (int64_t)nb * ppi;
@@ -868,9 +907,7 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
     g.ix = reinterpret_cast<const bf16_t*>(x) + (int64_t)b0 * x_bstride;
     g.B.p = g.ix;
     g.K = (int)K;
-    // the LDS-DMA ring kernel (wgrad_tt_kernel<true>) where its 32-bit buffer offsets reach
-    if (!tt_off && K >= 4096 && cout % 8 == 0 && N % 8 == 0 && (int64_t)nb * x_bstride * 2 < 0x7ff00000ll &&
-        (K * dz_ld + cout) * 2 < 0x7ff00000ll) {
+    if (tt) {
       const int tmw = (cout + WT_BM - 1) / WT_BM, tnw = (N + WT_BN - 1) / WT_BN;
       const int ntl = tmw * tnw;
       const int ks64 = (int)((K + 63) / 64);

@@ -234,9 +234,9 @@ class TapePlan:
 
     # ------------------------------------------------------------------ GEMM helper
     def gemm(self, tape, name, a, a_rs, a_ks, b, b_ks, b_ns, c, c_rs, m, n, k, out_code=None, bias=None, beta=0.0,
-             act=0):
+             act=0, colsum=None):
         self.eng._gemm(tape, name, a, a_rs, a_ks, b, b_ks, b_ns, c, c_rs, m, n, k, self.code,
-                       self.code if out_code is None else out_code, bias=bias, beta=beta, act=act)
+                       self.code if out_code is None else out_code, bias=bias, beta=beta, act=act, colsum=colsum)
 
     # ------------------------------------------------------------------ layers
     def conv(self, name, wkey, segs, cout, k=1):
@@ -368,13 +368,16 @@ class TapePlan:
             if self.world > 1:
                 fw.op(f"{name}.bn{bi}.zero", lib.dp_zero, _p(parts), parts.numel() * 4)
             ws = self.f32(max(int(lib.dp_bn_stats_ws_bytes(rows, c)), 4) // 4)   # per-slice partial sums
-            fw.op(f"{name}.bn{bi}.stats", lib.dp_bn_stats, z.xp, z.ld, rows, c, _p(parts[self.rank]), _p(ws),
-                  ws.numel() * 4, code)
-            if self.world > 1:
-                fw.op(f"{name}.bn{bi}.sync", _host(lambda t=parts: all_reduce(t)))
             rm, rv = eng.running[p + ".running_mean"], eng.running[p + ".running_var"]
-            fw.op(f"{name}.bn{bi}.finalize", lib.dp_bn_finalize, _p(parts), self.world, C.c_float(rows), c,
-                  C.c_float(1e-5), C.c_float(0.1), _p(rm), _p(rv), _p(mr))
+            if self.world == 1:   # statistics + finalize in the statistics' launches
+                fw.op(f"{name}.bn{bi}.stats", lib.dp_bn_stats_finalize, z.xp, z.ld, rows, c, _p(parts), _p(ws),
+                      ws.numel() * 4, C.c_float(1e-5), C.c_float(0.1), _p(rm), _p(rv), _p(mr), code)
+            else:
+                fw.op(f"{name}.bn{bi}.stats", lib.dp_bn_stats, z.xp, z.ld, rows, c, _p(parts[self.rank]), _p(ws),
+                      ws.numel() * 4, code)
+                fw.op(f"{name}.bn{bi}.sync", _host(lambda t=parts: all_reduce(t)))
+                fw.op(f"{name}.bn{bi}.finalize", lib.dp_bn_finalize, _p(parts), self.world, C.c_float(rows), c,
+                      C.c_float(1e-5), C.c_float(0.1), _p(rm), _p(rv), _p(mr))
             st.append((z, mr, eng.params[p + ".weight"], eng.params[p + ".bias"], eng.grads[p + ".weight"],
                        eng.grads[p + ".bias"]))
         z1, mr1, g1, b1, dg1, db1 = st[0]
@@ -644,31 +647,26 @@ class EncoderTrainPlan(TapePlan):
             bw.op(f"aifi{i}.norm2.bwd", lib.dp_ln_bwd, ds.xp, out.gp, Cc, s2.xp, _p(st2), _p(n2g), rows, Cc,
                   _p(G[lp + ".norm2.weight"]), _p(G[lp + ".norm2.bias"]), 0, code)
             self.gemm(bw, f"aifi{i}.linear2.dW", ds.xp, 1, Cc, h.xp, F_, 1, _p(G[W2]), F_, Cc, F_, rows,
-                      out_code=DP_F32, beta=1.0)
-            bw.op(f"aifi{i}.linear2.db", lib.dp_colsum, ds.xp, Cc, rows, Cc, _p(G[lp + ".linear2.bias"]), 1, code)
+                      out_code=DP_F32, beta=1.0, colsum=_p(G[lp + ".linear2.bias"]))
             self.gemm(bw, f"aifi{i}.linear2.dx", ds.xp, Cc, 1, W2p, F_, 1, dh_.xp, F_, rows, F_, Cc)
             bw.op(f"aifi{i}.act.bwd", lib.dp_act_bwd, pre.xp, F_, dh_.xp, F_, dh_.xp, F_, rows, F_, act, code)
             self.gemm(bw, f"aifi{i}.linear1.dW", dh_.xp, 1, F_, x1.xp, Cc, 1, _p(G[W1]), Cc, F_, Cc, rows,
-                      out_code=DP_F32, beta=1.0)
-            bw.op(f"aifi{i}.linear1.db", lib.dp_colsum, dh_.xp, F_, rows, F_, _p(G[lp + ".linear1.bias"]), 1, code)
+                      out_code=DP_F32, beta=1.0, colsum=_p(G[lp + ".linear1.bias"]))
             self.gemm(bw, f"aifi{i}.linear1.dx", dh_.xp, F_, 1, W1p, Cc, 1, ds.xp, Cc, rows, Cc, F_, beta=1.0)
             bw.op(f"aifi{i}.norm1.bwd", lib.dp_ln_bwd, dsum1.xp, ds.xp, Cc, s1.xp, _p(st1), _p(n1g), rows, Cc,
                   _p(G[lp + ".norm1.weight"]), _p(G[lp + ".norm1.bias"]), 0, code)
             self.gemm(bw, f"aifi{i}.out.dW", dsum1.xp, 1, Cc, att.xp, Cc, 1, _p(G[Wo]), Cc, Cc, Cc, rows,
-                      out_code=DP_F32, beta=1.0)
-            bw.op(f"aifi{i}.out.db", lib.dp_colsum, dsum1.xp, Cc, rows, Cc, _p(G[lp + ".self_attn.out_proj.bias"]), 1,
-                  code)
+                      out_code=DP_F32, beta=1.0, colsum=_p(G[lp + ".self_attn.out_proj.bias"]))
             self.gemm(bw, f"aifi{i}.out.dx", dsum1.xp, Cc, 1, self.wptr(Wo), Cc, 1, datt.xp, Cc, rows, Cc, Cc)
             bw.op(f"aifi{i}.attn.bwd", lib.dp_attn_bwd, qkv.xp, 3 * Cc, qkv.xp + Cc * e, qkv.xp + 2 * Cc * e, 3 * Cc,
                   _p(Pm), datt.xp, att.xp, Cc, dqkv.xp, 3 * Cc, dqkv.xp + Cc * e, dqkv.xp + 2 * Cc * e, 3 * Cc,
                   B, 1, n, 0, 1, n, nh, dh, code)
             GW = G[Wi]
+            gib = G[lp + ".self_attn.in_proj_bias"]
             self.gemm(bw, f"aifi{i}.qk.dW", dqkv.xp, 1, 3 * Cc, q.xp, Cc, 1, _p(GW), Cc, 2 * Cc, Cc, rows,
-                      out_code=DP_F32, beta=1.0)
+                      out_code=DP_F32, beta=1.0, colsum=_p(gib))
             self.gemm(bw, f"aifi{i}.v.dW", dqkv.xp + 2 * Cc * e, 1, 3 * Cc, src.xp, Cc, 1, _p(GW, 2 * Cc * Cc), Cc, Cc,
-                      Cc, rows, out_code=DP_F32, beta=1.0)
-            bw.op(f"aifi{i}.in.db", lib.dp_colsum, dqkv.xp, 3 * Cc, rows, 3 * Cc, _p(G[lp + ".self_attn.in_proj_bias"]),
-                  1, code)
+                      Cc, rows, out_code=DP_F32, beta=1.0, colsum=_p(gib, 2 * Cc))
             # d src = d(src + attn) + (d q through q = src + pos) + d v
             bw.op(f"aifi{i}.dsrc", lib.dp_axpby_rows, src.gp, src.ld, dsum1.xp, Cc, C.c_float(1.0), None, 0,
                   C.c_float(0.0), rows, Cc, 1, code)

@@ -435,7 +435,7 @@ class TrainEngine:
     # ------------------------------------------------------------------ launch helpers
     def _gemm(self, tape, name, a, a_rs, a_ks, b, b_ks, b_ns, c, c_rs, m, n, k, in_code, out_code, bias=None,
               alpha=1.0, beta=0.0, act=0, gate=None, gate_rs=0, gate_code=None, batch=1, a_bs=0, b_bs=0, c_bs=0,
-              gate_bs=0):
+              gate_bs=0, colsum=None):
         d = GemmDesc()
         d.a, d.a_bs, d.a_rs, d.a_ks = a, a_bs, a_rs, a_ks
         d.b, d.b_bs, d.b_ks, d.b_ns = b, b_bs, b_ks, b_ns
@@ -447,6 +447,7 @@ class TrainEngine:
         d.gate, d.gate_bs, d.gate_rs = gate, gate_bs, gate_rs
         d.gate_dtype = self.code if gate_code is None else gate_code
         d.split_k = 0
+        d.colsum = colsum
         tape.keep.append(d)
         tape.op(name, self.lib.dp_gemm, C.byref(d))
         self.cur.cost(name, 2.0 * batch * m * n * k)
@@ -530,11 +531,12 @@ class TrainEngine:
         G = self.grads[gkey]
         N, K = G.shape
         code = self.code if in_code is None else in_code
-        self._gemm(tape, name + ".dW", dy, 1, ldy, x, ldx, 1, _p(G), K, N, K, rows, code, DP_F32, beta=1.0)
         bk = gkey[:-len("weight")] + "bias"
-        if bk in self.grads:
-            src, ld, sc = (dy, ldy, code) if dy32 is None else (dy32, ld32, DP_F32)
-            tape.op(name + ".db", self.lib.dp_colsum, src, ld, rows, N, _p(self.grads[bk]), 1, sc)
+        fuse = bk in self.grads and dy32 is None   # db += colsum(dy) inside the dW GEMM, which streams dy
+        self._gemm(tape, name + ".dW", dy, 1, ldy, x, ldx, 1, _p(G), K, N, K, rows, code, DP_F32, beta=1.0,
+                   colsum=_p(self.grads[bk]) if fuse else None)
+        if bk in self.grads and not fuse:
+            tape.op(name + ".db", self.lib.dp_colsum, dy32, ld32, rows, N, _p(self.grads[bk]), 1, DP_F32)
             self.cur.cost(name + ".db", 4.0 * rows * N)
 
     # ------------------------------------------------------------------ plan

@@ -441,6 +441,10 @@ typedef struct dp_gemm_desc {
   int32_t act;
   const void* gate; int64_t gate_bs, gate_rs; int32_t gate_dtype;
   int32_t split_k;
+  /* optional (NULL: none): colsum[m] += alpha * sum_k A(0, m, k) -- a Linear's bias gradient
+   * (the column sums of dy) from the weight-gradient GEMM dW += dy^T x that already streams dy;
+   * batch 1 */
+  float* colsum;
 } dp_gemm_desc;
 int dp_gemm(const dp_gemm_desc* d, void* stream);
 
@@ -600,6 +604,12 @@ int dp_bn_stats(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, 
  * running statistics as F.batch_norm does (momentum, unbiased variance; NULL: no update). */
 int dp_bn_finalize(const float* parts, int32_t nparts, float count, int32_t c, float eps, float momentum,
                    float* running_mean, float* running_var, float* mean_rstd, void* stream);
+/* dp_bn_stats then dp_bn_finalize of its single part (nparts 1, count = rows) in the statistics'
+ * launches: BatchNorm on one rank, no SyncBN exchange between the two. Same arithmetic, so the
+ * same outputs (out, mean_rstd, running statistics) bit for bit. */
+int dp_bn_stats_finalize(const void* x, int64_t ld, int32_t rows, int32_t c, float* out, float* ws, int64_t ws_bytes,
+                         float eps, float momentum, float* running_mean, float* running_var, float* mean_rstd,
+                         int32_t dtype, void* stream);
 /* y = act(g1 (z1 - mean1) rstd1 + b1 [+ g2 (z2 - mean2) rstd2 + b2]) [+ res]: ConvNormLayer's
  * norm + act (one branch) and VGGBlock's act(BN(conv3x3) + BN(conv1x1)) (two branches); res is
  * the CSP sum's other operand when fused. act: DP_ACT_*. */

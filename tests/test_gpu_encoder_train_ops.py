@@ -431,6 +431,33 @@ def test_conv_wgrad_implicit(B, h, w, cin, cout, k, st, pad, xpad):
     assert err < 2e-3, err
 
 
+@pytest.mark.parametrize("rows,c,dt", [(6400, 256, DP_BF16), (1000, 96, DP_F32), (409600, 64, DP_BF16)])
+def test_bn_stats_finalize_fused_equals_two_launch(rows, c, dt):
+    """dp_bn_stats_finalize (the one-rank BatchNorm statistics with the finalize in the same
+    launches) equals dp_bn_stats then dp_bn_finalize BIT FOR BIT: parts, (mean, rstd), running
+    statistics."""
+    lib = _lib.load()
+    torch.manual_seed(rows + c)
+    z = (torch.randn(rows, c, device=DEV) * 2 + 0.5).to(torch.bfloat16 if dt == DP_BF16 else torch.float32)
+    nb = int(lib.dp_bn_stats_ws_bytes(rows, c))
+    ws = torch.empty(nb // 4, device=DEV)
+    outs = []
+    for fused in (False, True):
+        parts, mr = torch.zeros(3, c, device=DEV), torch.empty(2, c, device=DEV)
+        rm, rv = torch.linspace(-1, 1, c, device=DEV), torch.linspace(0.5, 2, c, device=DEV)
+        if fused:
+            _lib.check(lib.dp_bn_stats_finalize(z.data_ptr(), c, rows, c, parts.data_ptr(), ws.data_ptr(), nb, 1e-5, 0.1,
+                                                rm.data_ptr(), rv.data_ptr(), mr.data_ptr(), dt, _s()), "stats+fin")
+        else:
+            _lib.check(lib.dp_bn_stats(z.data_ptr(), c, rows, c, parts.data_ptr(), ws.data_ptr(), nb, dt, _s()), "st")
+            _lib.check(lib.dp_bn_finalize(parts.data_ptr(), 1, float(rows), c, 1e-5, 0.1, rm.data_ptr(), rv.data_ptr(),
+                                          mr.data_ptr(), _s()), "fin")
+        torch.cuda.synchronize()
+        outs.append((parts, mr, rm, rv))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_conv_wgrad_more_than_2p24_pixels():
     """dp_conv_wgrad past 2^24 output pixels (its gather's float-reciprocal split is exact below
     2^24): the batch runs as image chunks accumulating into one scratch. 4100 images of 64 x 64

@@ -19,7 +19,8 @@ def _s():
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def gemm(a, a_st, b, b_st, c, c_rs, m, n, k, bias=None, alpha=1.0, beta=0.0, act=0, gate=None, gate_rs=0, split_k=0):
+def gemm(a, a_st, b, b_st, c, c_rs, m, n, k, bias=None, alpha=1.0, beta=0.0, act=0, gate=None, gate_rs=0, split_k=0,
+         colsum=None):
     lib = _lib.load()
     d = GemmDesc()
     d.a, d.a_bs, d.a_rs, d.a_ks = a.data_ptr(), 0, a_st[0], a_st[1]
@@ -33,6 +34,7 @@ def gemm(a, a_st, b, b_st, c, c_rs, m, n, k, bias=None, alpha=1.0, beta=0.0, act
     d.gate_rs = gate_rs
     d.gate_dtype = CODE[gate.dtype] if gate is not None else 0
     d.split_k = split_k
+    d.colsum = colsum.data_ptr() if colsum is not None else None
     _lib.check(lib.dp_gemm(C.byref(d), _s()), "dp_gemm")
 
 
@@ -65,7 +67,9 @@ def test_gemm_linear_dgrad_wgrad(dt, m, n, k):
 
 
 @pytest.mark.parametrize("m,n,k,lda,ldb", [(512, 1536, 25600, 520, 1552), (136, 104, 9999, 136, 104),
-                                            (256, 256, 409600, 256, 256), (1024, 264, 6400, 1032, 264)])
+                                            (256, 256, 409600, 256, 256), (1024, 264, 6400, 1032, 264),
+                                            (48, 336, 409600, 48, 336), (64, 32, 8400, 72, 40), (66, 256, 8640, 72, 256),
+                                            (256, 256, 1000, 256, 256)])
 def test_gemm_wgrad_dma_ring(m, n, k, lda, ldb):
     """dp_gemm's weight-gradient route (wgrad_tt_kernel: C += alpha dy^T x with dy [k][m] and x
     [k][n] in k-major rows, LDS-DMA ring, split-K float atomics) vs torch fp32 on the same bf16
@@ -79,8 +83,15 @@ def test_gemm_wgrad_dma_ring(m, n, k, lda, ldb):
     gemm(dy, (1, lda), x, (ldb, 1), dW, n, m, n, k, alpha=0.5, beta=1.0)
     ref = c0 + 0.5 * (dy[:, :m].float().t() @ x[:, :n].float())
     err = (dW - ref).abs().max().item() / ref.abs().max().item()
-    print(f"wgrad {m}x{n} over {k}: max err {err:.3g} of scale")
-    assert err <= 1e-4
+    # the fused bias gradient (colsum += sum over k of dy, alpha 1), onto existing values
+    db0 = torch.randn(m, device=DEV)
+    db, dW2 = db0.clone(), c0.clone()
+    gemm(dy, (1, lda), x, (ldb, 1), dW2, n, m, n, k, beta=1.0, colsum=db)
+    rdb = db0 + dy[:, :m].float().sum(0)
+    e_db = (db - rdb).abs().max().item() / rdb.abs().max().item()
+    e_w2 = (dW2 - (c0 + dy[:, :m].float().t() @ x[:, :n].float())).abs().max().item() / ref.abs().max().item()
+    print(f"wgrad {m}x{n} over {k}: max err {err:.3g} of scale, fused bias grad {e_db:.3g}")
+    assert err <= 1e-4 and e_w2 <= 2e-4 and e_db <= 1e-4
 
 
 def test_gemm_generic_strides_and_forced_split():
