@@ -19,6 +19,7 @@
 // Split-K (when the M x N grid cannot fill the chip, e.g. wgrad over 10^5 rows): each block
 // adds alpha * its partial product into f32 C with atomics (C pre-initialised by the caller).
 #include "common.h"
+#include <cmath>
 #include "conv_lds.h"
 
 extern "C" int dp_colsum(const void* x, int64_t ld, int32_t rows, int32_t n, float* out, int32_t accumulate,
@@ -701,6 +702,20 @@ void wgrad_tt_kernel(const GemmArgs g, int ntiles, int tiles_n) {
   }
 }
 
+// K splits of the weight-gradient kernel: each split adds a 128 x 256 f32 tile with float atomics
+// (131 KB, ~0.1 us of the chip's ~1.3 TB/s atomic rate per split and tile), each K-step costs a
+// block ~0.9 us, so a launch takes about ks64 / sp * 0.9 + ntl * sp * 0.1 us: sp ~ sqrt(8.6 ks64 /
+// ntl), at most one round of blocks (one per CU) and at least 4 K-steps per split. (One block per
+// CU regardless measured 27 us a call on the decoder's 256 x 256 weight gradients over 13824 rows,
+// 2 K-steps a block behind 33 MB of atomics.)
+inline int wgrad_tt_splits(int ntl, int ks64) {
+  int sp = (int)std::lround(std::sqrt(8.6 * ks64 / (double)ntl));
+  const int cap = (dpconv::num_cus() + ntl - 1) / ntl;
+  if (sp > cap) sp = cap;
+  if (sp > ks64 / 4) sp = ks64 / 4;
+  return sp < 1 ? 1 : sp;
+}
+
 // dw[co][ci][tap] += s[co][tap][ci] (the reference's [cout][cin][kh][kw] from the tap-major sums)
 __global__ void wgrad_permute_kernel(const float* __restrict__ s, float* __restrict__ dw, int cout, int cin, int taps) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over dw
@@ -768,9 +783,7 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
     const int tmw = (d.m + WT_BM - 1) / WT_BM, tnw = (d.n + WT_BN - 1) / WT_BN;
     const int ntl = tmw * tnw;
     const int ksteps64 = (d.k + 63) / 64;
-    int sp = (dpconv::num_cus() + ntl - 1) / ntl;   // one block per CU, one round
-    if (sp > ksteps64 / 4) sp = ksteps64 / 4;
-    if (sp < 1) sp = 1;
+    const int sp = wgrad_tt_splits(ntl, ksteps64);
     const int kchunk = ((ksteps64 + sp - 1) / sp) * 64;
     // 32-bit buffer offsets from each split's first row
     if (((int64_t)kchunk * d.a_ks + d.m) * 2 < 0x7ff00000ll && ((int64_t)kchunk * d.b_ks + d.n) * 2 < 0x7ff00000ll) {
@@ -911,9 +924,7 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
       const int tmw = (cout + WT_BM - 1) / WT_BM, tnw = (N + WT_BN - 1) / WT_BN;
       const int ntl = tmw * tnw;
       const int ks64 = (int)((K + 63) / 64);
-      int sp = (dpconv::num_cus() + ntl - 1) / ntl;
-      if (sp > ks64 / 4) sp = ks64 / 4;
-      if (sp < 1) sp = 1;
+      const int sp = wgrad_tt_splits(ntl, ks64);
       g.splits = sp;
       g.kchunk = ((ks64 + sp - 1) / sp) * 64;
       static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_tt_kernel<true>),

@@ -515,7 +515,9 @@ class TrainEngine:
         N, K = W.shape
         code = self.code if in_code is None else in_code
         gc = self.code if gate_code is None else gate_code
-        if (code == DP_BF16 and wt is None and wkey in self.sd32 and N % 8 == 0 and self._rows_ok(dy, ldy) and self._rows_ok(dx, ldx) and
+        # (N % 8 != 0: dy's rows are padded to 16 bytes with zeros -- to_dt -- and the kernel reads
+        # their last 16-byte chunk whole against zero-padded packed weights)
+        if (code == DP_BF16 and wt is None and wkey in self.sd32 and self._rows_ok(dy, ldy) and self._rows_ok(dx, ldx) and
                 (beta == 0.0 or (beta == 1.0 and gate is None)) and (gate is None or gc == DP_BF16)):
             Wt, kpad = self._wt_pack(wkey)
             self._conv1x1(tape, name, dy, ldy, rows, _p(Wt), kpad, N, K, dx, ldx, None, 0, res=beta == 1.0)
@@ -1002,9 +1004,14 @@ class TrainPlan:
             """f32 gradient rows as the GEMM dtype (a copy in bf16 mode, the buffer itself in fp32)."""
             if not conv:
                 return src, (ld or n)
-            d = buf(rows_, n)
-            bw.op(name, lib.dp_convert_rows, _p(src), DP_F32, ld or n, _p(d), code, n, rows_, n, C.c_float(1.0), 0)
-            return d, n
+            # rows padded to a 16-byte multiple: the GEMMs then load whole 16-byte row chunks (the
+            # pose head's 66 columns otherwise took dp_gemm's per-element path)
+            ldp = -(-n // 8) * 8
+            d = buf(rows_, ldp)
+            if ldp != n:
+                d.zero_()   # the pad columns stay zero (the convert writes the first n)
+            bw.op(name, lib.dp_convert_rows, _p(src), DP_F32, ld or n, _p(d), code, ldp, rows_, n, C.c_float(1.0), 0)
+            return d, ldp
 
         def mlp_bwd(name, dout_dt, ld_out, dout32, ld32, rows_, layers, ins, wkeys):
             """Backward of an MLP chain: layers[i] output i (ReLU between); ins[i] input of layer i.
