@@ -520,7 +520,8 @@ class TrainEngine:
         if (code == DP_BF16 and wt is None and wkey in self.sd32 and self._rows_ok(dy, ldy) and self._rows_ok(dx, ldx) and
                 (beta == 0.0 or (beta == 1.0 and gate is None)) and (gate is None or gc == DP_BF16)):
             Wt, kpad = self._wt_pack(wkey)
-            self._conv1x1(tape, name, dy, ldy, rows, _p(Wt), kpad, N, K, dx, ldx, None, 0, res=beta == 1.0)
+            # K of the conv = N rounded up to 8: dy's pad columns are zeros (to_dt) against zero weights
+            self._conv1x1(tape, name, dy, ldy, rows, _p(Wt), kpad, -(-N // 8) * 8, K, dx, ldx, None, 0, res=beta == 1.0)
             if gate is not None:   # relu'(gate): the mask applied in place
                 tape.op(name + ".mask", self.lib.dp_act_bwd, gate, ld_gate, dx, ldx, dx, ldx, rows, K, 1, code)
             return
