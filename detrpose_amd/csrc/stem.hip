@@ -15,6 +15,7 @@
 // cin 32 -> lane g holds taps 0..3 of channels 8g..8g+7; cin 16 -> taps {g>>1, 2+(g>>1)} of
 // channels 8(g&1)..+7, completed by one cross-half exchange (lane ^ 32).
 #include "common.h"
+#include "stem_k.h"
 
 namespace {
 
@@ -60,12 +61,13 @@ __device__ __forceinline__ void stem_store(bf16_t* op, const f32x4 (&acc)[NT], c
 }
 
 // StemBlock.stem1 (hgnetv2.py:171-177): 3x3 stride-2 pad-1 conv over the f32 NCHW image,
-// 3 -> COUT channels, folded BN + ReLU (+ LAB), NHWC bf16 out. K = 27 taps (c, ky, kx) fit
-// one 32-wide MFMA slab: lane (q, g) gathers k = 8g .. 8g+7 of output pixel x0 + q straight
-// from the image (f32 -> bf16 in registers; k >= 27 is zero), the f32 weights are converted
-// into the A fragments once per wave. 864 FMAs per pixel become 2 MFMAs per 16 pixels, so
-// the kernel is a stream: 12 image bytes in (L1/L2 absorb the 3x3/stride-2 overlap) and
-// 2*COUT bytes out per pixel.
+// 3 -> COUT channels, folded BN + ReLU (+ LAB), NHWC bf16 out. The 27 products (c, ky, kx)
+// are two MFMA K slabs in the order of stem_k.h (the one-launch stem's, so the two kernels
+// agree bit for bit): lane (q, g) gathers its slots of output pixel x0 + q straight from the
+// image (f32 -> bf16 in registers; a zero slot loads nothing: out-of-range offset), the f32
+// weights are converted into the A fragments once per wave. 864 FMAs per pixel become
+// 4 MFMAs per 16 pixels, so the kernel is a stream: 12 image bytes in (L1/L2 absorb the
+// 3x3/stride-2 overlap) and 2*COUT bytes out per pixel.
 template <int COUT>
 __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict__ img, int batch, int H, int W,
                                                          const float* __restrict__ wt, const float* __restrict__ bias,
@@ -75,19 +77,24 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
   constexpr int G = 4;                          // 16-pixel groups in flight per wave
   const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
   const int OH = (H + 1) / 2, OW = (W + 1) / 2;
-  bf16x8 wa[NT];
-  int tc[8], tky[8], tkx[8];
-  bool tok[8];
+  bf16x8 wa[2][NT];   // [slab][tile]
+  int tky[2][8], tkx[2][8];
+  bool tok[2][8];
+  int loff[2][8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = 8 * g + e;
-    const int c = k / 9, t = k - 9 * c;
-    tok[e] = k < 27;
-    tky[e] = t / 3, tkx[e] = t - 3 * (t / 3);
-    tc[e] = k < 27 ? c : 0;
+  for (int sl = 0; sl < 2; ++sl)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) wa[j][e] = (bf16_t)(k < 27 ? wt[stem_chan<NT>(j, q >> 2, q & 3) * 27 + k] : 0.f);
-  }
+    for (int e = 0; e < 8; ++e) {
+      int c = 0, ky = 0, kx = 0;
+      const bool ok = stem1_slot(sl, g, e, c, ky, kx);
+      tok[sl][e] = ok, tky[sl][e] = ky, tkx[sl][e] = kx;
+      // lane-constant part of the gather offset: plane c, row ky, column kx, this lane's pixel 2q;
+      // the per-group part (image, row 2oy-1, column 2*ox0-1) is wave-uniform
+      loff[sl][e] = (c * H + ky) * W + kx + 2 * q;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        wa[sl][j][e] = (bf16_t)(ok ? wt[stem_chan<NT>(j, q >> 2, q & 3) * 27 + c * 9 + ky * 3 + kx] : 0.f);
+    }
   float bsum[NT][4];
 #pragma unroll
   for (int j = 0; j < NT; ++j)
@@ -98,13 +105,8 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
   const int ngroups = batch * OH * gx;
   const int nw = gridDim.x * 4;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  // lane-constant part of each gather offset: plane c, row ky, column kx, and this lane's
-  // pixel 2q; the per-group part (image, row 2oy-1, column 2*ox0-1) is wave-uniform
-  int loff[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) loff[e] = (tc[e] * H + tky[e]) * W + tkx[e] + 2 * q;
   for (int base = wid * G; base < ngroups; base += nw * G) {
-    bf16x8 xb[G];
+    bf16x8 xb[G][2];
     int pb[G], py[G], px0[G];
 #pragma unroll
     for (int i = 0; i < G; ++i) {
@@ -123,12 +125,19 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
       const int u = (2 * oy - 1) * W + 2 * ox0 - 1;
       const int ix0 = 2 * (ox0 + q) - 1;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int iy = 2 * oy - 1 + tky[e], ix = ix0 + tkx[e];
-        const bool ok = tok[e] && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-        const unsigned bits = __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? 4 * (u + loff[e]) : 0x7ffffff0, 0, 0);
-        xb[i][e] = (bf16_t)__builtin_bit_cast(float, bits);   // the builtin returns the raw dword
-      }
+      for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if ((e & 3) == 3 || (sl == 1 && e >= 4)) {   // zero in every lane (stem_k.h): no load
+            xb[i][sl][e] = (bf16_t)0.f;
+            continue;
+          }
+          const int iy = 2 * oy - 1 + tky[sl][e], ix = ix0 + tkx[sl][e];
+          const bool ok = tok[sl][e] && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+          const unsigned bits =
+              __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? 4 * (u + loff[sl][e]) : 0x7ffffff0, 0, 0);
+          xb[i][sl][e] = (bf16_t)__builtin_bit_cast(float, bits);   // the builtin returns the raw dword
+        }
     }
 #pragma unroll
     for (int i = 0; i < G; ++i) {
@@ -137,8 +146,10 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
       bf16_t* op = out + (int64_t)pb[i] * obs + ((int64_t)py[i] * OW + ox) * ops;
       f32x4 acc[NT];
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j], xb[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      for (int j = 0; j < NT; ++j) {
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][j], xb[i][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][j], xb[i][1], acc[j], 0, 0, 0);
+      }
       stem_store<NT, DP_ACT_RELU>(op, acc, bsum, g, COUT, has_lab, ls, lb);
     }
   }

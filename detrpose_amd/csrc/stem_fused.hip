@@ -20,26 +20,33 @@
 //
 // Every stage is 16x16x32 bf16 MFMAs with the weights as the A operand and 16 pixels as the
 // B operand (C^T = W X^T: lane (q, g) ends with output channels of pixel q), the K order of
-// the packed weights (tap-major, k = tap * cin + ci) and f32 accumulation in the same
-// sequence as the unfused kernels, bf16 rounding at the same points (each stage's output):
-// the result matches the five-launch path bit for bit. 32-channel outputs use the permuted
-// weight rows of stem.hip (lane g holds channels 8g .. 8g+7: one 16-byte LDS store).
+// the packed weights (tap-major, k = tap * cin + ci; stem1: stem_k.h) and f32 accumulation in
+// the same sequence as the unfused kernels, bf16 rounding at the same points (each stage's
+// output): the result matches the five-launch path bit for bit. 32-channel outputs use the
+// permuted weight rows of stem.hip (lane g holds channels 8g .. 8g+7: one 16-byte LDS store).
 // Weights: stem1/2a/2b/4 fragments in registers for the block's life, stem3's 32 x 576 in
 // LDS. The image: the tile's (4TH+7) x (4TW+8) x 3 window is loaded with coalesced 16-byte
-// loads (issued before this tile's stem3 for the next tile, so the HBM latency hides behind
-// stem3/stem4), rounded to bf16 into an LDS patch, and stem1's B fragments are built from it.
+// loads two tiles ahead, rounded to bf16 into a pixel-major LDS patch ([row][col][c0 c1 c2 0],
+// 8 bytes a pixel), so each stem1 B fragment is two 8-byte reads of two taps' channels.
+//
+// Pipeline (per-stage ablation, profiles/r6h_stem_ablation.txt: every stage of the five-barrier
+// form cost 70-130 us at L b64, latency rather than work at two waves per SIMD): one block per
+// CU walks its tiles in three barrier phases per tile,
+//   A: waves 0-3: stem3 of tile t (one output row each, both 16-channel halves) and stem4
+//      straight from stem3's registers (the C layout of stem3 is stem4's B fragment), to HBM;
+//      waves 4-7: stem1 of tile t+1 (image patch -> s1); every wave issues tile t+2's image loads
+//   B: stem2a (s1 -> s2a) and the max-pool (s1 -> cat 0..31) of tile t+1
+//   C: stem2b (s2a -> cat 32..63) of tile t+1; tile t+2's image -> LDS patch
+// so stem1 overlaps stem3/stem4 and the image latency hides behind three phases. Barriers wait
+// for LDS traffic only (lgkmcnt), never for the image loads in flight.
 #include "common.h"
+#include "stem_k.h"
 
 //
 // LDS layout: the stage maps are stored planar by 16-byte channel chunk ([chunk][pixel],
 // 16 B per pixel per plane) so that the 16 lanes of an MFMA B-fragment read (16 consecutive
 // pixels, one chunk per lane group) hit 16 distinct bank slots: plane strides are multiples of
-// 256 B (cat: 16 mod 256, whose stem3 reads step 2 pixels per lane). Every address a stage
-// reads or writes is a lane constant (the tile geometry is the same for every tile) plus a
-// compile-time offset: the per-tile work is MFMAs, LDS traffic and the epilogues.
-#ifndef DP_STEM_ABL
-#define DP_STEM_ABL 0   // ablation builds only: skip stage 1 / 2 / 3 / 4 / 5 (bits 0..4), 32: no image loads
-#endif
+// 256 B (cat: 16 mod 256, whose stem3 reads step 2 pixels per lane).
 
 namespace {
 
@@ -49,22 +56,24 @@ constexpr int R1H = 2 * TH + 3, R1W = 2 * TW + 3, N1 = R1H * R1W;   // 11 x 35 s
 constexpr int R2H = 2 * TH + 2, R2W = 2 * TW + 2, N2 = R2H * R2W;   // 10 x 34 stem2a region
 constexpr int RCH = 2 * TH + 1, RCW = 2 * TW + 1, NC = RCH * RCW;   //  9 x 33 cat region
 constexpr int G1 = (N1 + 15) / 16, G2 = (N2 + 15) / 16, GC = (NC + 15) / 16;
-constexpr int PF1 = (G1 + NWAVE - 1) / NWAVE, PF2 = (G2 + NWAVE - 1) / NWAVE, PFC = (GC + NWAVE - 1) / NWAVE;
+constexpr int PF2 = (G2 + NWAVE - 1) / NWAVE, PFC = (GC + NWAVE - 1) / NWAVE;
 constexpr int NPOOL = NC * 4, PFP = (NPOOL + NTHR - 1) / NTHR;      // max-pool items (pixel, chunk)
 constexpr int K3 = 9 * 64;
 constexpr int W3ROW = K3 * 2 + 16;             // +16 B: 16 consecutive rows hit 16 distinct bank slots
 constexpr int rup(int x, int m) { return (x + m - 1) / m * m; }
-constexpr int P1 = rup(N1 * 16, 256), P2 = rup(N2 * 16, 256), PC = rup(NC * 16 - 16, 256) + 16, P3 = TH * TW * 16;
-constexpr int OFF_S1 = 0, OFF_S2 = OFF_S1 + 4 * P1, OFF_CAT = OFF_S2 + 2 * P2, OFF_S3 = OFF_CAT + 8 * PC;
-constexpr int OFF_W3 = OFF_S3 + 4 * P3;
-// image patch: rows 4 oy0 - 3 .. +IPH-1, columns 4 ox0 - 4 .. +IPW-1 (16-byte aligned starts)
+constexpr int P1 = rup(N1 * 16, 256), P2 = rup(N2 * 16, 256), PC = rup(NC * 16 - 16, 256) + 16;
+constexpr int OFF_S1 = 0, OFF_S2 = OFF_S1 + 4 * P1, OFF_CAT = OFF_S2 + 2 * P2, OFF_W3 = OFF_CAT + 8 * PC;
+// image patch: rows 4 oy0 - 3 .. +IPH-1, columns 4 ox0 - 4 .. +IPW-1 (16-byte aligned starts),
+// 8 bytes a pixel; the row stride is 8 mod 16 bytes (146 dwords, 18 mod 64 banks), so the two
+// rows of one fragment read (and lane groups g, g+1) land on disjoint bank pairs
 constexpr int IPH = 2 * R1H + 1, IPW = 2 * R1W + 2;                 // 23 x 72
-constexpr int IPV = IPW / 4, NIMG = 3 * IPH * IPV;                  // float4 per row, per tile
-constexpr int PFV = (NIMG + NTHR - 1) / NTHR;                        // float4 loads per thread
-// 4 planes: stem1's K = 27 is padded to 32 with k = 27..31 -> plane 3, which stays zero
-constexpr int IPP = IPH * IPW * 2, OFF_IMG = OFF_W3 + 32 * W3ROW;
-constexpr int LDS_BYTES = OFF_IMG + 4 * IPP;
-static_assert(LDS_BYTES <= 160 * 1024 && TH * TW == 16 * 4 && IPW % 4 == 0 && OFF_IMG % 16 == 0 && IPP % 16 == 0,
+constexpr int IRS = IPW * 8 + 8;
+constexpr int IPV = IPW / 4, NIMG = IPH * IPV;                      // 4-column items (3 float4 loads each)
+constexpr int OFF_IMG = OFF_W3 + 32 * W3ROW;
+constexpr int OFF_Z = OFF_IMG + IPH * IRS;                          // 8 zero bytes (slab 1 of lanes g > 0)
+constexpr int LDS_BYTES = OFF_Z + 16;
+static_assert(LDS_BYTES <= 160 * 1024 && TH * TW == 16 * 4 && IPW % 4 == 0 && OFF_IMG % 16 == 0 && NIMG <= NTHR &&
+                  TH == NWAVE / 2,
               "stem tile");
 
 // output channel of C element (tile j, lane group g, row r) for the permuted 32-channel convs
@@ -97,6 +106,14 @@ __device__ __forceinline__ void lds_st(char* smem, int off, const T& v) {
   *reinterpret_cast<T*>(smem + off) = v;
 }
 
+// block barrier for LDS hand-offs: LDS traffic retired, then s_barrier; the image loads in
+// flight (vmcnt) are not waited for
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // folded-BN bias + ReLU (+ LAB); + 0.f turns a -0 into +0, so the non-negative bf16 maps can
 // be max-pooled as unsigned 16-bit integers
 template <bool LAB>
@@ -106,12 +123,12 @@ __device__ __forceinline__ float relu_lab(float x, const StemArgs& P, int s) {
   return x;
 }
 
-// region pixel p -> (row, column) packed as row << 8 | column
-template <int RW>
-__device__ __forceinline__ int rc_of(int p) {
-  const int r = p / RW;
-  return (r << 8) | (p - r * RW);
-}
+// a tile's place: image b, stem3 output origin (oy0, ox0), region origin (cy0, cx0) in the
+// 320x320 stage maps, and whether every region pixel lies inside them (no zeroing checks)
+struct TileGeom {
+  int b, oy0, ox0, cy0, cx0;
+  bool interior;
+};
 
 template <int COUT, bool LAB>
 __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restrict__ img, int H, int W, StemArgs P,
@@ -133,18 +150,21 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
     const int ch = chan32(row >> 4, (row & 15) >> 2, row & 3);
     lds_st(smem, OFF_W3 + row * W3ROW + kc * 16, *reinterpret_cast<const bf16x8*>(P.w3 + (int64_t)ch * P.k3 + kc * 8));
   }
-  for (int e = tid; e < IPP / 16; e += NTHR) lds_st(smem, OFF_IMG + 3 * IPP + 16 * e, u32x4{0u, 0u, 0u, 0u});
+  if (tid == 0) lds_st(smem, OFF_Z, u32x4{0u, 0u, 0u, 0u});
   // ---- register weights and biases
-  bf16x8 wa1[2], wa2[4], wb2[2][2], w4f[NT4];
-  int poff[8];   // stem1 K value 8g + e: patch byte offset of (c, ky, kx + 1); k >= 27 lands in plane 3
+  bf16x8 wa1[2][2], wa2[4], wb2[2][2], w4f[NT4];   // wa1: [K slab][16-channel tile]
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = 8 * g + e;   // stem1 K: k = c*9 + ky*3 + kx (the OIHW flattening of the f32 weights)
-    const int c = k / 9, t = k - 9 * (k / 9), ky = t / 3, kx = t - 3 * (t / 3);
-    poff[e] = OFF_IMG + ((c * IPH + ky) * IPW + kx + 1) * 2;
+  for (int sl = 0; sl < 2; ++sl)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) wa1[j][e] = (bf16_t)(k < 27 ? P.w1[chan32(j, q >> 2, q & 3) * 27 + k] : 0.f);
-  }
+    for (int e = 0; e < 8; ++e) {
+      int c = 0, ky = 0, kx = 0;
+      const bool ok = stem1_slot(sl, g, e, c, ky, kx);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        wa1[sl][j][e] = (bf16_t)(ok ? P.w1[chan32(j, q >> 2, q & 3) * 27 + c * 9 + ky * 3 + kx] : 0.f);
+    }
+  // stem1 slab-0 fragment: two taps' 8-byte pixels at these offsets from the pixel's tap (0, 0)
+  const int o1a = g < 3 ? g * IRS : IRS + 16, o1b = g < 3 ? g * IRS + 8 : 16;
 #pragma unroll
   for (int s = 0; s < 4; ++s) wa2[s] = *reinterpret_cast<const bf16x8*>(P.w2a + (int64_t)q * P.k2a + 32 * s + 8 * g);
 #pragma unroll
@@ -168,224 +188,227 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
     for (int j = 0; j < NT4; ++j) bs4[j][r] = P.b4[16 * j + 4 * g + r];
   }
 
-  // ---- tile-invariant lane geometry (region pixel of each item this lane handles)
-  int rc1[PF1], a1[PF1];             // stem1: (row, col), patch byte offset of the window corner
-#pragma unroll
-  for (int i = 0; i < PF1; ++i) {
-    const int p = min((wave + NWAVE * i) * 16 + q, N1 - 1);
-    rc1[i] = rc_of<R1W>(p);
-    a1[i] = ((rc1[i] >> 8) * 2 * IPW + (rc1[i] & 255) * 2) * 2;
-  }
-  int rc2[PF2], a2[PF2];             // stem2a: (row, col), s1 read address of tap (0, 0), chunk g
-#pragma unroll
-  for (int i = 0; i < PF2; ++i) {
-    const int p = min((wave + NWAVE * i) * 16 + q, N2 - 1);
-    rc2[i] = rc_of<R2W>(p);
-    a2[i] = OFF_S1 + g * P1 + ((rc2[i] >> 8) * R1W + (rc2[i] & 255)) * 16;
-  }
-  int rcp[PFP], ap[PFP], sp[PFP];    // pool item (chunk c = it / NC, pixel it % NC): s1 read, cat write
-#pragma unroll
-  for (int t = 0; t < PFP; ++t) {
-    const int it = min(tid + NTHR * t, NPOOL - 1);
-    const int c = it / NC, p = it - c * NC;
-    rcp[t] = rc_of<RCW>(p);
-    ap[t] = OFF_S1 + c * P1 + ((rcp[t] >> 8) * R1W + (rcp[t] & 255)) * 16;
-    sp[t] = OFF_CAT + c * PC + p * 16;
-  }
-  int rcc[PFC], ac[PFC];             // stem2b: (row, col), s2a read address of k-slab 0
-#pragma unroll
-  for (int i = 0; i < PFC; ++i) {
-    const int p = min((wave + NWAVE * i) * 16 + q, NC - 1);
-    rcc[i] = rc_of<RCW>(p);
-    ac[i] = OFF_S2 + (g & 1) * P2 + ((rcc[i] >> 8) * R2W + (rcc[i] & 255) + (g >> 1)) * 16;
-  }
-  const int i3 = wave & 3, j3 = wave >> 2;   // stem3: output row i3, N tile j3
-  const int a3 = OFF_CAT + g * PC + (2 * i3 * RCW + 2 * q) * 16;
-  const int w3a = OFF_W3 + (16 * j3 + q) * W3ROW + 16 * g;
+  auto geom = [&](int tile) __attribute__((always_inline)) {
+    TileGeom t;
+    const int tx = tile % tiles_x, rest = tile / tiles_x;
+    const int ty = rest % tiles_y;
+    t.b = rest / tiles_y;
+    t.oy0 = ty * TH, t.ox0 = tx * TW;
+    t.cy0 = 2 * t.oy0 - 1, t.cx0 = 2 * t.ox0 - 1;
+    t.interior = t.cy0 >= 0 && t.cx0 >= 0 && t.cy0 + R1H <= OH1 && t.cx0 + R1W <= OW1;
+    return t;
+  };
+  auto in_map = [&](const TileGeom& t, int ry, int rx) __attribute__((always_inline)) {
+    return t.interior || ((unsigned)(t.cy0 + ry) < (unsigned)OH1 && (unsigned)(t.cx0 + rx) < (unsigned)OW1);
+  };
 
-  // ---- image window of a tile: float4 loads into registers (issued a tile ahead), then
-  // rounded to bf16 into the LDS patch [c][row][col]. Buffer loads: an out-of-range offset
-  // returns 0 (the conv's zero padding; W % 4 == 0 so a float4 is wholly in or out).
-  f32x4 xr[PFV];
+  // ---- image window of a tile: thread (row r, 4 columns v) loads the 3 channels' float4s
+  // (buffer loads: an out-of-range offset returns 0 = the conv's zero padding; W % 4 == 0 so a
+  // float4 is wholly in or out), then writes 4 pixels [c0 c1 c2 0] to the patch
+  f32x4 xr[3];
   auto load_img = [&](int tile) __attribute__((always_inline)) {
     const int tx = tile % tiles_x, rest = tile / tiles_x;
     const int ty = rest % tiles_y, b = rest / tiles_y;
     const int iy0 = 4 * ty * TH - 3, ix0 = 4 * tx * TW - 4;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(img + (int64_t)b * 3 * H * W), (short)0, 0x7ffffff0, 0x00020000);
+    const int r = tid / IPV, v = tid - r * IPV;
+    const int iy = iy0 + r, ix = ix0 + 4 * v;
+    const bool ok = tid < NIMG && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
 #pragma unroll
-    for (int t = 0; t < PFV; ++t) {
-      const int e = tid + NTHR * t;
-      const int c = e / (IPH * IPV), rem = e - c * (IPH * IPV);
-      const int r = rem / IPV, v = rem - r * IPV;
-      const int iy = iy0 + r, ix = ix0 + 4 * v;
-      const bool ok = e < NIMG && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    for (int c = 0; c < 3; ++c) {
       int o = ok ? 4 * ((c * H + iy) * W + ix) : 0x7ffffff0;
       asm volatile("" : "+v"(o));   // keep the select: a split into branches would drain vmcnt
-      xr[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+      xr[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
     }
   };
   auto store_img = [&]() __attribute__((always_inline)) {
+    if (tid < NIMG) {
+      const int r = tid / IPV, v = tid - r * IPV;
 #pragma unroll
-    for (int t = 0; t < PFV; ++t) {
-      const int e = tid + NTHR * t;
-      if (e < NIMG) {
-        const int c = e / (IPH * IPV), rem = e - c * (IPH * IPV);
-        const int r = rem / IPV, v = rem - r * IPV;
+      for (int x = 0; x < 4; ++x) {
         bf16x4 h4;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) h4[k] = (bf16_t)xr[t][k];
-        lds_st(smem, OFF_IMG + ((c * IPH + r) * IPW + 4 * v) * 2, h4);
+        h4[0] = (bf16_t)xr[0][x], h4[1] = (bf16_t)xr[1][x], h4[2] = (bf16_t)xr[2][x], h4[3] = (bf16_t)0.f;
+        lds_st(smem, OFF_IMG + r * IRS + (4 * v + x) * 8, h4);
       }
     }
   };
-  load_img(L);
-  store_img();
-  for (int tile = L; tile < ntiles; tile += G) {
-    const int tx = tile % tiles_x, rest = tile / tiles_x;
-    const int ty = rest % tiles_y, b = rest / tiles_y;
-    const int oy0 = ty * TH, ox0 = tx * TW;
-    const int cy0 = 2 * oy0 - 1, cx0 = 2 * ox0 - 1;
-    // interior tile: every region pixel inside the 320x320 map (no zeroing checks)
-    const bool interior = cy0 >= 0 && cx0 >= 0 && cy0 + R1H <= OH1 && cx0 + R1W <= OW1;
-    auto in_map = [&](int rc) __attribute__((always_inline)) {
-      return interior || ((unsigned)(cy0 + (rc >> 8)) < (unsigned)OH1 && (unsigned)(cx0 + (rc & 255)) < (unsigned)OW1);
-    };
-    __syncthreads();   // the tile's image patch is in LDS
 
-    // ---- stage 1: stem1 over the s1 region: pixel (ry, rx) reads patch rows 2ry + ky,
-    // columns 2rx + kx + 1
-    if (!(DP_STEM_ABL & 1)) {
+  // ---- stem1 over the s1 region (groups wsub, wsub + NW, ...): pixel (ry, rx) reads patch
+  // rows 2ry + ky, columns 2rx + kx + 1
+  auto stage1 = [&](const TileGeom& t, int wsub, auto nw_c) __attribute__((always_inline)) {
+    constexpr int NW = decltype(nw_c)::value;
 #pragma unroll
-      for (int i = 0; i < PF1; ++i) {
-        const int grp = wave + NWAVE * i;
-        if (grp >= G1) break;
-        bf16x8 xb;
+    for (int i = 0; i < (G1 + NW - 1) / NW; ++i) {
+      const int grp = wsub + NW * i;
+      if (grp >= G1) break;
+      const int p = min(grp * 16 + q, N1 - 1);
+      const int ry = p / R1W, rx = p - ry * R1W;
+      const int base = OFF_IMG + 2 * ry * IRS + (2 * rx + 1) * 8;
+      const bf16x4 lo = lds_ld<bf16x4>(smem, base + o1a), hi = lds_ld<bf16x4>(smem, base + o1b);
+      const bf16x4 z = lds_ld<bf16x4>(smem, g == 0 ? base + 2 * IRS + 16 : OFF_Z);   // tap (2, 2)
+      const bf16x8 xb0 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const bf16x8 xb1 = {z[0], z[1], z[2], z[3], (bf16_t)0.f, (bf16_t)0.f, (bf16_t)0.f, (bf16_t)0.f};
+      f32x4 acc[2];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) xb[e] = lds_ld<bf16_t>(smem, poff[e] + a1[i]);
-        f32x4 acc[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[j], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const bool ok = in_map(rc1[i]);
-        bf16x8 o;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ok ? relu_lab<LAB>(acc[j][r] + bs1[j][r], P, 0) : 0.f);
-        if (grp * 16 + q < N1) lds_st(smem, OFF_S1 + g * P1 + (grp * 16 + q) * 16, o);
+      for (int j = 0; j < 2; ++j) {
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[0][j], xb0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[1][j], xb1, acc[j], 0, 0, 0);
       }
+      const bool ok = in_map(t, ry, rx);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ok ? relu_lab<LAB>(acc[j][r] + bs1[j][r], P, 0) : 0.f);
+      if (grp * 16 + q < N1) lds_st(smem, OFF_S1 + g * P1 + (grp * 16 + q) * 16, o);
     }
-    __syncthreads();
+  };
 
-    // ---- stage 2: stem2a over the s2a region, max-pool into cat channels 0..31
-    if (!(DP_STEM_ABL & 2)) {
+  // ---- stem2a over the s2a region, max-pool into cat channels 0..31 (all waves)
+  auto stage2 = [&](const TileGeom& t) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < PF2; ++i) {
-        const int grp = wave + NWAVE * i;
-        if (grp >= G2) break;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {   // slab s = tap (dy, dx) = (s >> 1, s & 1), channels 8g..8g+7
-          const bf16x8 xb = lds_ld<bf16x8>(smem, a2[i] + ((s >> 1) * R1W + (s & 1)) * 16);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa2[s], xb, acc, 0, 0, 0);
-        }
-        const bool ok = in_map(rc2[i]);
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)(ok ? relu_lab<LAB>(acc[r] + bs2a[r], P, 1) : 0.f);
-        if (grp * 16 + q < N2) lds_st(smem, OFF_S2 + (g >> 1) * P2 + (grp * 16 + q) * 16 + (g & 1) * 8, o);
-      }
-#pragma unroll
-      for (int t = 0; t < PFP; ++t) {
-        if (tid + NTHR * t >= NPOOL) break;
-        const bool ok = in_map(rcp[t]);
-        u16x8 m;
-        if constexpr (!LAB) {   // non-negative bf16: the unsigned 16-bit order is the value order
-          const u16x8 v0 = lds_ld<u16x8>(smem, ap[t]), v1 = lds_ld<u16x8>(smem, ap[t] + 16);
-          const u16x8 v2 = lds_ld<u16x8>(smem, ap[t] + R1W * 16), v3 = lds_ld<u16x8>(smem, ap[t] + R1W * 16 + 16);
-          m = __builtin_elementwise_max(__builtin_elementwise_max(v0, v1), __builtin_elementwise_max(v2, v3));
-        } else {
-          const bf16x8 v0 = lds_ld<bf16x8>(smem, ap[t]), v1 = lds_ld<bf16x8>(smem, ap[t] + 16);
-          const bf16x8 v2 = lds_ld<bf16x8>(smem, ap[t] + R1W * 16), v3 = lds_ld<bf16x8>(smem, ap[t] + R1W * 16 + 16);
-          bf16x8 f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            f[e] = (bf16_t)fmaxf(fmaxf((float)v0[e], (float)v1[e]), fmaxf((float)v2[e], (float)v3[e]));
-          m = __builtin_bit_cast(u16x8, f);
-        }
-        if (!ok) m = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        lds_st(smem, sp[t], m);
-      }
-    }
-    __syncthreads();
-
-    // ---- stage 3: stem2b over the cat region -> cat channels 32..63
-    if (!(DP_STEM_ABL & 4)) {
-#pragma unroll
-      for (int i = 0; i < PFC; ++i) {
-        const int grp = wave + NWAVE * i;
-        if (grp >= GC) break;
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {   // k = 32s + 8g: tap 2s + (g>>1) = (dy, dx) = (s, g>>1), channels 8(g&1)..
-          const bf16x8 xb = lds_ld<bf16x8>(smem, ac[i] + s * R2W * 16);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb2[j][s], xb, acc[j], 0, 0, 0);
-        }
-        const bool ok = in_map(rcc[i]);
-        bf16x8 o;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ok ? relu_lab<LAB>(acc[j][r] + bs2b[j][r], P, 2) : 0.f);
-        if (grp * 16 + q < NC) lds_st(smem, OFF_CAT + (4 + g) * PC + (grp * 16 + q) * 16, o);
-      }
-    }
-    __syncthreads();
-
-    // ---- stage 4: next tile's image loads in flight, then stem3: wave (row i3, N tile j3),
-    // K-step kk = (tap, channel half): cat pixel (2 i3 + ky, 2q + kx), chunk 4 half + g
-    if (tile + G < ntiles && !(DP_STEM_ABL & 32)) load_img(tile + G);
-    if (!(DP_STEM_ABL & 8)) {
+    for (int i = 0; i < PF2; ++i) {
+      const int grp = wave + NWAVE * i;
+      if (grp >= G2) break;
+      const int p = min(grp * 16 + q, N2 - 1);
+      const int ry = p / R2W, rx = p - ry * R2W;
+      const int a2 = OFF_S1 + g * P1 + (ry * R1W + rx) * 16;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < K3 / 32; ++kk) {
-        const int tap = kk >> 1, half = kk & 1;
-        const int ky = tap / 3, kx = tap % 3;
-        const bf16x8 xb = lds_ld<bf16x8>(smem, a3 + 4 * half * PC + (ky * RCW + kx) * 16);
-        const bf16x8 wf = lds_ld<bf16x8>(smem, w3a + kk * 64);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xb, acc, 0, 0, 0);
+      for (int s = 0; s < 4; ++s) {   // slab s = tap (dy, dx) = (s >> 1, s & 1), channels 8g..8g+7
+        const bf16x8 xb = lds_ld<bf16x8>(smem, a2 + ((s >> 1) * R1W + (s & 1)) * 16);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa2[s], xb, acc, 0, 0, 0);
       }
+      const bool ok = in_map(t, ry, rx);
       bf16x4 o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (bf16_t)relu_lab<LAB>(acc[r] + bs3[j3][r], P, 3);
-      lds_st(smem, OFF_S3 + g * P3 + (16 * i3 + q) * 16 + 8 * j3, o);   // channels 8g + 4 j3 .. +3
+      for (int r = 0; r < 4; ++r) o[r] = (bf16_t)(ok ? relu_lab<LAB>(acc[r] + bs2a[r], P, 1) : 0.f);
+      if (grp * 16 + q < N2) lds_st(smem, OFF_S2 + (g >> 1) * P2 + (grp * 16 + q) * 16 + (g & 1) * 8, o);
     }
-    __syncthreads();
+#pragma unroll
+    for (int tt = 0; tt < PFP; ++tt) {
+      const int it = tid + NTHR * tt;
+      if (it >= NPOOL) break;
+      const int c = it / NC, p = it - c * NC;   // chunk c, cat pixel p
+      const int ry = p / RCW, rx = p - ry * RCW;
+      const int ap = OFF_S1 + c * P1 + (ry * R1W + rx) * 16;
+      u16x8 m;
+      if constexpr (!LAB) {   // non-negative bf16: the unsigned 16-bit order is the value order
+        const u16x8 v0 = lds_ld<u16x8>(smem, ap), v1 = lds_ld<u16x8>(smem, ap + 16);
+        const u16x8 v2 = lds_ld<u16x8>(smem, ap + R1W * 16), v3 = lds_ld<u16x8>(smem, ap + R1W * 16 + 16);
+        m = __builtin_elementwise_max(__builtin_elementwise_max(v0, v1), __builtin_elementwise_max(v2, v3));
+      } else {
+        const bf16x8 v0 = lds_ld<bf16x8>(smem, ap), v1 = lds_ld<bf16x8>(smem, ap + 16);
+        const bf16x8 v2 = lds_ld<bf16x8>(smem, ap + R1W * 16), v3 = lds_ld<bf16x8>(smem, ap + R1W * 16 + 16);
+        bf16x8 f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          f[e] = (bf16_t)fmaxf(fmaxf((float)v0[e], (float)v1[e]), fmaxf((float)v2[e], (float)v3[e]));
+        m = __builtin_bit_cast(u16x8, f);
+      }
+      if (!in_map(t, ry, rx)) m = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      lds_st(smem, OFF_CAT + c * PC + p * 16, m);
+    }
+  };
 
-    // ---- stage 5: stem4 (1x1, K = 32) of row i = wave, straight to HBM
-    if (wave < TH && !(DP_STEM_ABL & 16)) {
-      const int i = wave;
-      const int oy = oy0 + i, ox = ox0 + q;
-      const bf16x8 xb = lds_ld<bf16x8>(smem, OFF_S3 + g * P3 + (16 * i + q) * 16);
-      f32x4 acc[NT4];
+  // ---- stem2b over the cat region -> cat channels 32..63 (all waves)
+  auto stage3 = [&](const TileGeom& t) __attribute__((always_inline)) {
 #pragma unroll
-      for (int j = 0; j < NT4; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w4f[j], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      if (oy < OH3 && ox < OW3) {
-        bf16_t* op = out + (int64_t)b * obs + ((int64_t)oy * OW3 + ox) * ops;
+    for (int i = 0; i < PFC; ++i) {
+      const int grp = wave + NWAVE * i;
+      if (grp >= GC) break;
+      const int p = min(grp * 16 + q, NC - 1);
+      const int ry = p / RCW, rx = p - ry * RCW;
+      const int ac = OFF_S2 + (g & 1) * P2 + (ry * R2W + rx + (g >> 1)) * 16;
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-        for (int j = 0; j < NT4; ++j) {
-          bf16x4 o;
+      for (int s = 0; s < 2; ++s) {   // k = 32s + 8g: tap 2s + (g>>1) = (dy, dx) = (s, g>>1), channels 8(g&1)..
+        const bf16x8 xb = lds_ld<bf16x8>(smem, ac + s * R2W * 16);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (bf16_t)relu_lab<LAB>(acc[j][r] + bs4[j][r], P, 4);
-          *reinterpret_cast<bf16x4*>(op + 16 * j + 4 * g) = o;
-        }
+        for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb2[j][s], xb, acc[j], 0, 0, 0);
+      }
+      const bool ok = in_map(t, ry, rx);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ok ? relu_lab<LAB>(acc[j][r] + bs2b[j][r], P, 2) : 0.f);
+      if (grp * 16 + q < NC) lds_st(smem, OFF_CAT + (4 + g) * PC + (grp * 16 + q) * 16, o);
+    }
+  };
+
+  // ---- stem3 of output row i = wave (waves 0..3), both 16-channel halves: K-step kk = (tap,
+  // channel half) reads cat pixel (2i + ky, 2q + kx), chunk 4 half + g; then stem4 (1x1, K = 32)
+  // on stem3's bf16 output as the B fragment (lane (q, g) holds channels 8g..8g+7), to HBM
+  auto stage45 = [&](const TileGeom& t) __attribute__((always_inline)) {
+    const int i = wave;
+    const int a3 = OFF_CAT + g * PC + (2 * i * RCW + 2 * q) * 16;
+    const int w3a = OFF_W3 + q * W3ROW + 16 * g;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kk = 0; kk < K3 / 32; ++kk) {
+      const int tap = kk >> 1, half = kk & 1;
+      const int ky = tap / 3, kx = tap % 3;
+      const bf16x8 xb = lds_ld<bf16x8>(smem, a3 + 4 * half * PC + (ky * RCW + kx) * 16);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 wf = lds_ld<bf16x8>(smem, w3a + 16 * j * W3ROW + kk * 64);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xb, acc[j], 0, 0, 0);
       }
     }
-    // next tile's image window -> LDS (its last reader, stage 1, is three barriers back)
-    if (tile + G < ntiles) store_img();
+    bf16x8 x4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x4[4 * j + r] = (bf16_t)relu_lab<LAB>(acc[j][r] + bs3[j][r], P, 3);
+    f32x4 a4[NT4];
+#pragma unroll
+    for (int j = 0; j < NT4; ++j)
+      a4[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w4f[j], x4, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    const int oy = t.oy0 + i, ox = t.ox0 + q;
+    if (oy < OH3 && ox < OW3) {
+      bf16_t* op = out + (int64_t)t.b * obs + ((int64_t)oy * OW3 + ox) * ops;
+#pragma unroll
+      for (int j = 0; j < NT4; ++j) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)relu_lab<LAB>(a4[j][r] + bs4[j][r], P, 4);
+        *reinterpret_cast<bf16x4*>(op + 16 * j + 4 * g) = o;
+      }
+    }
+  };
+
+  // ---- prologue: tile L through stem2b
+  TileGeom cur = geom(L);
+  load_img(L);
+  store_img();
+  lds_barrier();
+  stage1(cur, wave, std::integral_constant<int, NWAVE>{});
+  lds_barrier();
+  int nxt = L + G;
+  if (nxt < ntiles) load_img(nxt);
+  stage2(cur);
+  lds_barrier();
+  stage3(cur);
+  if (nxt < ntiles) store_img();
+  lds_barrier();
+  // ---- steady state: phase A (stem3/stem4 of cur | stem1 of nxt), B, C (stem2a/pool, stem2b of nxt)
+  for (;;) {
+    const bool more = nxt < ntiles;
+    const TileGeom nx = geom(more ? nxt : L);
+    if (more && nxt + G < ntiles) load_img(nxt + G);
+    if (wave < NWAVE / 2) stage45(cur);
+    else if (more) stage1(nx, wave - NWAVE / 2, std::integral_constant<int, NWAVE / 2>{});
+    if (!more) break;
+    lds_barrier();
+    stage2(nx);
+    lds_barrier();
+    stage3(nx);
+    if (nxt + G < ntiles) store_img();
+    lds_barrier();
+    cur = nx;
+    nxt += G;
   }
 }
 
@@ -425,7 +448,7 @@ extern "C" int dp_stem_fused(const float* image, int32_t batch, int32_t h, int32
   P.k2a = s.k2a, P.k2b = s.k2b, P.k3 = s.k3, P.k4 = s.k4;
   for (int i = 0; i < 5; ++i) P.lab[i][0] = s.lab[i][0], P.lab[i][1] = s.lab[i][1];
   const int ntiles = (int)nt;
-  int grid = dpconv::num_cus();   // one 8-wave block per CU (115 KB of LDS)
+  int grid = dpconv::num_cus();   // one 8-wave block per CU (124 KB of LDS)
   const int need = (ntiles + 7) / 8 * 8;
   if (grid > need) grid = need;
   grid = grid / 8 * 8;

@@ -322,11 +322,13 @@ def test_deploy_model_boundary(golden_dir):
         model(torch.rand(1, 3, 320, 320, device="cuda"))
 
 
-@pytest.mark.parametrize("size,batch", [("l", 2), ("x", 1)])
+@pytest.mark.parametrize("size,batch", [("l", 2), ("l", 9), ("x", 1)])
 def test_stem_fused_bit_identical(golden_dir, size, batch, monkeypatch):
     """dp_stem_fused (the whole StemBlock in one launch, hgnetv2.py:204-220) writes exactly
     the map of the five-launch path (stem1, stem2a + pool, stem2b, stem3, stem4): same K
-    order, f32 accumulation sequence and bf16 rounding points. Also the end outputs."""
+    order, f32 accumulation sequence and bf16 rounding points. Also the end outputs. L b9
+    has 900 tiles, more than the one-block-per-CU grid: blocks run the pipelined steady state
+    (stem3/stem4 of one tile beside stem1 of the next) over several tiles."""
     from detrpose_amd.engine import Engine
     with open(os.path.join(golden_dir, "manifest.json")) as f:
         man = json.load(f)
