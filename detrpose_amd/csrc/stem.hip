@@ -61,32 +61,34 @@ __device__ __forceinline__ void stem_store(bf16_t* op, const f32x4 (&acc)[NT], c
 }
 
 // StemBlock.stem1 (hgnetv2.py:171-177): 3x3 stride-2 pad-1 conv over the f32 NCHW image,
-// 3 -> COUT channels, folded BN + ReLU (+ LAB), NHWC bf16 out. The 27 products (c, ky, kx)
-// are two MFMA K slabs in the order of stem_k.h (the one-launch stem's, so the two kernels
-// agree bit for bit): lane (q, g) gathers its slots of output pixel x0 + q straight from the
-// image (f32 -> bf16 in registers; a zero slot loads nothing: out-of-range offset), the f32
-// weights are converted into the A fragments once per wave. 864 FMAs per pixel become
-// 4 MFMAs per 16 pixels, so the kernel is a stream: 12 image bytes in (L1/L2 absorb the
-// 3x3/stride-2 overlap) and 2*COUT bytes out per pixel.
+// 3 -> COUT channels, folded BN + ReLU (+ LAB), NHWC bf16 out. The 27 products (c, ky, kx) are
+// MFMA K slabs in the order of stem_k.h: COUT 32 (B4 / B5) two slabs in the one-launch stem's
+// order, so the two kernels agree bit for bit; COUT 16 one slab, k = c * 9 + ky * 3 + kx. Lane
+// (q, g) gathers its slots of output pixel x0 + q straight from the image (f32 -> bf16 in
+// registers; a zero slot loads nothing: out-of-range offset), the f32 weights are converted
+// into the A fragments once per wave. 864 FMAs per pixel become 2 or 4 MFMAs per 16 pixels, so
+// the kernel is a stream: 12 image bytes in (L1/L2 absorb the 3x3/stride-2 overlap) and
+// 2*COUT bytes out per pixel.
 template <int COUT>
 __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict__ img, int batch, int H, int W,
                                                          const float* __restrict__ wt, const float* __restrict__ bias,
                                                          int has_lab, float ls, float lb, bf16_t* __restrict__ out,
                                                          int64_t obs, int ops) {
   constexpr int NT = COUT / 16;
+  constexpr int NS = COUT == 32 ? 2 : 1;        // K slabs (stem_k.h)
   constexpr int G = 4;                          // 16-pixel groups in flight per wave
   const int lane = threadIdx.x & 63, q = lane & 15, g = lane >> 4;
   const int OH = (H + 1) / 2, OW = (W + 1) / 2;
-  bf16x8 wa[2][NT];   // [slab][tile]
-  int tky[2][8], tkx[2][8];
-  bool tok[2][8];
-  int loff[2][8];
+  bf16x8 wa[NS][NT];   // [slab][tile]
+  int tky[NS][8], tkx[NS][8];
+  bool tok[NS][8];
+  int loff[NS][8];
 #pragma unroll
-  for (int sl = 0; sl < 2; ++sl)
+  for (int sl = 0; sl < NS; ++sl)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       int c = 0, ky = 0, kx = 0;
-      const bool ok = stem1_slot(sl, g, e, c, ky, kx);
+      const bool ok = NS == 2 ? stem1_slot(sl, g, e, c, ky, kx) : stem1_slot_c9(g, e, c, ky, kx);
       tok[sl][e] = ok, tky[sl][e] = ky, tkx[sl][e] = kx;
       // lane-constant part of the gather offset: plane c, row ky, column kx, this lane's pixel 2q;
       // the per-group part (image, row 2oy-1, column 2*ox0-1) is wave-uniform
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
   const int nw = gridDim.x * 4;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
   for (int base = wid * G; base < ngroups; base += nw * G) {
-    bf16x8 xb[G][2];
+    bf16x8 xb[G][NS];
     int pb[G], py[G], px0[G];
 #pragma unroll
     for (int i = 0; i < G; ++i) {
@@ -125,10 +127,10 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
       const int u = (2 * oy - 1) * W + 2 * ox0 - 1;
       const int ix0 = 2 * (ox0 + q) - 1;
 #pragma unroll
-      for (int sl = 0; sl < 2; ++sl)
+      for (int sl = 0; sl < NS; ++sl)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          if ((e & 3) == 3 || (sl == 1 && e >= 4)) {   // zero in every lane (stem_k.h): no load
+          if (NS == 2 && ((e & 3) == 3 || (sl == 1 && e >= 4))) {   // zero in every lane (stem_k.h): no load
             xb[i][sl][e] = (bf16_t)0.f;
             continue;
           }
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(256) void stem1_mfma_kernel(const float* __restrict
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][j], xb[i][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][j], xb[i][1], acc[j], 0, 0, 0);
+        if constexpr (NS == 2) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][j], xb[i][1], acc[j], 0, 0, 0);
       }
       stem_store<NT, DP_ACT_RELU>(op, acc, bsum, g, COUT, has_lab, ls, lb);
     }

@@ -57,7 +57,6 @@ constexpr int R2H = 2 * TH + 2, R2W = 2 * TW + 2, N2 = R2H * R2W;   // 10 x 34 s
 constexpr int RCH = 2 * TH + 1, RCW = 2 * TW + 1, NC = RCH * RCW;   //  9 x 33 cat region
 constexpr int G1 = (N1 + 15) / 16, G2 = (N2 + 15) / 16, GC = (NC + 15) / 16;
 constexpr int PF2 = (G2 + NWAVE - 1) / NWAVE, PFC = (GC + NWAVE - 1) / NWAVE;
-constexpr int NPOOL = NC * 4, PFP = (NPOOL + NTHR - 1) / NTHR;      // max-pool items (pixel, chunk)
 constexpr int K3 = 9 * 64;
 constexpr int W3ROW = K3 * 2 + 16;             // +16 B: 16 consecutive rows hit 16 distinct bank slots
 constexpr int rup(int x, int m) { return (x + m - 1) / m * m; }
@@ -121,6 +120,64 @@ __device__ __forceinline__ float relu_lab(float x, const StemArgs& P, int s) {
   x = fmaxf(x, 0.f) + 0.f;
   if constexpr (LAB) x = P.lab[s][0] * x + P.lab[s][1];
   return x;
+}
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// bf16(relu(a + ba)), bf16(relu(b + bb)) as one dword: the f32 bias adds (one packed add), round
+// to bf16 (RNE), then ReLU on the bf16 bits: a negative value or -0 has the sign bit set, so
+// max with 0 as int16 gives +0 — the same bits as rounding relu(x) for every finite x
+__device__ __forceinline__ unsigned relu_pk(float a, float b, float ba, float bb) {
+  const f32x2 v = f32x2{a, b} + f32x2{ba, bb};
+  const bf16x2 h = {(bf16_t)v[0], (bf16_t)v[1]};
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2, h), s16x2{0, 0}));
+}
+
+// a stage's output of 8 channels (C tiles j = 0, 1; element 4j + r): bias + ReLU (+ LAB),
+// zero outside the map (!ok)
+template <bool LAB>
+__device__ __forceinline__ bf16x8 epi8(const f32x4 (&acc)[2], const float (&bs)[2][4], bool ok, const StemArgs& P,
+                                       int s) {
+  if constexpr (LAB) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ok ? relu_lab<LAB>(acc[j][r] + bs[j][r], P, s) : 0.f);
+    return o;
+  } else {
+    u32x4 w;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const unsigned v = relu_pk(acc[j][2 * h], acc[j][2 * h + 1], bs[j][2 * h], bs[j][2 * h + 1]);
+        w[2 * j + h] = ok ? v : 0u;
+      }
+    return __builtin_bit_cast(bf16x8, w);
+  }
+}
+
+// 4 channels of one C tile
+template <bool LAB>
+__device__ __forceinline__ bf16x4 epi4(const f32x4& acc, const float (&bs)[4], bool ok, const StemArgs& P, int s) {
+  if constexpr (LAB) {
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (bf16_t)(ok ? relu_lab<LAB>(acc[r] + bs[r], P, s) : 0.f);
+    return o;
+  } else {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 w;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const unsigned v = relu_pk(acc[2 * h], acc[2 * h + 1], bs[2 * h], bs[2 * h + 1]);
+      w[h] = ok ? v : 0u;
+    }
+    return __builtin_bit_cast(bf16x4, w);
+  }
 }
 
 // a tile's place: image b, stem3 output origin (oy0, ox0), region origin (cy0, cx0) in the
@@ -255,17 +312,14 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[0][j], xb0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[1][j], xb1, acc[j], 0, 0, 0);
       }
-      const bool ok = in_map(t, ry, rx);
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ok ? relu_lab<LAB>(acc[j][r] + bs1[j][r], P, 0) : 0.f);
+      const bf16x8 o = epi8<LAB>(acc, bs1, in_map(t, ry, rx), P, 0);
       if (grp * 16 + q < N1) lds_st(smem, OFF_S1 + g * P1 + (grp * 16 + q) * 16, o);
     }
   };
 
-  // ---- stem2a over the s2a region, max-pool into cat channels 0..31 (all waves)
+  // ---- stem2a over the s2a region (all waves). Its four K slabs are the 2x2 window's taps of
+  // channels 8g..8g+7, the max-pool's window at the same position (the cat region is the s2a
+  // region minus its last row and column): their max is the pool output, cat channels 0..31
   auto stage2 = [&](const TileGeom& t) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PF2; ++i) {
@@ -274,41 +328,30 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
       const int p = min(grp * 16 + q, N2 - 1);
       const int ry = p / R2W, rx = p - ry * R2W;
       const int a2 = OFF_S1 + g * P1 + (ry * R1W + rx) * 16;
+      bf16x8 xb[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xb[s] = lds_ld<bf16x8>(smem, a2 + ((s >> 1) * R1W + (s & 1)) * 16);
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {   // slab s = tap (dy, dx) = (s >> 1, s & 1), channels 8g..8g+7
-        const bf16x8 xb = lds_ld<bf16x8>(smem, a2 + ((s >> 1) * R1W + (s & 1)) * 16);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa2[s], xb, acc, 0, 0, 0);
-      }
+      for (int s = 0; s < 4; ++s)   // slab s = tap (dy, dx) = (s >> 1, s & 1), channels 8g..8g+7
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa2[s], xb[s], acc, 0, 0, 0);
       const bool ok = in_map(t, ry, rx);
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (bf16_t)(ok ? relu_lab<LAB>(acc[r] + bs2a[r], P, 1) : 0.f);
+      const bf16x4 o = epi4<LAB>(acc, bs2a, ok, P, 1);
       if (grp * 16 + q < N2) lds_st(smem, OFF_S2 + (g >> 1) * P2 + (grp * 16 + q) * 16 + (g & 1) * 8, o);
-    }
-#pragma unroll
-    for (int tt = 0; tt < PFP; ++tt) {
-      const int it = tid + NTHR * tt;
-      if (it >= NPOOL) break;
-      const int c = it / NC, p = it - c * NC;   // chunk c, cat pixel p
-      const int ry = p / RCW, rx = p - ry * RCW;
-      const int ap = OFF_S1 + c * P1 + (ry * R1W + rx) * 16;
       u16x8 m;
       if constexpr (!LAB) {   // non-negative bf16: the unsigned 16-bit order is the value order
-        const u16x8 v0 = lds_ld<u16x8>(smem, ap), v1 = lds_ld<u16x8>(smem, ap + 16);
-        const u16x8 v2 = lds_ld<u16x8>(smem, ap + R1W * 16), v3 = lds_ld<u16x8>(smem, ap + R1W * 16 + 16);
+        const u16x8 v0 = __builtin_bit_cast(u16x8, xb[0]), v1 = __builtin_bit_cast(u16x8, xb[1]);
+        const u16x8 v2 = __builtin_bit_cast(u16x8, xb[2]), v3 = __builtin_bit_cast(u16x8, xb[3]);
         m = __builtin_elementwise_max(__builtin_elementwise_max(v0, v1), __builtin_elementwise_max(v2, v3));
       } else {
-        const bf16x8 v0 = lds_ld<bf16x8>(smem, ap), v1 = lds_ld<bf16x8>(smem, ap + 16);
-        const bf16x8 v2 = lds_ld<bf16x8>(smem, ap + R1W * 16), v3 = lds_ld<bf16x8>(smem, ap + R1W * 16 + 16);
         bf16x8 f;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          f[e] = (bf16_t)fmaxf(fmaxf((float)v0[e], (float)v1[e]), fmaxf((float)v2[e], (float)v3[e]));
+          f[e] = (bf16_t)fmaxf(fmaxf((float)xb[0][e], (float)xb[1][e]), fmaxf((float)xb[2][e], (float)xb[3][e]));
         m = __builtin_bit_cast(u16x8, f);
       }
-      if (!in_map(t, ry, rx)) m = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      lds_st(smem, OFF_CAT + c * PC + p * 16, m);
+      if (!ok) m = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (grp * 16 + q < N2 && ry < RCH && rx < RCW) lds_st(smem, OFF_CAT + g * PC + (ry * RCW + rx) * 16, m);
     }
   };
 
@@ -328,12 +371,7 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb2[j][s], xb, acc[j], 0, 0, 0);
       }
-      const bool ok = in_map(t, ry, rx);
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[4 * j + r] = (bf16_t)(ok ? relu_lab<LAB>(acc[j][r] + bs2b[j][r], P, 2) : 0.f);
+      const bf16x8 o = epi8<LAB>(acc, bs2b, in_map(t, ry, rx), P, 2);
       if (grp * 16 + q < NC) lds_st(smem, OFF_CAT + (4 + g) * PC + (grp * 16 + q) * 16, o);
     }
   };
@@ -357,11 +395,7 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xb, acc[j], 0, 0, 0);
       }
     }
-    bf16x8 x4;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) x4[4 * j + r] = (bf16_t)relu_lab<LAB>(acc[j][r] + bs3[j][r], P, 3);
+    const bf16x8 x4 = epi8<LAB>(acc, bs3, true, P, 3);
     f32x4 a4[NT4];
 #pragma unroll
     for (int j = 0; j < NT4; ++j)
@@ -370,12 +404,7 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
     if (oy < OH3 && ox < OW3) {
       bf16_t* op = out + (int64_t)t.b * obs + ((int64_t)oy * OW3 + ox) * ops;
 #pragma unroll
-      for (int j = 0; j < NT4; ++j) {
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)relu_lab<LAB>(a4[j][r] + bs4[j][r], P, 4);
-        *reinterpret_cast<bf16x4*>(op + 16 * j + 4 * g) = o;
-      }
+      for (int j = 0; j < NT4; ++j) *reinterpret_cast<bf16x4*>(op + 16 * j + 4 * g) = epi4<LAB>(a4[j], bs4[j], true, P, 4);
     }
   };
 

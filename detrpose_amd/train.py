@@ -199,7 +199,7 @@ class Trainer:
         self.plan = plan
         self._set_graphs(plan, *((self.bb, self.ep) if full else ()))
         self._draw_dn(plan, packed, images, pad, groups, single)
-        plan.forward()
+        plan.forward(pack=self._pack_due(plan))
         keys, vals = plan.criterion(packed, sizes, groups, weights=self.weights)
         plan.backward()
         after("transformer")

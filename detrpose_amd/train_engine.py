@@ -314,22 +314,46 @@ class TrainEngine:
         offsets | logits weights and the masked-row constant follow the new values (in place:
         the recorded tapes keep their pointers)."""
         with torch.no_grad():
+            copies = []   # (f32 source, destination): every copy of this refresh
             if self.tdtype != torch.float32:
-                for k, v in self.sd32.items():
-                    if k in self.w and self.w[k] is not v:
-                        self.w[k].copy_(v)
+                copies += [(v, self.w[k]) for k, v in self.sd32.items() if k in self.w and self.w[k] is not v]
             for l in range(self.L):
                 ca = f"{T_}decoder.layers.{l}.cross_attn."
                 no = self.sd32[ca + "sampling_offsets.weight"].shape[0]
-                self.w[ca + "offattn.weight"][:no].copy_(self.sd32[ca + "sampling_offsets.weight"])
-                self.w[ca + "offattn.weight"][no:].copy_(self.sd32[ca + "attention_weights.weight"])
-                self.sd32[ca + "offattn.bias"][:no].copy_(self.sd32[ca + "sampling_offsets.bias"])
-                self.sd32[ca + "offattn.bias"][no:].copy_(self.sd32[ca + "attention_weights.bias"])
+                copies += [(self.sd32[ca + "sampling_offsets.weight"], self.w[ca + "offattn.weight"][:no]),
+                           (self.sd32[ca + "attention_weights.weight"], self.w[ca + "offattn.weight"][no:]),
+                           (self.sd32[ca + "sampling_offsets.bias"], self.sd32[ca + "offattn.bias"][:no]),
+                           (self.sd32[ca + "attention_weights.bias"], self.sd32[ca + "offattn.bias"][no:])]
+            self._refresh_copies(copies, stream)
             g, b = self.sd32[T_ + "enc_output_norm.weight"].double(), self.sd32[T_ + "enc_output_norm.bias"].double()
             bias = self.sd32[T_ + "enc_output.bias"].double()
             self.masked_row.copy_(((bias - bias.mean()) / torch.sqrt(bias.var(unbiased=False) + 1e-5) * g + b).float())
         for p in self.plans.values():
             p.refresh_constants()
+
+    def _refresh_copies(self, copies, stream=None):
+        """The refresh's weight copies: on the GPU one dp_conv_pack_batch launch (mode 5: a plain
+        f32 -> dtype copy per table entry; the table is built once, the tensors never move), else
+        torch copies."""
+        if self.device.type != "cuda" or os.environ.get("DETRPOSE_PACK_BATCH", "1") == "0":
+            for src, dst in copies:
+                dst.copy_(src)
+            return
+        if getattr(self, "_refresh_tab", None) is None:
+            n = len(copies)
+            tab = (_lib.PackDesc * n)()
+            for i, (src, dst) in enumerate(copies):
+                assert src.dtype == torch.float32 and src.is_contiguous() and dst.is_contiguous()
+                assert src.numel() == dst.numel() < 2 ** 31
+                code = DP_F32 if dst.dtype == torch.float32 else self.code
+                tab[i] = _lib.PackDesc(_p(src), _p(dst), None, src.numel(), 1, 1, 1, 0, 0, 5, code)
+            _lib.check(self.lib.dp_conv_pack_check(tab, n), "refresh table")
+            dev = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(self.device)
+            self._refresh_tab = (dev, n, [(src.data_ptr(), dst.data_ptr()) for src, dst in copies])
+        dev, n, ptrs = self._refresh_tab
+        assert ptrs == [(src.data_ptr(), dst.data_ptr()) for src, dst in copies], "refresh tensors moved"
+        s = stream if stream is not None else C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(self.lib.dp_conv_pack_batch(_p(dev), n, 64, s), "refresh copies")
 
     def optimizer_step(self, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4, max_norm=0.1,
                        backbone_lr=1e-5):
@@ -475,8 +499,9 @@ class TrainEngine:
 
     def _wt_pack(self, wkey):
         """W^T of a linear's weight packed [K][pad64(N)] bf16 (dp_conv_pack mode 1 of the f32
-        master): the input-gradient conv's weights, re-packed by an op at the end of the current
-        plan's forward tape (after every update the next forward refreshes it)."""
+        master): the input-gradient conv's weights, re-packed by an op on the current plan's pack
+        tape (run before the first forward after every update; Tape.batch_packs merges the
+        plan's packs into one launch)."""
         if not hasattr(self, "_wts"):
             self._wts, self._wt_ops = {}, set()
         N, K = self.sd32[wkey].shape
@@ -486,7 +511,7 @@ class TrainEngine:
         t, kpad = self._wts[wkey]
         if (id(self.cur), wkey) not in self._wt_ops:
             self._wt_ops.add((id(self.cur), wkey))
-            self.cur.fw.op(f"pack.{wkey}.T", self.lib.dp_conv_pack, _p(self.sd32[wkey]), N, K, 1, 1, _p(t), kpad, N, 1,
+            self.cur.pk.op(f"pack.{wkey}.T", self.lib.dp_conv_pack, _p(self.sd32[wkey]), N, K, 1, 1, _p(t), kpad, N, 1,
                            None, DP_BF16)
         return t, kpad
 
@@ -641,6 +666,7 @@ class TrainPlan:
         fw = Tape(lib, dev)
         bw = Tape(lib, dev)
         self.fw, self.bw = fw, bw
+        self.pk = Tape(lib, dev)   # weight packs: run once per optimizer step (TrainEngine._wt_pack)
         cr = contiguous_rows
         kp_map = rowmap(Cc, K, T * Cc, Cc)   # keypoint token rows of a [rows][Cc] tensor
 
@@ -816,6 +842,8 @@ class TrainPlan:
         self._criterion_buffers()
         # ================= backward
         self._record_backward(tm, ep, delta)
+        if os.environ.get("DETRPOSE_PACK_BATCH", "1") != "0":
+            self.pk.batch_packs()
 
     # ------------------------------------------------------------------ criterion
     def _criterion_buffers(self):
@@ -1272,7 +1300,10 @@ class TrainPlan:
             for buf_, key in self._derived:
                 buf_.copy_(self.eng.sd32[key].repeat(buf_.numel() // self.eng.sd32[key].numel()))
 
-    def forward(self, debug=None):
+    def forward(self, debug=None, pack=True):
+        """pack=False: the weight packs of an earlier sub-batch of the same step are current."""
+        if pack:
+            self.pk.run(debug=debug)
         self.fw.run(debug=debug)
 
     def backward(self, debug=None):

@@ -293,10 +293,14 @@ FP32_CUT_BOUNDS = {"transformer": 1e-2, "encoder": 5e-2, "backbone": 5e-2}
 # At L the backbone / encoder worst parameters sit above 1.0 relative L2 end to end, so only the
 # medians are bounded there, below 1.0 (a zero gradient has relative L2 = 1 for every parameter
 # and fails them); test_l_step_bf16_split_backbone_encoder is the check that pins the bf16
-# backbone + encoder backward per parameter.
+# backbone + encoder backward per parameter. The L transformer's worst parameter is the LQE
+# head's first reg_conf layer (its input is the top-k statistics of the predicted corner
+# distributions): over round-6 runs it measured 0.49, 0.50, 0.72, 0.77 (float-atomic weight
+# gradients are not run-to-run deterministic), so its bound is 0.9, still below a zeroed
+# gradient's 1.0.
 BF16_BOUNDS = {
     "n": {"transformer": (0.03, 0.75), "encoder": (0.27, 0.6), "backbone": (0.32, 0.8), "backbone.lab": (0.32, None)},
-    "l": {"transformer": (0.06, 0.75), "encoder": (0.9, None), "backbone": (0.97, None)},
+    "l": {"transformer": (0.06, 0.9), "encoder": (0.9, None), "backbone": (0.97, None)},
 }
 BF16_LOSS_BOUND = {"n": 8e-2, "l": 0.25}   # measured N 1.4-5.2 % (over runs), L 18-20 %
 

@@ -53,17 +53,18 @@ def test_every_parameter_gets_a_gradient(size, B):
     assert ep.d_memory.data_ptr() in _pointers(plan.bw)
     assert all(v.buf.g is not None for v in bb.outs)
     assert len(bb.fw.ops) > 30 and len(ep.bw.ops) > 100
-    # the weight packs on their own tapes (run once per optimizer step), each tape's packs merged
+    # the weight packs on their own tapes (run once per optimizer step; the transformer's W^T
+    # input-gradient packs too), each tape's packs merged
     # into ONE dp_conv_pack_batch launch over a table of > 30 descriptors with distinct outputs;
     # none left in the forwards
     from detrpose_amd._lib import PackDesc
-    for pk in (bb.pk, ep.pk):
+    for pk, least in ((bb.pk, 30), (ep.pk, 30), (plan.pk, 20)):
         (name, fn, (tab, n, _)), = pk.ops
-        assert name == "pack.batch" and n > 30
+        assert name == "pack.batch" and n > least
         raw = next(t for t in pk.keep if t.data_ptr() == tab)
         descs = (PackDesc * n).from_buffer_copy(raw.cpu().numpy().tobytes())
         assert len({d.out for d in descs}) == n and all(d.w for d in descs)
-    assert not any(n.startswith("pack.") for n, _, _ in bb.fw.ops + ep.fw.ops)
+    assert not any(n.startswith("pack.") for n, _, _ in bb.fw.ops + ep.fw.ops + plan.fw.ops)
 
 
 def test_bf16_tapes_route_to_the_fast_kernels():
