@@ -18,14 +18,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--libs", default="", help="comma list of library builds to time side by side (A/B)")
     a = ap.parse_args()
     from detrpose_amd import _lib
     from detrpose_amd._lib import ConvDesc
-    lib = _lib.load()
+    libs = [("lib", _lib.load())]
+    for path in filter(None, a.libs.split(",")):
+        v = C.CDLL(path)
+        v.dp_dwconv2d.restype = C.c_int32
+        v.dp_dwconv2d.argtypes = [C.POINTER(ConvDesc), C.c_void_p]
+        libs.append((os.path.basename(os.path.dirname(path)), v))
     dev = torch.device("cuda")
     st = torch.cuda.current_stream()
     B = a.batch
-    for h, c in ((40, 192), (20, 384)):
+    for (h, c), (tag, lib) in [(hc, l) for hc in ((40, 192), (20, 384)) for l in libs]:
         torch.manual_seed(h)
         x = torch.randn(B, h, h, c, device=dev).bfloat16()
         y = torch.empty_like(x)
@@ -52,7 +58,7 @@ def main():
         t = sorted(ts)[len(ts) // 2]
         mb = 2 * x.numel() * 2 / 1e6
         chk = int(y.view(torch.int16).to(torch.int64).sum())   # variants must agree bit for bit
-        print(f"dw5 {h}x{h} c{c} b{B}: {t:7.1f} us  {mb / t:6.2f} TB/s (in + out)  out checksum {chk}",
+        print(f"{tag:>6s} dw5 {h}x{h} c{c} b{B}: {t:7.1f} us  {mb / t:6.2f} TB/s (in + out)  out checksum {chk}",
               flush=True)
 
 
