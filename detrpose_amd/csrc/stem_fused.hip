@@ -71,6 +71,9 @@ constexpr int IPV = IPW / 4, NIMG = IPH * IPV;                      // 4-column 
 constexpr int OFF_IMG = OFF_W3 + 32 * W3ROW;
 constexpr int OFF_Z = OFF_IMG + IPH * IRS;                          // 8 zero bytes (slab 1 of lanes g > 0)
 constexpr int LDS_BYTES = OFF_Z + 16;
+// every 16-pixel group's lanes store unconditionally: the planes hold whole groups (lanes past the
+// region write padding no stage reads)
+static_assert(P1 >= G1 * 16 * 16 && P2 >= G2 * 16 * 16 && PC >= GC * 16 * 16, "plane padding");
 static_assert(LDS_BYTES <= 160 * 1024 && TH * TW == 16 * 4 && IPW % 4 == 0 && OFF_IMG % 16 == 0 && NIMG <= NTHR &&
                   TH == NWAVE / 2,
               "stem tile");
@@ -131,7 +134,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // max with 0 as int16 gives +0 — the same bits as rounding relu(x) for every finite x
 __device__ __forceinline__ unsigned relu_pk(float a, float b, float ba, float bb) {
   const f32x2 v = f32x2{a, b} + f32x2{ba, bb};
-  const bf16x2 h = {(bf16_t)v[0], (bf16_t)v[1]};
+  const bf16x2 h = __builtin_convertvector(v, bf16x2);   // one v_cvt_pk_bf16_f32
   return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2, h), s16x2{0, 0}));
 }
 
@@ -284,9 +287,11 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
       const int r = tid / IPV, v = tid - r * IPV;
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
-        bf16x4 h4;
-        h4[0] = (bf16_t)xr[0][x], h4[1] = (bf16_t)xr[1][x], h4[2] = (bf16_t)xr[2][x], h4[3] = (bf16_t)0.f;
-        lds_st(smem, OFF_IMG + r * IRS + (4 * v + x) * 8, h4);
+        const bf16x2 h01 = __builtin_convertvector(f32x2{xr[0][x], xr[1][x]}, bf16x2);
+        const bf16x2 h2z = __builtin_convertvector(f32x2{xr[2][x], 0.f}, bf16x2);
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        lds_st(smem, OFF_IMG + r * IRS + (4 * v + x) * 8,
+               u32x2{__builtin_bit_cast(unsigned, h01), __builtin_bit_cast(unsigned, h2z)});
       }
     }
   };
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[1][j], xb1, acc[j], 0, 0, 0);
       }
       const bf16x8 o = epi8<LAB>(acc, bs1, in_map(t, ry, rx), P, 0);
-      if (grp * 16 + q < N1) lds_st(smem, OFF_S1 + g * P1 + (grp * 16 + q) * 16, o);
+      lds_st(smem, OFF_S1 + g * P1 + (grp * 16 + q) * 16, o);   // lanes past N1: plane padding
     }
   };
 
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa2[s], xb[s], acc, 0, 0, 0);
       const bool ok = in_map(t, ry, rx);
       const bf16x4 o = epi4<LAB>(acc, bs2a, ok, P, 1);
-      if (grp * 16 + q < N2) lds_st(smem, OFF_S2 + (g >> 1) * P2 + (grp * 16 + q) * 16 + (g & 1) * 8, o);
+      lds_st(smem, OFF_S2 + (g >> 1) * P2 + (grp * 16 + q) * 16 + (g & 1) * 8, o);   // past N2: padding
       u16x8 m;
       if constexpr (!LAB) {   // non-negative bf16: the unsigned 16-bit order is the value order
         const u16x8 v0 = __builtin_bit_cast(u16x8, xb[0]), v1 = __builtin_bit_cast(u16x8, xb[1]);
@@ -351,7 +356,7 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
         m = __builtin_bit_cast(u16x8, f);
       }
       if (!ok) m = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (grp * 16 + q < N2 && ry < RCH && rx < RCW) lds_st(smem, OFF_CAT + g * PC + (ry * RCW + rx) * 16, m);
+      if (ry < RCH && rx < RCW) lds_st(smem, OFF_CAT + g * PC + (ry * RCW + rx) * 16, m);   // clamped lanes: ry = 9
     }
   };
 
@@ -372,7 +377,7 @@ __global__ __launch_bounds__(NTHR) void stem_fused_kernel(const float* __restric
         for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb2[j][s], xb, acc[j], 0, 0, 0);
       }
       const bf16x8 o = epi8<LAB>(acc, bs2b, in_map(t, ry, rx), P, 2);
-      if (grp * 16 + q < NC) lds_st(smem, OFF_CAT + (4 + g) * PC + (grp * 16 + q) * 16, o);
+      lds_st(smem, OFF_CAT + (4 + g) * PC + (grp * 16 + q) * 16, o);   // past NC: padding, never read
     }
   };
 
