@@ -727,6 +727,18 @@ __global__ void wgrad_permute_kernel(const float* __restrict__ s, float* __restr
   dw[e] += s[((int64_t)co * taps + tap) * cin + ci];
 }
 
+// C[m][n] = beta C[m][n] + bias[n] (beta 0: C is not read) over an M x N f32 block of row
+// stride c_rs: the start value of a split-K GEMM whose partial products then add with atomics
+__global__ void gemm_init_c_kernel(float* __restrict__ c, int64_t c_rs, int m, int n, float beta,
+                                   const float* __restrict__ bias) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)m * n) return;
+  const int r = (int)(e / n), col = (int)(e - (int64_t)r * n);
+  float* p = c + (int64_t)r * c_rs + col;
+  const float b = bias ? bias[col] : 0.f;
+  *p = beta != 0.f ? beta * *p + b : b;
+}
+
 }  // namespace
 
 extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
@@ -814,7 +826,14 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
     // 128 x 128 tiles: ~512 blocks (more splits only add atomics); 64 x 64 tiles (small M, the
     // stage-0/1 convs' weight gradients): ~4096 blocks, measured 535 -> 400 us (M 48, K 409600)
     // and 463 -> 312 us (M 96, K 102400) over the 512 target (scripts/gemm_bench.py)
-    const int target = big ? 512 : 4096, kmin = big ? 4 : 8;
+    // A split runs at least kmin K-steps (4 on 128 x 128 tiles, 8 on 64 x 64), except for small
+    // outputs (M N <= 512 x 512: the transformer heads' class / pose / LQE weight gradients), where
+    // each split's float atomics are few and a block's time is its K-steps' load latency: 1 there
+    // (the class-head dW, 2 x 256 over 768 rows: 45 -> 15 us; profiles/r6u_train_ops_all.json vs
+    // r6x_train_ops_all.json. A 4-deep register ring of K-step loads instead measured slower on
+    // the small forward GEMMs: 284 VGPRs, one wave per SIMD)
+    const bool small_out = (int64_t)d.m * d.n <= 512 * 512;
+    const int target = big ? 512 : 4096, kmin = big ? 4 : small_out ? 1 : 8;
     splits = (int)((target + tiles - 1) / tiles);
     if (splits > ksteps / kmin) splits = ksteps / kmin;
     // bounded float-atomic adds per output address: 512 for a one-tile output (stem1's 32 x 27
@@ -826,14 +845,36 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
     if (cap > 0 && splits > cap) splits = cap;
     if (splits < 1) splits = 1;
   }
+  // small f32 outputs with a bias or beta != 1 (the heads' class / LQE Linears and their input
+  // gradients: a few blocks of 4-8 K-steps, each step a full load latency): C starts as
+  // beta C + bias in one launch, then the K splits add into it as above
+  bool init_c = false;
+  if (!big && splits == 1 && d.split_k == 0 && d.out_dtype == DP_F32 && d.act == DP_ACT_NONE && !d.gate &&
+      d.batch == 1 && tiles < 512 && ksteps >= 4 && (int64_t)d.m * d.n <= 512 * 512 &&
+      (d.bias || d.beta != 1.f)) {
+    splits = (int)std::min<int64_t>((4096 + tiles - 1) / tiles, ksteps);
+    if (splits > 1) {
+      init_c = true;
+      g.bias = nullptr;
+      g.beta = 1.f;
+    } else {
+      splits = 1;
+    }
+  }
   if (splits > ksteps) splits = ksteps;
-  DP_REQUIRE(splits == 1 || (d.out_dtype == DP_F32 && !d.bias && d.act == DP_ACT_NONE && !d.gate && d.beta == 1.f),
+  DP_REQUIRE(splits == 1 || (d.out_dtype == DP_F32 && (init_c || (!d.bias && d.beta == 1.f)) && d.act == DP_ACT_NONE &&
+                             !d.gate),
              "dp_gemm: split-K accumulates into f32 C (beta 1, no bias / act / gate)");
   g.splits = splits;
   g.kchunk = ((ksteps + splits - 1) / splits) * BK;
   DP_REQUIRE(tiles * 1 < (1ll << 31) && (int64_t)d.batch * splits < 65536, "dp_gemm: grid too large");
   dim3 grid((unsigned)(tm * tn), (unsigned)(d.batch * splits)), block(256);
   hipStream_t s = as_stream(stream);
+  if (init_c) {
+    const int64_t mn = (int64_t)d.m * d.n;
+    hipLaunchKernelGGL(gemm_init_c_kernel, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<float*>(d.c), d.c_rs, d.m, d.n, d.beta, d.bias);
+  }
   if (big) {
     constexpr size_t lds = sizeof(bf16_t) * 4 * IMG;   // 72 KB: two buffers of both operands
     static const bool attr_ok = [] {

@@ -89,6 +89,7 @@ def main():
         print(tname, out["tapes"][tname]["ms"], "ms", out["tapes"][tname]["top_families"][:6], flush=True)
     allops.sort(reverse=True)
     out["top_ops"] = [(round(ms, 3), t, n) for ms, t, n in allops[:40]]
+    out["all_ops"] = [(round(ms, 4), t, n) for ms, t, n in allops]
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)

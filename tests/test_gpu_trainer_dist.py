@@ -163,6 +163,10 @@ def test_trainer_step_two_ranks_equal_one_process():
             # (step 1: Adam's normalised update turns the ~1 % gradient difference into ~1e-6 moves on
             # most entries, so only the size of the move is bounded there: measured 1.6e-4)
             assert d.max() <= 2.5e-4 * (step + 1) and frac <= tol["frac"], k
+        # running statistics: step 1's batch statistics come from parameters that already differ by
+        # up to ~1.6e-4 (above), so near-zero entries can move by a few 1e-6 (measured 2.6e-6 on a
+        # 1.3e-4 running mean once the heads' weight-gradient GEMMs split K further)
         for k, v in ref["running"].items():
-            np.testing.assert_allclose(res[0]["running"][k], v, rtol=1e-4 if step == 0 else 1e-2, atol=1e-6, err_msg=k)
+            np.testing.assert_allclose(res[0]["running"][k], v, rtol=1e-4 if step == 0 else 1e-2,
+                                       atol=1e-6 if step == 0 else 1e-5, err_msg=k)
             np.testing.assert_array_equal(res[0]["running"][k], res[1]["running"][k], err_msg=k)
