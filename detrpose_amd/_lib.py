@@ -75,6 +75,12 @@ class PackDesc(C.Structure):
                 ("kpad", i32), ("kc", i32), ("mode", i32), ("dtype", i32)]
 
 
+class RowCopyDesc(C.Structure):
+    """Mirror of dp_rowcopy_desc."""
+    _fields_ = [("src0", vp), ("src1", vp), ("dst", vp), ("ld_src0", i64), ("ld_src1", i64), ("ld_dst", i64),
+                ("rows", i32), ("n", i32)]
+
+
 def rowmap(base=0, group=1, stride_g=0, stride_r=0) -> RowMap:
     return RowMap(int(base), int(group), int(stride_g), int(stride_r))
 
@@ -139,6 +145,8 @@ _SIGS = {
     "dp_ln_bwd": (i32, [vp, vp, i32, vp, vp, vp, i32, i32, vp, vp, i32, i32, vp]),
     "dp_conv_wgrad": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                             i32, vp]),
+    "dp_conv_wgrad_zs": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, i64, i32, i32, i32, i32, i32, i32, i32, vp,
+                               vp, i32, vp]),
     "dp_colsum": (i32, [vp, i64, i32, i32, vp, i32, i32, vp]),
     "dp_attn_fwd": (i32, [vp, i32, vp, vp, i32, vp, i32, vp, vp, i32, i32, i64, i64, i64, i32, i32, i32, i32, vp]),
     "dp_attn_bwd": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, i64, i64, i64, i32, i32,
@@ -153,6 +161,8 @@ _SIGS = {
     "dp_scatter_rows": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, vp, i64, i32, i32, i32, vp]),
     "dp_gather_rows_masked": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, vp, i32, vp]),
     "dp_convert_rows": (i32, [vp, i32, i64, vp, i32, i64, i32, i32, f32, i32, vp]),
+    "dp_copy_rows_check": (i32, [vp, i32]),
+    "dp_copy_rows_batch": (i32, [vp, i32, i32, vp]),
     "dp_zero": (i32, [vp, i64, vp]),
     "dp_cdn_build": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, i32, f32, f32, C.c_uint64, vp, vp, vp]),
     "dp_grad_sqnorm": (i32, [vp, i64, vp, vp, i64, vp]),

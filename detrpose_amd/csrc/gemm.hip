@@ -716,15 +716,20 @@ inline int wgrad_tt_splits(int ntl, int ks64) {
   return sp < 1 ? 1 : sp;
 }
 
-// dw[co][ci][tap] += s[co][tap][ci] (the reference's [cout][cin][kh][kw] from the tap-major sums)
-__global__ void wgrad_permute_kernel(const float* __restrict__ s, float* __restrict__ dw, int cout, int cin, int taps) {
+// dw[co][ci][tap] += s[co][tap][ci] (the reference's [cout][cin][kh][kw] from the tap-major sums);
+// CLEAR: each scratch element (read exactly once) is set back to zero, so the next call on this
+// scratch needs no zero-fill launch (dp_conv_wgrad_zs)
+template <bool CLEAR>
+__global__ void wgrad_permute_kernel(float* __restrict__ s, float* __restrict__ dw, int cout, int cin, int taps) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over dw
   const int64_t total = (int64_t)cout * cin * taps;
   if (e >= total) return;
   const int tap = (int)(e % taps);
   const int64_t r = e / taps;
   const int ci = (int)(r % cin), co = (int)(r / cin);
-  dw[e] += s[((int64_t)co * taps + tap) * cin + ci];
+  float* sp = s + ((int64_t)co * taps + tap) * cin + ci;
+  dw[e] += *sp;
+  if (CLEAR) *sp = 0.f;
 }
 
 // C[m][n] = beta C[m][n] + bias[n] (beta 0: C is not read) over an M x N f32 block of row
@@ -845,13 +850,14 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
     if (cap > 0 && splits > cap) splits = cap;
     if (splits < 1) splits = 1;
   }
-  // small f32 outputs with a bias or beta != 1 (the heads' class / LQE Linears and their input
-  // gradients: a few blocks of 4-8 K-steps, each step a full load latency): C starts as
-  // beta C + bias in one launch, then the K splits add into it as above
+  // small f32 outputs with beta != 1 and no bias (the heads' input gradients: a few blocks of 4-8
+  // K-steps, each step a full load latency): C starts as beta C in one launch, then the K splits
+  // add into it as above. Not for a GEMM with a bias, i.e. a Linear's forward: float atomics
+  // would make the forward differ run to run (tests/test_gpu_train_graphs.py asserts it is
+  // bit-identical, as the reference's is)
   bool init_c = false;
   if (!big && splits == 1 && d.split_k == 0 && d.out_dtype == DP_F32 && d.act == DP_ACT_NONE && !d.gate &&
-      d.batch == 1 && tiles < 512 && ksteps >= 4 && (int64_t)d.m * d.n <= 512 * 512 &&
-      (d.bias || d.beta != 1.f)) {
+      d.batch == 1 && tiles < 512 && ksteps >= 4 && (int64_t)d.m * d.n <= 512 * 512 && !d.bias && d.beta != 1.f) {
     splits = (int)std::min<int64_t>((4096 + tiles - 1) / tiles, ksteps);
     if (splits > 1) {
       init_c = true;
@@ -903,10 +909,10 @@ extern "C" int dp_gemm(const dp_gemm_desc* dp, void* stream) {
   return dp_check_launch("dp_gemm");
 }
 
-extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride, int32_t batch, int32_t h,
-                             int32_t w, int32_t cin, const void* dz, int64_t dz_ld, int32_t oh, int32_t ow,
-                             int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad, float* scratch,
-                             float* dw, int32_t dtype, void* stream) {
+static int conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride, int32_t batch, int32_t h, int32_t w,
+                      int32_t cin, const void* dz, int64_t dz_ld, int32_t oh, int32_t ow, int32_t cout, int32_t kh,
+                      int32_t kw, int32_t stride, int32_t pad, float* scratch, float* dw, int32_t dtype, void* stream,
+                      bool scratch_zero) {
   DP_REQUIRE(x && dz && scratch && dw && batch > 0 && h > 0 && w > 0 && oh > 0 && ow > 0 && cout > 0 && kh > 0 &&
                  kw > 0 && stride > 0 && pad >= 0,
              "dp_conv_wgrad: bad arguments");
@@ -927,7 +933,7 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
   static const bool tt_off = getenv("DETRPOSE_WGRAD_TT") && atoi(getenv("DETRPOSE_WGRAD_TT")) == 0;
   const bool tt = !tt_off && cout % 8 == 0 && N % 8 == 0 && (int64_t)chunk * x_bstride * 2 < 0x7ff00000ll &&
                   ((int64_t)chunk * ppi * dz_ld + cout) * 2 < 0x7ff00000ll;
-  if (dp_zero_async(scratch, (size_t)cout * N * sizeof(float), s)) {
+  if (!scratch_zero && dp_zero_async(scratch, (size_t)cout * N * sizeof(float), s)) {
     dp_set_error("dp_conv_wgrad: memset failed");
     return DP_EINVAL;
   }
@@ -985,7 +991,27 @@ extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride
     hipLaunchKernelGGL((gemm128_kernel<1, 3>), dim3((unsigned)(tm * tn), (unsigned)splits), dim3(256), lds, s, g);
   }
   const int64_t total = (int64_t)cout * N;
-  hipLaunchKernelGGL(wgrad_permute_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, scratch, dw, cout,
-                     cin, taps);
+  if (scratch_zero)
+    hipLaunchKernelGGL(wgrad_permute_kernel<true>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, scratch, dw,
+                       cout, cin, taps);
+  else
+    hipLaunchKernelGGL(wgrad_permute_kernel<false>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, scratch,
+                       dw, cout, cin, taps);
   return dp_check_launch("dp_conv_wgrad");
+}
+
+extern "C" int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride, int32_t batch, int32_t h,
+                             int32_t w, int32_t cin, const void* dz, int64_t dz_ld, int32_t oh, int32_t ow,
+                             int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad, float* scratch,
+                             float* dw, int32_t dtype, void* stream) {
+  return conv_wgrad(x, x_bstride, x_pstride, batch, h, w, cin, dz, dz_ld, oh, ow, cout, kh, kw, stride, pad, scratch,
+                    dw, dtype, stream, false);
+}
+
+extern "C" int dp_conv_wgrad_zs(const void* x, int64_t x_bstride, int32_t x_pstride, int32_t batch, int32_t h,
+                                int32_t w, int32_t cin, const void* dz, int64_t dz_ld, int32_t oh, int32_t ow,
+                                int32_t cout, int32_t kh, int32_t kw, int32_t stride, int32_t pad, float* scratch,
+                                float* dw, int32_t dtype, void* stream) {
+  return conv_wgrad(x, x_bstride, x_pstride, batch, h, w, cin, dz, dz_ld, oh, ow, cout, kh, kw, stride, pad, scratch,
+                    dw, dtype, stream, true);
 }

@@ -1357,6 +1357,41 @@ extern "C" int dp_convert_rows(const void* src, int32_t src_dtype, int64_t ld_sr
   return dp_check_launch("dp_convert_rows");
 }
 
+// ---------------------------------------------------------------- batched f32 row copies
+// One launch for a table of strided f32 row copies (the criterion's head packing and its
+// gradient hand-off: ~70 small dp_convert_rows launches per sub-batch before). Block (x, e)
+// strides over entry e's rows x n elements; dst = src0 (+ src1): the same f32 sum as a copy
+// followed by an accumulating dp_convert_rows (a + b == b + a in f32).
+__global__ void copy_rows_batch_kernel(const dp_rowcopy_desc* __restrict__ tab) {
+  const dp_rowcopy_desc d = tab[blockIdx.y];
+  const unsigned tot = (unsigned)d.rows * (unsigned)d.n, un = (unsigned)d.n;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
+    const unsigned r = e / un, j = e - r * un;
+    float v = d.src0[(int64_t)r * d.ld_src0 + j];
+    if (d.src1) v += d.src1[(int64_t)r * d.ld_src1 + j];
+    d.dst[(int64_t)r * d.ld_dst + j] = v;
+  }
+}
+
+extern "C" int dp_copy_rows_check(const dp_rowcopy_desc* tab, int32_t n) {
+  DP_REQUIRE(tab && n > 0 && n < 65536, "dp_copy_rows_check: bad table");
+  for (int i = 0; i < n; ++i) {
+    const dp_rowcopy_desc& d = tab[i];
+    const bool ok = d.src0 && d.dst && d.rows > 0 && d.n > 0 && (int64_t)d.rows * d.n < (1ll << 31) &&
+                    d.ld_src0 >= d.n && d.ld_dst >= d.n && (!d.src1 || d.ld_src1 >= d.n);
+    DP_REQUIRE(ok, "dp_copy_rows_check: entry %d (rows %d, n %d, ld %lld / %lld / %lld)", i, d.rows, d.n,
+               (long long)d.ld_src0, (long long)d.ld_src1, (long long)d.ld_dst);
+  }
+  return 0;
+}
+
+extern "C" int dp_copy_rows_batch(const dp_rowcopy_desc* tab_dev, int32_t n, int32_t blocks_per_entry, void* stream) {
+  DP_REQUIRE(tab_dev && n > 0 && n < 65536 && blocks_per_entry > 0, "dp_copy_rows_batch: bad arguments");
+  hipLaunchKernelGGL(copy_rows_batch_kernel, dim3((unsigned)blocks_per_entry, (unsigned)n), dim3(256), 0,
+                     as_stream(stream), tab_dev);
+  return dp_check_launch("dp_copy_rows_batch");
+}
+
 extern "C" int dp_cdn_build(const int32_t* tgt_off, const int32_t* tgt_label, const float* tgt_kps,
                             const float* tgt_area, const float* tgt_boxes, const float* sigmas, int32_t batch,
                             int32_t pad, int32_t single_pad, int32_t nkp, float label_noise_ratio, int32_t num_classes,

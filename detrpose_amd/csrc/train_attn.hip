@@ -30,6 +30,38 @@ namespace {
 template <int KT>
 constexpr int wpb_of() { return KT > 8 ? 2 : 4; }
 
+// SH (the 400-token AIFI instantiation): every wave of a block works on the SAME (sequence, head)
+// pair, one query (or key) tile each, and the block stages the pair's transposed operands into
+// LDS once (was once per wave: 25 waves per pair re-staged the same 26 KB, the backward's dK/dV
+// kernel also recomputed D over all 400 queries per wave). Block = nw waves (nw | tiles when a
+// divisor in 4..8 exists), grid = pairs x ceil(tiles / nw); waves past the tiles only stage.
+template <int KT>
+constexpr bool shared_of() { return KT > 8; }
+constexpr int SH_MAXW = 8;
+
+// block width (waves) of a shared-staging launch over `tiles` tiles per pair
+static inline int sh_waves(int tiles) {
+  for (int w = SH_MAXW; w >= 4; --w)
+    if (tiles % w == 0) return w;
+  return tiles < SH_MAXW ? tiles : SH_MAXW;
+}
+
+// (pair, tile, live) of this wave: SH from the block's pair and the wave's slot, else one item
+// per wave (item = pair * tiles + tile)
+template <bool SH>
+__device__ __forceinline__ bool wave_item(int tiles, int items, int wpb, int wave, int& pair, int& t) {
+  if (SH) {
+    const int nw = blockDim.x >> 6, bpp = (tiles + nw - 1) / nw;
+    pair = blockIdx.x / bpp;
+    t = (blockIdx.x - pair * bpp) * nw + wave;
+    return t < tiles;
+  }
+  const int item = blockIdx.x * wpb + wave;
+  pair = item / tiles;
+  t = item - pair * tiles;
+  return item < items;
+}
+
 __device__ __forceinline__ int64_t row_base(int pair, int nhead, int n_inner, int64_t so, int64_t si) {
   const int sq = pair / nhead;
   const int o = sq / n_inner, ii = sq - o * n_inner;
@@ -47,9 +79,9 @@ __device__ __forceinline__ bf16x8 frag_row(const bf16_t* p, int64_t base, int64_
 // rows 0 .. NK-1 of a head (zero past L), transposed into dst[DH][VP]
 template <int DH, int NK, int VP>
 __device__ __forceinline__ void stage_t(bf16_t* dst, const bf16_t* src, int64_t base, int64_t st, int64_t ld, int col0,
-                                        int L, int lane) {
+                                        int L, int lane, int nthreads = 64) {
   constexpr int CH = DH / 8;
-  for (int c = lane; c < NK * CH; c += 64) {
+  for (int c = lane; c < NK * CH; c += nthreads) {
     const int row = c / CH, dc = c - row * CH;
     bf16x8 v = bf16x8{};
     if (row < L) v = *reinterpret_cast<const bf16x8*>(src + (base + (int64_t)row * st) * ld + col0 + dc * 8);
@@ -73,7 +105,7 @@ __device__ __forceinline__ void lds_sync() {
 }
 
 template <int DH, int KT>
-__global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16_t* __restrict__ q, int ldq,
+__global__ __launch_bounds__(shared_of<KT>() ? 64 * SH_MAXW : 256) void attn_fwd_mfma_kernel(const bf16_t* __restrict__ q, int ldq,
                                                             const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                             int ldkv, bf16_t* __restrict__ out, int ldo,
                                                             float* __restrict__ psave,
@@ -82,17 +114,24 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16_t* __rest
                                                             float scale) {
   constexpr int KS = (DH + 31) / 32, ND = DH / 16, NK = 16 * KT, VP = NK + 8, NM = (KT + 1) / 2;
   static_assert(KT % 2 == 0, "tiles are read in pairs: an odd KT would read past a V^T row");
-  __shared__ __attribute__((aligned(16))) bf16_t lds[wpb_of<KT>()][DH * VP];
+  constexpr bool SH = shared_of<KT>();
+  __shared__ __attribute__((aligned(16))) bf16_t lds[SH ? 1 : wpb_of<KT>()][DH * VP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int item = blockIdx.x * wpb_of<KT>() + wave;
-  if (item >= items) return;   // wave-uniform
   const int nqt = (L + 15) / 16;
-  const int pair = item / nqt, it = item - pair * nqt;
+  int pair, it;
+  const bool live = wave_item<SH>(nqt, items, wpb_of<KT>(), wave, pair, it);
+  if (!SH && !live) return;   // wave-uniform
   const int h = pair % nhead;
   const int64_t base = row_base(pair, nhead, n_inner, so, si);
   const int lr = lane & 15, lg = lane >> 4;
-  bf16_t* Vt = lds[wave];
-  stage_t<DH, NK, VP>(Vt, v, base, st, ldkv, h * DH, L, lane);
+  bf16_t* Vt = lds[SH ? 0 : wave];
+  if (SH) {
+    stage_t<DH, NK, VP>(Vt, v, base, st, ldkv, h * DH, L, threadIdx.x, blockDim.x);
+    __syncthreads();
+    if (!live) return;
+  } else {
+    stage_t<DH, NK, VP>(Vt, v, base, st, ldkv, h * DH, L, lane);
+  }
   const int qi = 16 * it + lr;
   bf16x8 qf[KS];
 #pragma unroll
@@ -172,7 +211,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(const bf16_t* __rest
 }
 
 template <int DH, int KT>
-__global__ __launch_bounds__(256) void attn_bwd_q_mfma_kernel(const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+__global__ __launch_bounds__(shared_of<KT>() ? 64 * SH_MAXW : 256) void attn_bwd_q_mfma_kernel(const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                               int ldkv, const float* __restrict__ psave,
                                                               const bf16_t* __restrict__ dout,
                                                               const bf16_t* __restrict__ out, int ldo,
@@ -181,17 +220,24 @@ __global__ __launch_bounds__(256) void attn_bwd_q_mfma_kernel(const bf16_t* __re
                                                               int items, float scale) {
   constexpr int KS = (DH + 31) / 32, ND = DH / 16, NK = 16 * KT, VP = NK + 8, NM = (KT + 1) / 2;
   static_assert(KT % 2 == 0, "tiles are read in pairs: an odd KT would read past a V^T row");
-  __shared__ __attribute__((aligned(16))) bf16_t lds[wpb_of<KT>()][DH * VP];
+  constexpr bool SH = shared_of<KT>();
+  __shared__ __attribute__((aligned(16))) bf16_t lds[SH ? 1 : wpb_of<KT>()][DH * VP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int item = blockIdx.x * wpb_of<KT>() + wave;
-  if (item >= items) return;
   const int nqt = (L + 15) / 16;
-  const int pair = item / nqt, it = item - pair * nqt;
+  int pair, it;
+  const bool live = wave_item<SH>(nqt, items, wpb_of<KT>(), wave, pair, it);
+  if (!SH && !live) return;
   const int h = pair % nhead;
   const int64_t base = row_base(pair, nhead, n_inner, so, si);
   const int lr = lane & 15, lg = lane >> 4;
-  bf16_t* Kt = lds[wave];
-  stage_t<DH, NK, VP>(Kt, k, base, st, ldkv, h * DH, L, lane);
+  bf16_t* Kt = lds[SH ? 0 : wave];
+  if (SH) {
+    stage_t<DH, NK, VP>(Kt, k, base, st, ldkv, h * DH, L, threadIdx.x, blockDim.x);
+    __syncthreads();
+    if (!live) return;
+  } else {
+    stage_t<DH, NK, VP>(Kt, k, base, st, ldkv, h * DH, L, lane);
+  }
   const int qi = 16 * it + lr;
   bf16x8 gf[KS];
   float D = 0.f;
@@ -250,7 +296,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_mfma_kernel(const bf16_t* __re
 }
 
 template <int DH, int KT>
-__global__ __launch_bounds__(256) void attn_bwd_kv_mfma_kernel(const bf16_t* __restrict__ q, int ldq,
+__global__ __launch_bounds__(shared_of<KT>() ? 64 * SH_MAXW : 256) void attn_bwd_kv_mfma_kernel(const bf16_t* __restrict__ q, int ldq,
                                                                const bf16_t* __restrict__ v, int ldkv,
                                                                const float* __restrict__ psave,
                                                                const bf16_t* __restrict__ dout,
@@ -260,21 +306,26 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_mfma_kernel(const bf16_t* __r
                                                                int64_t st, int L, int nhead, int items, float scale) {
   constexpr int KS = (DH + 31) / 32, ND = DH / 16, NK = 16 * KT, VP = NK + 8, NM = (KT + 1) / 2;
   static_assert(KT % 2 == 0, "tiles are read in pairs: an odd KT would read past a V^T row");
-  __shared__ __attribute__((aligned(16))) bf16_t lds[wpb_of<KT>()][2 * DH * VP];
-  __shared__ float Ds[wpb_of<KT>()][NK];
+  constexpr bool SH = shared_of<KT>();
+  constexpr int NSL = SH ? 1 : wpb_of<KT>();
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NSL][2 * DH * VP];
+  __shared__ float Ds[NSL][NK];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int item = blockIdx.x * wpb_of<KT>() + wave;
-  if (item >= items) return;
   const int nkt = (L + 15) / 16;
-  const int pair = item / nkt, jt = item - pair * nkt;
+  int pair, jt;
+  const bool live = wave_item<SH>(nkt, items, wpb_of<KT>(), wave, pair, jt);
+  if (!SH && !live) return;
   const int h = pair % nhead;
   const int64_t base = row_base(pair, nhead, n_inner, so, si);
   const int lr = lane & 15, lg = lane >> 4;
-  bf16_t* Gt = lds[wave];             // dO^T [DH][VP]
-  bf16_t* Qt = lds[wave] + DH * VP;   // Q^T  [DH][VP]
-  stage_t<DH, NK, VP>(Gt, dout, base, st, ldo, h * DH, L, lane);
-  stage_t<DH, NK, VP>(Qt, q, base, st, ldq, h * DH, L, lane);
-  for (int qq = lane; qq < NK; qq += 64) {   // D_q = dO_q . O_q
+  const int sl = SH ? 0 : wave;
+  bf16_t* Gt = lds[sl];             // dO^T [DH][VP]
+  bf16_t* Qt = lds[sl] + DH * VP;   // Q^T  [DH][VP]
+  // SH: the block stages once (all its threads); otherwise each wave its own slice
+  const int t0 = SH ? (int)threadIdx.x : lane, tn = SH ? (int)blockDim.x : 64;
+  stage_t<DH, NK, VP>(Gt, dout, base, st, ldo, h * DH, L, t0, tn);
+  stage_t<DH, NK, VP>(Qt, q, base, st, ldq, h * DH, L, t0, tn);
+  for (int qq = t0; qq < NK; qq += tn) {   // D_q = dO_q . O_q
     float D = 0.f;
     if (qq < L) {
       const int64_t rb = (base + (int64_t)qq * st) * ldo + h * DH;
@@ -286,7 +337,11 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_mfma_kernel(const bf16_t* __r
         for (int e = 0; e < 8; ++e) D = fmaf((float)g[e], (float)o[e], D);
       }
     }
-    Ds[wave][qq] = D;
+    Ds[sl][qq] = D;
+  }
+  if (SH) {
+    __syncthreads();
+    if (!live) return;
   }
   const int kj = 16 * jt + lr;   // this lane's key column
   bf16x8 vf[KS];
@@ -309,7 +364,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_mfma_kernel(const bf16_t* __r
       const float pv = P[min(qq, L - 1)];
       const bool ok = qq < L && kj < L;
       p[i][r] = ok ? pv : 0.f;
-      ds[i][r] = ok ? pv * (a[r] - Ds[wave][min(qq, NK - 1)]) : 0.f;
+      ds[i][r] = ok ? pv * (a[r] - Ds[sl][min(qq, NK - 1)]) : 0.f;
     }
   }
   f32x4 av[ND], ak[ND];
@@ -352,9 +407,11 @@ template <int DH, int KT>
 void launch_fwd(const bf16_t* q, int ldq, const bf16_t* k, const bf16_t* v, int ldkv, bf16_t* out, int ldo, float* ps,
                 const uint8_t* mask, int npairs, int n_inner, int64_t so, int64_t si, int64_t st, int L, int nhead,
                 float scale, hipStream_t s) {
-  const int items = npairs * ((L + 15) / 16);
+  const int tiles = (L + 15) / 16, items = npairs * tiles;
   constexpr int WPB = wpb_of<KT>();
-  hipLaunchKernelGGL((attn_fwd_mfma_kernel<DH, KT>), dim3((items + WPB - 1) / WPB), dim3(64 * WPB), 0, s, q, ldq, k, v,
+  const int nw = shared_of<KT>() ? sh_waves(tiles) : WPB;
+  const dim3 grid(shared_of<KT>() ? npairs * ((tiles + nw - 1) / nw) : (items + WPB - 1) / WPB), block(64 * nw);
+  hipLaunchKernelGGL((attn_fwd_mfma_kernel<DH, KT>), grid, block, 0, s, q, ldq, k, v,
                      ldkv, out, ldo, ps, mask, n_inner, so, si, st, L, nhead, items, scale);
 }
 
@@ -363,9 +420,10 @@ void launch_bwd(const bf16_t* q, int ldq, const bf16_t* k, const bf16_t* v, int 
                 const bf16_t* dout, const bf16_t* out, int ldo, bf16_t* dq, int lddq, bf16_t* dk, bf16_t* dv, int lddkv,
                 int npairs, int n_inner, int64_t so, int64_t si, int64_t st, int L, int nhead, float scale,
                 hipStream_t s) {
-  const int items = npairs * ((L + 15) / 16);
+  const int tiles = (L + 15) / 16, items = npairs * tiles;
   constexpr int WPB = wpb_of<KT>();
-  const dim3 grid((items + WPB - 1) / WPB), block(64 * WPB);
+  const int nw = shared_of<KT>() ? sh_waves(tiles) : WPB;
+  const dim3 grid(shared_of<KT>() ? npairs * ((tiles + nw - 1) / nw) : (items + WPB - 1) / WPB), block(64 * nw);
   hipLaunchKernelGGL((attn_bwd_q_mfma_kernel<DH, KT>), grid, block, 0, s, k, v, ldkv, ps, dout, out, ldo, dq, lddq,
                      n_inner, so, si, st, L, nhead, items, scale);
   hipLaunchKernelGGL((attn_bwd_kv_mfma_kernel<DH, KT>), grid, block, 0, s, q, ldq, v, ldkv, ps, dout, out, ldo, dk, dv,

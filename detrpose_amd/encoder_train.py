@@ -147,6 +147,7 @@ class TapePlan:
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             self.world, self.rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
         self.fw, self.bw = _lib_tape(self.lib, self.dev), _lib_tape(self.lib, self.dev)
+        self.fw.deterministic = True
         # the weight packs (bf16 copies / conv layouts of the f32 master) on a tape of their own:
         # run once per optimizer step, not once per grad_accum sub-batch (forward(pack=False))
         self.pk = _lib_tape(self.lib, self.dev)
@@ -290,9 +291,10 @@ class TapePlan:
         (implicit GEMM, no im2col columns), else dp_im2col + dp_gemm (dz^T col)."""
         lib = self.lib
         if self.code == DP_BF16 and cin % 8 == 0 and x_ld % 8 == 0 and dz_ld % 8 == 0:
-            scratch = self.f32(cout * cin * k * k)
-            bw.op(name + ".dW", lib.dp_conv_wgrad, xp, H * W * x_ld, x_ld, B, H, W, cin, dzp, dz_ld, oh, ow, cout, k, k,
-                  stride, pad, _p(scratch), _p(G), self.code)
+            # zeroed once here and left zeroed by every call (dp_conv_wgrad_zs): no zero-fill launch
+            scratch = self.f32(cout * cin * k * k).zero_()
+            bw.op(name + ".dW", lib.dp_conv_wgrad_zs, xp, H * W * x_ld, x_ld, B, H, W, cin, dzp, dz_ld, oh, ow, cout, k,
+                  k, stride, pad, _p(scratch), _p(G), self.code)
             self.cost(name + ".dW", 2.0 * B * oh * ow * cout * cin * k * k)
             return
         K = cin * k * k

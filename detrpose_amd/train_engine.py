@@ -77,6 +77,9 @@ class Tape:
         self.use_graph = False
         self.runs = 0
         self._graph = None   # [("graph", CUDAGraph) | ("host", fn)] once captured
+        # a forward tape: its GEMMs never split K (float atomics would make the forward differ
+        # run to run; the reference's forward is deterministic, tests/test_gpu_train_graphs.py)
+        self.deterministic = False
 
     def op(self, name, fn, *args):
         self.ops.append((name, fn, args))
@@ -246,11 +249,21 @@ class TrainEngine:
             "a non-backbone parameter inside the backbone learning-rate range"
         self.ema = None
         self.ema_updates = 0
+        # the encoder's BatchNorm running statistics: views of ONE flat f32 buffer, so ModelEMA's
+        # update of all of them is one launch (was one per tensor: 178 per L step)
         self.running = {}
+        self.running_flat = None
         if train_encoder:
-            for n, b in model.named_buffers():
-                if n.startswith("encoder.") and (n.endswith(".running_mean") or n.endswith(".running_var")):
-                    self.running[n] = b.detach().to(dev, torch.float32).clone()
+            rb = [(n, b) for n, b in model.named_buffers()
+                  if n.startswith("encoder.") and (n.endswith(".running_mean") or n.endswith(".running_var"))]
+            rsz = [(b.numel() + 63) // 64 * 64 for _, b in rb]
+            self.running_flat = torch.zeros(max(sum(rsz), 1), dtype=torch.float32, device=dev)
+            ro = 0
+            for (n, b), sz in zip(rb, rsz):
+                v = self.running_flat[ro:ro + b.numel()].view(b.shape)
+                v.copy_(b.detach().to(dev, torch.float32))
+                self.running[n] = v
+                ro += sz
         self.load_weights()
         self.plans = {}          # TrainPlan per (batch, DN pad, shapes, ...), LRU order
         self.max_plans = 6
@@ -428,7 +441,11 @@ class TrainEngine:
 
     def ema_init(self):
         self.ema = self.master.clone()
-        self.ema_running = {k: v.clone() for k, v in self.running.items()}
+        self.ema_running_flat = self.running_flat.clone() if self.running_flat is not None else None
+        self.ema_running = {}
+        for k, v in self.running.items():   # same offsets as the running views
+            o = (v.data_ptr() - self.running_flat.data_ptr()) // 4
+            self.ema_running[k] = self.ema_running_flat[o:o + v.numel()].view(v.shape)
         self.ema_updates = 0
 
     def ema_update(self, decay=0.9999, warmups=2000):
@@ -441,7 +458,9 @@ class TrainEngine:
             self.ema_init()
         self.ema_updates += 1
         d = decay * (1 - math.exp(-self.ema_updates / warmups)) if warmups else decay
-        pairs = [(self.ema, self.master)] + [(self.ema_running[k], v) for k, v in self.running.items()]
+        pairs = [(self.ema, self.master)]
+        if self.running:   # every running statistic in one launch (the pads are zero in both)
+            pairs.append((self.ema_running_flat, self.running_flat))
         for e, p in pairs:
             _lib.check(lib.dp_ema(_p(e), _p(p), e.numel(), C.c_float(d), _p(self.bad), s), "dp_ema")
 
@@ -470,7 +489,7 @@ class TrainEngine:
         d.alpha, d.beta, d.act = alpha, beta, act
         d.gate, d.gate_bs, d.gate_rs = gate, gate_bs, gate_rs
         d.gate_dtype = self.code if gate_code is None else gate_code
-        d.split_k = 0
+        d.split_k = 1 if tape.deterministic else 0
         d.colsum = colsum
         tape.keep.append(d)
         tape.op(name, self.lib.dp_gemm, C.byref(d))
@@ -664,6 +683,7 @@ class TrainPlan:
         sort_ok = nws > 0 and Cc // nh in (8, 16, 32, 64) and os.environ.get("DETRPOSE_MSDA_BWD", "sorted") == "sorted"
         self.msda_ws = buf(nws, dtype=torch.uint8) if sort_ok else None
         fw = Tape(lib, dev)
+        fw.deterministic = True
         bw = Tape(lib, dev)
         self.fw, self.bw = fw, bw
         self.pk = Tape(lib, dev)   # weight packs: run once per optimizer step (TrainEngine._wt_pack)
@@ -881,39 +901,54 @@ class TrainPlan:
         self.d_interm_logits = torch.zeros_like(self.interm_logits)
         self.d_interm_kps = torch.empty(B, nq, 2 * K, dtype=torch.float32, device=dev)
 
+    def _copy_rows(self, key, entries, s):
+        """The f32 row copies `entries` [(dst, ld_dst, src0, ld_src0, src1 | None, ld_src1, rows, n)]
+        (pointers) in ONE dp_copy_rows_batch launch; the device table is built once per key (the
+        plan's buffers never move) and rebuilt if the pointers change."""
+        lib = self.eng.lib
+        cache = self.__dict__.setdefault("_row_copies", {})
+        ent = tuple(entries)
+        got = cache.get(key)
+        if got is None or got[2] != ent:
+            n = len(ent)
+            tab = (_lib.RowCopyDesc * n)()
+            for i, (dst, ldd, s0, ld0, s1, ld1, rows, cols) in enumerate(ent):
+                tab[i] = _lib.RowCopyDesc(s0, s1, dst, ld0, ld1 if s1 else 0, ldd, rows, cols)
+            _lib.check(lib.dp_copy_rows_check(tab, n), "row-copy table " + key)
+            dev = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(self.eng.device)
+            bpe = max(1, min(64, -(-max(r * c for *_, r, c in ent) // 512)))
+            got = cache[key] = (dev, n, ent, bpe)
+        dev, n, _, bpe = got
+        _lib.check(lib.dp_copy_rows_batch(_p(dev), n, bpe, s), "dp_copy_rows_batch " + key)
+
     def heads_pack(self):
         """The H heads in the reference's matching order (final, aux 0..L-2, pre, interm) as
-        contiguous (B, nq, .) f32 blocks (their matching rows; DN rows separately)."""
-        eng, lib = self.eng, self.eng.lib
+        contiguous (B, nq, .) f32 blocks (their matching rows; DN rows separately): one launch."""
+        eng = self.eng
         B, P, nq, K, L, Qt, T = self.B, self.P, eng.nq, eng.K, eng.L, self.Qt, eng.T
         ncls = eng.ncls
         s = C.c_void_p(torch.cuda.current_stream(eng.device).cuda_stream)
         order = [L - 1] + list(range(L - 1))
-        chk = _lib.check
+        e = []
+
+        def cp(dst, ldd, src, lds, rows, n):
+            e.append((dst, ldd, src, lds, None, 0, rows, n))
+
         for h, l in enumerate(order):
-            chk(lib.dp_convert_rows(_p(self.logits[l], P * ncls), DP_F32, Qt * ncls, _p(self.hl[h]), DP_F32, nq * ncls,
-                                    B, nq * ncls, 1.0, 0, s), "pack")
-            chk(lib.dp_convert_rows(_p(self.kps[l], P * 2 * K), DP_F32, Qt * 2 * K, _p(self.hk[h]), DP_F32, nq * 2 * K,
-                                    B, nq * 2 * K, 1.0, 0, s), "pack")
-        chk(lib.dp_convert_rows(_p(self.pre_logits, P * ncls), DP_F32, Qt * ncls, _p(self.hl[L]), DP_F32, nq * ncls, B,
-                                nq * ncls, 1.0, 0, s), "pack")
-        chk(lib.dp_convert_rows(_p(self.pre_out, P * 2 * K), DP_F32, Qt * 2 * K, _p(self.hk[L]), DP_F32, nq * 2 * K, B,
-                                nq * 2 * K, 1.0, 0, s), "pack")
-        chk(lib.dp_convert_rows(_p(self.interm_logits), DP_F32, nq * ncls, _p(self.hl[L + 1]), DP_F32, nq * ncls, B,
-                                nq * ncls, 1.0, 0, s), "pack")
+            cp(_p(self.hl[h]), nq * ncls, _p(self.logits[l], P * ncls), Qt * ncls, B, nq * ncls)
+            cp(_p(self.hk[h]), nq * 2 * K, _p(self.kps[l], P * 2 * K), Qt * 2 * K, B, nq * 2 * K)
+        cp(_p(self.hl[L]), nq * ncls, _p(self.pre_logits, P * ncls), Qt * ncls, B, nq * ncls)
+        cp(_p(self.hk[L]), nq * 2 * K, _p(self.pre_out, P * 2 * K), Qt * 2 * K, B, nq * 2 * K)
+        cp(_p(self.hl[L + 1]), nq * ncls, _p(self.interm_logits), nq * ncls, B, nq * ncls)
         # interm keypoints = enc_outputs_pose_coord[:, :, 1:] (skip the centre)
-        chk(lib.dp_convert_rows(_p(self.ref0, 2), DP_F32, T * 2, _p(self.hk[L + 1]), DP_F32, 2 * K, B * nq, 2 * K, 1.0,
-                                0, s), "pack")
+        cp(_p(self.hk[L + 1]), 2 * K, _p(self.ref0, 2), T * 2, B * nq, 2 * K)
         if P:
             for l in range(L):
-                chk(lib.dp_convert_rows(_p(self.logits[l]), DP_F32, Qt * ncls, _p(self.dl[l]), DP_F32, P * ncls, B,
-                                        P * ncls, 1.0, 0, s), "pack")
-                chk(lib.dp_convert_rows(_p(self.kps[l]), DP_F32, Qt * 2 * K, _p(self.dk[l]), DP_F32, P * 2 * K, B,
-                                        P * 2 * K, 1.0, 0, s), "pack")
-            chk(lib.dp_convert_rows(_p(self.pre_logits), DP_F32, Qt * ncls, _p(self.dl[L]), DP_F32, P * ncls, B,
-                                    P * ncls, 1.0, 0, s), "pack")
-            chk(lib.dp_convert_rows(_p(self.pre_out), DP_F32, Qt * 2 * K, _p(self.dk[L]), DP_F32, P * 2 * K, B,
-                                    P * 2 * K, 1.0, 0, s), "pack")
+                cp(_p(self.dl[l]), P * ncls, _p(self.logits[l]), Qt * ncls, B, P * ncls)
+                cp(_p(self.dk[l]), P * 2 * K, _p(self.kps[l]), Qt * 2 * K, B, P * 2 * K)
+            cp(_p(self.dl[L]), P * ncls, _p(self.pre_logits), Qt * ncls, B, P * ncls)
+            cp(_p(self.dk[L]), P * 2 * K, _p(self.pre_out), Qt * 2 * K, B, P * 2 * K)
+        self._copy_rows("heads", e, s)
 
     def criterion(self, packed, sizes, num_group, weights=(2.0, 10.0, 4.0), cost=(2.0, 10.0, 4.0), alpha=0.25,
                   gamma=2.0):
@@ -971,27 +1006,26 @@ class TrainPlan:
         # ---- hand-off: d loss_total / d head outputs
         order = [L - 1] + list(range(L - 1))
 
-        def put(dst, dst_off, ld_dst, src, n, acc=0):
-            chk(lib.dp_convert_rows(_p(src), DP_F32, n, _p(dst, dst_off), DP_F32, ld_dst, B, n, 1.0, acc, s), "hand-off")
+        # one launch; keypoint gradients = the L1 part + the OKS part (dst = src0 + src1)
+        e = []
+
+        def put(dst, dst_off, ld_dst, src, n, src1=None):
+            e.append((_p(dst, dst_off), ld_dst, _p(src), n, _p(src1) if src1 is not None else None, n, B, n))
 
         for h, l in enumerate(order):
             put(self.d_logits[l], P * ncls, Qt * ncls, self.g_lg[h], nq * ncls)
-            put(self.d_kps[l], P * 2 * K, Qt * 2 * K, self.g_l1[h], nq * 2 * K)
-            put(self.d_kps[l], P * 2 * K, Qt * 2 * K, self.g_oks[h], nq * 2 * K, 1)
+            put(self.d_kps[l], P * 2 * K, Qt * 2 * K, self.g_l1[h], nq * 2 * K, self.g_oks[h])
         put(self.d_pre_logits, P * ncls, Qt * ncls, self.g_lg[L], nq * ncls)
-        put(self.d_pre_out, P * 2 * K, Qt * 2 * K, self.g_l1[L], nq * 2 * K)
-        put(self.d_pre_out, P * 2 * K, Qt * 2 * K, self.g_oks[L], nq * 2 * K, 1)
+        put(self.d_pre_out, P * 2 * K, Qt * 2 * K, self.g_l1[L], nq * 2 * K, self.g_oks[L])
         put(self.d_interm_logits, 0, nq * ncls, self.g_lg[L + 1], nq * ncls)
-        put(self.d_interm_kps, 0, nq * 2 * K, self.g_l1[L + 1], nq * 2 * K)
-        put(self.d_interm_kps, 0, nq * 2 * K, self.g_oks[L + 1], nq * 2 * K, 1)
+        put(self.d_interm_kps, 0, nq * 2 * K, self.g_l1[L + 1], nq * 2 * K, self.g_oks[L + 1])
         if P:
             for l in range(L):
                 put(self.d_logits[l], 0, Qt * ncls, self.dg_lg[l], P * ncls)
-                put(self.d_kps[l], 0, Qt * 2 * K, self.dg_l1[l], P * 2 * K)
-                put(self.d_kps[l], 0, Qt * 2 * K, self.dg_oks[l], P * 2 * K, 1)
+                put(self.d_kps[l], 0, Qt * 2 * K, self.dg_l1[l], P * 2 * K, self.dg_oks[l])
             put(self.d_pre_logits, 0, Qt * ncls, self.dg_lg[L], P * ncls)
-            put(self.d_pre_out, 0, Qt * 2 * K, self.dg_l1[L], P * 2 * K)
-            put(self.d_pre_out, 0, Qt * 2 * K, self.dg_oks[L], P * 2 * K, 1)
+            put(self.d_pre_out, 0, Qt * 2 * K, self.dg_l1[L], P * 2 * K, self.dg_oks[L])
+        self._copy_rows("hand-off", e, s)
         keys = []
         for n in names:
             keys += ["loss_vfl" + n, "loss_keypoints" + n, "loss_oks" + n]

@@ -459,6 +459,12 @@ int dp_gemm(const dp_gemm_desc* d, void* stream);
 int dp_conv_wgrad(const void* x, int64_t x_bstride, int32_t x_pstride, int32_t batch, int32_t h, int32_t w,
                   int32_t cin, const void* dz, int64_t dz_ld, int32_t oh, int32_t ow, int32_t cout, int32_t kh,
                   int32_t kw, int32_t stride, int32_t pad, float* scratch, float* dw, int32_t dtype, void* stream);
+/* dp_conv_wgrad on a scratch that holds zeros on entry and is left zeroed on return (the permute
+ * clears each element it consumes), so no zero-fill launch per call: a training plan allocates each
+ * conv's scratch zeroed once (torch.zeros). Same arguments and result. */
+int dp_conv_wgrad_zs(const void* x, int64_t x_bstride, int32_t x_pstride, int32_t batch, int32_t h, int32_t w,
+                     int32_t cin, const void* dz, int64_t dz_ld, int32_t oh, int32_t ow, int32_t cout, int32_t kh,
+                     int32_t kw, int32_t stride, int32_t pad, float* scratch, float* dw, int32_t dtype, void* stream);
 
 /* y = LayerNorm(x [+ res]) over contiguous rows of c (nn.LayerNorm, eps): writes y, the pre-norm
  * sum s = x + res (if s != NULL; the backward's input) and stats f32 [rows][2] = (mean, rstd);
@@ -586,6 +592,22 @@ int dp_zero(void* p, int64_t bytes, void* stream);
  * hand-offs): dst[r][j] = src[r][j] (+ dst when accumulate) * scale. */
 int dp_convert_rows(const void* src, int32_t src_dtype, int64_t ld_src, void* dst, int32_t dst_dtype,
                     int64_t ld_dst, int32_t rows, int32_t n, float scale, int32_t accumulate, void* stream);
+/* A table of f32 row copies in ONE launch: dst[r][j] = src0[r][j] (+ src1[r][j] when src1 is not
+ * NULL) for r < rows, j < n, each operand at its own row pitch (elements). The criterion's head
+ * packing and gradient hand-off (criterion.py:285-435's outputs -> loss inputs, loss gradients ->
+ * head-output gradients), which were one dp_convert_rows each. Entries must not write what
+ * another entry reads or writes. dp_copy_rows_check validates a host copy of the table (once,
+ * when it is built); dp_copy_rows_batch reads it from device memory (tab_dev), blocks_per_entry
+ * blocks striding over each entry's elements. */
+typedef struct dp_rowcopy_desc {
+  const float* src0;
+  const float* src1;
+  float* dst;
+  int64_t ld_src0, ld_src1, ld_dst;
+  int32_t rows, n;
+} dp_rowcopy_desc;
+int dp_copy_rows_check(const dp_rowcopy_desc* tab, int32_t n);
+int dp_copy_rows_batch(const dp_rowcopy_desc* tab_dev, int32_t n, int32_t blocks_per_entry, void* stream);
 
 /* ---- HybridEncoder training step (BASELINE config 5; hybrid_encoder.py:56-212, 246-296,
  * 462-507 in training mode). Activations are NHWC rows [rows = batch*h*w][c] with a row stride

@@ -429,6 +429,17 @@ def test_conv_wgrad_implicit(B, h, w, cin, cout, k, st, pad, xpad):
     ref = wr.grad + 0.5
     err = (dw - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-3, err
+    # dp_conv_wgrad_zs: a zeroed scratch, left zeroed by each call (so two calls in a row accumulate
+    # exactly twice the gradient with no zero-fill between them)
+    dw2 = torch.full((cout, cin, k, k), 0.5, device=DEV)
+    scratch2 = torch.zeros(cout * cin * k * k, device=DEV)
+    for _ in range(2):
+        _lib.check(lib.dp_conv_wgrad_zs(x.data_ptr(), h * w * ps, ps, B, h, w, cin, dz.data_ptr(), ldz, oh, ow, cout,
+                                        k, k, st, pad, scratch2.data_ptr(), dw2.data_ptr(), DP_BF16, _s()), "zs")
+    torch.cuda.synchronize()
+    ref2 = 2 * wr.grad + 0.5
+    err2 = (dw2 - ref2).abs().max().item() / ref2.abs().max().item()
+    assert err2 < 2e-3 and int(scratch2.count_nonzero()) == 0, (err2, int(scratch2.count_nonzero()))
 
 
 @pytest.mark.parametrize("rows,c,dt", [(6400, 256, DP_BF16), (1000, 96, DP_F32), (409600, 64, DP_BF16)])

@@ -313,3 +313,37 @@ def test_colsum_bias_gradient(dtype, rows, n, ld, acc):
     torch.cuda.synchronize()
     tol = 1e-5 * x[:, :n].double().abs().sum(0) + 1e-6
     assert ((out.double() - ref).abs() <= tol).all(), float((out.double() - ref).abs().max())
+
+
+def test_copy_rows_batch_matches_convert_rows():
+    """dp_copy_rows_batch (the criterion's head packing / gradient hand-off in one launch) equals the
+    dp_convert_rows calls it replaces BIT FOR BIT: strided f32 row copies, and dst = src0 + src1 as a
+    copy followed by an accumulating copy; the pitch padding of dst is left untouched. The table
+    checker refuses an entry whose pitch is below its row length."""
+    lib = _lib.load()
+    torch.manual_seed(3)
+    shapes = [(8, 120, 136, 140), (8, 2040, 2040, 2160), (480, 34, 36, 34), (1, 1, 1, 1), (8, 1020, 1020, 1090)]
+    e, ref_ops, dsts = [], [], []
+    for i, (rows, n, ld0, ldd) in enumerate(shapes):
+        s0 = torch.randn(rows, ld0, device=DEV)
+        s1 = torch.randn(rows, n, device=DEV) if i % 2 else None
+        d = torch.full((rows, ldd), 5.0, device=DEV)
+        d_ref = d.clone()
+        _lib.check(lib.dp_convert_rows(s0.data_ptr(), DP_F32, ld0, d_ref.data_ptr(), DP_F32, ldd, rows, n,
+                                       C.c_float(1.0), 0, _s()), "convert")
+        if s1 is not None:
+            _lib.check(lib.dp_convert_rows(s1.data_ptr(), DP_F32, n, d_ref.data_ptr(), DP_F32, ldd, rows, n,
+                                           C.c_float(1.0), 1, _s()), "convert acc")
+        e.append(_lib.RowCopyDesc(s0.data_ptr(), s1.data_ptr() if s1 is not None else None, d.data_ptr(), ld0,
+                                  n if s1 is not None else 0, ldd, rows, n))
+        dsts.append((d, d_ref, s0, s1))
+    tab = (_lib.RowCopyDesc * len(e))(*e)
+    _lib.check(lib.dp_copy_rows_check(tab, len(e)), "check")
+    dev = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(DEV)
+    _lib.check(lib.dp_copy_rows_batch(dev.data_ptr(), len(e), 16, _s()), "batch")
+    torch.cuda.synchronize()
+    for d, d_ref, _, _ in dsts:
+        assert torch.equal(d, d_ref)
+    bad = (_lib.RowCopyDesc * 1)(_lib.RowCopyDesc(dsts[0][2].data_ptr(), None, dsts[0][0].data_ptr(), 10, 0, 140, 8,
+                                                  120))
+    assert lib.dp_copy_rows_check(bad, 1) != 0
