@@ -534,6 +534,21 @@ class TrainEngine:
                            None, DP_BF16)
         return t, kpad
 
+    def _wt_f32(self, wkey):
+        """W^T of a linear's weight as f32 [K][N] (dp_conv_pack mode 4 of the f32 master, kpad = N):
+        dp_linear_small's weight layout, re-packed on the current plan's pack tape as _wt_pack."""
+        if not hasattr(self, "_wtf"):
+            self._wtf, self._wtf_ops = {}, set()
+        N, K = self.sd32[wkey].shape
+        if wkey not in self._wtf:
+            self._wtf[wkey] = torch.zeros(K, N, dtype=torch.float32, device=self.device)
+        t = self._wtf[wkey]
+        if (id(self.cur), wkey) not in self._wtf_ops:
+            self._wtf_ops.add((id(self.cur), wkey))
+            self.cur.pk.op(f"pack.{wkey}.Tf", self.lib.dp_conv_pack, _p(self.sd32[wkey]), N, K, 1, 1, _p(t), N, 0, 4,
+                           None, DP_F32)
+        return t
+
     def lin(self, tape, name, x, ldx, rows, wkey, out, ldo, act=0, out_code=None, bias=True, beta=0.0, wt=None,
             in_code=None):
         """out = act(x W^T + b): nn.Linear forward."""
@@ -543,6 +558,17 @@ class TrainEngine:
         b = self.sd32.get(bk) if bias else None
         ic = self.code if in_code is None else in_code
         oc = self.code if out_code is None else out_code
+        if (tape.deterministic and self.code == DP_BF16 and ic == oc == DP_F32 and N <= 128 and rows <= 4096 and ldo == N and act in (0, 1) and
+                beta in (0.0, 1.0) and wkey in self.sd32 and os.environ.get("DETRPOSE_TRAIN_LINEAR_SMALL", "1") != "0"):
+            # the all-f32 heads of a bf16 forward tape (the LQE Linears over <= 4096 rows; f32 input
+            # and f32 weights, as the GEMM had them): one wave per row (dp_linear_small, the inference heads' kernel) instead of a GEMM of a few
+            # 64-row tiles whose K-steps each wait a full load latency (the GEMM may not split K here:
+            # the forward stays deterministic). The fp32 parity mode keeps the GEMM's summation order
+            wT = _p(self.sd32[wkey]) if N == 1 else _p(self._wt_f32(wkey))
+            tape.op(name, self.lib.dp_linear_small, x, contiguous_rows(ldx), ic, rows, K, wT,
+                    _p(b) if b is not None else None, N, N, act, out if beta == 1.0 else None, out)
+            self.cur.cost(name, 2.0 * rows * N * K)
+            return
         if (ic == oc == DP_BF16 and K % 64 == 0 and W.is_contiguous() and self._rows_ok(x, ldx) and
                 self._rows_ok(out, ldo) and act in (0, 1) and (beta == 0.0 or (beta == 1.0 and act == 0))):
             self._conv1x1(tape, name, x, ldx, rows, _p(W), K, K, N, out, ldo,
@@ -849,8 +875,14 @@ class TrainPlan:
             b2 = sd[qe + "1.bias"].repeat(eng.ncls).contiguous()
             self.arena.append(b2)
             self._derived.append((b2, qe + "1.bias"))
-            eng._gemm(fw, n + ".lqe1", _p(hq), nhid, 1, _p(w1), 1, 0, _p(logits[l]), eng.ncls, qrows, eng.ncls, nhid,
-                      DP_F32, DP_F32, bias=_p(b2), beta=1.0)
+            if code == DP_BF16 and os.environ.get("DETRPOSE_TRAIN_LINEAR_SMALL", "1") != "0":
+                # w1 [1][nhid] is its own transpose: nw = 1 broadcasts the one output to the ncls columns
+                fw.op(n + ".lqe1", lib.dp_linear_small, _p(hq), contiguous_rows(nhid), DP_F32, qrows, nhid, _p(w1),
+                      _p(sd[qe + "1.bias"]), 1, eng.ncls, 0, _p(logits[l]), _p(logits[l]))
+                self.cost(n + ".lqe1", 2.0 * qrows * eng.ncls * nhid)
+            else:
+                eng._gemm(fw, n + ".lqe1", _p(hq), nhid, 1, _p(w1), 1, 0, _p(logits[l]), eng.ncls, qrows, eng.ncls,
+                          nhid, DP_F32, DP_F32, bias=_p(b2), beta=1.0)
             S_.update(se=se, ph=ph, pos=pos, x0=x0, qkv_w=qkv_w, att_w=att_w, P_w=P_w, x1=x1, s_w=s_w, st_w=st_w,
                       qkv_a=qkv_a, att_a=att_a, P_a=P_a, xcat=xcat, s_a=s_a, st_a=st_a, oa=oa, gs=gs, yg=yg, s_g=s_g,
                       st_g=st_g, h=h, y=y, s_2=s_2, st_2=st_2, u=u, c0=c0, c1=c1, stt=stt, hq=hq)

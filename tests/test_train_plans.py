@@ -82,7 +82,9 @@ def test_bf16_tapes_route_to_the_fast_kernels():
     names = lambda t, fn: [n for n, f, _ in t.ops if f is fn]   # noqa: E731
     im2col = names(bb.bw, lib.dp_im2col) + names(ep.bw, lib.dp_im2col)
     assert im2col == ["stem1.im2col"], im2col
-    assert len(names(bb.bw, lib.dp_conv_wgrad)) >= 15 and len(names(ep.bw, lib.dp_conv_wgrad)) > 10
+    # dp_conv_wgrad_zs: the same kernel on a scratch kept zeroed (no zero-fill launch per call)
+    assert len(names(bb.bw, lib.dp_conv_wgrad_zs)) >= 15 and len(names(ep.bw, lib.dp_conv_wgrad_zs)) > 10
+    assert not names(bb.bw, lib.dp_conv_wgrad) + names(ep.bw, lib.dp_conv_wgrad)
     fw_conv = names(plan.fw, lib.dp_conv2d)
     assert any(n.endswith(".ffn1") for n in fw_conv) and any(n.endswith(".ffn2") for n in fw_conv), fw_conv[:8]
     assert any(n.endswith(".ffn2.dx") for n in names(plan.bw, lib.dp_conv2d))
