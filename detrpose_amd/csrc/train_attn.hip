@@ -30,13 +30,15 @@ namespace {
 template <int KT>
 constexpr int wpb_of() { return KT > 8 ? 2 : 4; }
 
-// SH (the 400-token AIFI instantiation): every wave of a block works on the SAME (sequence, head)
+// SH (sequences of more than 32 tokens: the decoder's across-instance attention with its DN
+// queries, the 400-token AIFI layer): every wave of a block works on the SAME (sequence, head)
 // pair, one query (or key) tile each, and the block stages the pair's transposed operands into
-// LDS once (was once per wave: 25 waves per pair re-staged the same 26 KB, the backward's dK/dV
-// kernel also recomputed D over all 400 queries per wave). Block = nw waves (nw | tiles when a
-// divisor in 4..8 exists), grid = pairs x ceil(tiles / nw); waves past the tiles only stage.
+// LDS once (was once per wave: AIFI's 25 waves per pair re-staged the same 26 KB, the backward's
+// dK/dV kernel also recomputed D over all the queries per wave). Block = nw waves (nw | tiles
+// when a divisor in 4..8 exists), grid = pairs x ceil(tiles / nw); waves past the tiles only
+// stage. The within-instance attention (18 tokens, 2 tiles) keeps one pair tile per wave.
 template <int KT>
-constexpr bool shared_of() { return KT > 8; }
+constexpr bool shared_of() { return KT >= 4; }
 constexpr int SH_MAXW = 8;
 
 // block width (waves) of a shared-staging launch over `tiles` tiles per pair
