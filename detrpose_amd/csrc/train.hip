@@ -640,50 +640,63 @@ __global__ void query_build_kernel(const float* __restrict__ te, const float* __
   tgt[e] = from_f32<T>(v);
 }
 
-// task (blockIdx.y): 0 tgt_embed [nq][c], 1 keypoint_embedding [nkp][c], 2 instance [c],
-// 3 pose_enc [nkp][c], 4 label_enc (atomics: DN slots share labels)
+// Column sums over row sets (the embedding gradients of the query build): block (x, task) owns 64
+// consecutive output elements (lane = channel, coalesced rows) and its QB_W waves split the task's
+// rows, partials summed in wave order through LDS (deterministic; was one thread per output element
+// walking all of its rows: the instance embedding's 256 threads each summed B * nq = 480 rows).
+// task 0 tgt_embed [nq][c] over (b, t >= 1); 1 keypoint_embedding [nkp][c] over (b, q); 2
+// instance_embedding [c] over (b, q); 3 pose_enc [nkp][c] over the labelled DN slots (b, i);
+// 4 label_enc rows (float atomics per DN slot, element-wise).
+constexpr int QB_W = 16;
 template <typename T>
-__global__ void query_build_bwd_kernel(const T* __restrict__ d, const int* __restrict__ lab, int B, int pad, int nq,
-                                       int nkp, int c, float* __restrict__ gte, float* __restrict__ gke,
-                                       float* __restrict__ gie, float* __restrict__ gle, float* __restrict__ gpe) {
+__global__ __launch_bounds__(64 * QB_W) void query_build_bwd_kernel(const T* __restrict__ d, const int* __restrict__ lab,
+                                                                   int B, int pad, int nq, int nkp, int c,
+                                                                   float* __restrict__ gte, float* __restrict__ gke,
+                                                                   float* __restrict__ gie, float* __restrict__ gle,
+                                                                   float* __restrict__ gpe) {
   const int T_ = nkp + 1, Qt = pad + nq;
   const int task = blockIdx.y;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   auto at = [&](int b, int qq, int t, int ch) { return to_f32(d[(((int64_t)b * Qt + qq) * T_ + t) * c + ch]); };
-  if (task == 0) {
-    if (e >= nq * c) return;
-    const int q = e / c, ch = e % c;
-    float s = 0.f;
-    for (int b = 0; b < B; ++b)
-      for (int t = 1; t < T_; ++t) s += at(b, pad + q, t, ch);
-    gte[e] += s;
-  } else if (task == 1) {
-    if (e >= nkp * c) return;
-    const int k = e / c, ch = e % c;
-    float s = 0.f;
-    for (int b = 0; b < B; ++b)
-      for (int q = 0; q < nq; ++q) s += at(b, pad + q, k + 1, ch);
-    gke[e] += s;
-  } else if (task == 2) {
-    if (e >= c) return;
-    float s = 0.f;
-    for (int b = 0; b < B; ++b)
-      for (int q = 0; q < nq; ++q) s += at(b, pad + q, 0, e);
-    gie[e] += s;
-  } else if (task == 3) {
-    if (e >= nkp * c || !gpe) return;
-    const int k = e / c, ch = e % c;
-    float s = 0.f;
-    for (int b = 0; b < B; ++b)
-      for (int i = 0; i < pad; ++i)
-        if (lab[(int64_t)b * pad + i] >= 0) s += at(b, i, k + 1, ch);
-    gpe[e] += s;
-  } else {
+  if (task == 4) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= B * pad * c || !gle) return;
     const int slot = e / c, ch = e % c;
     const int b = slot / pad, i = slot % pad;
     const int l = lab[slot];
     if (l >= 0) unsafeAtomicAdd(gle + (int64_t)l * c + ch, at(b, i, 0, ch));
+    return;
+  }
+  __shared__ float part[QB_W][64];
+  const int n_out = task == 0 ? nq * c : task == 2 ? c : nkp * c;
+  float* g = task == 0 ? gte : task == 1 ? gke : task == 2 ? gie : gpe;
+  if (!g || blockIdx.x * 64 >= n_out) return;   // block-uniform
+  const int e = blockIdx.x * 64 + lane;
+  const bool live = e < n_out;
+  const int row = live ? e / c : 0, ch = live ? e % c : 0;
+  const int nrows = task == 0 ? B * (T_ - 1) : task == 3 ? B * pad : B * nq;
+  float s = 0.f;
+  if (live) {
+    for (int r = w; r < nrows; r += QB_W) {
+      if (task == 0) {
+        const int b = r / (T_ - 1), t = 1 + r % (T_ - 1);
+        s += at(b, pad + row, t, ch);
+      } else if (task == 3) {
+        const int b = r / pad, i = r % pad;
+        if (lab[(int64_t)b * pad + i] >= 0) s += at(b, i, row + 1, ch);
+      } else {
+        const int b = r / nq, q = r % nq;
+        s += at(b, pad + q, task == 1 ? row + 1 : 0, ch);
+      }
+    }
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && live) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < QB_W; ++i) t += part[i][lane];
+    g[e] += t;
   }
 }
 
@@ -1248,17 +1261,19 @@ extern "C" int dp_query_build_bwd(const void* dtgt, const int32_t* dn_label, int
   DP_REQUIRE(dtgt && g_tgt_embed && g_kp_embed && g_inst_embed, "dp_query_build_bwd: null pointer");
   DP_REQUIRE(pad == 0 || dn_label, "dp_query_build_bwd: DN slots need dn_label");
   (void)n_label;
-  int most = nq * c;
-  if (nkp * c > most) most = nkp * c;
-  if (batch * pad * c > most) most = batch * pad * c;
-  dim3 grid(nblk(most, 256), pad > 0 ? 5 : 3);
+  // x blocks: 64 output elements each (tasks 0-3), or 64 * QB_W label_enc elements (task 4)
+  int most = (nq * c + 63) / 64;
+  if ((nkp * c + 63) / 64 > most) most = (nkp * c + 63) / 64;
+  if (pad > 0 && (batch * pad * c + 64 * QB_W - 1) / (64 * QB_W) > most)
+    most = (batch * pad * c + 64 * QB_W - 1) / (64 * QB_W);
+  dim3 grid(most, pad > 0 ? 5 : 3);
   hipStream_t s = as_stream(stream);
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(query_build_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dtgt, dn_label, batch, pad,
-                       nq, nkp, c, g_tgt_embed, g_kp_embed, g_inst_embed, g_label_enc, g_pose_enc);
+    hipLaunchKernelGGL(query_build_bwd_kernel<bf16_t>, grid, dim3(64 * QB_W), 0, s, (const bf16_t*)dtgt, dn_label, batch,
+                       pad, nq, nkp, c, g_tgt_embed, g_kp_embed, g_inst_embed, g_label_enc, g_pose_enc);
   else
-    hipLaunchKernelGGL(query_build_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)dtgt, dn_label, batch, pad,
-                       nq, nkp, c, g_tgt_embed, g_kp_embed, g_inst_embed, g_label_enc, g_pose_enc);
+    hipLaunchKernelGGL(query_build_bwd_kernel<float>, grid, dim3(64 * QB_W), 0, s, (const float*)dtgt, dn_label, batch,
+                       pad, nq, nkp, c, g_tgt_embed, g_kp_embed, g_inst_embed, g_label_enc, g_pose_enc);
   return dp_check_launch("dp_query_build_bwd");
 }
 
