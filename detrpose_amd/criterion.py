@@ -67,15 +67,27 @@ class PackedTargets:
     boxes: torch.Tensor = None   # (T, 4) f32 xyxy (the DN queries' centre points) when given
 
 
+def to_device_async(x: torch.Tensor, device, dtype=None) -> torch.Tensor:
+    """x on `device` (as dtype) without a host synchronisation: a host tensor goes through pinned
+    memory with a non-blocking copy (a pageable host -> GPU copy synchronises the stream, which made
+    the training step's host wait for the forward already queued before the targets were packed)."""
+    if dtype is not None and x.dtype != dtype:
+        x = x.to(dtype)
+    device = torch.device(device)
+    if x.device == device or device.type != "cuda" or x.device.type != "cpu":
+        return x.to(device)
+    return x.contiguous().pin_memory().to(device, non_blocking=True)
+
+
 def pack_targets(targets, num_body_points: int, device) -> PackedTargets:
     sizes = [int(t["labels"].shape[0]) for t in targets]
-    off = torch.tensor(np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32), device=device)
+    off = to_device_async(torch.from_numpy(np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)), device)
     K3 = 3 * num_body_points
     if sum(sizes):
-        label = torch.cat([t["labels"].reshape(-1) for t in targets]).to(device=device, dtype=torch.int32)
-        kps = torch.cat([t["keypoints"].reshape(-1, K3) for t in targets]).to(device=device, dtype=torch.float32)
-        area = torch.cat([t["area"].reshape(-1) for t in targets]).to(device=device, dtype=torch.float32)
-        boxes = (torch.cat([t["boxes"].reshape(-1, 4) for t in targets]).to(device=device, dtype=torch.float32)
+        label = to_device_async(torch.cat([t["labels"].reshape(-1) for t in targets]), device, torch.int32)
+        kps = to_device_async(torch.cat([t["keypoints"].reshape(-1, K3) for t in targets]), device, torch.float32)
+        area = to_device_async(torch.cat([t["area"].reshape(-1) for t in targets]), device, torch.float32)
+        boxes = (to_device_async(torch.cat([t["boxes"].reshape(-1, 4) for t in targets]), device, torch.float32)
                  if all("boxes" in t for t in targets) else None)
     else:
         label = torch.zeros(1, dtype=torch.int32, device=device)

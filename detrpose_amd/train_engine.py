@@ -1023,7 +1023,8 @@ class TrainPlan:
         names = ["", *[f"_{i}" for i in range(L - 1)], "_pre", "_enc_0"]
         if P:
             Hd = self.Hd
-            self.dn_m.copy_(torch.from_numpy(dn_match(sizes, P, num_group)))
+            # pinned + non-blocking: a pageable copy would make the host wait for the queued forward
+            self.dn_m.copy_(torch.from_numpy(dn_match(sizes, P, num_group)).pin_memory(), non_blocking=True)
             # num_boxes (all-reduced, / world, clamped to >= 1: criterion.py:316-322) * num_dn_group
             # (criterion.py:406); dp_pose_loss divides by `world` again, so pass it pre-multiplied
             self.n_dn.copy_(torch.clamp(self.n_boxes / world, min=1.0) * num_group * world)
