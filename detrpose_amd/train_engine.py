@@ -302,6 +302,12 @@ class TrainEngine:
                 self.tdtype).contiguous()
             self.sd32[ca + "offattn.bias"] = torch.cat([self.sd32[ca + "sampling_offsets.bias"],
                                                         self.sd32[ca + "attention_weights.bias"]], 0).contiguous()
+            # the f32 concatenation too (the fp32 mode's GEMM weight itself), so the input gradient
+            # packs its W^T from it and runs on the 1x1 conv kernel (TrainEngine.dgrad) instead of
+            # dp_gemm's 64 x 64 tiles (K = 288 output columns: 48 -> ~15 us per layer)
+            wc = self.w[ca + "offattn.weight"]
+            self.sd32[ca + "offattn.weight"] = wc if wc.dtype == torch.float32 else torch.cat(
+                [self.sd32[ca + "sampling_offsets.weight"], self.sd32[ca + "attention_weights.weight"]], 0).contiguous()
         self._derived(sd)
 
     def _derived(self, sd):
@@ -329,10 +335,16 @@ class TrainEngine:
         with torch.no_grad():
             copies = []   # (f32 source, destination): every copy of this refresh
             if self.tdtype != torch.float32:
-                copies += [(v, self.w[k]) for k, v in self.sd32.items() if k in self.w and self.w[k] is not v]
+                # (the offsets | logits concatenations: from the masters below, never through the f32
+                # concatenation, whose own copy runs in the same unordered batch)
+                copies += [(v, self.w[k]) for k, v in self.sd32.items()
+                           if k in self.w and self.w[k] is not v and not k.endswith("offattn.weight")]
             for l in range(self.L):
                 ca = f"{T_}decoder.layers.{l}.cross_attn."
                 no = self.sd32[ca + "sampling_offsets.weight"].shape[0]
+                if self.sd32[ca + "offattn.weight"] is not self.w[ca + "offattn.weight"]:
+                    copies += [(self.sd32[ca + "sampling_offsets.weight"], self.sd32[ca + "offattn.weight"][:no]),
+                               (self.sd32[ca + "attention_weights.weight"], self.sd32[ca + "offattn.weight"][no:])]
                 copies += [(self.sd32[ca + "sampling_offsets.weight"], self.w[ca + "offattn.weight"][:no]),
                            (self.sd32[ca + "attention_weights.weight"], self.w[ca + "offattn.weight"][no:]),
                            (self.sd32[ca + "sampling_offsets.bias"], self.sd32[ca + "offattn.bias"][:no]),
