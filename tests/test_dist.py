@@ -44,7 +44,9 @@ def _rank_main(rank, port, images, q):
         g = dp.unflatten(gathered, world, per)
         t = dp.max_over_ranks(float(r + 1), world, dev)
         dp.dist.barrier()
-        q.put((r, g["pred_logits"], g["pred_keypoints"], t))
+        # numpy copies: a tensor crosses the queue as a shared-memory fd the parent may try to fetch
+        # after this process has exited (a flaky FileNotFoundError under pytest-xdist)
+        q.put((r, g["pred_logits"].detach().numpy().copy(), g["pred_keypoints"].detach().numpy().copy(), t))
     finally:
         if dp.dist.is_initialized():
             dp.dist.destroy_process_group()
@@ -80,7 +82,7 @@ def test_two_rank_gather_matches_full_batch():
     res = {}
     for _ in range(WORLD):
         r, lg, kp, t = q.get(timeout=300)
-        res[r] = (lg, kp, t)
+        res[r] = (torch.from_numpy(lg), torch.from_numpy(kp), t)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
